@@ -1,0 +1,297 @@
+// pybind11 bindings of the native core: rocm_mpi_amd._C
+//
+// Pure C++ (no HIP headers): pointers travel as integers (torch
+// Tensor.data_ptr()), streams as integers (torch.cuda.Stream.cuda_stream).
+// Shape/dtype/device validation happens in rocm_mpi_amd/ops before any call.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstdint>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "rma/comm.h"
+#include "rma/common.h"
+#include "rma/executor.h"
+#include "rma/halo.h"
+#include "rma/kernels.h"
+#include "rma/topology.h"
+#include "rma/trace.h"
+
+namespace py = pybind11;
+using namespace rma;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+stream_t S(uintptr_t s) { return reinterpret_cast<stream_t>(s); }
+
+using Rect4 = std::tuple<int64_t, int64_t, int64_t, int64_t>;
+using Coef4 = std::tuple<double, double, double, double>;  // mlam, rdx, rdy, dt
+using Geom = std::tuple<int64_t, int64_t, int64_t, int64_t, double, double, double, double, int,
+                        int>;  // gx0 gy0 nxg nyg dx dy xoff yoff periodx periody
+
+std::vector<Rect> to_rects(const std::vector<Rect4>& v) {
+  std::vector<Rect> r;
+  for (auto& t : v) r.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
+  return r;
+}
+StencilCoef to_coef(const Coef4& c) {
+  return {std::get<0>(c), std::get<1>(c), std::get<2>(c), std::get<3>(c)};
+}
+TileGeom to_geom(const Geom& g) {
+  TileGeom t;
+  std::tie(t.gx0, t.gy0, t.nxg, t.nyg, t.dx, t.dy, t.xoff, t.yoff, t.periodx, t.periody) = g;
+  return t;
+}
+Rect4 from_rect(const Rect& r) { return {r.x0, r.x1, r.y0, r.y1}; }
+
+using FieldT = std::tuple<uintptr_t, std::array<int64_t, 3>, int, std::array<int64_t, 3>,
+                          std::array<int64_t, 3>>;
+std::vector<HaloField> to_fields(const std::vector<FieldT>& v) {
+  std::vector<HaloField> out;
+  for (auto& t : v) {
+    HaloField f;
+    f.ptr = reinterpret_cast<void*>(std::get<0>(t));
+    f.size = std::get<1>(t);
+    f.elem_bytes = std::get<2>(t);
+    f.ol = std::get<3>(t);
+    f.hw = std::get<4>(t);
+    out.push_back(f);
+  }
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "rocm_mpi_amd native core (HIP kernels for gfx950, RCCL halo exchange, executor)";
+  static py::exception<Error> exc(m, "NativeError", PyExc_RuntimeError);
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const Error& e) {
+      exc(e.what());
+    }
+  });
+
+  m.def("set_rank_for_errors", &set_rank_for_errors);
+  m.def("rccl_version", &rccl_version);
+  m.def("stencil_strip_cells", &stencil_strip_cells);
+
+  // ---------------- kernels ----------------
+  m.def(
+      "stencil_rects",
+      [](uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
+         const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
+         int kernel, uintptr_t stream, bool gpu) {
+        auto r = to_rects(rects);
+        StencilTuning tn;
+        tn.chunk_rows = chunk_rows;
+        tn.nontemporal = nontemporal;
+        tn.kernel = kernel;
+        if (gpu)
+          stencil_rects_gpu(P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
+                            r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
+        else {
+          py::gil_scoped_release nogil;
+          stencil_rects_cpu(P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
+                            r.data(), (int)r.size(), to_coef(coef));
+        }
+      },
+      py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"), py::arg("rects"),
+      py::arg("coef"), py::arg("chunk_rows") = 64, py::arg("nontemporal") = 0,
+      py::arg("kernel") = 0, py::arg("stream") = 0, py::arg("gpu") = true);
+
+  m.def("flux", [](uintptr_t qx, uintptr_t qy, uintptr_t T, int64_t nx, int64_t ny, double mlam,
+                   double rdx, double rdy, uintptr_t stream, bool gpu) {
+    if (gpu)
+      flux_gpu(P<double>(qx), P<double>(qy), P<const double>(T), nx, ny, mlam, rdx, rdy,
+               S(stream));
+    else
+      flux_cpu(P<double>(qx), P<double>(qy), P<const double>(T), nx, ny, mlam, rdx, rdy);
+  });
+  m.def("residual", [](uintptr_t dTdt, uintptr_t qx, uintptr_t qy, uintptr_t iCp, int64_t nx,
+                       int64_t ny, double rdx, double rdy, uintptr_t stream, bool gpu) {
+    if (gpu)
+      residual_gpu(P<double>(dTdt), P<const double>(qx), P<const double>(qy),
+                   P<const double>(iCp), nx, ny, rdx, rdy, S(stream));
+    else
+      residual_cpu(P<double>(dTdt), P<const double>(qx), P<const double>(qy),
+                   P<const double>(iCp), nx, ny, rdx, rdy);
+  });
+  m.def("update", [](uintptr_t T, uintptr_t dTdt, int64_t nx, int64_t ny, double dt,
+                     uintptr_t stream, bool gpu) {
+    if (gpu)
+      update_gpu(P<double>(T), P<const double>(dTdt), nx, ny, dt, S(stream));
+    else
+      update_cpu(P<double>(T), P<const double>(dTdt), nx, ny, dt);
+  });
+  m.def("init_gaussian", [](uintptr_t T, int64_t nx, int64_t ny, const Geom& g, double lx,
+                            double ly, uintptr_t stream, bool gpu) {
+    if (gpu)
+      init_gaussian_gpu(P<double>(T), nx, ny, to_geom(g), lx, ly, S(stream));
+    else
+      init_gaussian_cpu(P<double>(T), nx, ny, to_geom(g), lx, ly);
+  });
+  m.def("init_random", [](uintptr_t A, int64_t nx, int64_t ny, const Geom& g, uint64_t seed,
+                          double lo, double hi, uintptr_t stream, bool gpu) {
+    if (gpu)
+      init_random_gpu(P<double>(A), nx, ny, to_geom(g), seed, lo, hi, S(stream));
+    else
+      init_random_cpu(P<double>(A), nx, ny, to_geom(g), seed, lo, hi);
+  });
+  m.def("fill", [](uintptr_t A, int64_t n, double v, uintptr_t stream) {
+    fill_gpu(P<double>(A), n, v, S(stream));
+  });
+  m.def("copy2d", [](uintptr_t dst, int64_t dst_ld, uintptr_t src, int64_t src_ld, int64_t n_o,
+                     int64_t n_k, int elem_bytes, uintptr_t stream, bool gpu) {
+    if (gpu)
+      copy2d_gpu(P<void>(dst), dst_ld, P<const void>(src), src_ld, n_o, n_k, elem_bytes,
+                 S(stream));
+    else
+      copy2d_cpu(P<void>(dst), dst_ld, P<const void>(src), src_ld, n_o, n_k, elem_bytes);
+  });
+  m.def("reduce_workspace_doubles", &reduce_workspace_doubles);
+  m.def("reduce_gpu", [](uintptr_t A, int64_t n, int op, uintptr_t out, uintptr_t ws,
+                         uintptr_t stream) {
+    reduce_gpu(P<const double>(A), n, op, P<double>(out), P<double>(ws), S(stream));
+  });
+  m.def("reduce_cpu",
+        [](uintptr_t A, int64_t n, int op) { return reduce_cpu(P<const double>(A), n, op); });
+
+  // ---------------- topology ----------------
+  m.def("dims_create", &dims_create, py::arg("nprocs"), py::arg("dims"));
+  m.attr("PROC_NULL") = kProcNull;
+  py::class_<CartTopology>(m, "CartTopology")
+      .def(py::init<int, std::array<int, 3>, std::array<int, 3>>(), py::arg("nprocs"),
+           py::arg("dims"), py::arg("periods"))
+      .def_property_readonly("nprocs", &CartTopology::nprocs)
+      .def_property_readonly("dims", &CartTopology::dims)
+      .def_property_readonly("periods", &CartTopology::periods)
+      .def("coords", &CartTopology::coords)
+      .def("rank_of", &CartTopology::rank_of)
+      .def("shift", &CartTopology::shift)
+      .def("neighbors", &CartTopology::neighbors);
+
+  // ---------------- communication ----------------
+  py::enum_<DType>(m, "DType")
+      .value("float64", DType::kFloat64)
+      .value("float32", DType::kFloat32)
+      .value("int64", DType::kInt64)
+      .value("int32", DType::kInt32)
+      .value("uint8", DType::kUInt8);
+  py::enum_<RedOp>(m, "RedOp")
+      .value("sum", RedOp::kSum)
+      .value("max", RedOp::kMax)
+      .value("min", RedOp::kMin)
+      .value("prod", RedOp::kProd);
+  py::class_<RcclComm>(m, "RcclComm")
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def(py::init([](int nranks, int rank, py::bytes uid, int device) {
+             std::string s = uid;
+             py::gil_scoped_release nogil;
+             return new RcclComm(nranks, rank, s, device);
+           }),
+           py::arg("nranks"), py::arg("rank"), py::arg("uid"), py::arg("device"))
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def_property_readonly("device", &RcclComm::device)
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end)
+      .def("send", [](RcclComm& c, uintptr_t buf, size_t bytes, int peer,
+                      uintptr_t s) { c.send(P<const void>(buf), bytes, peer, S(s)); })
+      .def("recv", [](RcclComm& c, uintptr_t buf, size_t bytes, int peer,
+                      uintptr_t s) { c.recv(P<void>(buf), bytes, peer, S(s)); })
+      .def("allreduce",
+           [](RcclComm& c, uintptr_t sb, uintptr_t rb, size_t count, DType dt, RedOp op,
+              uintptr_t s) { c.allreduce(P<const void>(sb), P<void>(rb), count, dt, op, S(s)); })
+      .def("broadcast",
+           [](RcclComm& c, uintptr_t sb, uintptr_t rb, size_t count, DType dt, int root,
+              uintptr_t s) { c.broadcast(P<const void>(sb), P<void>(rb), count, dt, root, S(s)); })
+      .def("gather", [](RcclComm& c, uintptr_t sb, uintptr_t rb, size_t bytes, int root,
+                        uintptr_t s) { c.gather(P<const void>(sb), P<void>(rb), bytes, root, S(s)); })
+      .def(
+          "barrier", [](RcclComm& c, uintptr_t s, double t) { c.barrier(S(s), t); },
+          py::arg("stream"), py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "wait", [](RcclComm& c, uintptr_t s, double t) { c.wait(S(s), t); }, py::arg("stream"),
+          py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>())
+      .def("check_async", &RcclComm::check_async)
+      .def("abort", &RcclComm::abort)
+      .def_property_readonly("aborted", &RcclComm::aborted);
+
+  py::class_<HaloExchanger>(m, "HaloExchanger")
+      .def(py::init([](RcclComm* comm, int self_rank,
+                       std::array<std::array<int, 2>, 3> nbr) {
+             return new HaloExchanger(comm, self_rank, nbr);
+           }),
+           py::arg("comm").none(true), py::arg("self_rank"), py::arg("neighbors"),
+           py::keep_alive<1, 2>())
+      .def(
+          "exchange",
+          [](HaloExchanger& h, const std::vector<FieldT>& fields, uintptr_t s, int mask) {
+            h.exchange(to_fields(fields), S(s), mask);
+          },
+          py::arg("fields"), py::arg("stream"), py::arg("dims_mask") = 7)
+      .def(
+          "prepare",
+          [](HaloExchanger& h, const std::vector<FieldT>& fields, int mask) {
+            h.prepare(to_fields(fields), mask);
+          },
+          py::arg("fields"), py::arg("dims_mask") = 7)
+      .def("active", &HaloExchanger::active)
+      .def_property_readonly("neighbors", &HaloExchanger::neighbors)
+      .def_property_readonly("bytes_sent_last", &HaloExchanger::bytes_sent_last);
+
+  // ---------------- executor ----------------
+  py::class_<DiffusionExecutor>(m, "Executor")
+      .def(py::init([](uintptr_t T, uintptr_t T2, uintptr_t iCp, int64_t nx, int64_t ny, int mode,
+                       const Coef4& coef, int chunk_rows, int nontemporal, int kernel,
+                       int64_t bwx, int64_t bwy, int use_graph, int graph_steps,
+                       HaloExchanger* halo, uintptr_t qx, uintptr_t qy, uintptr_t dTdt) {
+             ExecParams p;
+             p.mode = static_cast<Mode>(mode);
+             p.coef = to_coef(coef);
+             p.tune.chunk_rows = chunk_rows;
+             p.tune.nontemporal = nontemporal;
+             p.tune.kernel = kernel;
+             p.bwx = bwx;
+             p.bwy = bwy;
+             p.use_graph = use_graph;
+             p.graph_steps = graph_steps;
+             return new DiffusionExecutor(P<double>(T), P<double>(T2), P<const double>(iCp), nx,
+                                          ny, p, halo, P<double>(qx), P<double>(qy),
+                                          P<double>(dTdt));
+           }),
+           py::arg("T"), py::arg("T2"), py::arg("iCp"), py::arg("nx"), py::arg("ny"),
+           py::arg("mode"), py::arg("coef"), py::arg("chunk_rows") = 64,
+           py::arg("nontemporal") = 0, py::arg("kernel") = 0, py::arg("bwx") = 127,
+           py::arg("bwy") = 4, py::arg("use_graph") = 0, py::arg("graph_steps") = 0,
+           py::arg("halo").none(true) = nullptr, py::arg("qx") = 0, py::arg("qy") = 0,
+           py::arg("dTdt") = 0, py::keep_alive<1, 16>())
+      .def(
+          "run", [](DiffusionExecutor& e, int64_t n, uintptr_t s) { e.run(n, S(s)); },
+          py::arg("nsteps"), py::arg("stream"))
+      .def_property_readonly("parity", &DiffusionExecutor::parity)
+      .def_property_readonly("steps_done", &DiffusionExecutor::steps_done)
+      .def_property_readonly("frame_rects",
+                             [](const DiffusionExecutor& e) {
+                               std::vector<Rect4> v;
+                               for (auto& r : e.frame_rects()) v.push_back(from_rect(r));
+                               return v;
+                             })
+      .def_property_readonly("interior_rect",
+                             [](const DiffusionExecutor& e) { return from_rect(e.interior_rect()); });
+
+  // ---------------- tracing ----------------
+  m.def("trace_enable", &trace_enable);
+  m.def("trace_enabled", &trace_enabled);
+  m.def("trace_push", [](const std::string& s) { trace_push(s.c_str()); });
+  m.def("trace_pop", &trace_pop);
+  m.def("trace_mark", [](const std::string& s) { trace_mark(s.c_str()); });
+}

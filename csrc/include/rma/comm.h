@@ -1,0 +1,68 @@
+// GPU-direct communicator: RCCL point-to-point and tiny collectives over xGMI.
+//
+// Replaces the reference's MPI.jl + ROCm-aware OpenMPI/UCX transport
+// (scripts/setenv.sh:11-18, scripts/rocmaware_test_selectdevice.jl:3-24) and
+// the MPI calls hidden inside ImplicitGlobalGrid. Bootstrap is
+// MPI-free: rank 0 calls unique_id(), the bytes travel through the
+// torch.distributed store, every rank constructs RcclComm(nranks, rank, id).
+//
+// Failure detection: every RCCL/HIP return code is checked and
+// turned into rma::Error carrying the rank; wait() polls the stream together
+// with ncclCommGetAsyncError and aborts the communicator after a timeout, so a
+// dead peer produces an exception instead of a hang.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+
+#include "rma/kernels.h"
+
+namespace rma {
+
+enum class DType : int { kFloat64 = 0, kFloat32 = 1, kInt64 = 2, kInt32 = 3, kUInt8 = 4 };
+enum class RedOp : int { kSum = 0, kMax = 1, kMin = 2, kProd = 3 };
+
+class RcclComm {
+ public:
+  static std::string unique_id();  // 128 opaque bytes, generate on ONE rank
+  RcclComm(int nranks, int rank, const std::string& uid, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+  int device() const { return device_; }
+
+  void group_start();
+  void group_end();
+  void send(const void* buf, size_t bytes, int peer, stream_t stream);
+  void recv(void* buf, size_t bytes, int peer, stream_t stream);
+  void allreduce(const void* sendbuf, void* recvbuf, size_t count, DType dt, RedOp op,
+                 stream_t stream);
+  void broadcast(const void* sendbuf, void* recvbuf, size_t count, DType dt, int root,
+                 stream_t stream);
+  // Root gathers `bytes` from every rank into recvbuf (rank-major); P2P-based.
+  void gather(const void* sendbuf, void* recvbuf, size_t bytes, int root, stream_t stream);
+  // Device-side barrier: 1-element all-reduce on `stream`, then wait().
+  void barrier(stream_t stream, double timeout_s);
+  // Block until `stream` drains; throw (after ncclCommAbort) on async error or
+  // timeout (timeout_s <= 0: no timeout).
+  void wait(stream_t stream, double timeout_s);
+  // Raises if RCCL reported an asynchronous error.
+  void check_async();
+  void abort();
+  bool aborted() const { return aborted_; }
+
+ private:
+  int nranks_, rank_, device_;
+  void* comm_ = nullptr;  // ncclComm_t
+  double* scratch_ = nullptr;  // 2 doubles of device memory for barrier()
+  bool aborted_ = false;
+};
+
+int rccl_version();
+
+}  // namespace rma

@@ -1,0 +1,87 @@
+// Native time-loop executor for the diffusion variants.
+//
+// The reference drives every step from the host with a blocking wait after
+// each kernel (scripts/diffusion_2D_perf.jl:49, diffusion_2D_kp.jl:88-90) and
+// never overlaps communication (perf_hide's overlap is commented "not ready
+// yet", diffusion_2D_perf_hide.jl:94-101). Here the whole loop is enqueued
+// from C++ with stream ordering only:
+//
+//   kPerf : [fused stencil] -> [halo(T2)] -> swap                    (1 stream)
+//   kHide : hi-prio stream: [frame rects] -> [halo(T2): pack, RCCL, unpack]
+//           lo-prio stream: [interior rect]            (concurrently)
+//           join both, swap. This is the reference's intended variant (3)
+//           with exact frame/interior grids.
+//   kKp   : [flux] -> [residual] -> [update T in place] -> [halo(T)]
+//
+// Python never waits inside the loop; run() returns as soon as n steps are
+// enqueued, ordered after the caller's stream and before its next work.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "rma/halo.h"
+#include "rma/kernels.h"
+
+namespace rma {
+
+enum class Mode : int { kPerf = 0, kHide = 1, kKp = 2 };
+
+struct ExecParams {
+  Mode mode = Mode::kPerf;
+  StencilCoef coef{};
+  StencilTuning tune{};
+  int64_t bwx = 127, bwy = 4;  // perf_hide frame widths (x rounded to a strip)
+  int use_graph = 0;           // capture steps into a hipGraph and replay
+  int graph_steps = 0;         // steps per captured graph (even; 0 = auto)
+};
+
+class DiffusionExecutor {
+ public:
+  // T, T2, iCp: (ny, nx) device fields; qx/qy/dTdt only for kKp.
+  DiffusionExecutor(double* T, double* T2, const double* iCp, int64_t nx, int64_t ny,
+                    const ExecParams& p, HaloExchanger* halo, double* qx = nullptr,
+                    double* qy = nullptr, double* dTdt = nullptr);
+  ~DiffusionExecutor();
+  DiffusionExecutor(const DiffusionExecutor&) = delete;
+  DiffusionExecutor& operator=(const DiffusionExecutor&) = delete;
+
+  // Enqueue n steps after the work already on caller_stream; caller_stream is
+  // made to wait for them. Asynchronous.
+  void run(int64_t nsteps, stream_t caller_stream);
+  // Number of completed buffer swaps mod 2: 0 -> current field is T, 1 -> T2.
+  int parity() const { return parity_; }
+  int64_t steps_done() const { return steps_; }
+  std::vector<Rect> frame_rects() const { return frame_; }
+  Rect interior_rect() const { return interior_; }
+  Rect full_rect() const { return full_; }
+
+ private:
+  void enqueue_step(double* Tin, double* Tout);
+  void exchange(double* A, stream_t s);
+  void build_graph(int64_t steps);
+  void run_eager(int64_t nsteps);
+
+  double* T_;
+  double* T2_;
+  const double* iCp_;
+  int64_t nx_, ny_;
+  ExecParams p_;
+  HaloExchanger* halo_;
+  double *qx_, *qy_, *dTdt_;
+  Rect full_{}, interior_{};
+  std::vector<Rect> frame_;
+  void* s_hi_ = nullptr;  // hipStream_t
+  void* s_lo_ = nullptr;
+  void* e_hi_ = nullptr;  // hipEvent_t
+  void* e_lo_ = nullptr;
+  void* e_in_ = nullptr;
+  void* graph_exec_ = nullptr;  // hipGraphExec_t
+  int64_t graph_len_ = 0;
+  int parity_ = 0;
+  int64_t steps_ = 0;
+};
+
+}  // namespace rma

@@ -1,0 +1,75 @@
+// Halo exchange engine: ImplicitGlobalGrid's update_halo! for
+// device arrays, GPU-direct over RCCL.
+//
+// Semantics kept from IGG (call sites scripts/diffusion_2D_ap.jl:42,
+// diffusion_2D_kp.jl:91, diffusion_2D_perf.jl:51):
+//   * dimensions are exchanged one after the other (x, then y, then z), so the
+//     later planes carry the corner values received earlier;
+//   * per side with a real neighbour: the send plane(s) [ol-hw, ol) (low side)
+//     and [n-ol, n-ol+hw) (high side) go to the neighbour, whose halo planes
+//     [0,hw) / [n-hw,n) receive them (0-based; ol = overlap of THIS array, which
+//     differs from the grid overlap by size(A)-n for staggered arrays);
+//   * periodic dimensions with a single process copy locally.
+// MI355X-first changes: contiguous planes (y-planes of 2D fields, z-planes)
+// are sent/received in place (zero-copy); only strided planes go through
+// persistent pack/unpack buffers (allocated once, reused — no allocation in
+// the steady state, so a step can be captured in a hipGraph); all sends and
+// receives of one dimension form ONE RCCL group on the caller's stream.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <vector>
+
+#include "rma/comm.h"
+#include "rma/kernels.h"
+
+namespace rma {
+
+struct HaloField {
+  void* ptr = nullptr;
+  std::array<int64_t, 3> size{1, 1, 1};  // extent along x, y, z (x fastest)
+  int elem_bytes = 8;
+  std::array<int64_t, 3> ol{2, 2, 2};    // overlap of this array per dim
+  std::array<int64_t, 3> hw{1, 1, 1};    // halo width per dim
+};
+
+// A strided view of one plane block of a field: n_o rows of n_k contiguous
+// elements, rows `ld` elements apart, starting at element `offset`.
+struct PlaneView {
+  int64_t offset, n_o, n_k, ld;
+  bool contiguous() const { return n_o == 1 || ld == n_k; }
+  int64_t elems() const { return n_o * n_k; }
+};
+PlaneView plane_view(const HaloField& f, int dim, int64_t index0);
+
+class HaloExchanger {
+ public:
+  // neighbors[d] = {low, high} ranks (kProcNull = -1 at open edges);
+  // comm may be null when every neighbour is either absent or this rank.
+  HaloExchanger(RcclComm* comm, int self_rank, std::array<std::array<int, 2>, 3> neighbors);
+  ~HaloExchanger();
+  HaloExchanger(const HaloExchanger&) = delete;
+  HaloExchanger& operator=(const HaloExchanger&) = delete;
+
+  // Enqueue the full exchange of all fields on `stream` (asynchronous).
+  // dims_mask bit d enables dimension d.
+  void exchange(const std::vector<HaloField>& fields, stream_t stream, int dims_mask = 7);
+  // Pre-allocate the pack buffers for this field set (call before capture).
+  void prepare(const std::vector<HaloField>& fields, int dims_mask = 7);
+
+  bool active(int dim) const;  // any neighbour in this dim?
+  const std::array<std::array<int, 2>, 3>& neighbors() const { return nbr_; }
+  int64_t bytes_sent_last() const { return bytes_last_; }
+
+ private:
+  void* buffer(size_t slot, size_t bytes);
+  RcclComm* comm_;
+  int self_;
+  std::array<std::array<int, 2>, 3> nbr_;
+  std::vector<void*> bufs_;
+  std::vector<size_t> buf_bytes_;
+  int64_t bytes_last_ = 0;
+};
+
+}  // namespace rma

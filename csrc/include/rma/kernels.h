@@ -1,0 +1,107 @@
+// rocm_mpi_amd native core — kernel launch API (host side).
+//
+// Every GPU entry point enqueues work on the given HIP stream (passed as an
+// opaque pointer so this header stays HIP-free for the pybind11 layer) and
+// returns immediately. The *_cpu twins are bit-identical host implementations
+// used for CPU-only runs (the reference's "ap 256² single-rank CPU array path",
+// BASELINE.json configs[0]) and as the numerics oracle in tests.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "rma/common.h"
+
+namespace rma {
+
+using stream_t = void*;  // hipStream_t
+
+// ---------------------------------------------------------------------------
+// Fused 5-point stencil (K4 of SURVEY.md §2.3; reference
+// scripts/diffusion_2D_perf.jl:3-13). Updates every cell of every rect in ONE
+// launch: T2[r] = f(T, iCp)[r]. The split boundary/interior steps of
+// perf_hide (K5, scripts/diffusion_2D_perf_hide.jl:15-29) are the same launch
+// with the frame rects / interior rect, so the arithmetic is shared bitwise.
+// ---------------------------------------------------------------------------
+constexpr int kMaxRects = 8;
+
+struct StencilTuning {
+  int chunk_rows = 64;     // rows marched by one wave-task
+  int nontemporal = 0;     // 1: non-temporal T2 stores
+  int kernel = 0;          // 0 = register march (default), 1 = LDS-tiled
+};
+
+void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                       const Rect* rects, int nrects, const StencilCoef& c,
+                       const StencilTuning& tune, stream_t stream);
+void stencil_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                       const Rect* rects, int nrects, const StencilCoef& c);
+
+// Width (in cells) of one wave's x-strip in the march kernel; perf_hide rounds
+// its x-frame so the interior rect starts on a strip boundary.
+int stencil_strip_cells(int64_t nx);
+
+// ---------------------------------------------------------------------------
+// kp: the three-kernel formulation (K1-K3; scripts/diffusion_2D_kp.jl:16-54).
+//   qx: (ny-2, nx-1)  qy: (ny-1, nx-2)  dTdt: (ny-2, nx-2)
+// ---------------------------------------------------------------------------
+void flux_gpu(double* qx, double* qy, const double* T, int64_t nx, int64_t ny, double mlam,
+              double rdx, double rdy, stream_t stream);
+void residual_gpu(double* dTdt, const double* qx, const double* qy, const double* iCp, int64_t nx,
+                  int64_t ny, double rdx, double rdy, stream_t stream);
+void update_gpu(double* T, const double* dTdt, int64_t nx, int64_t ny, double dt, stream_t stream);
+void flux_cpu(double* qx, double* qy, const double* T, int64_t nx, int64_t ny, double mlam,
+              double rdx, double rdy);
+void residual_cpu(double* dTdt, const double* qx, const double* qy, const double* iCp, int64_t nx,
+                  int64_t ny, double rdx, double rdy);
+void update_cpu(double* T, const double* dTdt, int64_t nx, int64_t ny, double dt);
+
+// ---------------------------------------------------------------------------
+// Initial conditions (K9/K10). Device-side so a 288 GB tile never touches the
+// host.
+// ---------------------------------------------------------------------------
+// Geometry of a local tile inside the implicit global grid: global coordinate
+// of local cell ix is x = (gx0 + ix)*dx + xoff, wrapped into [0, nxg*dx) when
+// periodic (ImplicitGlobalGrid x_g semantics).
+struct TileGeom {
+  int64_t gx0, gy0;    // global index of local cell (0,0)
+  int64_t nxg, nyg;    // global grid size
+  double dx, dy;
+  double xoff, yoff;   // staggering offsets 0.5*(n - size(A))*d
+  int periodx, periody;
+};
+
+// T = exp(-(x+dx/2-lx/2)^2 - (y+dy/2-ly/2)^2)   (ap.jl:28)
+void init_gaussian_gpu(double* T, int64_t nx, int64_t ny, const TileGeom& g, double lx, double ly,
+                       stream_t stream);
+void init_gaussian_cpu(double* T, int64_t nx, int64_t ny, const TileGeom& g, double lx, double ly);
+// Counter-based uniform [lo,hi) keyed by the GLOBAL cell index, so every
+// decomposition of the same global grid sees the same field (bitwise) and the
+// overlap cells of neighbouring ranks agree.
+void init_random_gpu(double* A, int64_t nx, int64_t ny, const TileGeom& g, uint64_t seed,
+                     double lo, double hi, stream_t stream);
+void init_random_cpu(double* A, int64_t nx, int64_t ny, const TileGeom& g, uint64_t seed,
+                     double lo, double hi);
+void fill_gpu(double* A, int64_t n, double value, stream_t stream);
+
+// ---------------------------------------------------------------------------
+// Halo pack / unpack (K7/K8): strided 2D block copy. Both sides have a
+// contiguous inner dimension of n_k elements; outer rows are dst_ld / src_ld
+// elements apart. Element size in bytes: 2, 4, 8 or 16.
+// ---------------------------------------------------------------------------
+void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int64_t n_o,
+                int64_t n_k, int elem_bytes, stream_t stream);
+void copy2d_cpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int64_t n_o,
+                int64_t n_k, int elem_bytes);
+
+// ---------------------------------------------------------------------------
+// Reductions for verification / NaN guards. Result is written
+// to out (device memory, 1 double). workspace must hold reduce_workspace_doubles().
+// ---------------------------------------------------------------------------
+enum ReduceOp : int { kSum = 0, kMax = 1, kMin = 2, kMaxAbs = 3, kNonFinite = 4 };
+int64_t reduce_workspace_doubles();
+void reduce_gpu(const double* A, int64_t n, int op, double* out, double* workspace,
+                stream_t stream);
+double reduce_cpu(const double* A, int64_t n, int op);
+
+}  // namespace rma

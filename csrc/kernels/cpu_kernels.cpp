@@ -1,0 +1,106 @@
+// Host (CPU) twins of the GPU kernels. Same expressions, same operation order,
+// compiled with -ffp-contract=off, so CPU and GPU results agree bitwise (the
+// exp() of init_gaussian excepted: libm vs OCML may differ by one ulp).
+// These serve the CPU array path (BASELINE.json configs[0]: "ap 256x256 fp64
+// single-rank CPU array path") and multi-rank CPU runs over gloo.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+#include "rma/kernels.h"
+#include "rma/parallel_for.h"
+
+namespace rma {
+
+namespace {
+inline double cell(double xl, double c, double xr, double up, double dn, double ic,
+                   const StencilCoef& k) {
+  const double qxR = (k.mlam * (xr - c)) * k.rdx;
+  const double qxL = (k.mlam * (c - xl)) * k.rdx;
+  const double qyU = (k.mlam * (dn - c)) * k.rdy;
+  const double qyD = (k.mlam * (c - up)) * k.rdy;
+  return c + k.dt * (ic * ((-(qxR - qxL)) * k.rdx - (qyU - qyD) * k.rdy));
+}
+}  // namespace
+
+void stencil_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                       const Rect* rects, int nrects, const StencilCoef& c) {
+  RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
+  for (int i = 0; i < nrects; ++i) {
+    const Rect r = rects[i];
+    if (r.empty()) continue;
+    RMA_CHECK_ARG(r.x0 >= 1 && r.x1 <= nx - 1 && r.y0 >= 1 && r.y1 <= ny - 1,
+                  "rect outside interior");
+    parallel_for(r.y0, r.y1, 64, [&](int64_t y) {
+      const double* up = T + (y - 1) * nx;
+      const double* cu = T + y * nx;
+      const double* dn = T + (y + 1) * nx;
+      const double* ic = iCp + y * nx;
+      double* out = T2 + y * nx;
+      for (int64_t x = r.x0; x < r.x1; ++x)
+        out[x] = cell(cu[x - 1], cu[x], cu[x + 1], up[x], dn[x], ic[x], c);
+    });
+  }
+}
+
+void flux_cpu(double* qx, double* qy, const double* T, int64_t nx, int64_t ny, double mlam,
+              double rdx, double rdy) {
+  parallel_for(0, ny - 1, 64, [&](int64_t j) {
+    if (j < ny - 2) {
+      const double* r = T + (j + 1) * nx;
+      for (int64_t i = 0; i < nx - 1; ++i) qx[j * (nx - 1) + i] = (mlam * (r[i + 1] - r[i])) * rdx;
+    }
+    for (int64_t i = 0; i < nx - 2; ++i)
+      qy[j * (nx - 2) + i] = (mlam * (T[(j + 1) * nx + i + 1] - T[j * nx + i + 1])) * rdy;
+  });
+}
+
+void residual_cpu(double* dTdt, const double* qx, const double* qy, const double* iCp, int64_t nx,
+                  int64_t ny, double rdx, double rdy) {
+  parallel_for(0, ny - 2, 64, [&](int64_t j) {
+    for (int64_t i = 0; i < nx - 2; ++i) {
+      const double ddx = (qx[j * (nx - 1) + i + 1] - qx[j * (nx - 1) + i]) * rdx;
+      const double ddy = (qy[(j + 1) * (nx - 2) + i] - qy[j * (nx - 2) + i]) * rdy;
+      dTdt[j * (nx - 2) + i] = iCp[(j + 1) * nx + i + 1] * (-(ddx + ddy));
+    }
+  });
+}
+
+void update_cpu(double* T, const double* dTdt, int64_t nx, int64_t ny, double dt) {
+  parallel_for(0, ny - 2, 64, [&](int64_t j) {
+    for (int64_t i = 0; i < nx - 2; ++i) {
+      double* p = T + (j + 1) * nx + i + 1;
+      *p = *p + dt * dTdt[j * (nx - 2) + i];
+    }
+  });
+}
+
+void copy2d_cpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int64_t n_o,
+                int64_t n_k, int elem_bytes) {
+  RMA_CHECK_ARG(elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16,
+                "unsupported element size " << elem_bytes);
+  char* d = static_cast<char*>(dst);
+  const char* s = static_cast<const char*>(src);
+  for (int64_t o = 0; o < n_o; ++o)
+    std::memcpy(d + o * dst_ld * elem_bytes, s + o * src_ld * elem_bytes, n_k * elem_bytes);
+}
+
+double reduce_cpu(const double* A, int64_t n, int op) {
+  double v = (op == kMax) ? -std::numeric_limits<double>::infinity()
+                          : (op == kMin ? std::numeric_limits<double>::infinity() : 0.0);
+  for (int64_t i = 0; i < n; ++i) {
+    const double a = A[i];
+    switch (op) {
+      case kSum: v += a; break;
+      case kMax: v = std::fmax(v, a); break;
+      case kMin: v = std::fmin(v, a); break;
+      case kMaxAbs: v = std::fmax(v, std::fabs(a)); break;
+      case kNonFinite: v += std::isfinite(a) ? 0.0 : 1.0; break;
+      default: RMA_CHECK_ARG(false, "bad reduce op " << op);
+    }
+  }
+  return v;
+}
+
+}  // namespace rma

@@ -1,0 +1,276 @@
+// Initial-condition, fill, halo pack/unpack and reduction kernels (gfx950).
+//
+//  * init_gaussian: device version of the host comprehension at
+//    scripts/diffusion_2D_ap.jl:28 (exp of the squared distance to the domain
+//    centre, using ImplicitGlobalGrid's x_g/y_g global coordinates).
+//  * init_random: synthetic random temperature field (BASELINE.json north
+//    star), counter-based and keyed by the global cell index so it is
+//    decomposition-invariant.
+//  * copy2d: the pack (K7) / unpack (K8) primitive of update_halo!: a strided
+//    plane <-> contiguous buffer copy; x-planes of a row-major (ny,nx) field
+//    are nx-strided, y-planes are contiguous (sent without packing).
+//  * reduce: sum / max / min / max|.| / non-finite count for verification and
+//    NaN guards.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "rma/hip_check.h"
+#include "rma/kernels.h"
+#include "rma/parallel_for.h"
+
+namespace rma {
+namespace {
+
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__host__ __device__ inline int64_t wrap_index(int64_t g, int64_t n, int periodic) {
+  if (!periodic) return g;
+  // first local cell of a periodic global grid is a ghost: shift by one.
+  int64_t k = (g - 1) % n;
+  return k < 0 ? k + n : k;
+}
+
+__host__ __device__ inline double global_coord(int64_t g, double d, double off, int64_t n,
+                                               int periodic) {
+  // ImplicitGlobalGrid x_g: (coords*(nx-ol) + ix-1)*dx + x0, periodic shift.
+  double x = (double)g * d + off;
+  if (periodic) {
+    x = x - d;
+    if (x > (double)(n - 1) * d) x = x - (double)n * d;
+    if (x < 0) x = x + (double)n * d;
+  }
+  return x;
+}
+
+__host__ __device__ inline double uniform01(uint64_t seed, uint64_t idx) {
+  const uint64_t z = mix64(seed + (idx + 1) * 0x9E3779B97F4A7C15ull);
+  return (double)(z >> 11) * 0x1.0p-53;
+}
+
+__global__ void init_gaussian_kernel(double* __restrict__ T, int64_t nx, int64_t ny, TileGeom g,
+                                     double lx, double ly) {
+  const int64_t n = nx * ny;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t iy = i / nx, ix = i - iy * nx;
+    const double x = global_coord(g.gx0 + ix, g.dx, g.xoff, g.nxg, g.periodx);
+    const double y = global_coord(g.gy0 + iy, g.dy, g.yoff, g.nyg, g.periody);
+    const double a = (x + g.dx / 2) - lx / 2;
+    const double b = (y + g.dy / 2) - ly / 2;
+    T[i] = exp(-(a * a) - (b * b));
+  }
+}
+
+__global__ void init_random_kernel(double* __restrict__ A, int64_t nx, int64_t ny, TileGeom g,
+                                   uint64_t seed, double lo, double hi) {
+  const int64_t n = nx * ny;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t iy = i / nx, ix = i - iy * nx;
+    const int64_t gx = wrap_index(g.gx0 + ix, g.nxg, g.periodx);
+    const int64_t gy = wrap_index(g.gy0 + iy, g.nyg, g.periody);
+    const double u = uniform01(seed, (uint64_t)(gy * g.nxg + gx));
+    A[i] = lo + (hi - lo) * u;
+  }
+}
+
+__global__ void fill_kernel(double* __restrict__ A, int64_t n, double v) {
+  const int64_t n2 = n / 2;
+  double2* A2 = reinterpret_cast<double2*>(A);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    A2[i] = make_double2(v, v);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) A[n - 1] = v;
+}
+
+__global__ void fill_scalar_kernel(double* __restrict__ A, int64_t n, double v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    A[i] = v;
+}
+
+template <typename E>
+__global__ void copy2d_kernel(E* __restrict__ dst, int64_t dst_ld, const E* __restrict__ src,
+                              int64_t src_ld, int64_t n_o, int64_t n_k) {
+  const int64_t n = n_o * n_k;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = i / n_k, k = i - o * n_k;
+    dst[o * dst_ld + k] = src[o * src_ld + k];
+  }
+}
+
+struct alignas(16) E16 {
+  uint64_t a, b;
+};
+
+constexpr int kRedBlock = 256;
+constexpr int kRedMaxBlocks = 1024;
+
+__device__ inline double red_init(int op) {
+  switch (op) {
+    case kMax: return -INFINITY;
+    case kMin: return INFINITY;
+    default: return 0.0;
+  }
+}
+
+__device__ inline double red_map(int op, double v) {
+  switch (op) {
+    case kMaxAbs: return fabs(v);
+    case kNonFinite: return isfinite(v) ? 0.0 : 1.0;
+    default: return v;
+  }
+}
+
+__device__ inline double red_comb(int op, double a, double b) {
+  switch (op) {
+    case kMax:
+    case kMaxAbs: return fmax(a, b);
+    case kMin: return fmin(a, b);
+    default: return a + b;
+  }
+}
+
+__device__ double block_reduce(double v, int op) {
+  __shared__ double part[kRedBlock / 64];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = red_comb(op, v, __shfl_down(v, off));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) part[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kRedBlock / 64; ++w) v = red_comb(op, v, part[w]);
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kRedBlock) void reduce_stage1(const double* __restrict__ A, int64_t n,
+                                                           int op, double* __restrict__ partial) {
+  double v = red_init(op);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    v = red_comb(op, v, red_map(op, A[i]));
+  v = block_reduce(v, op);
+  if (threadIdx.x == 0) partial[blockIdx.x] = v;
+}
+
+__global__ __launch_bounds__(kRedBlock) void reduce_stage2(const double* __restrict__ partial,
+                                                           int nparts, int op,
+                                                           double* __restrict__ out) {
+  // map already applied in stage 1; only combine here (non-finite: sum of counts).
+  const int cop = (op == kMaxAbs) ? kMax : (op == kNonFinite ? kSum : op);
+  double v = red_init(cop);
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) v = red_comb(cop, v, partial[i]);
+  v = block_reduce(v, cop);
+  if (threadIdx.x == 0) *out = v;
+}
+
+unsigned grid_stride_blocks(int64_t n, int block) {
+  int64_t b = (n + block - 1) / block;
+  if (b > 256 * 16) b = 256 * 16;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace
+
+void init_gaussian_gpu(double* T, int64_t nx, int64_t ny, const TileGeom& g, double lx, double ly,
+                       stream_t stream) {
+  RMA_CHECK_ARG(nx > 0 && ny > 0, "empty tile");
+  init_gaussian_kernel<<<grid_stride_blocks(nx * ny, 256), 256, 0, as_stream(stream)>>>(T, nx, ny, g,
+                                                                                        lx, ly);
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+void init_random_gpu(double* A, int64_t nx, int64_t ny, const TileGeom& g, uint64_t seed,
+                     double lo, double hi, stream_t stream) {
+  RMA_CHECK_ARG(nx > 0 && ny > 0, "empty tile");
+  init_random_kernel<<<grid_stride_blocks(nx * ny, 256), 256, 0, as_stream(stream)>>>(
+      A, nx, ny, g, seed, lo, hi);
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+void fill_gpu(double* A, int64_t n, double value, stream_t stream) {
+  if (n <= 0) return;
+  if ((reinterpret_cast<uintptr_t>(A) & 15) == 0)
+    fill_kernel<<<grid_stride_blocks(n / 2 + 1, 256), 256, 0, as_stream(stream)>>>(A, n, value);
+  else
+    fill_scalar_kernel<<<grid_stride_blocks(n, 256), 256, 0, as_stream(stream)>>>(A, n, value);
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int64_t n_o,
+                int64_t n_k, int elem_bytes, stream_t stream) {
+  if (n_o <= 0 || n_k <= 0) return;
+  RMA_CHECK_ARG(dst_ld >= n_k && src_ld >= n_k, "leading dims smaller than row length");
+  const unsigned g = grid_stride_blocks(n_o * n_k, 256);
+  hipStream_t s = as_stream(stream);
+  switch (elem_bytes) {
+    case 2:
+      copy2d_kernel<uint16_t><<<g, 256, 0, s>>>((uint16_t*)dst, dst_ld, (const uint16_t*)src,
+                                                src_ld, n_o, n_k);
+      break;
+    case 4:
+      copy2d_kernel<uint32_t><<<g, 256, 0, s>>>((uint32_t*)dst, dst_ld, (const uint32_t*)src,
+                                                src_ld, n_o, n_k);
+      break;
+    case 8:
+      copy2d_kernel<uint64_t><<<g, 256, 0, s>>>((uint64_t*)dst, dst_ld, (const uint64_t*)src,
+                                                src_ld, n_o, n_k);
+      break;
+    case 16:
+      copy2d_kernel<E16><<<g, 256, 0, s>>>((E16*)dst, dst_ld, (const E16*)src, src_ld, n_o, n_k);
+      break;
+    default: RMA_CHECK_ARG(false, "unsupported element size " << elem_bytes);
+  }
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+int64_t reduce_workspace_doubles() { return kRedMaxBlocks; }
+
+void reduce_gpu(const double* A, int64_t n, int op, double* out, double* workspace,
+                stream_t stream) {
+  RMA_CHECK_ARG(op >= kSum && op <= kNonFinite, "bad reduce op " << op);
+  int64_t nb = (n + kRedBlock * 8 - 1) / (kRedBlock * 8);
+  if (nb < 1) nb = 1;
+  if (nb > kRedMaxBlocks) nb = kRedMaxBlocks;
+  hipStream_t s = as_stream(stream);
+  reduce_stage1<<<(unsigned)nb, kRedBlock, 0, s>>>(A, n, op, workspace);
+  RMA_HIP_LAUNCH_CHECK();
+  reduce_stage2<<<1, kRedBlock, 0, s>>>(workspace, (int)nb, op, out);
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+// --------------------------- CPU twins (same formulas) ---------------------
+void init_gaussian_cpu(double* T, int64_t nx, int64_t ny, const TileGeom& g, double lx,
+                       double ly) {
+  parallel_for(0, ny, 16, [&](int64_t iy) {
+    const double y = global_coord(g.gy0 + iy, g.dy, g.yoff, g.nyg, g.periody);
+    const double b = (y + g.dy / 2) - ly / 2;
+    for (int64_t ix = 0; ix < nx; ++ix) {
+      const double x = global_coord(g.gx0 + ix, g.dx, g.xoff, g.nxg, g.periodx);
+      const double a = (x + g.dx / 2) - lx / 2;
+      T[iy * nx + ix] = std::exp(-(a * a) - (b * b));
+    }
+  });
+}
+
+void init_random_cpu(double* A, int64_t nx, int64_t ny, const TileGeom& g, uint64_t seed,
+                     double lo, double hi) {
+  parallel_for(0, ny, 16, [&](int64_t iy) {
+    const int64_t gy = wrap_index(g.gy0 + iy, g.nyg, g.periody);
+    for (int64_t ix = 0; ix < nx; ++ix) {
+      const int64_t gx = wrap_index(g.gx0 + ix, g.nxg, g.periodx);
+      A[iy * nx + ix] = lo + (hi - lo) * uniform01(seed, (uint64_t)(gy * g.nxg + gx));
+    }
+  });
+}
+
+}  // namespace rma

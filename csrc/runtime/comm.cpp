@@ -1,0 +1,173 @@
+#include "rma/comm.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "rma/hip_check.h"
+
+namespace rma {
+
+#define RMA_NCCL_CHECK(expr)                                                              \
+  do {                                                                                    \
+    ncclResult_t _r = (expr);                                                             \
+    if (_r != ncclSuccess && _r != ncclInProgress) {                                      \
+      ::rma::throw_error("RCCL call failed: " #expr, __FILE__, __LINE__,                  \
+                         std::string(ncclGetErrorString(_r)) + " / " +                    \
+                             (ncclGetLastError(nullptr) ? ncclGetLastError(nullptr) : "")); \
+    }                                                                                     \
+  } while (0)
+
+namespace {
+ncclComm_t C(void* p) { return reinterpret_cast<ncclComm_t>(p); }
+
+ncclDataType_t to_nccl(DType d) {
+  switch (d) {
+    case DType::kFloat64: return ncclFloat64;
+    case DType::kFloat32: return ncclFloat32;
+    case DType::kInt64: return ncclInt64;
+    case DType::kInt32: return ncclInt32;
+    case DType::kUInt8: return ncclUint8;
+  }
+  return ncclFloat64;
+}
+
+ncclRedOp_t to_nccl(RedOp o) {
+  switch (o) {
+    case RedOp::kSum: return ncclSum;
+    case RedOp::kMax: return ncclMax;
+    case RedOp::kMin: return ncclMin;
+    case RedOp::kProd: return ncclProd;
+  }
+  return ncclSum;
+}
+}  // namespace
+
+int rccl_version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return v;
+}
+
+std::string RcclComm::unique_id() {
+  ncclUniqueId id;
+  RMA_NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+RcclComm::RcclComm(int nranks, int rank, const std::string& uid, int device)
+    : nranks_(nranks), rank_(rank), device_(device) {
+  RMA_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "rank " << rank << "/" << nranks);
+  RMA_CHECK_ARG(uid.size() == sizeof(ncclUniqueId),
+                "unique id has " << uid.size() << " bytes, expected " << sizeof(ncclUniqueId));
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  RMA_HIP_CHECK(hipSetDevice(device));
+  ncclComm_t c;
+  RMA_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+  comm_ = c;
+  RMA_HIP_CHECK(hipMalloc(&scratch_, 2 * sizeof(double)));
+}
+
+RcclComm::~RcclComm() {
+  if (scratch_) (void)hipFree(scratch_);
+  if (comm_) {
+    if (aborted_) return;  // already torn down by abort()
+    (void)ncclCommDestroy(C(comm_));
+  }
+}
+
+void RcclComm::group_start() { RMA_NCCL_CHECK(ncclGroupStart()); }
+void RcclComm::group_end() { RMA_NCCL_CHECK(ncclGroupEnd()); }
+
+void RcclComm::send(const void* buf, size_t bytes, int peer, stream_t stream) {
+  RMA_CHECK_ARG(peer >= 0 && peer < nranks_, "peer " << peer);
+  RMA_NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, C(comm_), as_stream(stream)));
+}
+
+void RcclComm::recv(void* buf, size_t bytes, int peer, stream_t stream) {
+  RMA_CHECK_ARG(peer >= 0 && peer < nranks_, "peer " << peer);
+  RMA_NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, C(comm_), as_stream(stream)));
+}
+
+void RcclComm::allreduce(const void* sendbuf, void* recvbuf, size_t count, DType dt, RedOp op,
+                         stream_t stream) {
+  RMA_NCCL_CHECK(
+      ncclAllReduce(sendbuf, recvbuf, count, to_nccl(dt), to_nccl(op), C(comm_), as_stream(stream)));
+}
+
+void RcclComm::broadcast(const void* sendbuf, void* recvbuf, size_t count, DType dt, int root,
+                         stream_t stream) {
+  RMA_NCCL_CHECK(
+      ncclBroadcast(sendbuf, recvbuf, count, to_nccl(dt), root, C(comm_), as_stream(stream)));
+}
+
+void RcclComm::gather(const void* sendbuf, void* recvbuf, size_t bytes, int root,
+                      stream_t stream) {
+  hipStream_t s = as_stream(stream);
+  RMA_NCCL_CHECK(ncclGroupStart());
+  if (rank_ == root) {
+    for (int r = 0; r < nranks_; ++r) {
+      char* dst = static_cast<char*>(recvbuf) + (size_t)r * bytes;
+      if (r == root) {
+        RMA_HIP_CHECK(hipMemcpyAsync(dst, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
+      } else {
+        RMA_NCCL_CHECK(ncclRecv(dst, bytes, ncclUint8, r, C(comm_), s));
+      }
+    }
+  } else {
+    RMA_NCCL_CHECK(ncclSend(sendbuf, bytes, ncclUint8, root, C(comm_), s));
+  }
+  RMA_NCCL_CHECK(ncclGroupEnd());
+}
+
+void RcclComm::barrier(stream_t stream, double timeout_s) {
+  hipStream_t s = as_stream(stream);
+  RMA_HIP_CHECK(hipMemsetAsync(scratch_, 0, sizeof(double), s));
+  RMA_NCCL_CHECK(ncclAllReduce(scratch_, scratch_ + 1, 1, ncclFloat64, ncclSum, C(comm_), s));
+  wait(stream, timeout_s);
+}
+
+void RcclComm::check_async() {
+  if (aborted_) throw_error("communicator was aborted", __FILE__, __LINE__, "");
+  ncclResult_t ar = ncclSuccess;
+  RMA_NCCL_CHECK(ncclCommGetAsyncError(C(comm_), &ar));
+  if (ar != ncclSuccess && ar != ncclInProgress) {
+    abort();
+    throw_error("RCCL asynchronous error", __FILE__, __LINE__, ncclGetErrorString(ar));
+  }
+}
+
+void RcclComm::wait(stream_t stream, double timeout_s) {
+  hipStream_t s = as_stream(stream);
+  const auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) RMA_HIP_CHECK(q);
+    check_async();
+    if (timeout_s > 0) {
+      const double el =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s) {
+        abort();
+        throw_error("communication timeout", __FILE__, __LINE__,
+                    "stream did not drain within " + std::to_string(timeout_s) +
+                        " s (dead or stalled peer?); communicator aborted");
+      }
+    }
+    if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+void RcclComm::abort() {
+  if (aborted_ || !comm_) return;
+  aborted_ = true;
+  (void)ncclCommAbort(C(comm_));
+}
+
+}  // namespace rma

@@ -1,0 +1,136 @@
+"""In-tree build of the native core ``rocm_mpi_amd._C`` for gfx950.
+
+The reference has no build system: its GPU code is Julia JIT-compiled by
+AMDGPU.jl at run time and its environment bootstrap is
+``startup.sh:3-17``. Here the HIP kernels and the C++ runtime are compiled
+ahead of time with ``hipcc --offload-arch=gfx950`` into one pybind11
+extension that lives next to this file (so it ships with the repository
+snapshot to a GPU box and is what every process loads).
+
+Usage::
+
+    python -m rocm_mpi_amd._build            # incremental
+    python -m rocm_mpi_amd._build --clean    # from scratch
+
+Objects go to ``build/native`` and are rebuilt when their source or any header
+under ``csrc/include`` is newer. All device code is compiled with
+``-ffp-contract=off`` so the stencil is bit-reproducible against NumPy.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+INC = CSRC / "include"
+BUILD = ROOT / "build" / "native"
+PKG = ROOT / "rocm_mpi_amd"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("RMA_OFFLOAD_ARCH", "gfx950")
+
+HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "runtime").glob("*.cpp"))
+HOST_SOURCES = sorted(p for p in (CSRC / "kernels").glob("*.cpp")) + [CSRC / "bindings" / "module.cpp"]
+
+
+def ext_path() -> Path:
+    return PKG / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _pybind_include() -> str:
+    import pybind11
+
+    return pybind11.get_include()
+
+
+def _hipcc() -> str:
+    p = ROCM / "bin" / "hipcc"
+    return str(p) if p.exists() else "hipcc"
+
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", "-Wall",
+          "-Wno-unused-function", "-Wno-unknown-pragmas"]
+
+
+def _hip_cmd(src: Path, obj: Path) -> list[str]:
+    return [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", *COMMON, "-munsafe-fp-atomics",
+            "-c", str(src), "-o", str(obj)]
+
+
+def _host_cmd(src: Path, obj: Path) -> list[str]:
+    py_inc = sysconfig.get_paths()["include"]
+    cxx = os.environ.get("CXX", "g++")
+    return [cxx, *COMMON, "-fvisibility=hidden", f"-I{_pybind_include()}", f"-I{py_inc}",
+            "-c", str(src), "-o", str(obj)]
+
+
+def _stale(src: Path, obj: Path, newest_header: float) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or newest_header > t
+
+
+def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+    """Compile (incrementally) and link ``rocm_mpi_amd/_C*.so``; returns its path."""
+    if clean and BUILD.exists():
+        shutil.rmtree(BUILD)
+    BUILD.mkdir(parents=True, exist_ok=True)
+    newest_header = max((p.stat().st_mtime for p in INC.rglob("*.h")), default=0.0)
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    todo = []
+    objs = []
+    for src in HIP_SOURCES + HOST_SOURCES:
+        obj = BUILD / (src.parent.name + "_" + src.name + ".o")
+        objs.append(obj)
+        if _stale(src, obj, newest_header):
+            cmd = _hip_cmd(src, obj) if src in HIP_SOURCES else _host_cmd(src, obj)
+            todo.append((src, cmd))
+
+    def run(item):
+        src, cmd = item
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return src
+
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            for src in ex.map(run, todo):
+                print(f"[rocm_mpi_amd build] compiled {src.relative_to(ROOT)}", flush=True)
+    out = ext_path()
+    if todo or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
+        tmp = out.with_suffix(".tmp.so")
+        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs),
+               "-o", str(tmp), f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64", "-ldl", "-lpthread",
+               f"-Wl,-rpath,{ROCM / 'lib'}"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, out)
+        print(f"[rocm_mpi_amd build] linked {out.relative_to(ROOT)}", flush=True)
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    build(clean=a.clean, jobs=a.jobs, verbose=a.verbose)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

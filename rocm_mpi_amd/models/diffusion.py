@@ -1,0 +1,318 @@
+"""2D heat diffusion (explicit Euler, 5-point stencil, fp64) — all variants.
+
+Physics and numerics are those of the reference scripts
+(``scripts/diffusion_2D_{ap,kp,perf,perf_hide,perf_hide_prof}.jl``):
+``lx=ly=10, lam=1, Cp0=1``, ``dx=lx/nx_g()``, ``dt=min(dx^2,dy^2)*Cp0/lam/4.1``,
+initial Gaussian ``exp(-(x-lx/2)^2-(y-ly/2)^2)`` on cell centres (ap.jl:11-28).
+
+Variants:
+
+``ap``         array programming: torch tensor expressions (CPU or GPU), like
+               the reference's broadcasts (ap.jl:37-43) but with preallocated
+               temporaries (the reference allocates every step, §7.4 item 4).
+``kp``         three hand-written kernels Flux/Residual/Update (kp.jl:16-54).
+``perf``       one fused kernel, double-buffered (perf.jl:3-13,47-52).
+``perf_hide``  boundary frame on a high-priority stream, halo exchange right
+               behind it, interior on a low-priority stream — the reference's
+               intended-but-unfinished overlap (perf_hide.jl:94-101).
+
+All variants compute the same canonical per-cell expression, so their fields
+agree bitwise, across variants and across decompositions.
+
+On a GPU with the native halo engine the time loop runs inside the native
+executor (no per-step Python, no host waits). Elsewhere (CPU, host-staged or
+loopback transports) the same steps are issued from Python.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import asdict, dataclass, field
+
+import numpy as np
+import torch
+
+from .. import ops
+from .._native import native
+from ..parallel import implicit_grid as gg
+from ..parallel.halo import gather_, update_halo_
+from ..utils import metrics
+from ..utils import profiling as prof
+
+VARIANTS = ("ap", "kp", "perf", "perf_hide")
+_MODE = {"perf": 0, "perf_hide": 1, "kp": 2}
+
+
+@dataclass
+class DiffusionConfig:
+    variant: str = "perf"
+    nx: int = 128
+    ny: int = 128
+    nt: int = 1000
+    warmup: int = 10  # timer starts at it == warmup+1 (reference: it==11)
+    lx: float = 10.0
+    ly: float = 10.0
+    lam: float = 1.0
+    Cp0: float = 1.0
+    b_width: tuple = (32, 4)  # perf_hide frame widths (x rounded up to a wave-strip)
+    init: str = "gaussian"  # gaussian | random
+    init_on: str = "auto"  # auto | device | host
+    seed: int = 1234
+    dims: tuple = (0, 0, 0)
+    periods: tuple = (0, 0, 0)
+    transport: str = "auto"
+    device: str | None = None
+    chunk_rows: int = 64
+    nontemporal: bool = False
+    kernel: str = "march"
+    use_graph: bool = False
+    graph_steps: int = 0
+    executor: str = "auto"  # auto | native | python
+    do_vis: bool = False
+    outdir: str = "output"
+    profile: bool = False
+    check_every: int = 0  # NaN/Inf guard period (0 = off)
+    quiet: bool = False
+
+    def validate(self) -> None:
+        if self.variant not in VARIANTS:
+            raise ValueError(f"variant must be one of {VARIANTS}")
+        if self.nt < 1 or self.warmup < 0:
+            raise ValueError("nt >= 1 and warmup >= 0 required")
+        if self.init not in ("gaussian", "random"):
+            raise ValueError("init must be gaussian or random")
+        if self.nx < 3 or self.ny < 3:
+            raise ValueError("nx, ny >= 3 required")
+
+
+class Diffusion2D:
+    """One rank's share of the distributed diffusion problem."""
+
+    def __init__(self, cfg: DiffusionConfig, grid_kwargs: dict | None = None):
+        cfg.validate()
+        self.cfg = cfg
+        kw = dict(grid_kwargs or {})
+        if not gg.grid_is_initialized():
+            kw.setdefault("quiet", cfg.quiet)
+            gg.init_global_grid(cfg.nx, cfg.ny, 1, dimx=cfg.dims[0], dimy=cfg.dims[1],
+                                periodx=cfg.periods[0], periody=cfg.periods[1],
+                                transport=cfg.transport, device=cfg.device, **kw)
+            self._owns_grid = True
+        else:
+            self._owns_grid = False
+        g = self.g = gg.global_grid()
+        if (g.nx, g.ny) != (cfg.nx, cfg.ny):
+            raise ValueError(f"global grid local size {g.nxyz} != config {(cfg.nx, cfg.ny)}")
+        self.device = g.device
+        nx, ny = cfg.nx, cfg.ny
+        self.dx = cfg.lx / gg.nx_g()
+        self.dy = cfg.ly / gg.ny_g()
+        self.dt = min(self.dx * self.dx, self.dy * self.dy) * cfg.Cp0 / cfg.lam / 4.1
+        self.coef = ops.StencilCoef.from_physics(cfg.lam, self.dx, self.dy, self.dt)
+        dev = self.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        # 1/Cp (the reference's Cp0.*ones; stored inverted, see rma/common.h)
+        self.iCp = torch.empty((ny, nx), **f64)
+        ops.fill_(self.iCp, 1.0 / cfg.Cp0)
+        self.T = torch.empty((ny, nx), **f64)
+        self.init_field(self.T)
+        self.T2 = None
+        if cfg.variant in ("perf", "perf_hide"):
+            self.T2 = self.T.clone()  # perf.jl:36 T2 = copy(T)
+        if cfg.variant in ("kp", "ap"):
+            self.qx = torch.zeros((ny - 2, nx - 1), **f64)
+            self.qy = torch.zeros((ny - 2 + 1, nx - 2), **f64)
+            self.dTdt = torch.zeros((ny - 2, nx - 2), **f64)
+            self._tmp = torch.zeros((ny - 2, nx - 2), **f64)
+        self.parity = 0
+        self.steps_done = 0
+        self.executor = None
+        use_native = cfg.executor == "native" or (
+            cfg.executor == "auto" and dev.type == "cuda" and g.halo is not None)
+        if use_native and cfg.variant != "ap":
+            if dev.type != "cuda" or g.halo is None:
+                raise RuntimeError("native executor needs a GPU and the rccl/self transport")
+            bwx, bwy = cfg.b_width
+            self.executor = native().Executor(
+                self.T.data_ptr(), self.T2.data_ptr() if self.T2 is not None else 0,
+                self.iCp.data_ptr(), nx, ny, _MODE[cfg.variant], tuple(self.coef),
+                cfg.chunk_rows, int(cfg.nontemporal), ops.KERNELS[cfg.kernel], int(bwx), int(bwy),
+                int(cfg.use_graph), int(cfg.graph_steps), g.halo,
+                self.qx.data_ptr() if cfg.variant == "kp" else 0,
+                self.qy.data_ptr() if cfg.variant == "kp" else 0,
+                self.dTdt.data_ptr() if cfg.variant == "kp" else 0)
+        if cfg.variant == "perf_hide":
+            self.frame_rects, self.interior = ops.hide_rects(nx, ny, *cfg.b_width)
+        self.tuning = ops.StencilTuning(cfg.chunk_rows, cfg.nontemporal, cfg.kernel)
+
+    # ------------------------------------------------------------------
+    def geometry(self, A_shape=None) -> ops.TileGeometry:
+        g = self.g
+        ny_a, nx_a = A_shape or (g.ny, g.nx)
+        return ops.TileGeometry(
+            gx0=g.coords[0] * (g.nx - g.overlaps[0]), gy0=g.coords[1] * (g.ny - g.overlaps[1]),
+            nxg=g.nxyz_g[0], nyg=g.nxyz_g[1], dx=self.dx, dy=self.dy,
+            xoff=0.5 * (g.nx - nx_a) * self.dx, yoff=0.5 * (g.ny - ny_a) * self.dy,
+            periodx=g.periods[0], periody=g.periods[1])
+
+    def init_field(self, T: torch.Tensor) -> None:
+        cfg = self.cfg
+        geom = self.geometry(tuple(T.shape))
+        if cfg.init == "random":
+            ops.init_random_(T, geom, seed=cfg.seed)
+            return
+        where = cfg.init_on
+        if where == "auto":
+            where = "device"
+        if where == "host":  # the reference's host comprehension + copy (ap.jl:28)
+            ny, nx = T.shape
+            from ..parallel.geometry import coords_1d
+
+            x = coords_1d(geom.gx0, nx, self.dx, geom.xoff, geom.nxg, geom.periodx).numpy()
+            y = coords_1d(geom.gy0, ny, self.dy, geom.yoff, geom.nyg, geom.periody).numpy()
+            a = (x + self.dx / 2) - cfg.lx / 2
+            b = (y + self.dy / 2) - cfg.ly / 2
+            T.copy_(torch.from_numpy(np.exp(-(a * a)[None, :] - (b * b)[:, None])))
+        else:
+            ops.init_gaussian_(T, geom, cfg.lx, cfg.ly)
+
+    @property
+    def field(self) -> torch.Tensor:
+        """The current temperature field (after the last completed step)."""
+        if self.T2 is None:
+            return self.T
+        return self.T2 if self.parity else self.T
+
+    # ------------------------------------------------------------------
+    def step(self, n: int = 1) -> None:
+        """Advance n time steps (asynchronous on GPU)."""
+        if n <= 0:
+            return
+        if self.executor is not None:
+            self.executor.run(int(n), torch.cuda.current_stream(self.device).cuda_stream)
+            self.parity = self.executor.parity
+            self.steps_done += n
+            return
+        v = self.cfg.variant
+        for _ in range(n):
+            if v == "ap":
+                self._step_ap()
+            elif v == "kp":
+                ops.flux(self.qx, self.qy, self.T, self.coef.mlam, self.coef.rdx, self.coef.rdy)
+                ops.residual(self.dTdt, self.qx, self.qy, self.iCp, self.coef.rdx, self.coef.rdy)
+                ops.update(self.T, self.dTdt, self.coef.dt)
+                update_halo_(self.T)
+            else:
+                Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
+                if v == "perf":
+                    ops.stencil_step(Tout, Tin, self.iCp, self.coef, tuning=self.tuning)
+                    update_halo_(Tout)
+                else:  # perf_hide, sequential emulation: frame -> halo -> interior
+                    ops.stencil_step(Tout, Tin, self.iCp, self.coef, self.frame_rects, self.tuning)
+                    update_halo_(Tout)
+                    if self.interior is not None:
+                        ops.stencil_step(Tout, Tin, self.iCp, self.coef, [self.interior],
+                                         self.tuning)
+                self.parity ^= 1
+            self.steps_done += 1
+
+    def _step_ap(self) -> None:
+        """ap.jl:38-42 as torch expressions (canonical operation order)."""
+        c = self.coef
+        T, qx, qy, d, tmp = self.T, self.qx, self.qy, self.dTdt, self._tmp
+        torch.sub(T[1:-1, 1:], T[1:-1, :-1], out=qx)
+        qx.mul_(c.mlam).mul_(c.rdx)  # qx = -lam*d_xi(T)*_dx
+        torch.sub(T[1:, 1:-1], T[:-1, 1:-1], out=qy)
+        qy.mul_(c.mlam).mul_(c.rdy)  # qy = -lam*d_yi(T)*_dy
+        torch.sub(qx[:, 1:], qx[:, :-1], out=d)
+        d.mul_(c.rdx)
+        torch.sub(qy[1:, :], qy[:-1, :], out=tmp)
+        tmp.mul_(c.rdy)
+        d.add_(tmp).neg_().mul_(self.iCp[1:-1, 1:-1])  # dTdt = 1/Cp*(-(dqx+dqy))
+        d.mul_(c.dt)
+        T[1:-1, 1:-1].add_(d)  # T = T + dt*dTdt
+        update_halo_(T)
+
+    def synchronize(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def check_finite(self) -> None:
+        bad = float(ops.reduce(self.field, "nonfinite"))
+        if bad:
+            raise FloatingPointError(
+                f"rank {self.g.me}: {int(bad)} non-finite cells after step {self.steps_done}")
+
+    # ------------------------------------------------------------------
+    def run(self) -> metrics.RunResult:
+        """The reference protocol: nt steps, timer from step warmup+1, T_eff."""
+        cfg = self.cfg
+        g = self.g
+        if g.me == 0 and not cfg.quiet:
+            print("Starting the time loop 🚀...", end="", flush=True)
+        warm = min(cfg.warmup, cfg.nt)
+        timed = cfg.nt - warm
+        if warm:
+            self._advance(warm)
+        profiler = prof.LoopProfiler(enabled=cfg.profile, rank=g.me)
+        gg.tic()
+        with profiler:
+            self._advance(timed)
+            wtime = gg.toc()
+        if g.me == 0 and not cfg.quiet:
+            print("done", flush=True)
+        teff = metrics.t_eff(cfg.nx, cfg.ny, wtime, timed)
+        tmin = g.comm.allreduce(teff, "min")
+        tmax = g.comm.allreduce(teff, "max")
+        ttot = g.comm.allreduce(teff, "sum")
+        res = metrics.RunResult(
+            variant=cfg.variant, nprocs=g.nprocs, dims=g.dims, nx=cfg.nx, ny=cfg.ny,
+            nxg=g.nxyz_g[0], nyg=g.nxyz_g[1], nt=cfg.nt, timed_steps=timed, wtime=wtime,
+            t_it=wtime / timed if timed else float("nan"), teff=teff, teff_min=tmin,
+            teff_max=tmax, teff_total=ttot, transport=g.transport, device=str(self.device))
+        if g.me == 0 and not cfg.quiet:
+            print(metrics.reference_line(cfg.nt, wtime, teff), flush=True)
+        if cfg.profile:
+            profiler.write("prof.txt")
+        if cfg.do_vis:
+            res.extra["vis"] = self.visualise()
+        return res
+
+    def _advance(self, n: int) -> None:
+        k = self.cfg.check_every
+        if k <= 0:
+            self.step(n)
+            return
+        done = 0
+        while done < n:
+            m = min(k, n - done)
+            self.step(m)
+            done += m
+            self.check_finite()
+
+    # ------------------------------------------------------------------
+    def gather_interior(self, root: int = 0):
+        """T_v: the halo-stripped fields of all ranks assembled on root
+        (ap.jl:45-46: T_nh .= Array(T[2:end-1,2:end-1]); gather!(T_nh, T_v))."""
+        T_nh = self.field[1:-1, 1:-1].contiguous()
+        return gather_(T_nh, None, root)
+
+    def visualise(self) -> dict | None:
+        from ..utils import vis
+
+        T_v = self.gather_interior()
+        if self.g.me != 0:
+            return None
+        name = {"perf_hide": "hide"}.get(self.cfg.variant, self.cfg.variant)
+        path = vis.output_name(name, self.g.nprocs, gg.nx_g(), gg.ny_g(), self.cfg.outdir)
+        info = vis.heatmap_png(T_v, path)
+        if not self.cfg.quiet:
+            print(f"maximum(T_v) = {info['max']}", flush=True)  # perf_hide.jl:115
+        return info
+
+    def close(self) -> None:
+        self.synchronize()
+        self.executor = None
+        if self._owns_grid:
+            gg.finalize_global_grid()

@@ -1,0 +1,26 @@
+"""Halo pack/unpack primitive (K7/K8 of SURVEY.md §2.3) on torch tensors.
+
+``copy_plane(dst, src)`` copies one (possibly strided) plane view into another
+with the native ``copy2d`` kernel: both views must be 2-D with a unit-stride
+inner dimension (the shapes the halo engine produces: an x-plane of a
+row-major field is a column, i.e. rows of length hw at stride nx).
+"""
+from __future__ import annotations
+
+import torch
+
+from .._native import native
+from .stencil import stream_handle
+
+
+def copy_plane(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    if dst.shape != src.shape or dst.dim() != 2:
+        raise ValueError("copy_plane needs two 2-D views of equal shape")
+    if dst.dtype != src.dtype or dst.device != src.device:
+        raise ValueError("dtype/device mismatch")
+    if dst.stride(1) != 1 or src.stride(1) != 1:
+        raise ValueError("inner dimension must be unit-stride")
+    es = dst.element_size()
+    native().copy2d(dst.data_ptr(), dst.stride(0), src.data_ptr(), src.stride(0), dst.shape[0],
+                    dst.shape[1], es, stream_handle(dst), dst.is_cuda)
+    return dst

@@ -1,0 +1,293 @@
+"""Tensor-level entry points of the hand-written HIP kernels.
+
+Each op validates shapes, dtype, contiguity and device on the host BEFORE any
+launch (a bad shape must never reach a kernel), then dispatches:
+
+* CUDA (ROCm) tensors -> the gfx950 kernels in ``rocm_mpi_amd._C`` on the
+  current torch stream; the extension is mandatory (loud failure otherwise);
+* CPU tensors -> the bit-identical C++ twins in the same extension, or a pure
+  torch formulation when the extension is absent (CPU-only environments).
+
+Reference kernels: K4 fused step ``scripts/diffusion_2D_perf.jl:3-13``; K5
+split step ``scripts/diffusion_2D_perf_hide.jl:15-29``; K1-K3
+``scripts/diffusion_2D_kp.jl:16-54``; initial condition
+``scripts/diffusion_2D_ap.jl:28``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Iterable, NamedTuple, Sequence
+
+import torch
+
+from .._native import has_native, native
+
+Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
+
+KERNELS = {"march": 0, "lds": 1}
+
+
+class StencilCoef(NamedTuple):
+    """Coefficients of the canonical update (see csrc/include/rma/common.h)."""
+
+    mlam: float  # -lam
+    rdx: float  # 1/dx
+    rdy: float  # 1/dy
+    dt: float
+
+    @classmethod
+    def from_physics(cls, lam: float, dx: float, dy: float, dt: float) -> "StencilCoef":
+        return cls(-lam, 1.0 / dx, 1.0 / dy, dt)
+
+
+@dataclass
+class StencilTuning:
+    chunk_rows: int = 64
+    nontemporal: bool = False
+    kernel: str = "march"
+
+
+@dataclass
+class TileGeometry:
+    """Placement of a local tile in the implicit global grid (IGG x_g/y_g)."""
+
+    gx0: int
+    gy0: int
+    nxg: int
+    nyg: int
+    dx: float
+    dy: float
+    xoff: float = 0.0
+    yoff: float = 0.0
+    periodx: int = 0
+    periody: int = 0
+
+    def as_tuple(self):
+        return (int(self.gx0), int(self.gy0), int(self.nxg), int(self.nyg), float(self.dx),
+                float(self.dy), float(self.xoff), float(self.yoff), int(self.periodx),
+                int(self.periody))
+
+
+def stream_handle(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else 0
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def check_field(name: str, t: torch.Tensor, shape=None, device=None) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor, got {type(t).__name__}")
+    if t.dtype != torch.float64:
+        raise TypeError(f"{name} must be float64 (reference fields are Float64), got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+
+
+def _use_native_cpu() -> bool:
+    return has_native()
+
+
+def interior_rect(nx: int, ny: int) -> Rect:
+    return (1, nx - 1, 1, ny - 1)
+
+
+def validate_rects(rects: Sequence[Rect], nx: int, ny: int) -> list[Rect]:
+    out = []
+    if len(rects) > 8:
+        raise ValueError("at most 8 rects per launch")
+    for r in rects:
+        x0, x1, y0, y1 = (int(v) for v in r)
+        if x1 <= x0 or y1 <= y0:
+            continue
+        if x0 < 1 or y0 < 1 or x1 > nx - 1 or y1 > ny - 1:
+            raise ValueError(f"rect {r} outside the interior [1,{nx - 1})x[1,{ny - 1})")
+        out.append((x0, x1, y0, y1))
+    return out
+
+
+# --------------------------------------------------------------------------
+# fused / split stencil
+# --------------------------------------------------------------------------
+def stencil_torch(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, c: StencilCoef,
+                  rects: Iterable[Rect]) -> None:
+    """Pure-torch twin of the fused kernel (same operation order, bitwise)."""
+    for x0, x1, y0, y1 in rects:
+        cu = T[y0:y1, x0:x1]
+        xr = T[y0:y1, x0 + 1:x1 + 1]
+        xl = T[y0:y1, x0 - 1:x1 - 1]
+        dn = T[y0 + 1:y1 + 1, x0:x1]
+        up = T[y0 - 1:y1 - 1, x0:x1]
+        qxR = (c.mlam * (xr - cu)) * c.rdx
+        qxL = (c.mlam * (cu - xl)) * c.rdx
+        qyU = (c.mlam * (dn - cu)) * c.rdy
+        qyD = (c.mlam * (cu - up)) * c.rdy
+        d = iCp[y0:y1, x0:x1] * ((-(qxR - qxL)) * c.rdx - (qyU - qyD) * c.rdy)
+        T2[y0:y1, x0:x1] = cu + c.dt * d
+
+
+def stencil_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: StencilCoef,
+                 rects: Sequence[Rect] | None = None, tuning: StencilTuning | None = None) -> None:
+    """T2[r] = T[r] + dt*iCp*(div q)[r] for every rect r (default: the interior)."""
+    check_field("T", T)
+    ny, nx = T.shape
+    check_field("T2", T2, (ny, nx), T.device)
+    check_field("iCp", iCp, (ny, nx), T.device)
+    if T2.data_ptr() == T.data_ptr():
+        raise ValueError("T2 must not alias T (double buffering)")
+    rects = validate_rects(rects if rects is not None else [interior_rect(nx, ny)], nx, ny)
+    if not rects:
+        return
+    tn = tuning or StencilTuning()
+    if T.is_cuda:
+        native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
+                               tn.chunk_rows, int(tn.nontemporal), KERNELS[tn.kernel],
+                               stream_handle(T), True)
+    elif _use_native_cpu():
+        native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
+                               64, 0, 0, 0, False)
+    else:
+        stencil_torch(T2, T, iCp, coef, rects)
+
+
+def strip_cells(nx: int) -> int:
+    """x-width of one wave-strip of the march kernel (perf_hide frame rounding)."""
+    if has_native():
+        return native().stencil_strip_cells(nx)
+    return 128 if nx % 2 == 0 else 64
+
+
+def hide_rects(nx: int, ny: int, bwx: int, bwy: int) -> tuple[list[Rect], Rect | None]:
+    """Frame rects and interior rect of the boundary/interior split.
+
+    The x-frame is rounded up so the interior starts on a wave-strip boundary
+    (the reference's b_width=(32,4), perf_hide.jl:42, is a thread-block
+    multiple; ours is a wave-strip multiple). Mirrors DiffusionExecutor.
+    """
+    if bwx < 1 or bwy < 1:
+        raise ValueError("b_width must be >= 1 so the send planes are computed first")
+    s = strip_cells(nx)
+    xi0 = -(-(1 + bwx) // s) * s
+    xi1 = (nx - 1 - bwx) // s * s
+    yi0, yi1 = 1 + bwy, ny - 1 - bwy
+    full = interior_rect(nx, ny)
+    if xi0 >= xi1 or yi0 >= yi1:
+        return [full], None
+    frame = [(1, nx - 1, 1, yi0), (1, nx - 1, yi1, ny - 1), (1, xi0, yi0, yi1),
+             (xi1, nx - 1, yi0, yi1)]
+    return frame, (xi0, xi1, yi0, yi1)
+
+
+# --------------------------------------------------------------------------
+# kp kernels
+# --------------------------------------------------------------------------
+def flux(qx, qy, T, mlam: float, rdx: float, rdy: float) -> None:
+    check_field("T", T)
+    ny, nx = T.shape
+    check_field("qx", qx, (ny - 2, nx - 1), T.device)
+    check_field("qy", qy, (ny - 1, nx - 2), T.device)
+    if T.is_cuda or _use_native_cpu():
+        native().flux(_ptr(qx), _ptr(qy), _ptr(T), nx, ny, mlam, rdx, rdy, stream_handle(T),
+                      T.is_cuda)
+    else:
+        qx.copy_((mlam * (T[1:-1, 1:] - T[1:-1, :-1])) * rdx)
+        qy.copy_((mlam * (T[1:, 1:-1] - T[:-1, 1:-1])) * rdy)
+
+
+def residual(dTdt, qx, qy, iCp, rdx: float, rdy: float) -> None:
+    check_field("iCp", iCp)
+    ny, nx = iCp.shape
+    check_field("dTdt", dTdt, (ny - 2, nx - 2), iCp.device)
+    check_field("qx", qx, (ny - 2, nx - 1), iCp.device)
+    check_field("qy", qy, (ny - 1, nx - 2), iCp.device)
+    if iCp.is_cuda or _use_native_cpu():
+        native().residual(_ptr(dTdt), _ptr(qx), _ptr(qy), _ptr(iCp), nx, ny, rdx, rdy,
+                          stream_handle(iCp), iCp.is_cuda)
+    else:
+        ddx = (qx[:, 1:] - qx[:, :-1]) * rdx
+        ddy = (qy[1:, :] - qy[:-1, :]) * rdy
+        dTdt.copy_(iCp[1:-1, 1:-1] * (-(ddx + ddy)))
+
+
+def update(T, dTdt, dt: float) -> None:
+    check_field("T", T)
+    ny, nx = T.shape
+    check_field("dTdt", dTdt, (ny - 2, nx - 2), T.device)
+    if T.is_cuda or _use_native_cpu():
+        native().update(_ptr(T), _ptr(dTdt), nx, ny, dt, stream_handle(T), T.is_cuda)
+    else:
+        T[1:-1, 1:-1] = T[1:-1, 1:-1] + dt * dTdt
+
+
+# --------------------------------------------------------------------------
+# initial conditions
+# --------------------------------------------------------------------------
+def init_gaussian_(T: torch.Tensor, geom: TileGeometry, lx: float, ly: float) -> torch.Tensor:
+    """T = exp(-(x_g+dx/2-lx/2)^2 - (y_g+dy/2-ly/2)^2) evaluated on the device."""
+    check_field("T", T)
+    ny, nx = T.shape
+    if T.is_cuda or _use_native_cpu():
+        native().init_gaussian(_ptr(T), nx, ny, geom.as_tuple(), lx, ly, stream_handle(T),
+                               T.is_cuda)
+    else:
+        from ..parallel.geometry import coords_1d
+
+        x = coords_1d(geom.gx0, nx, geom.dx, geom.xoff, geom.nxg, geom.periodx)
+        y = coords_1d(geom.gy0, ny, geom.dy, geom.yoff, geom.nyg, geom.periody)
+        a = (x + geom.dx / 2) - lx / 2
+        b = (y + geom.dy / 2) - ly / 2
+        T.copy_(torch.exp(-(a * a)[None, :] - (b * b)[:, None]))
+    return T
+
+
+def init_random_(A: torch.Tensor, geom: TileGeometry, seed: int = 0, lo: float = 0.0,
+                 hi: float = 1.0) -> torch.Tensor:
+    """Counter-based uniform field keyed by the global cell index."""
+    check_field("A", A)
+    ny, nx = A.shape
+    native().init_random(_ptr(A), nx, ny, geom.as_tuple(), int(seed) & (2**64 - 1), lo, hi,
+                         stream_handle(A), A.is_cuda)
+    return A
+
+
+def fill_(A: torch.Tensor, value: float) -> torch.Tensor:
+    if A.is_cuda and A.dtype == torch.float64 and A.is_contiguous():
+        native().fill(_ptr(A), A.numel(), float(value), stream_handle(A))
+    else:
+        A.fill_(value)
+    return A
+
+
+# --------------------------------------------------------------------------
+# reductions
+# --------------------------------------------------------------------------
+_RED = {"sum": 0, "max": 1, "min": 2, "maxabs": 3, "nonfinite": 4}
+_ws_cache: dict = {}
+
+
+def reduce(A: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    """Device reduction of a float64 field -> 0-d float64 tensor (same device)."""
+    if op not in _RED:
+        raise ValueError(f"op must be one of {sorted(_RED)}")
+    if not (A.dtype == torch.float64 and A.is_contiguous()):
+        A = A.contiguous().to(torch.float64)
+    if A.is_cuda:
+        key = A.device
+        ws = _ws_cache.get(key)
+        if ws is None:
+            ws = torch.empty(native().reduce_workspace_doubles() + 1, dtype=torch.float64,
+                             device=A.device)
+            _ws_cache[key] = ws
+        out = torch.empty((), dtype=torch.float64, device=A.device)
+        native().reduce_gpu(_ptr(A), A.numel(), _RED[op], _ptr(out), _ptr(ws), stream_handle(A))
+        return out
+    if _use_native_cpu():
+        return torch.tensor(native().reduce_cpu(_ptr(A), A.numel(), _RED[op]), dtype=torch.float64)
+    f = {"sum": torch.sum, "max": torch.max, "min": torch.min,
+         "maxabs": lambda a: a.abs().max(), "nonfinite": lambda a: (~torch.isfinite(a)).sum()}[op]
+    return f(A).to(torch.float64)

@@ -1,0 +1,413 @@
+"""Communicators: bootstrap, device selection, P2P groups, tiny collectives.
+
+The reference's communication layer is MPI.jl over ROCm-aware OpenMPI/UCX or
+plain OpenMPI (``scripts/setenv.sh:11-18``, ``README.md:25-35``), selected by
+``IGG_ROCMAWARE_MPI``. Here one process drives one MI355X and the transports
+are:
+
+* ``rccl``     GPU-direct RCCL point-to-point over xGMI (native
+  :class:`rocm_mpi_amd._C.RcclComm`); default whenever a GPU is present.
+* ``staged``   host-staged: device planes are copied to pinned host memory and
+  exchanged with torch.distributed/gloo (parity with ``IGG_ROCMAWARE_MPI=0``;
+  validation only, never on the perf path).
+* ``gloo``     CPU tensors over torch.distributed/gloo (CPU-only runs, CI).
+* ``loopback`` N logical ranks as threads of ONE process exchanging through
+  in-memory mailboxes (multi-rank tests without a
+  cluster or a GPU).
+* ``self``     a single rank (no communication).
+
+Bootstrap is MPI-free: ``torch.distributed`` env:// rendezvous (RANK,
+WORLD_SIZE, MASTER_ADDR, MASTER_PORT — torchrun or our launcher), its store
+carries the RCCL unique id. The node-local rank (``MPI.Comm_split_type(
+COMM_TYPE_SHARED)`` in ``scripts/rocmaware_test_selectdevice.jl:7-9``) comes
+from LOCAL_RANK or, failing that, from a hostname exchange through the store.
+"""
+from __future__ import annotations
+
+import os
+import queue
+import socket
+import threading
+import time
+from dataclasses import dataclass
+from typing import Sequence
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_TIMEOUT_S = float(os.environ.get("RMA_COMM_TIMEOUT", "300"))
+
+
+@dataclass
+class P2P:
+    """One point-to-point operation of a group: send ``tensor`` to / receive it
+    from ``peer``. ``tag`` disambiguates several messages between one pair."""
+
+    kind: str  # "send" | "recv"
+    tensor: torch.Tensor
+    peer: int
+    tag: int = 0
+
+
+class Communicator:
+    name = "abstract"
+    rank: int = 0
+    size: int = 1
+
+    # --- collectives -----------------------------------------------------
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+    def allreduce(self, value: float, op: str = "sum") -> float:
+        raise NotImplementedError
+
+    def gather(self, t: torch.Tensor, root: int = 0) -> list[torch.Tensor] | None:
+        """Every rank contributes ``t`` (same shape everywhere); root gets the
+        list in rank order, others None."""
+        raise NotImplementedError
+
+    # --- point to point ---------------------------------------------------
+    def exchange(self, ops: Sequence[P2P]) -> None:
+        """Run all sends and receives as one group; returns when received data
+        is usable in stream order (GPU) or in memory (CPU)."""
+        raise NotImplementedError
+
+    def sendrecv(self, send: torch.Tensor, dst: int, recv: torch.Tensor, src: int,
+                 tag: int = 0) -> None:
+        self.exchange([P2P("send", send, dst, tag), P2P("recv", recv, src, tag)])
+
+    def supports(self, t: torch.Tensor) -> bool:
+        return True
+
+    def finalize(self) -> None:
+        pass
+
+
+class SelfComm(Communicator):
+    name = "self"
+
+    def barrier(self) -> None:
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+    def allreduce(self, value: float, op: str = "sum") -> float:
+        return float(value)
+
+    def gather(self, t, root=0):
+        return [t.clone()]
+
+    def exchange(self, ops):
+        sends = [o for o in ops if o.kind == "send"]
+        recvs = [o for o in ops if o.kind == "recv"]
+        for r in recvs:
+            match = [s for s in sends if s.tag == r.tag]
+            if not match:
+                raise RuntimeError("self exchange: unmatched receive")
+            s = match[0]
+            sends.remove(s)
+            r.tensor.copy_(s.tensor)
+
+
+_REDUCE = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
+class TorchDistComm(Communicator):
+    """torch.distributed (gloo) transport; GPU tensors are host-staged."""
+
+    def __init__(self, staged: bool = False):
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialized")
+        self.rank = dist.get_rank()
+        self.size = dist.get_world_size()
+        self.staged = staged
+        self.name = "staged" if staged else "gloo"
+        self._pg = _gloo_group()
+
+    def barrier(self) -> None:
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+        dist.barrier(group=self._pg)
+
+    def allreduce(self, value: float, op: str = "sum") -> float:
+        t = torch.tensor([float(value)], dtype=torch.float64)
+        dist.all_reduce(t, op=_REDUCE[op], group=self._pg)
+        return float(t.item())
+
+    def gather(self, t, root=0):
+        host = t.detach().to("cpu").contiguous()
+        lst = [torch.empty_like(host) for _ in range(self.size)] if self.rank == root else None
+        dist.gather(host, lst, dst=root, group=self._pg)
+        return lst
+
+    def exchange(self, ops):
+        if not ops:
+            return
+        staged = []
+        p2p = []
+        for o in ops:
+            t = o.tensor
+            if t.is_cuda:
+                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                if o.kind == "send":
+                    h.copy_(t)
+                staged.append((o, h))
+                t = h
+            fn = dist.isend if o.kind == "send" else dist.irecv
+            p2p.append(dist.P2POp(fn, t, o.peer, group=self._pg, tag=o.tag))
+        if any(o.tensor.is_cuda for o in ops):
+            torch.cuda.current_stream().synchronize()  # D2H of send planes complete
+        for w in dist.batch_isend_irecv(p2p):
+            w.wait()
+        for o, h in staged:
+            if o.kind == "recv":
+                o.tensor.copy_(h, non_blocking=False)
+
+
+_gloo_pg = None
+
+
+def _gloo_group():
+    """A gloo group for host-side metadata even when the default PG is nccl."""
+    global _gloo_pg
+    if _gloo_pg is None:
+        backend = dist.get_backend()
+        _gloo_pg = dist.group.WORLD if "gloo" in str(backend) else dist.new_group(backend="gloo")
+    return _gloo_pg
+
+
+class RcclComm(Communicator):
+    """GPU-direct RCCL communicator (native), bootstrapped through the store."""
+
+    name = "rccl"
+
+    def __init__(self, device: torch.device, timeout_s: float = DEFAULT_TIMEOUT_S,
+                 store=None, rank: int | None = None, size: int | None = None,
+                 key: str = "rma/rccl_uid/0"):
+        from .._native import native
+
+        n = native()
+        if store is None:
+            store = dist.distributed_c10d._get_default_store()
+        self.rank = dist.get_rank() if rank is None else rank
+        self.size = dist.get_world_size() if size is None else size
+        self.device = torch.device(device)
+        self.timeout_s = timeout_s
+        if self.rank == 0:
+            uid = n.RcclComm.unique_id()
+            store.set(key, uid)
+        else:
+            uid = store.get(key)
+        n.set_rank_for_errors(self.rank)
+        self._c = n.RcclComm(self.size, self.rank, bytes(uid), self.device.index or 0)
+        self._scratch = torch.zeros(2, dtype=torch.float64, device=self.device)
+
+    @property
+    def native(self):
+        return self._c
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def supports(self, t):
+        return t.is_cuda
+
+    def barrier(self) -> None:
+        self._c.barrier(self._stream(), self.timeout_s)
+
+    def wait(self) -> None:
+        self._c.wait(self._stream(), self.timeout_s)
+
+    def allreduce(self, value: float, op: str = "sum") -> float:
+        from .._native import native
+
+        n = native()
+        self._scratch[0] = float(value)
+        ptr = self._scratch.data_ptr()
+        self._c.allreduce(ptr, ptr + 8, 1, n.DType.float64, getattr(n.RedOp, op), self._stream())
+        self.wait()
+        return float(self._scratch[1].item())
+
+    def allreduce_tensor(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        from .._native import native
+
+        n = native()
+        if t.dtype != torch.float64 or not t.is_contiguous():
+            raise TypeError("allreduce_tensor expects a contiguous float64 device tensor")
+        self._c.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), n.DType.float64,
+                          getattr(n.RedOp, op), self._stream())
+        return t
+
+    def gather(self, t, root=0):
+        src = t.detach().to(self.device).contiguous()
+        nbytes = src.numel() * src.element_size()
+        out = torch.empty((self.size,) + tuple(src.shape), dtype=src.dtype, device=self.device) \
+            if self.rank == root else torch.empty(1, dtype=src.dtype, device=self.device)
+        self._c.gather(src.data_ptr(), out.data_ptr(), nbytes, root, self._stream())
+        self.wait()
+        return list(out.unbind(0)) if self.rank == root else None
+
+    def exchange(self, ops):
+        if not ops:
+            return
+        s = self._stream()
+        self._c.group_start()
+        try:
+            for o in ops:
+                t = o.tensor
+                if not t.is_cuda or not t.is_contiguous():
+                    raise ValueError("rccl exchange needs contiguous device tensors")
+                nb = t.numel() * t.element_size()
+                if o.kind == "send":
+                    self._c.send(t.data_ptr(), nb, o.peer, s)
+                else:
+                    self._c.recv(t.data_ptr(), nb, o.peer, s)
+        finally:
+            self._c.group_end()
+
+    def finalize(self) -> None:
+        if self._c is not None:
+            try:
+                self.wait()
+            finally:
+                self._c = None
+
+
+# ---------------------------------------------------------------------------
+# loopback: N logical ranks = N threads of one process
+# ---------------------------------------------------------------------------
+class LoopbackHub:
+    """Shared mailboxes/barrier for :class:`LoopbackComm` ranks."""
+
+    def __init__(self, size: int, timeout_s: float = 60.0):
+        self.size = size
+        self.timeout_s = timeout_s
+        self._boxes: dict = {}
+        self._lock = threading.Lock()
+        self._barrier = threading.Barrier(size)
+        self._slots: list = [None] * size
+
+    def box(self, src: int, dst: int, tag: int) -> queue.Queue:
+        k = (src, dst, tag)
+        with self._lock:
+            q = self._boxes.get(k)
+            if q is None:
+                q = self._boxes[k] = queue.Queue()
+            return q
+
+    def collect(self, rank: int, value):
+        """All ranks deposit a value; every rank gets the full list."""
+        self._slots[rank] = value
+        self._barrier.wait(self.timeout_s)
+        out = list(self._slots)
+        self._barrier.wait(self.timeout_s)
+        return out
+
+
+class LoopbackComm(Communicator):
+    name = "loopback"
+
+    def __init__(self, hub: LoopbackHub, rank: int):
+        self.hub = hub
+        self.rank = rank
+        self.size = hub.size
+
+    def barrier(self) -> None:
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+        self.hub._barrier.wait(self.hub.timeout_s)
+
+    def allreduce(self, value: float, op: str = "sum") -> float:
+        vals = self.hub.collect(self.rank, float(value))
+        return {"sum": sum, "max": max, "min": min}[op](vals)
+
+    def gather(self, t, root=0):
+        vals = self.hub.collect(self.rank, t.detach().clone())
+        return vals if self.rank == root else None
+
+    def exchange(self, ops):
+        if ops and any(o.tensor.is_cuda for o in ops):
+            torch.cuda.current_stream().synchronize()
+        for o in ops:
+            if o.kind == "send":
+                self.hub.box(self.rank, o.peer, o.tag).put(o.tensor.detach().clone())
+        for o in ops:
+            if o.kind == "recv":
+                try:
+                    v = self.hub.box(o.peer, self.rank, o.tag).get(timeout=self.hub.timeout_s)
+                except queue.Empty:
+                    raise RuntimeError(
+                        f"loopback rank {self.rank}: no message from {o.peer} tag {o.tag} "
+                        f"within {self.hub.timeout_s}s") from None
+                o.tensor.copy_(v)
+
+
+# ---------------------------------------------------------------------------
+# bootstrap helpers
+# ---------------------------------------------------------------------------
+def env_world() -> tuple[int, int, int | None]:
+    """(rank, world_size, local_rank or None) from torchrun/SLURM/OpenMPI env."""
+    def first(*names):
+        for n in names:
+            v = os.environ.get(n)
+            if v not in (None, ""):
+                return int(v)
+        return None
+
+    rank = first("RANK", "SLURM_PROCID", "OMPI_COMM_WORLD_RANK", "PMI_RANK")
+    size = first("WORLD_SIZE", "SLURM_NTASKS", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE")
+    local = first("LOCAL_RANK", "SLURM_LOCALID", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID")
+    return (rank or 0), (size or 1), local
+
+
+def init_distributed(backend: str | None = None, timeout_s: float = DEFAULT_TIMEOUT_S) -> None:
+    """Initialise torch.distributed from the environment if needed (env://)."""
+    if dist.is_initialized():
+        return
+    rank, size, _ = env_world()
+    os.environ.setdefault("RANK", str(rank))
+    os.environ.setdefault("WORLD_SIZE", str(size))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    import datetime
+
+    if backend is None:
+        backend = "cpu:gloo,cuda:nccl" if torch.cuda.is_available() else "gloo"
+    dist.init_process_group(backend=backend, rank=rank, world_size=size,
+                            timeout=datetime.timedelta(seconds=timeout_s))
+
+
+def node_local_rank(comm_rank: int, comm_size: int) -> tuple[int, int]:
+    """(local rank, ranks on this node). LOCAL_RANK if set, else a hostname
+    exchange over the store (MPI.Comm_split_type(COMM_TYPE_SHARED) analogue)."""
+    _, _, local = env_world()
+    lsize = os.environ.get("LOCAL_WORLD_SIZE")
+    if local is not None and lsize:
+        return local, int(lsize)
+    if comm_size == 1 or not dist.is_initialized():
+        return (local or 0), 1
+    host = os.environ.get("RMA_HOSTNAME", socket.gethostname())
+    names: list = [None] * comm_size
+    dist.all_gather_object(names, host, group=_gloo_group())
+    same = [r for r, h in enumerate(names) if h == host]
+    return same.index(comm_rank), len(same)
+
+
+def select_device(local_rank: int) -> torch.device:
+    """One GPU per process: device = local_rank mod visible devices."""
+    if not torch.cuda.is_available():
+        return torch.device("cpu")
+    n = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % n)
+    torch.cuda.set_device(dev)
+    return dev
+
+
+def wait_all(comm: Communicator) -> None:
+    if isinstance(comm, RcclComm):
+        comm.wait()
+    elif torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+
+
+def now() -> float:
+    return time.perf_counter()

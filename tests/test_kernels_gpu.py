@@ -1,0 +1,168 @@
+"""GPU numerics of the hand-written gfx950 kernels vs plain PyTorch references.
+
+Every kernel is compared against (a) a pure-torch formulation of the same op
+(float64, same operation order => bitwise) and (b) the C++ CPU twin.
+"""
+import pytest
+import torch
+
+from rocm_mpi_amd import ops
+from rocm_mpi_amd._native import native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def rand(shape, seed=0, device=DEV):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(shape, generator=g, dtype=torch.float64).to(device)
+
+
+def coef():
+    return ops.StencilCoef(-1.3, 1 / 0.037, 1 / 0.041, 0.00031)
+
+
+SHAPES = [(3, 3), (5, 4), (66, 130), (130, 66), (389, 515), (257, 1024), (100, 2050), (31, 4097)]
+
+
+@pytest.mark.parametrize("ny,nx", SHAPES)
+@pytest.mark.parametrize("chunk", [1, 7, 64])
+def test_stencil_march_bitwise(ny, nx, chunk):
+    T = rand((ny, nx), 1)
+    iCp = rand((ny, nx), 2) + 0.5
+    out = torch.full_like(T, -7.0)
+    ops.stencil_step(out, T, iCp, coef(), tuning=ops.StencilTuning(chunk_rows=chunk))
+    ref = torch.full((ny, nx), -7.0, dtype=torch.float64)
+    ops.stencil_torch(ref, T.cpu(), iCp.cpu(), coef(), [ops.interior_rect(nx, ny)])
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref)  # boundary untouched, interior bitwise
+
+
+@pytest.mark.parametrize("kernel", ["march", "lds"])
+@pytest.mark.parametrize("nt", [False, True])
+def test_stencil_variants_and_rect_lists(kernel, nt):
+    ny, nx = 300, 700
+    T = rand((ny, nx), 3)
+    iCp = rand((ny, nx), 4) + 0.5
+    frame, interior = ops.hide_rects(nx, ny, 5, 3)
+    tn = ops.StencilTuning(chunk_rows=16, nontemporal=nt, kernel=kernel)
+    out = torch.zeros_like(T)
+    ops.stencil_step(out, T, iCp, coef(), frame, tn)
+    ops.stencil_step(out, T, iCp, coef(), [interior], tn)
+    full = torch.zeros_like(T)
+    ops.stencil_step(full, T, iCp, coef(), tuning=tn)
+    ref = torch.zeros((ny, nx), dtype=torch.float64)
+    ops.stencil_torch(ref, T.cpu(), iCp.cpu(), coef(), [ops.interior_rect(nx, ny)])
+    assert torch.equal(out.cpu(), ref)
+    assert torch.equal(full.cpu(), ref)
+
+
+def test_stencil_unaligned_pointer_path():
+    # a view starting one element in: 8-byte aligned only -> scalar (V=1) path
+    base = rand(64 * 200 + 1, 5)
+    T = base[1:].view(200, 64)
+    iCp = torch.ones((200, 64), dtype=torch.float64, device=DEV)
+    out = torch.zeros((200, 64), dtype=torch.float64, device=DEV)
+    ops.stencil_step(out, T, iCp, coef())
+    ref = torch.zeros((200, 64), dtype=torch.float64)
+    ops.stencil_torch(ref, T.cpu(), iCp.cpu(), coef(), [ops.interior_rect(64, 200)])
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_stencil_rejects_bad_rect():
+    T = rand((10, 10))
+    with pytest.raises(ValueError):
+        ops.stencil_step(torch.empty_like(T), T, T, coef(), [(0, 5, 1, 5)])
+    with pytest.raises(RuntimeError):  # native validation (bypassing Python checks)
+        native().stencil_rects(T.data_ptr(), T.data_ptr(), T.data_ptr(), 10, 10, [(1, 10, 1, 9)],
+                               tuple(coef()), 64, 0, 0, 0, True)
+
+
+@pytest.mark.parametrize("ny,nx", [(3, 3), (67, 131), (256, 1024)])
+def test_kp_kernels_bitwise(ny, nx):
+    c = coef()
+    T = rand((ny, nx), 6)
+    iCp = rand((ny, nx), 7) + 0.5
+    res = {}
+    for dev in (DEV, "cpu"):
+        Td, iCpd = T.to(dev).clone(), iCp.to(dev)
+        qx = torch.zeros((ny - 2, nx - 1), dtype=torch.float64, device=dev)
+        qy = torch.zeros((ny - 1, nx - 2), dtype=torch.float64, device=dev)
+        d = torch.zeros((ny - 2, nx - 2), dtype=torch.float64, device=dev)
+        ops.flux(qx, qy, Td, c.mlam, c.rdx, c.rdy)
+        ops.residual(d, qx, qy, iCpd, c.rdx, c.rdy)
+        ops.update(Td, d, c.dt)
+        res[dev] = (qx.cpu(), qy.cpu(), d.cpu(), Td.cpu())
+    for a, b in zip(res[DEV], res["cpu"]):
+        assert torch.equal(a, b)
+    # kp == fused stencil
+    fused = T.cpu().clone()
+    ops.stencil_torch(fused, T.cpu(), iCp.cpu(), c, [ops.interior_rect(nx, ny)])
+    assert torch.equal(res[DEV][3], fused)
+
+
+def test_init_kernels():
+    geom = ops.TileGeometry(gx0=126, gy0=0, nxg=254, nyg=254, dx=10 / 254, dy=10 / 254)
+    a = torch.empty((128, 128), dtype=torch.float64, device=DEV)
+    b = torch.empty((128, 128), dtype=torch.float64)
+    ops.init_random_(a, geom, seed=42)
+    ops.init_random_(b, geom, seed=42)
+    assert torch.equal(a.cpu(), b)
+    assert 0.0 <= float(b.min()) and float(b.max()) < 1.0
+    ops.init_gaussian_(a, geom, 10.0, 10.0)
+    ops.init_gaussian_(b, geom, 10.0, 10.0)
+    torch.testing.assert_close(a.cpu(), b, rtol=4e-16, atol=1e-300)
+
+
+def test_init_random_is_decomposition_invariant():
+    geom_full = ops.TileGeometry(0, 0, 254, 254, 1.0, 1.0)
+    full = torch.empty((254, 254), dtype=torch.float64, device=DEV)
+    ops.init_random_(full, geom_full, seed=7)
+    part = torch.empty((128, 128), dtype=torch.float64, device=DEV)
+    ops.init_random_(part, ops.TileGeometry(126, 126, 254, 254, 1.0, 1.0), seed=7)
+    assert torch.equal(part, full[126:, 126:])
+
+
+@pytest.mark.parametrize("elem", [torch.float64, torch.float32, torch.float16])
+def test_copy_plane_strided(elem):
+    A = rand((37, 53), 8).to(elem)
+    col = A[:, 3:5]  # strided plane: 37 rows of 2
+    buf = torch.empty((37, 2), dtype=elem, device=DEV)
+    ops.copy_plane(buf, col)
+    assert torch.equal(buf, col)
+    B = torch.zeros_like(A)
+    ops.copy_plane(B[:, 50:52], buf)
+    assert torch.equal(B[:, 50:52], col)
+    assert float(B[:, :50].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("op", ["sum", "max", "min", "maxabs", "nonfinite"])
+def test_reduce(op):
+    A = rand((513, 257), 9) - 0.5
+    A[3, 7] = float("nan") if op == "nonfinite" else A[3, 7]
+    got = float(ops.reduce(A, op))
+    c = A.cpu()
+    want = {"sum": lambda: float(c.sum()), "max": lambda: float(c.max()),
+            "min": lambda: float(c.min()), "maxabs": lambda: float(c.abs().max()),
+            "nonfinite": lambda: 1.0}[op]()
+    assert got == pytest.approx(want, rel=1e-12, abs=1e-12)
+
+
+@pytest.mark.slow
+def test_stencil_int64_indexing():
+    """A tile beyond 2^31 cells (64-bit offsets), checked on the last rows."""
+    free, _ = torch.cuda.mem_get_info()
+    ny, nx = 33000, 65536  # 2.16e9 cells, 17.3 GB per array
+    if free < 3 * ny * nx * 8 * 1.1:
+        pytest.skip("not enough HBM")
+    T = torch.empty((ny, nx), dtype=torch.float64, device=DEV)
+    ops.init_random_(T, ops.TileGeometry(0, 0, nx, ny, 1.0, 1.0), seed=3)
+    iCp = torch.empty_like(T)
+    ops.fill_(iCp, 1.0)
+    out = torch.zeros_like(T)
+    ops.stencil_step(out, T, iCp, coef(), [(1, nx - 1, ny - 9, ny - 1)])
+    ref = torch.zeros((10, nx), dtype=torch.float64)
+    ops.stencil_torch(ref, T[ny - 10:].cpu(), iCp[ny - 10:].cpu(), coef(), [(1, nx - 1, 1, 9)])
+    assert torch.equal(out[ny - 9:ny - 1].cpu(), ref[1:9])
+    del T, iCp, out
+    torch.cuda.empty_cache()
