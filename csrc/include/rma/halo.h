@@ -42,6 +42,7 @@ struct PlaneView {
   int64_t elems() const { return n_o * n_k; }
 };
 PlaneView plane_view(const HaloField& f, int dim, int64_t index0);
+bool has_halo(const HaloField& f, int dim);
 
 class HaloExchanger {
  public:

@@ -51,16 +51,22 @@ void* HaloExchanger::buffer(size_t slot, size_t bytes) {
 }
 
 namespace {
-void validate(const HaloField& f, int d) {
+void validate(const HaloField& f) {
   RMA_CHECK_ARG(f.ptr != nullptr, "null field");
   RMA_CHECK_ARG(f.elem_bytes == 2 || f.elem_bytes == 4 || f.elem_bytes == 8 || f.elem_bytes == 16,
                 "elem_bytes=" << f.elem_bytes);
-  RMA_CHECK_ARG(f.hw[d] >= 1 && f.ol[d] >= 2 * f.hw[d],
-                "dim " << d << ": overlap " << f.ol[d] << " must be >= 2*halowidth " << f.hw[d]);
-  RMA_CHECK_ARG(f.size[d] >= f.ol[d] + f.hw[d],
-                "dim " << d << ": array extent " << f.size[d] << " too small for overlap "
-                       << f.ol[d]);
+  for (int d = 0; d < 3; ++d) RMA_CHECK_ARG(f.hw[d] >= 1 && f.size[d] >= 1, "bad field dims");
 }
+}  // namespace
+
+// A field has a halo along d when it is not flat there and its overlap holds
+// two halo planes (ImplicitGlobalGrid skips such dimensions for that field,
+// e.g. an array of size n-1 with overlap 2).
+bool has_halo(const HaloField& f, int d) {
+  return f.size[d] > 1 && f.ol[d] >= 2 * f.hw[d] && f.size[d] >= f.ol[d] + f.hw[d];
+}
+
+namespace {
 
 char* at(const HaloField& f, const PlaneView& v) {
   return static_cast<char*>(f.ptr) + v.offset * f.elem_bytes;
@@ -72,7 +78,7 @@ void HaloExchanger::prepare(const std::vector<HaloField>& fields, int dims_mask)
   for (int d = 0; d < 3; ++d) {
     if (!(dims_mask >> d & 1) || !active(d)) continue;
     for (const auto& f : fields) {
-      if (f.size[d] <= 1) continue;
+      if (!has_halo(f, d)) continue;
       const PlaneView v = plane_view(f, d, 0);
       const size_t bytes = (size_t)v.elems() * f.elem_bytes;
       for (int s = 0; s < 2; ++s) {
@@ -104,8 +110,8 @@ void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stre
     std::vector<Op> sends, recvs;  // sends in (lo, hi) order, recvs in (hi, lo) order per field
     std::vector<Pending> unpack;
     for (const auto& f : fields) {
-      if (f.size[d] <= 1) continue;
-      validate(f, d);
+      validate(f);
+      if (!has_halo(f, d)) continue;
       const int64_t n = f.size[d], ol = f.ol[d], hw = f.hw[d];
       // send planes: lo [ol-hw, ol), hi [n-ol, n-ol+hw); recv planes: lo [0,hw), hi [n-hw, n)
       const PlaneView send_v[2] = {plane_view(f, d, ol - hw), plane_view(f, d, n - ol)};

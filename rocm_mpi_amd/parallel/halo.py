@@ -45,6 +45,21 @@ def field_overlaps(g: GlobalGrid, A: torch.Tensor) -> tuple[int, int, int]:
     return tuple(out)
 
 
+def has_halo(g: GlobalGrid, A: torch.Tensor, d: int) -> bool:
+    """True when A exchanges planes along d (IGG skips dims where the array's
+    overlap cannot hold two halo planes, e.g. size n-1 with overlap 2)."""
+    n = _sizes(A)[d]
+    ol = field_overlaps(g, A)[d]
+    hw = g.halowidths[d]
+    return n > 1 and ol >= 2 * hw and n >= ol + hw
+
+
+def _check_has_some_halo(g: GlobalGrid, arrays) -> None:
+    for i, A in enumerate(arrays):
+        if not any(has_halo(g, A, d) for d in range(3)):
+            raise ValueError(f"field {i} (shape {tuple(A.shape)}) has no halo in any dimension")
+
+
 def _active_dims(g: GlobalGrid) -> list[int]:
     return [d for d in range(3) if g.neighbors[d][0] >= 0 or g.neighbors[d][1] >= 0]
 
@@ -63,16 +78,12 @@ def update_halo_(*arrays: torch.Tensor, dims=(0, 1, 2)) -> None:
     mask = 0
     for d in dims:
         mask |= 1 << d
+    _check_has_some_halo(g, arrays)
     if dev.type == "cuda" and g.halo is not None:
         fields = []
         for A in arrays:
             sz = _sizes(A)
             ol = field_overlaps(g, A)
-            for d in range(3):
-                if sz[d] > 1 and (mask >> d & 1) and (g.neighbors[d][0] >= 0 or g.neighbors[d][1] >= 0):
-                    if ol[d] < 2 * g.halowidths[d] or sz[d] < ol[d] + g.halowidths[d]:
-                        raise ValueError(f"dim {d}: overlap {ol[d]} / size {sz[d]} too small "
-                                         f"for halowidth {g.halowidths[d]}")
             fields.append((A.data_ptr(), list(sz), A.element_size(), list(ol),
                            list(g.halowidths)))
         g.halo.exchange(fields, torch.cuda.current_stream(dev).cuda_stream, mask)
@@ -94,13 +105,10 @@ def _update_halo_python(g: GlobalGrid, arrays, mask: int) -> None:
         hw = g.halowidths[d]
         sends, recvs, unpack = [], [], []
         for i, A in enumerate(arrays):
-            sz = _sizes(A)
-            n = sz[d]
-            if n <= 1:
+            if not has_halo(g, A, d):
                 continue
+            n = _sizes(A)[d]
             ol = field_overlaps(g, A)[d]
-            if ol < 2 * hw or n < ol + hw:
-                raise ValueError(f"dim {d}: overlap {ol} / size {n} too small for halowidth {hw}")
             send_p = [_plane(A, d, ol - hw, hw), _plane(A, d, n - ol, hw)]
             recv_p = [_plane(A, d, 0, hw), _plane(A, d, n - hw, hw)]
             s_ops, r_ops = [None, None], [None, None]

@@ -1,0 +1,49 @@
+"""Process entry points for multi-process (gloo) tests; see helpers.run_procs."""
+import os
+
+import numpy as np
+import torch
+
+
+def diffusion(rank, world, outdir, variant, nx, ny, nt, dims, transport="gloo", init="gaussian"):
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    m = Diffusion2D(DiffusionConfig(variant=variant, nx=nx, ny=ny, nt=nt, dims=tuple(dims) + (0,),
+                                    transport=transport, quiet=True, init=init, init_on="host",
+                                    b_width=(4, 2), device="cpu"))
+    res = m.run() if nt > 10 else None
+    if res is None:
+        m.step(nt)
+    Tv = m.gather_interior()
+    if gg.global_grid().me == 0:
+        np.save(os.path.join(outdir, "Tv.npy"), Tv.numpy())
+        with open(os.path.join(outdir, "meta.txt"), "w") as f:
+            g = gg.global_grid()
+            f.write(f"{g.nxyz_g[0]} {g.nxyz_g[1]} {g.transport}")
+            if res is not None:
+                f.write(f" {res.teff_total} {res.timed_steps}")
+    m.close()
+
+
+def ring(rank, world, outdir):
+    from rocm_mpi_amd.apps import rocmaware_test_selectdevice as app
+
+    vals = app.run(4, transport="gloo", verbose=False)
+    np.save(os.path.join(outdir, f"ring{rank}.npy"), np.array(vals))
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def collectives(rank, world, outdir):
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    me, dims, nprocs, coords, comm = gg.init_global_grid(6, 6, 1, quiet=True, device="cpu")
+    s = comm.allreduce(float(rank + 1), "sum")
+    mx = comm.allreduce(float(rank), "max")
+    gg.tic()
+    t = gg.toc()
+    np.save(os.path.join(outdir, f"coll{rank}.npy"), np.array([s, mx, t, nprocs] + list(dims)))
+    gg.finalize_global_grid()

@@ -1,0 +1,142 @@
+"""update_halo_ / gather_ semantics against a global ground truth (CPU).
+
+Each rank's local block is a slice of one global array; after corrupting the
+halo planes that face a neighbour, update_halo_ must restore exactly the
+global values — for 1-D/2-D/3-D fields, several fields per call, staggered
+fields (size n+-1), halowidth 2 (overlap 4) and periodic dimensions.
+"""
+import itertools
+
+import pytest
+import torch
+
+from helpers import run_loopback
+from rocm_mpi_amd.parallel import implicit_grid as gg
+from rocm_mpi_amd.parallel.halo import gather_, has_halo, update_halo_
+
+
+def local_block(G, g, shape_local, stagger):
+    idx = []
+    nd = len(shape_local)
+    for ax in range(nd):
+        d = nd - 1 - ax
+        off = g.coords[d] * (g.nxyz[d] - g.overlaps[d])
+        idx.append(torch.arange(off, off + shape_local[ax]) % G.shape[ax])
+    return G[torch.meshgrid(*idx, indexing="ij")].clone()
+
+
+def corrupt(A, g):
+    nd = A.dim()
+    for d in range(nd):
+        if not has_halo(g, A, d):  # e.g. size n-1: no halo along d, left untouched
+            continue
+        ax = nd - 1 - d
+        hw = g.halowidths[d]
+        n = A.shape[ax]
+        if g.neighbors[d][0] >= 0:
+            A.narrow(ax, 0, hw).fill_(-1.0)
+        if g.neighbors[d][1] >= 0:
+            A.narrow(ax, n - hw, hw).fill_(-1.0)
+
+
+def spmd(rank, hub, nxyz, dims, periods, overlaps, staggers, nfields):
+    gg.init_global_grid(*nxyz, dimx=dims[0], dimy=dims[1], dimz=dims[2], periodx=periods[0],
+                        periody=periods[1], periodz=periods[2], overlaps=overlaps, quiet=True,
+                        loopback=(hub, rank), select_device=False)
+    g = gg.global_grid()
+    nd = 3 if nxyz[2] > 1 else (2 if nxyz[1] > 1 else 1)
+    fields, expect = [], []
+    for f in range(nfields):
+        st = staggers[f % len(staggers)]
+        shp_l = tuple(nxyz[d] + st[d] for d in reversed(range(nd)))
+        shp_g = tuple(g.nxyz_g[d] + st[d] + (0 if not periods[d] else 0) for d in reversed(range(nd)))
+        gen = torch.Generator().manual_seed(100 + f)
+        G = torch.rand(shp_g, generator=gen, dtype=torch.float64)
+        A = local_block(G, g, shp_l, st)
+        expect.append(A.clone())
+        corrupt(A, g)
+        fields.append(A)
+    update_halo_(*fields)
+    ok = all(torch.equal(a, e) for a, e in zip(fields, expect))
+    gg.finalize_global_grid()
+    return ok
+
+
+CASES = [
+    # nxyz, dims, periods, overlaps, staggers, nfields
+    ((9,), (3, 1, 1), (0, 0, 0), (2, 2, 2), [(0, 0, 0)], 1),
+    ((9, 7), (2, 2, 1), (0, 0, 0), (2, 2, 2), [(0, 0, 0)], 1),
+    ((9, 7), (2, 2, 1), (0, 0, 0), (2, 2, 2), [(0, 0, 0), (1, 0, 0), (0, 1, 0), (-1, 0, 0)], 4),
+    ((12, 10), (2, 2, 1), (0, 0, 0), (4, 4, 2), [(0, 0, 0)], 2),
+    ((6, 5, 7), (2, 2, 2), (0, 0, 0), (2, 2, 2), [(0, 0, 0), (0, 0, 1)], 2),
+    ((9, 7), (4, 1, 1), (0, 0, 0), (2, 2, 2), [(0, 0, 0)], 1),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"n{c[0]}-d{c[1]}-ol{c[3][0]}-f{c[5]}")
+def test_update_halo_matches_global(case):
+    nxyz, dims, periods, overlaps, staggers, nf = case
+    nxyz3 = tuple(nxyz) + (1,) * (3 - len(nxyz))
+    P = dims[0] * dims[1] * dims[2]
+    assert all(run_loopback(P, spmd, nxyz3, dims, periods, overlaps, staggers, nf))
+
+
+def spmd_periodic(rank, hub, P):
+    # periodic x on P ranks (P=1 -> local self copy), field values = global index
+    n, ol = 8, 2
+    gg.init_global_grid(n, 6, 1, dimx=P, periodx=1, quiet=True, loopback=(hub, rank),
+                        select_device=False)
+    g = gg.global_grid()
+    nxg = g.nxyz_g[0]
+    off = g.coords[0] * (n - ol)
+    gx = (torch.arange(off, off + n) - 1) % nxg  # first local cell is the ghost
+    A = gx.to(torch.float64).repeat(6, 1).contiguous()
+    want = A.clone()
+    A[:, 0] = -1
+    A[:, -1] = -1
+    update_halo_(A)
+    ok = torch.equal(A, want)
+    gg.finalize_global_grid()
+    return ok
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_periodic_halo(P):
+    assert all(run_loopback(P, spmd_periodic, P))
+
+
+def spmd_gather(rank, hub):
+    gg.init_global_grid(5, 4, 3, dimx=2, dimy=1, dimz=2, quiet=True, loopback=(hub, rank),
+                        select_device=False)
+    g = gg.global_grid()
+    A = torch.full((3, 4, 5), float(rank), dtype=torch.float64)
+    out = gather_(A)
+    coords = list(g.coords)
+    gg.finalize_global_grid()
+    return out, coords
+
+
+def test_gather_3d_places_blocks_by_coords():
+    res = run_loopback(4, spmd_gather)
+    G = res[0][0]
+    assert G.shape == (6, 4, 10)
+    for r, (_, c) in enumerate(res):
+        blk = G[c[2] * 3:(c[2] + 1) * 3, c[1] * 4:(c[1] + 1) * 4, c[0] * 5:(c[0] + 1) * 5]
+        assert torch.all(blk == r)
+    assert all(o is None for o, _ in res[1:])
+
+
+def spmd_nohalo(rank, hub):
+    gg.init_global_grid(9, 7, 1, dimx=2, dimy=2, quiet=True, loopback=(hub, rank),
+                        select_device=False)
+    try:
+        update_halo_(torch.zeros(6, 8, dtype=torch.float64))  # n-1 in x and y: no halo at all
+    except ValueError:
+        return True
+    finally:
+        gg.finalize_global_grid()
+    return False
+
+
+def test_field_without_halo_is_rejected():
+    assert all(run_loopback(4, spmd_nohalo))

@@ -1,0 +1,39 @@
+"""Real multi-process runs over torch.distributed/gloo (world_size 2 and 4).
+
+The same SPMD code that runs one rank per MI355X over RCCL, here with CPU
+tensors: decomposition invariance against the global NumPy golden model, the
+T_eff reference protocol, collectives, and the ring P2P smoke test
+(scripts/rocmaware_test_selectdevice.jl)."""
+import os
+
+import numpy as np
+import pytest
+
+import golden
+from helpers import run_procs
+
+
+@pytest.mark.parametrize("variant,world,dims", [("perf_hide", 2, (2, 1)), ("kp", 2, (1, 2)),
+                                                ("perf", 4, (2, 2)), ("ap", 4, (4, 1))])
+def test_gloo_decomposition_invariance(tmp_path, variant, world, dims):
+    nx, ny, nt = 40, 36, 30
+    run_procs(world, "mp_targets:diffusion", str(tmp_path), variant, nx, ny, nt, dims)
+    Tv = np.load(tmp_path / "Tv.npy")
+    nxg, nyg, transport, teff, timed = open(tmp_path / "meta.txt").read().split()
+    assert transport == "gloo" and int(timed) == nt - 10 and float(teff) > 0
+    G = golden.run(int(nxg), int(nyg), nt)
+    assert np.array_equal(Tv, G[1:-1, 1:-1])
+
+
+def test_ring_sendrecv(tmp_path):
+    run_procs(3, "mp_targets:ring", str(tmp_path))
+    for r in range(3):
+        v = np.load(tmp_path / f"ring{r}.npy")
+        assert np.all(v == (r - 1) % 3)
+
+
+def test_collectives_and_timers(tmp_path):
+    run_procs(2, "mp_targets:collectives", str(tmp_path))
+    for r in range(2):
+        s, mx, t, n, d0, d1, d2 = np.load(tmp_path / f"coll{r}.npy")
+        assert s == 3 and mx == 1 and t >= 0 and n == 2 and (d0, d1, d2) == (2, 1, 1)
