@@ -1,0 +1,39 @@
+#!/usr/bin/env python
+"""Fixed workload for rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE per kernel).
+
+Runs the march stencil, the LDS stencil, the kp kernels and the copy/triad
+roofline probes a few times each on an N x N fp64 tile (far beyond the 256 MiB
+Infinity Cache), so per-dispatch HBM bytes can be compared with the T_eff
+model (24 B/cell). See scripts/profile.sh.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from rocm_mpi_amd import ops  # noqa: E402
+from rocm_mpi_amd._native import native  # noqa: E402
+
+n = int(os.environ.get("RMA_PROBE_N", "16384"))
+reps = int(os.environ.get("RMA_PROBE_REPS", "3"))
+f = dict(dtype=torch.float64, device="cuda")
+T = torch.empty((n, n), **f)
+ops.init_random_(T, ops.TileGeometry(0, 0, n, n, 1.0, 1.0), seed=1)
+T2 = torch.empty_like(T)
+iCp = torch.empty_like(T)
+ops.fill_(iCp, 1.0)
+c = ops.StencilCoef(-1.0, 1.0, 1.0, 0.2)
+s = torch.cuda.current_stream().cuda_stream
+nat = native()
+for _ in range(reps):
+    ops.stencil_step(T2, T, iCp, c)
+for _ in range(reps):
+    ops.stencil_step(T2, T, iCp, c, tuning=ops.StencilTuning(kernel="lds"))
+for _ in range(reps):
+    nat.stream_copy(T2.data_ptr(), T.data_ptr(), n * n, s)
+for _ in range(reps):
+    nat.stream_triad(T2.data_ptr(), T.data_ptr(), iCp.data_ptr(), 0.5, n * n, s)
+torch.cuda.synchronize()
+print(f"probe done n={n} reps={reps}")

@@ -1,0 +1,105 @@
+#!/usr/bin/env python
+"""Kernel-level tuning sweep + same-box HBM roofline (one process, interleaved).
+
+Times every stencil variant (march: chunk_rows x unroll x nontemporal; the
+LDS-tiled kernel) on an N x N fp64 tile and the streaming probes (copy = 1R1W,
+triad = 2R1W, the stencil's byte mix) in interleaved rounds (§5.4 rule 24 of
+the CDNA guide: A/B in one process, report median and min). Prints one JSON
+document; the bytes model is the reference's T_eff (24 B/cell).
+
+    python bench/stencil_sweep.py --n 16384 --rounds 5 --iters 20
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--chunks", default="16,32,64,128,256")
+    ap.add_argument("--unrolls", default="2,4,8")
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from rocm_mpi_amd import ops
+    from rocm_mpi_amd._native import native
+
+    n = a.n
+    dev = torch.device("cuda", 0)
+    f = dict(dtype=torch.float64, device=dev)
+    T = torch.empty((n, n), **f)
+    ops.init_random_(T, ops.TileGeometry(0, 0, n, n, 1.0, 1.0), seed=1)
+    T2 = torch.empty_like(T)
+    iCp = torch.empty_like(T)
+    ops.fill_(iCp, 1.0)
+    coef = ops.StencilCoef(-1.0, 1.0, 1.0, 0.2)
+    cells = (n - 2) * (n - 2)
+    bytes_model = 24.0 * n * n  # T_eff model: local nx*ny incl. halo
+    nat = native()
+    s = torch.cuda.current_stream().cuda_stream
+
+    variants = {}
+    chunks = [int(c) for c in a.chunks.split(",")]
+    unrolls = [int(u) for u in a.unrolls.split(",")]
+    if a.quick:
+        chunks, unrolls = [64], [4]
+    for c in chunks:
+        for u in unrolls:
+            for nt in (False, True):
+                tn = ops.StencilTuning(chunk_rows=c, unroll=u, nontemporal=nt)
+                variants[f"march_c{c}_u{u}{'_nt' if nt else ''}"] = (
+                    lambda tn=tn: ops.stencil_step(T2, T, iCp, coef, tuning=tn), bytes_model)
+    variants["lds"] = (lambda: ops.stencil_step(T2, T, iCp, coef,
+                                                tuning=ops.StencilTuning(kernel="lds")),
+                       bytes_model)
+    nn = n * n
+    variants["roof_copy"] = (lambda: nat.stream_copy(T2.data_ptr(), T.data_ptr(), nn, s),
+                             16.0 * nn)
+    variants["roof_triad"] = (lambda: nat.stream_triad(T2.data_ptr(), T.data_ptr(),
+                                                       iCp.data_ptr(), 0.5, nn, s), 24.0 * nn)
+    times = {k: [] for k in variants}
+    for fn, _ in variants.values():  # warm
+        fn()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(a.rounds):
+        for k, (fn, _) in variants.items():
+            ev0.record()
+            for _ in range(a.iters):
+                fn()
+            ev1.record()
+            ev1.synchronize()
+            times[k].append(ev0.elapsed_time(ev1) / a.iters / 1e3)
+    res = {}
+    for k, (fn, b) in variants.items():
+        med = statistics.median(times[k])
+        res[k] = {"median_ms": med * 1e3, "min_ms": min(times[k]) * 1e3,
+                  "GBps_median": b / med / 1e9, "GBps_best": b / min(times[k]) / 1e9}
+    best = max((k for k in res if k.startswith("march")), key=lambda k: res[k]["GBps_median"])
+    doc = {"n": n, "cells": cells, "rounds": a.rounds, "iters": a.iters, "results": res,
+           "best_march": best, "best_march_GBps": res[best]["GBps_median"],
+           "triad_GBps": res["roof_triad"]["GBps_median"],
+           "copy_GBps": res["roof_copy"]["GBps_median"],
+           "best_vs_triad": res[best]["GBps_median"] / res["roof_triad"]["GBps_median"],
+           "device": torch.cuda.get_device_name(0)}
+    txt = json.dumps(doc, indent=1)
+    print(txt)
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(txt)
+
+
+if __name__ == "__main__":
+    main()

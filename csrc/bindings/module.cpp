@@ -16,6 +16,8 @@
 #include "rma/executor.h"
 #include "rma/halo.h"
 #include "rma/kernels.h"
+#include "rma/loopback.h"
+#include "rma/p2p.h"
 #include "rma/topology.h"
 #include "rma/trace.h"
 
@@ -88,12 +90,13 @@ PYBIND11_MODULE(_C, m) {
       "stencil_rects",
       [](uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
          const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
-         int kernel, uintptr_t stream, bool gpu) {
+         int kernel, uintptr_t stream, bool gpu, int unroll) {
         auto r = to_rects(rects);
         StencilTuning tn;
         tn.chunk_rows = chunk_rows;
         tn.nontemporal = nontemporal;
         tn.kernel = kernel;
+        tn.unroll = unroll;
         if (gpu)
           stencil_rects_gpu(P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
                             r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
@@ -105,7 +108,15 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"), py::arg("rects"),
       py::arg("coef"), py::arg("chunk_rows") = 64, py::arg("nontemporal") = 0,
-      py::arg("kernel") = 0, py::arg("stream") = 0, py::arg("gpu") = true);
+      py::arg("kernel") = 0, py::arg("stream") = 0, py::arg("gpu") = true,
+      py::arg("unroll") = 4);
+  m.def("stream_copy", [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s) {
+    stream_copy_gpu(P<double>(b), P<const double>(a), n, S(s));
+  });
+  m.def("stream_triad", [](uintptr_t c, uintptr_t a, uintptr_t b, double x, int64_t n,
+                           uintptr_t s) {
+    stream_triad_gpu(P<double>(c), P<const double>(a), P<const double>(b), x, n, S(s));
+  });
 
   m.def("flux", [](uintptr_t qx, uintptr_t qy, uintptr_t T, int64_t nx, int64_t ny, double mlam,
                    double rdx, double rdy, uintptr_t stream, bool gpu) {
@@ -190,7 +201,23 @@ PYBIND11_MODULE(_C, m) {
       .value("max", RedOp::kMax)
       .value("min", RedOp::kMin)
       .value("prod", RedOp::kProd);
-  py::class_<RcclComm>(m, "RcclComm")
+  py::class_<P2PTransport>(m, "P2PTransport")
+      .def_property_readonly("rank", &P2PTransport::rank)
+      .def_property_readonly("size", &P2PTransport::size)
+      .def("group_start", &P2PTransport::group_start)
+      .def("group_end", &P2PTransport::group_end, py::call_guard<py::gil_scoped_release>())
+      .def("send", [](P2PTransport& c, uintptr_t buf, size_t bytes, int peer,
+                      uintptr_t s) { c.send(P<const void>(buf), bytes, peer, S(s)); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("recv", [](P2PTransport& c, uintptr_t buf, size_t bytes, int peer,
+                      uintptr_t s) { c.recv(P<void>(buf), bytes, peer, S(s)); },
+           py::call_guard<py::gil_scoped_release>());
+  py::class_<LoopbackHub, std::shared_ptr<LoopbackHub>>(m, "LoopbackHub")
+      .def(py::init<int, double>(), py::arg("nranks"), py::arg("timeout_s") = 60.0)
+      .def_property_readonly("size", &LoopbackHub::size);
+  py::class_<LoopbackEndpoint, P2PTransport>(m, "LoopbackEndpoint")
+      .def(py::init<std::shared_ptr<LoopbackHub>, int>(), py::arg("hub"), py::arg("rank"));
+  py::class_<RcclComm, P2PTransport>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def(py::init([](int nranks, int rank, py::bytes uid, int device) {
              std::string s = uid;
@@ -198,15 +225,7 @@ PYBIND11_MODULE(_C, m) {
              return new RcclComm(nranks, rank, s, device);
            }),
            py::arg("nranks"), py::arg("rank"), py::arg("uid"), py::arg("device"))
-      .def_property_readonly("rank", &RcclComm::rank)
-      .def_property_readonly("size", &RcclComm::size)
       .def_property_readonly("device", &RcclComm::device)
-      .def("group_start", &RcclComm::group_start)
-      .def("group_end", &RcclComm::group_end)
-      .def("send", [](RcclComm& c, uintptr_t buf, size_t bytes, int peer,
-                      uintptr_t s) { c.send(P<const void>(buf), bytes, peer, S(s)); })
-      .def("recv", [](RcclComm& c, uintptr_t buf, size_t bytes, int peer,
-                      uintptr_t s) { c.recv(P<void>(buf), bytes, peer, S(s)); })
       .def("allreduce",
            [](RcclComm& c, uintptr_t sb, uintptr_t rb, size_t count, DType dt, RedOp op,
               uintptr_t s) { c.allreduce(P<const void>(sb), P<void>(rb), count, dt, op, S(s)); })
@@ -226,7 +245,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("aborted", &RcclComm::aborted);
 
   py::class_<HaloExchanger>(m, "HaloExchanger")
-      .def(py::init([](RcclComm* comm, int self_rank,
+      .def(py::init([](P2PTransport* comm, int self_rank,
                        std::array<std::array<int, 2>, 3> nbr) {
              return new HaloExchanger(comm, self_rank, nbr);
            }),
@@ -235,7 +254,9 @@ PYBIND11_MODULE(_C, m) {
       .def(
           "exchange",
           [](HaloExchanger& h, const std::vector<FieldT>& fields, uintptr_t s, int mask) {
-            h.exchange(to_fields(fields), S(s), mask);
+            auto f = to_fields(fields);
+            py::gil_scoped_release nogil;  // loopback transports block on peer threads
+            h.exchange(f, S(s), mask);
           },
           py::arg("fields"), py::arg("stream"), py::arg("dims_mask") = 7)
       .def(
@@ -245,6 +266,7 @@ PYBIND11_MODULE(_C, m) {
           },
           py::arg("fields"), py::arg("dims_mask") = 7)
       .def("active", &HaloExchanger::active)
+      .def("set_self_via_transport", &HaloExchanger::set_self_via_transport)
       .def_property_readonly("neighbors", &HaloExchanger::neighbors)
       .def_property_readonly("bytes_sent_last", &HaloExchanger::bytes_sent_last);
 
@@ -253,13 +275,15 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init([](uintptr_t T, uintptr_t T2, uintptr_t iCp, int64_t nx, int64_t ny, int mode,
                        const Coef4& coef, int chunk_rows, int nontemporal, int kernel,
                        int64_t bwx, int64_t bwy, int use_graph, int graph_steps,
-                       HaloExchanger* halo, uintptr_t qx, uintptr_t qy, uintptr_t dTdt) {
+                       HaloExchanger* halo, uintptr_t qx, uintptr_t qy, uintptr_t dTdt,
+                       int unroll) {
              ExecParams p;
              p.mode = static_cast<Mode>(mode);
              p.coef = to_coef(coef);
              p.tune.chunk_rows = chunk_rows;
              p.tune.nontemporal = nontemporal;
              p.tune.kernel = kernel;
+             p.tune.unroll = unroll;
              p.bwx = bwx;
              p.bwy = bwy;
              p.use_graph = use_graph;
@@ -273,10 +297,10 @@ PYBIND11_MODULE(_C, m) {
            py::arg("nontemporal") = 0, py::arg("kernel") = 0, py::arg("bwx") = 127,
            py::arg("bwy") = 4, py::arg("use_graph") = 0, py::arg("graph_steps") = 0,
            py::arg("halo").none(true) = nullptr, py::arg("qx") = 0, py::arg("qy") = 0,
-           py::arg("dTdt") = 0, py::keep_alive<1, 16>())
+           py::arg("dTdt") = 0, py::arg("unroll") = 4, py::keep_alive<1, 16>())
       .def(
           "run", [](DiffusionExecutor& e, int64_t n, uintptr_t s) { e.run(n, S(s)); },
-          py::arg("nsteps"), py::arg("stream"))
+          py::arg("nsteps"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("parity", &DiffusionExecutor::parity)
       .def_property_readonly("steps_done", &DiffusionExecutor::steps_done)
       .def_property_readonly("frame_rects",

@@ -18,13 +18,14 @@
 #include <string>
 
 #include "rma/kernels.h"
+#include "rma/p2p.h"
 
 namespace rma {
 
 enum class DType : int { kFloat64 = 0, kFloat32 = 1, kInt64 = 2, kInt32 = 3, kUInt8 = 4 };
 enum class RedOp : int { kSum = 0, kMax = 1, kMin = 2, kProd = 3 };
 
-class RcclComm {
+class RcclComm : public P2PTransport {
  public:
   static std::string unique_id();  // 128 opaque bytes, generate on ONE rank
   RcclComm(int nranks, int rank, const std::string& uid, int device);
@@ -32,14 +33,14 @@ class RcclComm {
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
 
-  int rank() const { return rank_; }
-  int size() const { return nranks_; }
+  int rank() const override { return rank_; }
+  int size() const override { return nranks_; }
   int device() const { return device_; }
 
-  void group_start();
-  void group_end();
-  void send(const void* buf, size_t bytes, int peer, stream_t stream);
-  void recv(void* buf, size_t bytes, int peer, stream_t stream);
+  void group_start() override;
+  void group_end() override;
+  void send(const void* buf, size_t bytes, int peer, stream_t stream) override;
+  void recv(void* buf, size_t bytes, int peer, stream_t stream) override;
   void allreduce(const void* sendbuf, void* recvbuf, size_t count, DType dt, RedOp op,
                  stream_t stream);
   void broadcast(const void* sendbuf, void* recvbuf, size_t count, DType dt, int root,

@@ -48,7 +48,7 @@ class HaloExchanger {
  public:
   // neighbors[d] = {low, high} ranks (kProcNull = -1 at open edges);
   // comm may be null when every neighbour is either absent or this rank.
-  HaloExchanger(RcclComm* comm, int self_rank, std::array<std::array<int, 2>, 3> neighbors);
+  HaloExchanger(P2PTransport* comm, int self_rank, std::array<std::array<int, 2>, 3> neighbors);
   ~HaloExchanger();
   HaloExchanger(const HaloExchanger&) = delete;
   HaloExchanger& operator=(const HaloExchanger&) = delete;
@@ -60,13 +60,17 @@ class HaloExchanger {
   void prepare(const std::vector<HaloField>& fields, int dims_mask = 7);
 
   bool active(int dim) const;  // any neighbour in this dim?
+  // Route self-neighbours (periodic, one process along a dim) through the
+  // transport instead of a local copy (tests the P2P path on one GPU).
+  void set_self_via_transport(bool on) { self_via_comm_ = on && comm_ != nullptr; }
   const std::array<std::array<int, 2>, 3>& neighbors() const { return nbr_; }
   int64_t bytes_sent_last() const { return bytes_last_; }
 
  private:
   void* buffer(size_t slot, size_t bytes);
-  RcclComm* comm_;
+  P2PTransport* comm_;
   int self_;
+  bool self_via_comm_ = false;
   std::array<std::array<int, 2>, 3> nbr_;
   std::vector<void*> bufs_;
   std::vector<size_t> buf_bytes_;

@@ -29,6 +29,7 @@ struct StencilTuning {
   int chunk_rows = 64;     // rows marched by one wave-task
   int nontemporal = 0;     // 1: non-temporal T2 stores
   int kernel = 0;          // 0 = register march (default), 1 = LDS-tiled
+  int unroll = 4;          // rows per march iteration whose loads are issued together
 };
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
@@ -93,6 +94,16 @@ void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int6
                 int64_t n_k, int elem_bytes, stream_t stream);
 void copy2d_cpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int64_t n_o,
                 int64_t n_k, int elem_bytes);
+
+// ---------------------------------------------------------------------------
+// Streaming roofline probes (same-box HBM ceiling for the T_eff comparison):
+//   copy : b[i] = a[i]              (1 read + 1 write)
+//   triad: c[i] = a[i] + s*b[i]     (2 reads + 1 write = the stencil's mix)
+// 16-byte vector accesses, grid-stride.
+// ---------------------------------------------------------------------------
+void stream_copy_gpu(double* b, const double* a, int64_t n, stream_t stream);
+void stream_triad_gpu(double* c, const double* a, const double* b, double s, int64_t n,
+                      stream_t stream);
 
 // ---------------------------------------------------------------------------
 // Reductions for verification / NaN guards. Result is written

@@ -172,6 +172,24 @@ __global__ __launch_bounds__(kRedBlock) void reduce_stage2(const double* __restr
   if (threadIdx.x == 0) *out = v;
 }
 
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(256) void stream_copy_kernel(dbl2* __restrict__ b,
+                                                          const dbl2* __restrict__ a, int64_t n2) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2;
+       i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = a[i];
+}
+
+__global__ __launch_bounds__(256) void stream_triad_kernel(dbl2* __restrict__ c,
+                                                           const dbl2* __restrict__ a,
+                                                           const dbl2* __restrict__ b, double s,
+                                                           int64_t n2) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2;
+       i += (int64_t)gridDim.x * blockDim.x)
+    c[i] = a[i] + s * b[i];
+}
+
 unsigned grid_stride_blocks(int64_t n, int block) {
   int64_t b = (n + block - 1) / block;
   if (b > 256 * 16) b = 256 * 16;
@@ -230,6 +248,23 @@ void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int6
       break;
     default: RMA_CHECK_ARG(false, "unsupported element size " << elem_bytes);
   }
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+void stream_copy_gpu(double* b, const double* a, int64_t n, stream_t stream) {
+  RMA_CHECK_ARG(n % 2 == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0,
+                "stream_copy needs even n and 16-byte aligned buffers");
+  stream_copy_kernel<<<256 * 8, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+void stream_triad_gpu(double* c, const double* a, const double* b, double s, int64_t n,
+                      stream_t stream) {
+  RMA_CHECK_ARG(n % 2 == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+                                reinterpret_cast<uintptr_t>(c)) & 15) == 0,
+                "stream_triad needs even n and 16-byte aligned buffers");
+  stream_triad_kernel<<<256 * 8, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
+                                                               (const dbl2*)b, s, n / 2);
   RMA_HIP_LAUNCH_CHECK();
 }
 

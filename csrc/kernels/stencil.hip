@@ -39,7 +39,6 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
-constexpr int kUnroll = 4;
 typedef double dbl2 __attribute__((ext_vector_type(2)));  // native 16-byte vector
 
 struct RectList {
@@ -119,7 +118,7 @@ __device__ __forceinline__ void row_update(double (&res)[V], const double (&up)[
   }
 }
 
-template <int V, bool NT>
+template <int V, bool NT, int kUnroll>
 __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restrict__ T2,
                                                                const double* __restrict__ T,
                                                                const double* __restrict__ iCp,
@@ -302,16 +301,25 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
       stencil_lds_kernel<true><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c);
     else
       stencil_lds_kernel<false><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c);
-  } else if (V == 2) {
-    if (tune.nontemporal)
-      stencil_march_kernel<2, true><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, tune.chunk_rows);
-    else
-      stencil_march_kernel<2, false><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, tune.chunk_rows);
   } else {
-    if (tune.nontemporal)
-      stencil_march_kernel<1, true><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, tune.chunk_rows);
-    else
-      stencil_march_kernel<1, false><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, tune.chunk_rows);
+    const int u = tune.unroll;
+    RMA_CHECK_ARG(u == 1 || u == 2 || u == 4 || u == 8, "unroll must be 1, 2, 4 or 8");
+#define RMA_MARCH(VV, NTT, UU)                                                           \
+  stencil_march_kernel<VV, NTT, UU><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, tune.chunk_rows)
+#define RMA_MARCH_U(VV, NTT)          \
+  switch (u) {                        \
+    case 1: RMA_MARCH(VV, NTT, 1); break; \
+    case 2: RMA_MARCH(VV, NTT, 2); break; \
+    case 8: RMA_MARCH(VV, NTT, 8); break; \
+    default: RMA_MARCH(VV, NTT, 4); break; \
+  }
+    if (V == 2) {
+      if (tune.nontemporal) { RMA_MARCH_U(2, true) } else { RMA_MARCH_U(2, false) }
+    } else {
+      if (tune.nontemporal) { RMA_MARCH_U(1, true) } else { RMA_MARCH_U(1, false) }
+    }
+#undef RMA_MARCH_U
+#undef RMA_MARCH
   }
   RMA_HIP_LAUNCH_CHECK();
 }

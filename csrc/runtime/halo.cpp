@@ -17,7 +17,7 @@ PlaneView plane_view(const HaloField& f, int dim, int64_t i0) {
   }
 }
 
-HaloExchanger::HaloExchanger(RcclComm* comm, int self_rank,
+HaloExchanger::HaloExchanger(P2PTransport* comm, int self_rank,
                              std::array<std::array<int, 2>, 3> neighbors)
     : comm_(comm), self_(self_rank), nbr_(neighbors) {
   for (int d = 0; d < 3; ++d)
@@ -83,7 +83,7 @@ void HaloExchanger::prepare(const std::vector<HaloField>& fields, int dims_mask)
       const size_t bytes = (size_t)v.elems() * f.elem_bytes;
       for (int s = 0; s < 2; ++s) {
         const int p = nbr_[d][s];
-        if (p < 0 || p == self_ || v.contiguous()) continue;
+        if (p < 0 || (p == self_ && !self_via_comm_) || v.contiguous()) continue;
         buffer(slot++, bytes);  // send
         buffer(slot++, bytes);  // recv
       }
@@ -122,7 +122,7 @@ void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stre
       for (int s = 0; s < 2; ++s) {
         const int p = nbr_[d][s];
         if (p < 0) continue;
-        if (p == self_) {
+        if (p == self_ && !self_via_comm_) {
           // periodic, single process along d: my side-s halo <- my opposite send plane
           const PlaneView& src = send_v[1 - s];
           const PlaneView& dst = recv_v[s];

@@ -32,7 +32,7 @@ def run(n: int = 4, transport: str = "auto", verbose: bool = True) -> list[float
     dev = C.select_device(local)
     t = _choose_transport(transport, size, dev)
     if t == "rccl":
-        comm = C.RcclComm(dev, key="rma/rccl_uid/smoke")
+        comm = C.RcclComm(dev)
     elif t == "self":
         comm = C.SelfComm()
     else:

@@ -66,6 +66,7 @@ class DiffusionConfig:
     chunk_rows: int = 64
     nontemporal: bool = False
     kernel: str = "march"
+    unroll: int = 4
     use_graph: bool = False
     graph_steps: int = 0
     executor: str = "auto"  # auto | native | python
@@ -141,10 +142,10 @@ class Diffusion2D:
                 int(cfg.use_graph), int(cfg.graph_steps), g.halo,
                 self.qx.data_ptr() if cfg.variant == "kp" else 0,
                 self.qy.data_ptr() if cfg.variant == "kp" else 0,
-                self.dTdt.data_ptr() if cfg.variant == "kp" else 0)
+                self.dTdt.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll))
         if cfg.variant == "perf_hide":
             self.frame_rects, self.interior = ops.hide_rects(nx, ny, *cfg.b_width)
-        self.tuning = ops.StencilTuning(cfg.chunk_rows, cfg.nontemporal, cfg.kernel)
+        self.tuning = ops.StencilTuning(cfg.chunk_rows, cfg.nontemporal, cfg.kernel, cfg.unroll)
 
     # ------------------------------------------------------------------
     def geometry(self, A_shape=None) -> ops.TileGeometry:

@@ -45,6 +45,7 @@ class StencilTuning:
     chunk_rows: int = 64
     nontemporal: bool = False
     kernel: str = "march"
+    unroll: int = 4
 
 
 @dataclass
@@ -147,7 +148,7 @@ def stencil_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: Ste
     if T.is_cuda:
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                tn.chunk_rows, int(tn.nontemporal), KERNELS[tn.kernel],
-                               stream_handle(T), True)
+                               stream_handle(T), True, tn.unroll)
     elif _use_native_cpu():
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                64, 0, 0, 0, False)

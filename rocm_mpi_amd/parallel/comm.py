@@ -175,28 +175,45 @@ def _gloo_group():
     return _gloo_pg
 
 
+_rccl_generation = 0
+
+
 class RcclComm(Communicator):
-    """GPU-direct RCCL communicator (native), bootstrapped through the store."""
+    """GPU-direct RCCL communicator (native), bootstrapped through the store.
+
+    Every rank creates its communicators in the same order, so a per-process
+    generation counter gives all ranks the same store key for the unique id
+    of the n-th communicator (re-initialising a grid never reads a stale id).
+    """
 
     name = "rccl"
 
     def __init__(self, device: torch.device, timeout_s: float = DEFAULT_TIMEOUT_S,
                  store=None, rank: int | None = None, size: int | None = None,
-                 key: str = "rma/rccl_uid/0"):
+                 key: str | None = None):
         from .._native import native
 
+        global _rccl_generation
+        if key is None:
+            key = f"rma/rccl_uid/{_rccl_generation}"
+            _rccl_generation += 1
+
         n = native()
-        if store is None:
-            store = dist.distributed_c10d._get_default_store()
-        self.rank = dist.get_rank() if rank is None else rank
-        self.size = dist.get_world_size() if size is None else size
+        standalone = not dist.is_initialized()
+        self.rank = (0 if standalone else dist.get_rank()) if rank is None else rank
+        self.size = (1 if standalone else dist.get_world_size()) if size is None else size
         self.device = torch.device(device)
         self.timeout_s = timeout_s
-        if self.rank == 0:
-            uid = n.RcclComm.unique_id()
-            store.set(key, uid)
+        if self.size == 1 and store is None:
+            uid = n.RcclComm.unique_id()  # single rank: nothing to distribute
         else:
-            uid = store.get(key)
+            if store is None:
+                store = dist.distributed_c10d._get_default_store()
+            if self.rank == 0:
+                uid = n.RcclComm.unique_id()
+                store.set(key, uid)
+            else:
+                uid = store.get(key)
         n.set_rank_for_errors(self.rank)
         self._c = n.RcclComm(self.size, self.rank, bytes(uid), self.device.index or 0)
         self._scratch = torch.zeros(2, dtype=torch.float64, device=self.device)
@@ -285,6 +302,16 @@ class LoopbackHub:
         self._lock = threading.Lock()
         self._barrier = threading.Barrier(size)
         self._slots: list = [None] * size
+        self._native = None
+
+    def native_hub(self):
+        """Shared native hub for the device loopback transport (GPU halo path)."""
+        with self._lock:
+            if self._native is None:
+                from .._native import native
+
+                self._native = native().LoopbackHub(self.size, self.timeout_s)
+            return self._native
 
     def box(self, src: int, dst: int, tag: int) -> queue.Queue:
         k = (src, dst, tag)

@@ -121,14 +121,19 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
                      device: str | torch.device | None = None, select_device: bool = True,
                      quiet: bool = False, init_dist: bool = True,
                      loopback: tuple | None = None,
-                     timeout_s: float = C.DEFAULT_TIMEOUT_S):
+                     timeout_s: float = C.DEFAULT_TIMEOUT_S,
+                     self_via_transport: bool = False):
     """Create the implicit global grid and return ``(me, dims, nprocs, coords, comm)``.
 
     Mirrors ``ImplicitGlobalGrid.init_global_grid``: MPI-style
     ``Dims_create`` (``nz==1`` forces ``dimz=1``), a row-major Cartesian
     topology (open by default), neighbours by ``Cart_shift``, node-local device
     selection, and the halo transport. ``loopback=(hub, rank)`` creates one
-    logical rank of an in-process group (tests); its grid is thread-local.
+    logical rank of an in-process group (tests); its grid is thread-local and,
+    on a GPU, its halo runs through the native engine over the device loopback
+    transport (the production code path with RCCL swapped for D2D copies).
+    ``self_via_transport`` routes periodic self-neighbours through the P2P
+    transport (exercises RCCL send/recv on a single GPU).
     """
     nxyz = (int(nx), int(ny), int(nz))
     if min(nxyz) < 1:
@@ -198,17 +203,28 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
                    for d in range(3))
 
     halo = None
-    if dev.type == "cuda" and tname in ("rccl", "self"):
+    extra = {}
+    if dev.type == "cuda" and tname in ("rccl", "self", "loopback"):
         from .._native import native
 
-        ncomm = comm.native if isinstance(comm, C.RcclComm) else None
+        if tname == "loopback":
+            ncomm = native().LoopbackEndpoint(hub.native_hub(), me)
+            extra["endpoint"] = ncomm
+            # each logical rank drives its own stream (threads share the default one)
+            stream = torch.cuda.Stream(dev)
+            extra["stream"] = stream
+            torch.cuda.set_stream(stream)
+        else:
+            ncomm = comm.native if isinstance(comm, C.RcclComm) else None
         halo = native().HaloExchanger(ncomm, me, [list(p) for p in neighbors])
+        if self_via_transport:
+            halo.set_self_via_transport(True)
 
     g = GlobalGrid(nxyz=nxyz, nxyz_g=nxyz_g, dims=dims, overlaps=overlaps, halowidths=halowidths,
                    periods=periods, nprocs=comm_size, me=me, coords=coords, neighbors=neighbors,
                    disp=disp, reorder=reorder, comm=comm, device=dev, transport=tname,
                    quiet=quiet, local_rank=local_rank, local_size=local_size, owns_dist=owns_dist,
-                   halo=halo, topo=topo)
+                   halo=halo, topo=topo, extra=extra)
     _set_grid(g, thread_local)
     if not quiet and me == 0:
         print(g.describe(), flush=True)

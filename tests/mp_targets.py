@@ -47,3 +47,20 @@ def collectives(rank, world, outdir):
     t = gg.toc()
     np.save(os.path.join(outdir, f"coll{rank}.npy"), np.array([s, mx, t, nprocs] + list(dims)))
     gg.finalize_global_grid()
+
+
+def diffusion_gpu(rank, world, outdir, variant, nx, ny, nt, dims):
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    m = Diffusion2D(DiffusionConfig(variant=variant, nx=nx, ny=ny, nt=nt, dims=tuple(dims) + (0,),
+                                    quiet=True, init="gaussian", init_on="host", b_width=(4, 2),
+                                    device="cuda:0"))
+    m.step(nt)
+    Tv = m.gather_interior()
+    g = gg.global_grid()
+    if g.me == 0:
+        np.save(os.path.join(outdir, "Tv.npy"), Tv.numpy())
+        with open(os.path.join(outdir, "meta.txt"), "w") as f:
+            f.write(f"{g.nxyz_g[0]} {g.nxyz_g[1]} {g.transport}")
+    m.close()
