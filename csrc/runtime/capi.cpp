@@ -1,0 +1,264 @@
+// C ABI implementation (see rma/capi.h).
+#include "rma/capi.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "rma/comm.h"
+#include "rma/executor.h"
+#include "rma/halo.h"
+#include "rma/hip_check.h"
+#include "rma/kernels.h"
+#include "rma/topology.h"
+
+struct rma_grid {
+  int nprocs = 1, me = 0, device = 0;
+  std::array<int, 3> nxyz{1, 1, 1}, dims{1, 1, 1}, periods{0, 0, 0}, overlaps{2, 2, 2},
+      hw{1, 1, 1}, coords{0, 0, 0};
+  std::array<int64_t, 3> nxyz_g{1, 1, 1};
+  std::unique_ptr<rma::CartTopology> topo;
+  std::unique_ptr<rma::RcclComm> comm;
+  std::unique_ptr<rma::HaloExchanger> halo;
+  std::chrono::steady_clock::time_point t0;
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <typename F>
+int guard(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return 1;
+  }
+}
+
+double coord(const rma_grid* g, int d, int64_t ix, double dd, int64_t size_A) {
+  const double x0 = 0.5 * (double)(g->nxyz[d] - size_A) * dd;
+  double x = (double)((int64_t)g->coords[d] * (g->nxyz[d] - g->overlaps[d]) + ix) * dd + x0;
+  if (g->periods[d]) {
+    const int64_t n = g->nxyz_g[d];
+    x = x - dd;
+    if (x > (double)(n - 1) * dd) x = x - (double)n * dd;
+    if (x < 0) x = x + (double)n * dd;
+  }
+  return x;
+}
+}  // namespace
+
+extern "C" {
+
+const char* rma_last_error(void) { return g_err.c_str(); }
+
+int rma_unique_id(char out[128]) {
+  return guard([&] {
+    const std::string id = rma::RcclComm::unique_id();
+    RMA_CHECK_ARG(id.size() <= 128, "unique id too large");
+    std::memset(out, 0, 128);
+    std::memcpy(out, id.data(), id.size());
+  });
+}
+
+int rma_init_global_grid(int nx, int ny, int nz, const int dims[3], const int periods[3],
+                         const int overlaps[3], const int halowidths[3], int nprocs, int rank,
+                         const char* unique_id, int device, rma_grid** out_grid, int* out_me,
+                         int out_dims[3], int out_coords[3]) {
+  return guard([&] {
+    RMA_CHECK_ARG(out_grid != nullptr, "out_grid is NULL");
+    auto g = std::make_unique<rma_grid>();
+    g->nxyz = {nx, ny, nz};
+    g->nprocs = nprocs;
+    g->me = rank;
+    g->device = device;
+    std::array<int, 3> din{0, 0, 0};
+    for (int d = 0; d < 3; ++d) {
+      din[d] = dims ? dims[d] : 0;
+      g->periods[d] = periods ? periods[d] : 0;
+      g->overlaps[d] = overlaps ? overlaps[d] : 2;
+      g->hw[d] = halowidths ? halowidths[d] : std::max(1, g->overlaps[d] / 2);
+      if (g->nxyz[d] == 1) din[d] = 1;
+    }
+    g->dims = rma::dims_create(nprocs, din);
+    g->topo = std::make_unique<rma::CartTopology>(nprocs, g->dims, g->periods);
+    g->coords = g->topo->coords(rank);
+    for (int d = 0; d < 3; ++d)
+      g->nxyz_g[d] = g->nxyz[d] == 1 ? 1
+                                     : (int64_t)g->dims[d] * (g->nxyz[d] - g->overlaps[d]) +
+                                           (g->periods[d] ? 0 : g->overlaps[d]);
+    RMA_HIP_CHECK(hipSetDevice(device));
+    if (nprocs > 1) {
+      RMA_CHECK_ARG(unique_id != nullptr, "unique_id required when nprocs > 1");
+      g->comm = std::make_unique<rma::RcclComm>(nprocs, rank, std::string(unique_id, 128), device);
+    }
+    rma::set_rank_for_errors(rank);
+    g->halo = std::make_unique<rma::HaloExchanger>(g->comm.get(), rank, g->topo->neighbors(rank));
+    if (out_me) *out_me = rank;
+    for (int d = 0; d < 3; ++d) {
+      if (out_dims) out_dims[d] = g->dims[d];
+      if (out_coords) out_coords[d] = g->coords[d];
+    }
+    *out_grid = g.release();
+  });
+}
+
+int rma_finalize_global_grid(rma_grid* g) {
+  return guard([&] {
+    if (!g) return;
+    g->halo.reset();
+    g->comm.reset();
+    delete g;
+  });
+}
+
+int64_t rma_nx_g(const rma_grid* g) { return g->nxyz_g[0]; }
+int64_t rma_ny_g(const rma_grid* g) { return g->nxyz_g[1]; }
+int64_t rma_nz_g(const rma_grid* g) { return g->nxyz_g[2]; }
+double rma_x_g(const rma_grid* g, int64_t ix, double dx, int64_t s) { return coord(g, 0, ix, dx, s); }
+double rma_y_g(const rma_grid* g, int64_t iy, double dy, int64_t s) { return coord(g, 1, iy, dy, s); }
+double rma_z_g(const rma_grid* g, int64_t iz, double dz, int64_t s) { return coord(g, 2, iz, dz, s); }
+
+int rma_neighbors(const rma_grid* g, int out[6]) {
+  return guard([&] {
+    const auto nb = g->topo->neighbors(g->me);
+    for (int d = 0; d < 3; ++d) {
+      out[2 * d] = nb[d][0];
+      out[2 * d + 1] = nb[d][1];
+    }
+  });
+}
+
+int rma_update_halo(rma_grid* g, int nfields, void* const* fields, const int64_t* sizes,
+                    const int* elem_bytes, void* stream) {
+  return guard([&] {
+    std::vector<rma::HaloField> fs;
+    for (int i = 0; i < nfields; ++i) {
+      rma::HaloField f;
+      f.ptr = fields[i];
+      f.elem_bytes = elem_bytes ? elem_bytes[i] : 8;
+      for (int d = 0; d < 3; ++d) {
+        f.size[d] = sizes[3 * i + d];
+        // staggered arrays: overlap of this array = ol + (size(A) - n)
+        f.ol[d] = g->overlaps[d] + (f.size[d] - g->nxyz[d]);
+        f.hw[d] = g->hw[d];
+      }
+      fs.push_back(f);
+    }
+    g->halo->exchange(fs, stream, 7);
+  });
+}
+
+int rma_gather(rma_grid* g, const void* sendbuf, void* recvbuf, size_t bytes, int root,
+               void* stream) {
+  return guard([&] {
+    if (g->comm) {
+      g->comm->gather(sendbuf, recvbuf, bytes, root, stream);
+    } else {
+      RMA_HIP_CHECK(hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDefault,
+                                   rma::as_stream(stream)));
+    }
+  });
+}
+
+int rma_tic(rma_grid* g, void* stream) {
+  return guard([&] {
+    if (g->comm)
+      g->comm->barrier(stream, 300.0);
+    else
+      RMA_HIP_CHECK(hipStreamSynchronize(rma::as_stream(stream)));
+    g->t0 = std::chrono::steady_clock::now();
+  });
+}
+
+int rma_toc(rma_grid* g, void* stream, double* seconds) {
+  return guard([&] {
+    if (g->comm)
+      g->comm->barrier(stream, 300.0);
+    else
+      RMA_HIP_CHECK(hipStreamSynchronize(rma::as_stream(stream)));
+    *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - g->t0).count();
+  });
+}
+
+int rma_diffusion_step(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                       const double coef[4], void* stream) {
+  return guard([&] {
+    const rma::Rect r{1, nx - 1, 1, ny - 1};
+    const rma::StencilCoef c{coef[0], coef[1], coef[2], coef[3]};
+    rma::stencil_rects_gpu(T2, T, iCp, nx, ny, &r, 1, c, rma::StencilTuning{}, stream);
+  });
+}
+
+namespace {
+rma::TileGeom geom(const rma_grid* g, int64_t nx, int64_t ny, double dx, double dy) {
+  rma::TileGeom t;
+  t.gx0 = (int64_t)g->coords[0] * (g->nxyz[0] - g->overlaps[0]);
+  t.gy0 = (int64_t)g->coords[1] * (g->nxyz[1] - g->overlaps[1]);
+  t.nxg = g->nxyz_g[0];
+  t.nyg = g->nxyz_g[1];
+  t.dx = dx;
+  t.dy = dy;
+  t.xoff = 0.5 * (double)(g->nxyz[0] - nx) * dx;
+  t.yoff = 0.5 * (double)(g->nxyz[1] - ny) * dy;
+  t.periodx = g->periods[0];
+  t.periody = g->periods[1];
+  return t;
+}
+}  // namespace
+
+struct rma_executor {
+  std::unique_ptr<rma::DiffusionExecutor> ex;
+};
+
+int rma_init_gaussian(rma_grid* g, double* T, int64_t nx, int64_t ny, double dx, double dy,
+                      double lx, double ly, void* stream) {
+  return guard([&] { rma::init_gaussian_gpu(T, nx, ny, geom(g, nx, ny, dx, dy), lx, ly, stream); });
+}
+
+int rma_init_random(rma_grid* g, double* A, int64_t nx, int64_t ny, double dx, double dy,
+                    uint64_t seed, void* stream) {
+  return guard(
+      [&] { rma::init_random_gpu(A, nx, ny, geom(g, nx, ny, dx, dy), seed, 0.0, 1.0, stream); });
+}
+
+int rma_fill(double* A, int64_t n, double value, void* stream) {
+  return guard([&] { rma::fill_gpu(A, n, value, stream); });
+}
+
+int rma_executor_create(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
+                        int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
+                        double* qx, double* qy, double* dTdt, rma_executor** out) {
+  return guard([&] {
+    RMA_CHECK_ARG(out && mode >= 0 && mode <= 2, "bad executor arguments");
+    rma::ExecParams p;
+    p.mode = static_cast<rma::Mode>(mode);
+    p.coef = {coef[0], coef[1], coef[2], coef[3]};
+    p.bwx = bwx;
+    p.bwy = bwy;
+    auto e = std::make_unique<rma_executor>();
+    e->ex = std::make_unique<rma::DiffusionExecutor>(T, T2, iCp, nx, ny, p, g->halo.get(), qx, qy,
+                                                     dTdt);
+    *out = e.release();
+  });
+}
+
+int rma_executor_run(rma_executor* e, int64_t nsteps, void* stream) {
+  return guard([&] { e->ex->run(nsteps, stream); });
+}
+
+int rma_executor_parity(const rma_executor* e) { return e->ex->parity(); }
+
+int rma_executor_destroy(rma_executor* e) {
+  return guard([&] { delete e; });
+}
+
+}  // extern "C"

@@ -35,12 +35,21 @@ PKG = ROOT / "rocm_mpi_amd"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RMA_OFFLOAD_ARCH", "gfx950")
 
+# librma_core.so: every kernel + the runtime + the C ABI (usable without Python)
 HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "runtime").glob("*.cpp"))
-HOST_SOURCES = sorted(p for p in (CSRC / "kernels").glob("*.cpp")) + [CSRC / "bindings" / "module.cpp"]
+CORE_HOST_SOURCES = sorted((CSRC / "kernels").glob("*.cpp"))
+# _C*.so: the pybind11 bindings, linked against librma_core.so ($ORIGIN rpath)
+BIND_SOURCES = [CSRC / "bindings" / "module.cpp"]
+HOST_SOURCES = CORE_HOST_SOURCES + BIND_SOURCES
+EXAMPLES = sorted((ROOT / "examples").glob("*.cpp"))
 
 
 def ext_path() -> Path:
     return PKG / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def core_path() -> Path:
+    return PKG / "librma_core.so"
 
 
 def _pybind_include() -> str:
@@ -106,19 +115,44 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             for src in ex.map(run, todo):
                 print(f"[rocm_mpi_amd build] compiled {src.relative_to(ROOT)}", flush=True)
-    out = ext_path()
-    if todo or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
-        tmp = out.with_suffix(".tmp.so")
-        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs),
-               "-o", str(tmp), f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64", "-ldl", "-lpthread",
-               f"-Wl,-rpath,{ROCM / 'lib'}"]
+    core = core_path()
+    core_objs = [o for o, src in zip(objs, HIP_SOURCES + HOST_SOURCES) if src not in BIND_SOURCES]
+    bind_objs = [o for o, src in zip(objs, HIP_SOURCES + HOST_SOURCES) if src in BIND_SOURCES]
+
+    def newer(target: Path, deps) -> bool:
+        return not target.exists() or any(d.stat().st_mtime > target.stat().st_mtime for d in deps)
+
+    def link(target: Path, cmd: list[str]) -> None:
+        tmp = target.with_suffix(".tmp.so")
+        full = cmd + ["-o", str(tmp)]
         if verbose:
-            print(" ".join(cmd), flush=True)
-        r = subprocess.run(cmd, capture_output=True, text=True)
+            print(" ".join(full), flush=True)
+        r = subprocess.run(full, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, out)
-        print(f"[rocm_mpi_amd build] linked {out.relative_to(ROOT)}", flush=True)
+            raise RuntimeError(f"link failed\n{' '.join(full)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, target)
+        print(f"[rocm_mpi_amd build] linked {target.relative_to(ROOT)}", flush=True)
+
+    if newer(core, core_objs):
+        link(core, [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, core_objs),
+                    "-Wl,-soname,librma_core.so", f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64",
+                    "-ldl", "-lpthread", f"-Wl,-rpath,{ROCM / 'lib'}"])
+    out = ext_path()
+    if newer(out, bind_objs + [core]):
+        link(out, ["g++", "-shared", "-fPIC", *map(str, bind_objs), f"-L{PKG}", "-lrma_core",
+                   "-Wl,-rpath,$ORIGIN"])
+    exdir = ROOT / "build" / "examples"
+    for src in EXAMPLES:
+        exe = exdir / src.stem
+        if newer(exe, [src, core]) or newest_header > exe.stat().st_mtime:
+            exdir.mkdir(parents=True, exist_ok=True)
+            cmd = [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", *COMMON, str(src), "-o",
+                   str(exe), f"-L{PKG}", "-lrma_core", f"-Wl,-rpath,{PKG}",
+                   f"-L{ROCM / 'lib'}", "-lamdhip64", f"-Wl,-rpath,{ROCM / 'lib'}"]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"example build failed: {src}\n{r.stdout}\n{r.stderr}")
+            print(f"[rocm_mpi_amd build] built {exe.relative_to(ROOT)}", flush=True)
     return out
 
 

@@ -1,0 +1,148 @@
+"""Shared command line of the diffusion entry points.
+
+The reference hard-codes its parameters per script (e.g.
+``scripts/diffusion_2D_perf.jl:17-25``) and selects the variant by
+(un)commenting ``scripts/runme.sh:5-9``. Every entry point here keeps the
+reference's defaults and exposes them as flags, plus the BASELINE.json
+configurations as named presets (``--preset``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+
+# Reference defaults per script.
+DEFAULTS = {
+    "ap": dict(nx=128, ny=128, nt=1000, do_vis=True),                      # ap.jl:15-16
+    "kp": dict(nx=128, ny=128, nt=1000, do_vis=True),                      # kp.jl:62-65
+    "perf": dict(nx=12 * 1024, ny=12 * 1024, nt=1000, do_vis=False),       # perf.jl:21-25
+    "perf_hide": dict(nx=12 * 1024, ny=12 * 1024, nt=100, b_width=(32, 4),  # perf_hide.jl:37-43
+                      do_vis=False),
+    "perf_hide_prof": dict(nx=8 * 1024, ny=8 * 1024, nt=300, b_width=(32, 8),  # _prof.jl:71-77
+                           do_vis=False, profile=True),
+}
+
+# BASELINE.json "configs", in order.
+PRESETS = {
+    "ap256_cpu": dict(variant="ap", nx=256, ny=256, nt=1000, device="cpu"),
+    "kp16k": dict(variant="kp", nx=16384, ny=16384, nt=1000),
+    "perf_2x1": dict(variant="perf", nx=16384, ny=16384, nt=1000, dims=(2, 1, 0)),
+    "hide_2x2": dict(variant="perf_hide", nx=16384, ny=16384, nt=1000, dims=(2, 2, 0)),
+    "hide_4x2_288GB": dict(variant="perf_hide", auto_size=True, nt=1000, dims=(4, 2, 0)),
+}
+
+
+def _pair(s: str) -> tuple:
+    return tuple(int(v) for v in s.split(","))
+
+
+def build_parser(variant: str) -> argparse.ArgumentParser:
+    d = DEFAULTS[variant]
+    ap = argparse.ArgumentParser(
+        prog=f"diffusion_2D_{variant}",
+        description=f"2D heat diffusion, {variant} variant (reference "
+                    f"scripts/diffusion_2D_{variant}.jl) on MI355X")
+    ap.add_argument("--preset", choices=sorted(PRESETS), help="a BASELINE.json configuration")
+    ap.add_argument("--nx", type=int, default=d["nx"], help="local grid points in x (halo incl.)")
+    ap.add_argument("--ny", type=int, default=d["ny"])
+    ap.add_argument("--nt", type=int, default=d["nt"], help="time steps (first 10 untimed)")
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--b-width", type=_pair, default=d.get("b_width", (32, 4)))
+    ap.add_argument("--dims", type=_pair, default=(0, 0), help="process grid dimx,dimy")
+    ap.add_argument("--periods", type=_pair, default=(0, 0))
+    ap.add_argument("--init", choices=["gaussian", "random"], default="gaussian")
+    ap.add_argument("--init-on", choices=["auto", "device", "host"], default="auto")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--transport", default=os.environ.get("RMA_TRANSPORT", "auto"),
+                    choices=["auto", "rccl", "staged", "gloo", "self"])
+    ap.add_argument("--device", default=None, help="cpu, cuda, cuda:N (default: one GPU per rank)")
+    ap.add_argument("--vis", dest="do_vis", action="store_true", default=d["do_vis"])
+    ap.add_argument("--no-vis", dest="do_vis", action="store_false")
+    ap.add_argument("--outdir", default="output")
+    ap.add_argument("--profile", action="store_true", default=d.get("profile", False))
+    ap.add_argument("--auto-size", action="store_true",
+                    help="size the local tile to fill --hbm-frac of free HBM (288 GB MI355X)")
+    ap.add_argument("--hbm-frac", type=float, default=0.80)
+    ap.add_argument("--chunk-rows", type=int, default=64)
+    ap.add_argument("--unroll", type=int, default=4)
+    ap.add_argument("--kernel", choices=["march", "lds"], default="march")
+    ap.add_argument("--nontemporal", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
+    ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf guard period")
+    ap.add_argument("--checkpoint", default="", help="save the final state to this directory")
+    ap.add_argument("--resume", default="", help="start from a checkpoint directory")
+    ap.add_argument("--json", action="store_true", help="print the run record as JSON (rank 0)")
+    ap.add_argument("--quiet", action="store_true")
+    return ap
+
+
+def auto_tile(frac: float) -> int:
+    import torch
+
+    if not torch.cuda.is_available():
+        raise RuntimeError("--auto-size needs a GPU")
+    free, _ = torch.cuda.mem_get_info()
+    return max(512, int(math.isqrt(int(frac * free / 24.0))) // 256 * 256)
+
+
+def run_variant(variant: str, argv=None) -> int:
+    from ..models import Diffusion2D, DiffusionConfig
+    from ..parallel import comm as C
+    from ..utils import checkpoint as ckpt
+
+    a = build_parser(variant).parse_args(argv)
+    base = "perf_hide" if variant == "perf_hide_prof" else variant
+    opts = dict(variant=base, nx=a.nx, ny=a.ny, nt=a.nt, warmup=a.warmup, b_width=a.b_width,
+                init=a.init, init_on=a.init_on, seed=a.seed, dims=tuple(a.dims) + (0,),
+                periods=tuple(a.periods) + (0,), transport=a.transport, device=a.device,
+                chunk_rows=a.chunk_rows, unroll=a.unroll, kernel=a.kernel,
+                nontemporal=a.nontemporal, use_graph=a.graph, do_vis=a.do_vis, outdir=a.outdir,
+                profile=a.profile, check_every=a.check_every, quiet=a.quiet)
+    auto = a.auto_size
+    if a.preset:
+        p = dict(PRESETS[a.preset])
+        auto = p.pop("auto_size", False) or auto
+        opts.update(p)
+    if auto:
+        rank, size, _ = C.env_world()
+        if size > 1:
+            C.init_distributed()
+        local, _ = C.node_local_rank(rank, size)
+        C.select_device(local)
+        n = auto_tile(a.hbm_frac)
+        if size > 1:
+            import torch
+            import torch.distributed as dist
+
+            t = torch.tensor([n], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=C._gloo_group())
+            n = int(t.item())
+        opts["nx"] = opts["ny"] = n
+    cfg = DiffusionConfig(**opts)
+    model = Diffusion2D(cfg)
+    if variant == "perf_hide_prof":  # warm-up call before the profiled run (_prof.jl:110)
+        model.step(12)
+        model.synchronize()
+    if a.resume:
+        ckpt.load_checkpoint(model, a.resume)
+    res = model.run()
+    if a.checkpoint:
+        ckpt.save_checkpoint(model, a.checkpoint)
+    if a.json and model.g.me == 0:
+        print(res.to_json(), flush=True)
+    model.close()
+    return 0
+
+
+def main_for(variant: str):
+    def _main(argv=None) -> int:
+        return run_variant(variant, argv)
+
+    return _main
+
+
+if __name__ == "__main__":
+    sys.exit(run_variant(sys.argv[1], sys.argv[2:]))

@@ -1,0 +1,13 @@
+"""Entry point mirroring scripts/diffusion_2D_kp.jl of the reference.
+
+    python -m rocm_mpi_amd.apps.diffusion_2D_kp [--help]
+    python -m rocm_mpi_amd.launch -n 4 -m rocm_mpi_amd.apps.diffusion_2D_kp
+"""
+import sys
+
+from .cli import main_for
+
+main = main_for("kp")
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -419,11 +419,23 @@ def node_local_rank(comm_rank: int, comm_size: int) -> tuple[int, int]:
     return same.index(comm_rank), len(same)
 
 
+def visible_devices() -> int:
+    """Number of visible GPUs. torch.cuda.device_count() goes through amdsmi on
+    ROCm and was observed to return 0 from worker threads on the GPU box while
+    the HIP runtime sees the device; fall back to the runtime's own count."""
+    n = torch.cuda.device_count()
+    if n <= 0 and torch.cuda.is_available():
+        n = torch._C._cuda_getDeviceCount()
+    return n
+
+
 def select_device(local_rank: int) -> torch.device:
     """One GPU per process: device = local_rank mod visible devices."""
     if not torch.cuda.is_available():
         return torch.device("cpu")
-    n = torch.cuda.device_count()
+    n = visible_devices()
+    if n <= 0:
+        raise RuntimeError("torch reports a GPU but no visible device")
     dev = torch.device("cuda", local_rank % n)
     torch.cuda.set_device(dev)
     return dev

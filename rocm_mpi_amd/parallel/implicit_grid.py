@@ -177,7 +177,7 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
         dev = torch.device(device)
         if dev.type == "cuda":
             if dev.index is None:
-                dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+                dev = torch.device("cuda", local_rank % max(1, C.visible_devices()))
             torch.cuda.set_device(dev)
     elif select_device and torch.cuda.is_available():
         dev = C.select_device(local_rank)
