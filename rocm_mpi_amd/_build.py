@@ -73,10 +73,12 @@ def _hip_cmd(src: Path, obj: Path) -> list[str]:
 
 
 def _host_cmd(src: Path, obj: Path) -> list[str]:
-    py_inc = sysconfig.get_paths()["include"]
     cxx = os.environ.get("CXX", "g++")
-    return [cxx, *COMMON, "-fvisibility=hidden", f"-I{_pybind_include()}", f"-I{py_inc}",
-            "-c", str(src), "-o", str(obj)]
+    if src in BIND_SOURCES:  # pybind11 module: hide everything but PyInit__C
+        py_inc = sysconfig.get_paths()["include"]
+        return [cxx, *COMMON, "-fvisibility=hidden", f"-I{_pybind_include()}", f"-I{py_inc}",
+                "-c", str(src), "-o", str(obj)]
+    return [cxx, *COMMON, "-c", str(src), "-o", str(obj)]
 
 
 def _stale(src: Path, obj: Path, newest_header: float) -> bool:
