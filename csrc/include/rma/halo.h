@@ -60,6 +60,7 @@ class HaloExchanger {
   void prepare(const std::vector<HaloField>& fields, int dims_mask = 7);
 
   bool active(int dim) const;  // any neighbour in this dim?
+  bool capturable() const { return comm_ == nullptr || comm_->capturable(); }
   // Route self-neighbours (periodic, one process along a dim) through the
   // transport instead of a local copy (tests the P2P path on one GPU).
   void set_self_via_transport(bool on) { self_via_comm_ = on && comm_ != nullptr; }

@@ -59,6 +59,7 @@ class LoopbackEndpoint : public P2PTransport {
   void group_end() override;
   void send(const void* buf, size_t bytes, int peer, stream_t stream) override;
   void recv(void* buf, size_t bytes, int peer, stream_t stream) override;
+  bool capturable() const override { return false; }
 
  private:
   struct Op {

@@ -27,6 +27,9 @@ class P2PTransport {
   virtual void group_end() = 0;
   virtual void send(const void* buf, size_t bytes, int peer, stream_t stream) = 0;
   virtual void recv(void* buf, size_t bytes, int peer, stream_t stream) = 0;
+  // Can a group be recorded by hipStreamBeginCapture and replayed later?
+  // (RCCL: yes; the loopback transport synchronises on the host: no.)
+  virtual bool capturable() const { return true; }
 };
 
 }  // namespace rma

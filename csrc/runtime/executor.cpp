@@ -26,6 +26,9 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   RMA_CHECK_ARG(T && iCp, "null field");
   RMA_CHECK_ARG(p.mode == Mode::kKp || T2 != nullptr, "T2 required");
   RMA_CHECK_ARG(p.mode != Mode::kKp || (qx && qy && dTdt), "kp needs qx, qy, dTdt");
+  RMA_CHECK_ARG(!p.use_graph || !halo || halo->capturable(),
+                "hipGraph replay needs a capturable halo transport (RCCL or none); the loopback "
+                "transport synchronises on the host");
   full_ = {1, nx - 1, 1, ny - 1};
   if (p.mode == Mode::kHide) {
     RMA_CHECK_ARG(p.bwx >= 1 && p.bwy >= 1,
@@ -156,16 +159,27 @@ void DiffusionExecutor::build_graph(int64_t steps) {
   const int saved_parity = parity_;
   const int64_t saved_steps = steps_;
   RMA_HIP_CHECK(hipStreamBeginCapture(lo, hipStreamCaptureModeThreadLocal));
-  // fork hi into the capture
-  RMA_HIP_CHECK(hipEventRecord(E(e_in_), lo));
-  RMA_HIP_CHECK(hipStreamWaitEvent(hi, E(e_in_), 0));
-  RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
-  RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
-  run_eager(steps);
-  // join hi back
-  RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
-  RMA_HIP_CHECK(hipStreamWaitEvent(lo, E(e_hi_), 0));
-  hipGraph_t g;
+  hipGraph_t g = nullptr;
+  try {
+    // fork hi into the capture
+    RMA_HIP_CHECK(hipEventRecord(E(e_in_), lo));
+    RMA_HIP_CHECK(hipStreamWaitEvent(hi, E(e_in_), 0));
+    RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
+    RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
+    run_eager(steps);
+    // join hi back
+    RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
+    RMA_HIP_CHECK(hipStreamWaitEvent(lo, E(e_hi_), 0));
+  } catch (...) {
+    // never leave a stream capturing: it would poison every later sync call
+    hipGraph_t junk = nullptr;
+    (void)hipStreamEndCapture(lo, &junk);
+    if (junk) (void)hipGraphDestroy(junk);
+    (void)hipGetLastError();
+    parity_ = saved_parity;
+    steps_ = saved_steps;
+    throw;
+  }
   RMA_HIP_CHECK(hipStreamEndCapture(lo, &g));
   hipGraphExec_t ge;
   RMA_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));

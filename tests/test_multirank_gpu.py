@@ -52,23 +52,31 @@ def test_loopback_gpu_reference_oracle():
     assert np.array_equal(Tv, golden.run(254, 254, 1000)[1:-1, 1:-1])
 
 
-def test_loopback_gpu_periodic_and_graph():
+def test_loopback_gpu_periodic():
     a = run_loopback(4, spmd, "perf_hide", 200, 100, 30, (2, 2), periods=(1, 1, 0),
-                     init="random", graph=True)[0][0]
+                     init="random")[0][0]
     b = run_loopback(4, spmd, "perf", 200, 100, 30, (2, 2), periods=(1, 1, 0),
                      init="random")[0][0]
     assert np.array_equal(a, b)
 
 
-def test_rccl_self_send_periodic():
-    """Single rank, periodic: halo planes travel through RCCL send/recv to self."""
+def test_loopback_rejects_graph_capture():
+    with pytest.raises(AssertionError, match="capturable"):
+        run_loopback(2, spmd, "perf_hide", 200, 100, 8, (2, 1), graph=True, timeout=30)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rccl_self_send_periodic(graph):
+    """Single rank, periodic: halo planes travel through RCCL send/recv to self
+    (optionally captured in a hipGraph and replayed) == local self-copy path."""
     outs = []
     for via in (True, False):
         gg.init_global_grid(300, 200, 1, periodx=1, periody=1, quiet=True, transport="rccl",
                             self_via_transport=via)
         assert gg.global_grid().transport == "rccl"
         m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=300, ny=200, nt=20, quiet=True,
-                                        init="random", periods=(1, 1, 0), b_width=(4, 4)))
+                                        init="random", periods=(1, 1, 0), b_width=(4, 4),
+                                        use_graph=graph and via, graph_steps=6))
         m.step(20)
         outs.append(m.field.cpu().clone())
         m.close()
