@@ -266,6 +266,7 @@ PYBIND11_MODULE(_C, m) {
           },
           py::arg("fields"), py::arg("dims_mask") = 7)
       .def("active", &HaloExchanger::active)
+      .def("capturable", &HaloExchanger::capturable)
       .def("set_self_via_transport", &HaloExchanger::set_self_via_transport)
       .def_property_readonly("neighbors", &HaloExchanger::neighbors)
       .def_property_readonly("bytes_sent_last", &HaloExchanger::bytes_sent_last);

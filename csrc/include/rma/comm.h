@@ -41,6 +41,10 @@ class RcclComm : public P2PTransport {
   void group_end() override;
   void send(const void* buf, size_t bytes, int peer, stream_t stream) override;
   void recv(void* buf, size_t bytes, int peer, stream_t stream) override;
+  // RCCL P2P inside hipStreamBeginCapture crashed (SIGSEGV) with the RCCL
+  // 2.26 bundled by torch on MI355X (scripts/rccl_probe.py, 2026-10-15):
+  // graph replay is refused unless RMA_RCCL_GRAPH=1.
+  bool capturable() const override;
   void allreduce(const void* sendbuf, void* recvbuf, size_t count, DType dt, RedOp op,
                  stream_t stream);
   void broadcast(const void* sendbuf, void* recvbuf, size_t count, DType dt, int root,

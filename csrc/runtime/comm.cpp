@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -78,6 +79,11 @@ RcclComm::~RcclComm() {
     if (aborted_) return;  // already torn down by abort()
     (void)ncclCommDestroy(C(comm_));
   }
+}
+
+bool RcclComm::capturable() const {
+  const char* v = std::getenv("RMA_RCCL_GRAPH");
+  return v && v[0] == '1';
 }
 
 void RcclComm::group_start() { RMA_NCCL_CHECK(ncclGroupStart()); }

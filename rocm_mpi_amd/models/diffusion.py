@@ -135,11 +135,20 @@ class Diffusion2D:
             if dev.type != "cuda" or g.halo is None:
                 raise RuntimeError("native executor needs a GPU and the rccl/self transport")
             bwx, bwy = cfg.b_width
+            use_graph = bool(cfg.use_graph)
+            if use_graph and not g.halo.capturable():
+                import warnings
+
+                warnings.warn(f"hipGraph replay disabled: the {g.transport} halo transport cannot "
+                              "be stream-captured (set RMA_RCCL_GRAPH=1 to force for RCCL)",
+                              RuntimeWarning, stacklevel=2)
+                use_graph = False
+            self.use_graph = use_graph
             self.executor = native().Executor(
                 self.T.data_ptr(), self.T2.data_ptr() if self.T2 is not None else 0,
                 self.iCp.data_ptr(), nx, ny, _MODE[cfg.variant], tuple(self.coef),
                 cfg.chunk_rows, int(cfg.nontemporal), ops.KERNELS[cfg.kernel], int(bwx), int(bwy),
-                int(cfg.use_graph), int(cfg.graph_steps), g.halo,
+                int(use_graph), int(cfg.graph_steps), g.halo,
                 self.qx.data_ptr() if cfg.variant == "kp" else 0,
                 self.qy.data_ptr() if cfg.variant == "kp" else 0,
                 self.dTdt.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll))
