@@ -46,9 +46,12 @@ def parse(argv=None):
     ap.add_argument("--max-tile", type=int, default=0, help="cap auto-sized edge (0 = none)")
     ap.add_argument("--dims", default="0,0", help="process grid dimx,dimy (0 = auto)")
     ap.add_argument("--b-width", default="32,4")
-    ap.add_argument("--chunk-rows", type=int, default=64)
+    ap.add_argument("--chunk-rows", type=int, default=16)
     ap.add_argument("--kernel", default="march", choices=["march", "lds"])
-    ap.add_argument("--nontemporal", action="store_true")
+    ap.add_argument("--unroll", type=int, default=8)
+    ap.add_argument("--nontemporal", type=int, default=1,
+                    help="bitmask: 1 = non-temporal T2 stores, 2 = non-temporal 1/Cp loads")
+    ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
@@ -107,6 +110,7 @@ def main(argv=None) -> int:
     cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup,
                           warmup=a.warmup, init="random", b_width=bw, dims=dims,
                           chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
+                          unroll=a.unroll, vec=a.vec,
                           use_graph=a.graph, quiet=True)
     t_setup = time.perf_counter()
     model = Diffusion2D(cfg)
@@ -159,6 +163,9 @@ def main(argv=None) -> int:
             "a_eff_GB_per_step": round(3 * nx * ny * 8 / 1e9, 6),
             "kernel": a.kernel,
             "chunk_rows": a.chunk_rows,
+            "unroll": a.unroll,
+            "vec": a.vec,
+            "nontemporal": a.nontemporal,
             "b_width": list(bw),
             "hipgraph": bool(a.graph),
             "setup_s": round(setup_s, 3),

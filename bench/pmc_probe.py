@@ -32,8 +32,8 @@ for _ in range(reps):
 for _ in range(reps):
     ops.stencil_step(T2, T, iCp, c, tuning=ops.StencilTuning(kernel="lds"))
 for _ in range(reps):
-    nat.stream_copy(T2.data_ptr(), T.data_ptr(), n * n, s)
+    nat.stream_copy(T2.data_ptr(), T.data_ptr(), n * n, s, 1)
 for _ in range(reps):
-    nat.stream_triad(T2.data_ptr(), T.data_ptr(), iCp.data_ptr(), 0.5, n * n, s)
+    nat.stream_triad(T2.data_ptr(), T.data_ptr(), iCp.data_ptr(), 0.5, n * n, s, 1)
 torch.cuda.synchronize()
 print(f"probe done n={n} reps={reps}")

@@ -25,8 +25,10 @@ def main(argv=None):
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--chunks", default="16,32,64,128,256")
-    ap.add_argument("--unrolls", default="2,4,8")
+    ap.add_argument("--chunks", default="8,16,32")
+    ap.add_argument("--unrolls", default="4,8")
+    ap.add_argument("--vecs", default="2,4")
+    ap.add_argument("--nts", default="0,1,3")
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
@@ -55,20 +57,30 @@ def main(argv=None):
     unrolls = [int(u) for u in a.unrolls.split(",")]
     if a.quick:
         chunks, unrolls = [64], [4]
+    vecs = [int(v) for v in a.vecs.split(",")]
+    nts = [int(v) for v in a.nts.split(",")]
+    if a.quick:
+        vecs, nts = [2], [1]
     for c in chunks:
         for u in unrolls:
-            for nt in (False, True):
-                tn = ops.StencilTuning(chunk_rows=c, unroll=u, nontemporal=nt)
-                variants[f"march_c{c}_u{u}{'_nt' if nt else ''}"] = (
-                    lambda tn=tn: ops.stencil_step(T2, T, iCp, coef, tuning=tn), bytes_model)
+            for v in vecs:
+                for nt in nts:
+                    tn = ops.StencilTuning(chunk_rows=c, unroll=u, nontemporal=nt, vec=v)
+                    variants[f"march_c{c}_u{u}_v{v}_nt{nt}"] = (
+                        lambda tn=tn: ops.stencil_step(T2, T, iCp, coef, tuning=tn), bytes_model)
     variants["lds"] = (lambda: ops.stencil_step(T2, T, iCp, coef,
                                                 tuning=ops.StencilTuning(kernel="lds")),
                        bytes_model)
     nn = n * n
-    variants["roof_copy"] = (lambda: nat.stream_copy(T2.data_ptr(), T.data_ptr(), nn, s),
-                             16.0 * nn)
-    variants["roof_triad"] = (lambda: nat.stream_triad(T2.data_ptr(), T.data_ptr(),
-                                                       iCp.data_ptr(), 0.5, nn, s), 24.0 * nn)
+    for nt in (0, 1):
+        for blocks in (2048, 4096, 8192):
+            variants[f"roof_copy_nt{nt}_b{blocks}"] = (
+                lambda nt=nt, b=blocks: nat.stream_copy(T2.data_ptr(), T.data_ptr(), nn, s, nt, b),
+                16.0 * nn)
+            variants[f"roof_triad_nt{nt}_b{blocks}"] = (
+                lambda nt=nt, b=blocks: nat.stream_triad(T2.data_ptr(), T.data_ptr(),
+                                                         iCp.data_ptr(), 0.5, nn, s, nt, b),
+                24.0 * nn)
     times = {k: [] for k in variants}
     for fn, _ in variants.values():  # warm
         fn()
@@ -87,12 +99,16 @@ def main(argv=None):
         med = statistics.median(times[k])
         res[k] = {"median_ms": med * 1e3, "min_ms": min(times[k]) * 1e3,
                   "GBps_median": b / med / 1e9, "GBps_best": b / min(times[k]) / 1e9}
-    best = max((k for k in res if k.startswith("march")), key=lambda k: res[k]["GBps_median"])
+    def best_of(prefix):
+        return max((k for k in res if k.startswith(prefix)), key=lambda k: res[k]["GBps_median"])
+
+    best = best_of("march")
+    tri, cop = best_of("roof_triad"), best_of("roof_copy")
     doc = {"n": n, "cells": cells, "rounds": a.rounds, "iters": a.iters, "results": res,
            "best_march": best, "best_march_GBps": res[best]["GBps_median"],
-           "triad_GBps": res["roof_triad"]["GBps_median"],
-           "copy_GBps": res["roof_copy"]["GBps_median"],
-           "best_vs_triad": res[best]["GBps_median"] / res["roof_triad"]["GBps_median"],
+           "best_triad": tri, "triad_GBps": res[tri]["GBps_median"],
+           "best_copy": cop, "copy_GBps": res[cop]["GBps_median"],
+           "best_vs_triad": res[best]["GBps_median"] / res[tri]["GBps_median"],
            "device": torch.cuda.get_device_name(0)}
     txt = json.dumps(doc, indent=1)
     print(txt)

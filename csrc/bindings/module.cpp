@@ -83,20 +83,28 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("set_rank_for_errors", &set_rank_for_errors);
   m.def("rccl_version", &rccl_version);
-  m.def("stencil_strip_cells", &stencil_strip_cells);
+  m.def(
+      "stencil_strip_cells",
+      [](int64_t nx, int vec) {
+        StencilTuning t;
+        t.vec = vec;
+        return stencil_strip_cells(nx, t);
+      },
+      py::arg("nx"), py::arg("vec") = 2);
 
   // ---------------- kernels ----------------
   m.def(
       "stencil_rects",
       [](uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
          const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
-         int kernel, uintptr_t stream, bool gpu, int unroll) {
+         int kernel, uintptr_t stream, bool gpu, int unroll, int vec) {
         auto r = to_rects(rects);
         StencilTuning tn;
         tn.chunk_rows = chunk_rows;
         tn.nontemporal = nontemporal;
         tn.kernel = kernel;
         tn.unroll = unroll;
+        tn.vec = vec;
         if (gpu)
           stencil_rects_gpu(P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
                             r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
@@ -107,16 +115,25 @@ PYBIND11_MODULE(_C, m) {
         }
       },
       py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"), py::arg("rects"),
-      py::arg("coef"), py::arg("chunk_rows") = 64, py::arg("nontemporal") = 0,
+      py::arg("coef"), py::arg("chunk_rows") = 16, py::arg("nontemporal") = 1,
       py::arg("kernel") = 0, py::arg("stream") = 0, py::arg("gpu") = true,
-      py::arg("unroll") = 4);
-  m.def("stream_copy", [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s) {
-    stream_copy_gpu(P<double>(b), P<const double>(a), n, S(s));
-  });
-  m.def("stream_triad", [](uintptr_t c, uintptr_t a, uintptr_t b, double x, int64_t n,
-                           uintptr_t s) {
-    stream_triad_gpu(P<double>(c), P<const double>(a), P<const double>(b), x, n, S(s));
-  });
+      py::arg("unroll") = 8, py::arg("vec") = 2);
+  m.def(
+      "stream_copy",
+      [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {
+        stream_copy_gpu(P<double>(b), P<const double>(a), n, nt, blocks, S(s));
+      },
+      py::arg("b"), py::arg("a"), py::arg("n"), py::arg("stream"), py::arg("nt") = 0,
+      py::arg("blocks") = 0);
+  m.def(
+      "stream_triad",
+      [](uintptr_t c, uintptr_t a, uintptr_t b, double x, int64_t n, uintptr_t s, int nt,
+         int blocks) {
+        stream_triad_gpu(P<double>(c), P<const double>(a), P<const double>(b), x, n, nt, blocks,
+                         S(s));
+      },
+      py::arg("c"), py::arg("a"), py::arg("b"), py::arg("x"), py::arg("n"), py::arg("stream"),
+      py::arg("nt") = 0, py::arg("blocks") = 0);
 
   m.def("flux", [](uintptr_t qx, uintptr_t qy, uintptr_t T, int64_t nx, int64_t ny, double mlam,
                    double rdx, double rdy, uintptr_t stream, bool gpu) {
@@ -277,7 +294,7 @@ PYBIND11_MODULE(_C, m) {
                        const Coef4& coef, int chunk_rows, int nontemporal, int kernel,
                        int64_t bwx, int64_t bwy, int use_graph, int graph_steps,
                        HaloExchanger* halo, uintptr_t qx, uintptr_t qy, uintptr_t dTdt,
-                       int unroll) {
+                       int unroll, int vec) {
              ExecParams p;
              p.mode = static_cast<Mode>(mode);
              p.coef = to_coef(coef);
@@ -285,6 +302,7 @@ PYBIND11_MODULE(_C, m) {
              p.tune.nontemporal = nontemporal;
              p.tune.kernel = kernel;
              p.tune.unroll = unroll;
+             p.tune.vec = vec;
              p.bwx = bwx;
              p.bwy = bwy;
              p.use_graph = use_graph;
@@ -294,11 +312,12 @@ PYBIND11_MODULE(_C, m) {
                                           P<double>(dTdt));
            }),
            py::arg("T"), py::arg("T2"), py::arg("iCp"), py::arg("nx"), py::arg("ny"),
-           py::arg("mode"), py::arg("coef"), py::arg("chunk_rows") = 64,
-           py::arg("nontemporal") = 0, py::arg("kernel") = 0, py::arg("bwx") = 127,
+           py::arg("mode"), py::arg("coef"), py::arg("chunk_rows") = 16,
+           py::arg("nontemporal") = 1, py::arg("kernel") = 0, py::arg("bwx") = 127,
            py::arg("bwy") = 4, py::arg("use_graph") = 0, py::arg("graph_steps") = 0,
            py::arg("halo").none(true) = nullptr, py::arg("qx") = 0, py::arg("qy") = 0,
-           py::arg("dTdt") = 0, py::arg("unroll") = 4, py::keep_alive<1, 16>())
+           py::arg("dTdt") = 0, py::arg("unroll") = 8, py::arg("vec") = 2,
+           py::keep_alive<1, 16>())
       .def(
           "run", [](DiffusionExecutor& e, int64_t n, uintptr_t s) { e.run(n, S(s)); },
           py::arg("nsteps"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())

@@ -60,7 +60,15 @@ class HaloExchanger {
   void prepare(const std::vector<HaloField>& fields, int dims_mask = 7);
 
   bool active(int dim) const;  // any neighbour in this dim?
-  bool capturable() const { return comm_ == nullptr || comm_->capturable(); }
+  // Graph capture is possible when no message goes through a non-capturable
+  // transport (local self copies and the pack kernels always capture).
+  bool capturable() const {
+    if (comm_ == nullptr || comm_->capturable()) return true;
+    for (int d = 0; d < 3; ++d)
+      for (int s = 0; s < 2; ++s)
+        if (nbr_[d][s] >= 0 && (nbr_[d][s] != self_ || self_via_comm_)) return false;
+    return true;
+  }
   // Route self-neighbours (periodic, one process along a dim) through the
   // transport instead of a local copy (tests the P2P path on one GPU).
   void set_self_via_transport(bool on) { self_via_comm_ = on && comm_ != nullptr; }

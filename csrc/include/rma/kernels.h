@@ -26,10 +26,11 @@ using stream_t = void*;  // hipStream_t
 constexpr int kMaxRects = 8;
 
 struct StencilTuning {
-  int chunk_rows = 64;     // rows marched by one wave-task
-  int nontemporal = 0;     // 1: non-temporal T2 stores
+  int chunk_rows = 16;     // rows marched by one wave-task
+  int nontemporal = 1;     // bit 0: non-temporal T2 stores; bit 1: non-temporal 1/Cp loads
   int kernel = 0;          // 0 = register march (default), 1 = LDS-tiled
-  int unroll = 4;          // rows per march iteration whose loads are issued together
+  int unroll = 8;          // rows per march iteration whose loads are issued together
+  int vec = 2;             // cells per lane (2: one 16-B access per row, 4: two)
 };
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
@@ -40,7 +41,8 @@ void stencil_rects_cpu(double* T2, const double* T, const double* iCp, int64_t n
 
 // Width (in cells) of one wave's x-strip in the march kernel; perf_hide rounds
 // its x-frame so the interior rect starts on a strip boundary.
-int stencil_strip_cells(int64_t nx);
+int stencil_vec(int64_t nx, const StencilTuning& tune);
+int stencil_strip_cells(int64_t nx, const StencilTuning& tune);
 
 // ---------------------------------------------------------------------------
 // kp: the three-kernel formulation (K1-K3; scripts/diffusion_2D_kp.jl:16-54).
@@ -101,9 +103,9 @@ void copy2d_cpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int6
 //   triad: c[i] = a[i] + s*b[i]     (2 reads + 1 write = the stencil's mix)
 // 16-byte vector accesses, grid-stride.
 // ---------------------------------------------------------------------------
-void stream_copy_gpu(double* b, const double* a, int64_t n, stream_t stream);
-void stream_triad_gpu(double* c, const double* a, const double* b, double s, int64_t n,
-                      stream_t stream);
+void stream_copy_gpu(double* b, const double* a, int64_t n, int nt, int blocks, stream_t stream);
+void stream_triad_gpu(double* c, const double* a, const double* b, double s, int64_t n, int nt,
+                      int blocks, stream_t stream);
 
 // ---------------------------------------------------------------------------
 // Reductions for verification / NaN guards. Result is written

@@ -174,20 +174,48 @@ __global__ __launch_bounds__(kRedBlock) void reduce_stage2(const double* __restr
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
+// Roofline probes: each thread keeps 4 independent 16-byte loads in flight per
+// array (grid-strided so every wave-instruction is one contiguous 1 KiB).
+template <bool NT>
 __global__ __launch_bounds__(256) void stream_copy_kernel(dbl2* __restrict__ b,
                                                           const dbl2* __restrict__ a, int64_t n2) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2;
-       i += (int64_t)gridDim.x * blockDim.x)
-    b[i] = a[i];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    dbl2 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = a[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (NT) __builtin_nontemporal_store(v[k], b + i + k * stride);
+      else b[i + k * stride] = v[k];
+    }
+  }
+  for (; i < n2; i += stride) b[i] = a[i];
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256) void stream_triad_kernel(dbl2* __restrict__ c,
                                                            const dbl2* __restrict__ a,
                                                            const dbl2* __restrict__ b, double s,
                                                            int64_t n2) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2;
-       i += (int64_t)gridDim.x * blockDim.x)
-    c[i] = a[i] + s * b[i];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    dbl2 va[4], vb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      va[k] = a[i + k * stride];
+      vb[k] = b[i + k * stride];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const dbl2 r = va[k] + s * vb[k];
+      if constexpr (NT) __builtin_nontemporal_store(r, c + i + k * stride);
+      else c[i + k * stride] = r;
+    }
+  }
+  for (; i < n2; i += stride) c[i] = a[i] + s * b[i];
 }
 
 unsigned grid_stride_blocks(int64_t n, int block) {
@@ -251,20 +279,29 @@ void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int6
   RMA_HIP_LAUNCH_CHECK();
 }
 
-void stream_copy_gpu(double* b, const double* a, int64_t n, stream_t stream) {
+void stream_copy_gpu(double* b, const double* a, int64_t n, int nt, int blocks, stream_t stream) {
   RMA_CHECK_ARG(n % 2 == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0,
                 "stream_copy needs even n and 16-byte aligned buffers");
-  stream_copy_kernel<<<256 * 8, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
+  const unsigned g = blocks > 0 ? blocks : 256 * 16;
+  if (nt)
+    stream_copy_kernel<true><<<g, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
+  else
+    stream_copy_kernel<false><<<g, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
   RMA_HIP_LAUNCH_CHECK();
 }
 
-void stream_triad_gpu(double* c, const double* a, const double* b, double s, int64_t n,
-                      stream_t stream) {
+void stream_triad_gpu(double* c, const double* a, const double* b, double s, int64_t n, int nt,
+                      int blocks, stream_t stream) {
   RMA_CHECK_ARG(n % 2 == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
                                 reinterpret_cast<uintptr_t>(c)) & 15) == 0,
                 "stream_triad needs even n and 16-byte aligned buffers");
-  stream_triad_kernel<<<256 * 8, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
-                                                               (const dbl2*)b, s, n / 2);
+  const unsigned g = blocks > 0 ? blocks : 256 * 16;
+  if (nt)
+    stream_triad_kernel<true><<<g, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
+                                                                 (const dbl2*)b, s, n / 2);
+  else
+    stream_triad_kernel<false><<<g, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
+                                                                  (const dbl2*)b, s, n / 2);
   RMA_HIP_LAUNCH_CHECK();
 }
 

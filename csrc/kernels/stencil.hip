@@ -50,29 +50,40 @@ struct RectList {
   int n;
 };
 
-template <int V>
+template <int V, bool NTL = false>
 __device__ __forceinline__ void load_row(double (&out)[V], const double* __restrict__ p) {
-  if constexpr (V == 2) {
-    const dbl2 t = *reinterpret_cast<const dbl2*>(p);
-    out[0] = t.x;
-    out[1] = t.y;
+  if constexpr (V == 1) {
+    out[0] = NTL ? __builtin_nontemporal_load(p) : *p;
   } else {
-    out[0] = *p;
+#pragma unroll
+    for (int h = 0; h < V / 2; ++h) {
+      const dbl2* q = reinterpret_cast<const dbl2*>(p) + h;
+      const dbl2 t = NTL ? __builtin_nontemporal_load(q) : *q;
+      out[2 * h] = t.x;
+      out[2 * h + 1] = t.y;
+    }
   }
 }
 
 template <int V, bool NT>
 __device__ __forceinline__ void store_row(double* __restrict__ p, const double (&v)[V],
                                           const bool (&m)[V]) {
-  if constexpr (V == 2) {
-    if (m[0] && m[1]) {
-      dbl2 t;
-      t.x = v[0];
-      t.y = v[1];
-      if constexpr (NT) {
-        __builtin_nontemporal_store(t, reinterpret_cast<dbl2*>(p));
-      } else {
-        *reinterpret_cast<dbl2*>(p) = t;
+  if constexpr (V >= 2) {
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < V; ++i) all = all && m[i];
+    if (all) {
+#pragma unroll
+      for (int h = 0; h < V / 2; ++h) {
+        dbl2 t;
+        t.x = v[2 * h];
+        t.y = v[2 * h + 1];
+        dbl2* q = reinterpret_cast<dbl2*>(p) + h;
+        if constexpr (NT) {
+          __builtin_nontemporal_store(t, q);
+        } else {
+          *q = t;
+        }
       }
       return;
     }
@@ -118,7 +129,7 @@ __device__ __forceinline__ void row_update(double (&res)[V], const double (&up)[
   }
 }
 
-template <int V, bool NT, int kUnroll>
+template <int V, bool NT, int kUnroll, bool NTL>
 __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restrict__ T2,
                                                                const double* __restrict__ T,
                                                                const double* __restrict__ iCp,
@@ -158,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restric
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       load_row<V>(rows[u + 2], T + (y + u + 1) * nx + xl);
-      load_row<V>(ic[u], iCp + (y + u) * nx + xl);
+      load_row<V, NTL>(ic[u], iCp + (y + u) * nx + xl);
       ed[u] = T[(y + u) * nx + eidx];
     }
 #pragma unroll
@@ -176,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restric
   for (; y < yb; ++y) {
     double ic[V];
     load_row<V>(rows[2], T + (y + 1) * nx + xl);
-    load_row<V>(ic, iCp + y * nx + xl);
+    load_row<V, NTL>(ic, iCp + y * nx + xl);
     const double ed = T[y * nx + eidx];
     double res[V];
     row_update<V>(res, rows[0], rows[1], rows[2], ic, ed, lane, k);
@@ -257,17 +268,27 @@ void validate_rects(int64_t nx, int64_t ny, const Rect* rects, int nrects) {
 
 }  // namespace
 
-int stencil_strip_cells(int64_t nx) { return (nx % 2 == 0) ? kWave * 2 : kWave; }
+int stencil_vec(int64_t nx, const StencilTuning& tune) {
+  // cells per lane: 16-byte rows need an even nx; V=4 also needs nx % 4 == 0
+  // (a clamped lane past the row end must still load its own cells)
+  if (nx % 2) return 1;
+  if (tune.vec == 4 && nx % 4 == 0) return 4;
+  return 2;
+}
+
+int stencil_strip_cells(int64_t nx, const StencilTuning& tune) {
+  return kWave * stencil_vec(nx, tune);
+}
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
                        const Rect* rects, int nrects, const StencilCoef& c,
                        const StencilTuning& tune, stream_t stream) {
   validate_rects(nx, ny, rects, nrects);
   RMA_CHECK_ARG(tune.chunk_rows >= 1, "chunk_rows=" << tune.chunk_rows);
-  const bool aligned = (nx % 2 == 0) && ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
+  const bool aligned = ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(T2) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
-  const int V = aligned ? 2 : 1;
+  const int V = aligned ? stencil_vec(nx, tune) : 1;
   const bool lds = tune.kernel == 1;
   RectList L{};
   int64_t total = 0;
@@ -303,22 +324,35 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
       stencil_lds_kernel<false><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c);
   } else {
     const int u = tune.unroll;
-    RMA_CHECK_ARG(u == 1 || u == 2 || u == 4 || u == 8, "unroll must be 1, 2, 4 or 8");
-#define RMA_MARCH(VV, NTT, UU)                                                           \
-  stencil_march_kernel<VV, NTT, UU><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, tune.chunk_rows)
-#define RMA_MARCH_U(VV, NTT)          \
-  switch (u) {                        \
-    case 1: RMA_MARCH(VV, NTT, 1); break; \
-    case 2: RMA_MARCH(VV, NTT, 2); break; \
-    case 8: RMA_MARCH(VV, NTT, 8); break; \
-    default: RMA_MARCH(VV, NTT, 4); break; \
+    RMA_CHECK_ARG(u == 2 || u == 4 || u == 8, "unroll must be 2, 4 or 8");
+    const bool nts = tune.nontemporal & 1, ntl = (tune.nontemporal >> 1) & 1;
+#define RMA_MARCH(VV, UU, NTS, NTL)                                                  \
+  stencil_march_kernel<VV, NTS, UU, NTL><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, \
+                                                                 tune.chunk_rows)
+#define RMA_MARCH_NT(VV, UU)                 \
+  if (nts) {                                 \
+    if (ntl) RMA_MARCH(VV, UU, true, true);   \
+    else RMA_MARCH(VV, UU, true, false);      \
+  } else {                                   \
+    if (ntl) RMA_MARCH(VV, UU, false, true);  \
+    else RMA_MARCH(VV, UU, false, false);     \
   }
-    if (V == 2) {
-      if (tune.nontemporal) { RMA_MARCH_U(2, true) } else { RMA_MARCH_U(2, false) }
+#define RMA_MARCH_U(VV)                     \
+  switch (u) {                              \
+    case 2: RMA_MARCH_NT(VV, 2) break;      \
+    case 8: RMA_MARCH_NT(VV, 8) break;      \
+    default: RMA_MARCH_NT(VV, 4) break;     \
+  }
+    if (V == 4) {
+      RMA_MARCH_U(4)
+    } else if (V == 2) {
+      RMA_MARCH_U(2)
     } else {
-      if (tune.nontemporal) { RMA_MARCH_U(1, true) } else { RMA_MARCH_U(1, false) }
+      if (nts) RMA_MARCH(1, 4, true, false);
+      else RMA_MARCH(1, 4, false, false);
     }
 #undef RMA_MARCH_U
+#undef RMA_MARCH_NT
 #undef RMA_MARCH
   }
   RMA_HIP_LAUNCH_CHECK();

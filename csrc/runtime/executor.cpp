@@ -33,7 +33,7 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   if (p.mode == Mode::kHide) {
     RMA_CHECK_ARG(p.bwx >= 1 && p.bwy >= 1,
                   "b_width must be >= 1 so the send planes belong to the boundary kernel");
-    const int64_t strip = stencil_strip_cells(nx);
+    const int64_t strip = stencil_strip_cells(nx, p.tune);
     const int64_t xi0 = round_up(1 + p.bwx, strip);
     const int64_t xi1 = round_down(nx - 1 - p.bwx, strip);
     const int64_t yi0 = 1 + p.bwy, yi1 = ny - 1 - p.bwy;

@@ -66,10 +66,12 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--auto-size", action="store_true",
                     help="size the local tile to fill --hbm-frac of free HBM (288 GB MI355X)")
     ap.add_argument("--hbm-frac", type=float, default=0.80)
-    ap.add_argument("--chunk-rows", type=int, default=64)
-    ap.add_argument("--unroll", type=int, default=4)
+    ap.add_argument("--chunk-rows", type=int, default=16)
+    ap.add_argument("--unroll", type=int, default=8)
     ap.add_argument("--kernel", choices=["march", "lds"], default="march")
-    ap.add_argument("--nontemporal", action="store_true")
+    ap.add_argument("--nontemporal", type=int, default=1,
+                    help="bitmask: 1 = non-temporal T2 stores, 2 = non-temporal 1/Cp loads")
+    ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
     ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf guard period")
     ap.add_argument("--checkpoint", default="", help="save the final state to this directory")
@@ -98,7 +100,7 @@ def run_variant(variant: str, argv=None) -> int:
     opts = dict(variant=base, nx=a.nx, ny=a.ny, nt=a.nt, warmup=a.warmup, b_width=a.b_width,
                 init=a.init, init_on=a.init_on, seed=a.seed, dims=tuple(a.dims) + (0,),
                 periods=tuple(a.periods) + (0,), transport=a.transport, device=a.device,
-                chunk_rows=a.chunk_rows, unroll=a.unroll, kernel=a.kernel,
+                chunk_rows=a.chunk_rows, unroll=a.unroll, vec=a.vec, kernel=a.kernel,
                 nontemporal=a.nontemporal, use_graph=a.graph, do_vis=a.do_vis, outdir=a.outdir,
                 profile=a.profile, check_every=a.check_every, quiet=a.quiet)
     auto = a.auto_size

@@ -63,10 +63,11 @@ class DiffusionConfig:
     periods: tuple = (0, 0, 0)
     transport: str = "auto"
     device: str | None = None
-    chunk_rows: int = 64
-    nontemporal: bool = False
+    chunk_rows: int = 16
+    nontemporal: int = 1  # bit 0: NT T2 stores, bit 1: NT 1/Cp loads
     kernel: str = "march"
-    unroll: int = 4
+    unroll: int = 8
+    vec: int = 2
     use_graph: bool = False
     graph_steps: int = 0
     executor: str = "auto"  # auto | native | python
@@ -151,10 +152,12 @@ class Diffusion2D:
                 int(use_graph), int(cfg.graph_steps), g.halo,
                 self.qx.data_ptr() if cfg.variant == "kp" else 0,
                 self.qy.data_ptr() if cfg.variant == "kp" else 0,
-                self.dTdt.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll))
+                self.dTdt.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
+                int(cfg.vec))
         if cfg.variant == "perf_hide":
-            self.frame_rects, self.interior = ops.hide_rects(nx, ny, *cfg.b_width)
-        self.tuning = ops.StencilTuning(cfg.chunk_rows, cfg.nontemporal, cfg.kernel, cfg.unroll)
+            self.frame_rects, self.interior = ops.hide_rects(nx, ny, *cfg.b_width, vec=cfg.vec)
+        self.tuning = ops.StencilTuning(cfg.chunk_rows, int(cfg.nontemporal), cfg.kernel,
+                                        cfg.unroll, cfg.vec)
 
     # ------------------------------------------------------------------
     def geometry(self, A_shape=None) -> ops.TileGeometry:

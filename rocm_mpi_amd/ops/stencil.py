@@ -42,10 +42,16 @@ class StencilCoef(NamedTuple):
 
 @dataclass
 class StencilTuning:
-    chunk_rows: int = 64
-    nontemporal: bool = False
+    """Knobs of the march kernel (defaults = the fastest measured on MI355X,
+    profiles/sweep_16k.md): rows per wave-task, rows whose loads are issued
+    together, non-temporal bitmask (1: T2 stores, 2: 1/Cp loads), cells per
+    lane (2 or 4), and the kernel family ("march" or the "lds" baseline)."""
+
+    chunk_rows: int = 16
+    nontemporal: int = 1
     kernel: str = "march"
-    unroll: int = 4
+    unroll: int = 8
+    vec: int = 2
 
 
 @dataclass
@@ -148,7 +154,7 @@ def stencil_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: Ste
     if T.is_cuda:
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                tn.chunk_rows, int(tn.nontemporal), KERNELS[tn.kernel],
-                               stream_handle(T), True, tn.unroll)
+                               stream_handle(T), True, tn.unroll, tn.vec)
     elif _use_native_cpu():
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                64, 0, 0, 0, False)
@@ -156,14 +162,17 @@ def stencil_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: Ste
         stencil_torch(T2, T, iCp, coef, rects)
 
 
-def strip_cells(nx: int) -> int:
+def strip_cells(nx: int, vec: int = 2) -> int:
     """x-width of one wave-strip of the march kernel (perf_hide frame rounding)."""
     if has_native():
-        return native().stencil_strip_cells(nx)
-    return 128 if nx % 2 == 0 else 64
+        return native().stencil_strip_cells(nx, vec)
+    if nx % 2:
+        return 64
+    return 256 if vec == 4 and nx % 4 == 0 else 128
 
 
-def hide_rects(nx: int, ny: int, bwx: int, bwy: int) -> tuple[list[Rect], Rect | None]:
+def hide_rects(nx: int, ny: int, bwx: int, bwy: int,
+               vec: int = 2) -> tuple[list[Rect], Rect | None]:
     """Frame rects and interior rect of the boundary/interior split.
 
     The x-frame is rounded up so the interior starts on a wave-strip boundary
@@ -172,7 +181,7 @@ def hide_rects(nx: int, ny: int, bwx: int, bwy: int) -> tuple[list[Rect], Rect |
     """
     if bwx < 1 or bwy < 1:
         raise ValueError("b_width must be >= 1 so the send planes are computed first")
-    s = strip_cells(nx)
+    s = strip_cells(nx, vec)
     xi0 = -(-(1 + bwx) // s) * s
     xi1 = (nx - 1 - bwx) // s * s
     yi0, yi1 = 1 + bwy, ny - 1 - bwy
