@@ -46,11 +46,11 @@ def parse(argv=None):
     ap.add_argument("--max-tile", type=int, default=0, help="cap auto-sized edge (0 = none)")
     ap.add_argument("--dims", default="0,0", help="process grid dimx,dimy (0 = auto)")
     ap.add_argument("--b-width", default="32,4")
-    ap.add_argument("--chunk-rows", type=int, default=16)
+    ap.add_argument("--chunk-rows", type=int, default=8)
     ap.add_argument("--kernel", default="march", choices=["march", "lds"])
     ap.add_argument("--unroll", type=int, default=8)
-    ap.add_argument("--nontemporal", type=int, default=1,
-                    help="bitmask: 1 = non-temporal T2 stores, 2 = non-temporal 1/Cp loads")
+    ap.add_argument("--nontemporal", type=int, default=3,
+                    help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
     ap.add_argument("--json-out", default="")

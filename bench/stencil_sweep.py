@@ -25,10 +25,10 @@ def main(argv=None):
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--chunks", default="8,16,32")
+    ap.add_argument("--chunks", default="4,8,16")
     ap.add_argument("--unrolls", default="4,8")
-    ap.add_argument("--vecs", default="2,4")
-    ap.add_argument("--nts", default="0,1,3")
+    ap.add_argument("--vecs", default="2")
+    ap.add_argument("--nts", default="1,3,7")
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
@@ -73,7 +73,7 @@ def main(argv=None):
                        bytes_model)
     nn = n * n
     for nt in (0, 1):
-        for blocks in (2048, 4096, 8192):
+        for blocks in (0, 4096, 16384):
             variants[f"roof_copy_nt{nt}_b{blocks}"] = (
                 lambda nt=nt, b=blocks: nat.stream_copy(T2.data_ptr(), T.data_ptr(), nn, s, nt, b),
                 16.0 * nn)

@@ -194,6 +194,30 @@ __global__ __launch_bounds__(256) void stream_copy_kernel(dbl2* __restrict__ b,
   for (; i < n2; i += stride) b[i] = a[i];
 }
 
+// one 16-byte element per thread, full grid (the simplest streaming form)
+template <bool NT>
+__global__ __launch_bounds__(256) void stream_copy_flat(dbl2* __restrict__ b,
+                                                        const dbl2* __restrict__ a, int64_t n2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n2) {
+    if constexpr (NT) __builtin_nontemporal_store(a[i], b + i);
+    else b[i] = a[i];
+  }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void stream_triad_flat(dbl2* __restrict__ c,
+                                                         const dbl2* __restrict__ a,
+                                                         const dbl2* __restrict__ b, double s,
+                                                         int64_t n2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n2) {
+    const dbl2 r = a[i] + s * b[i];
+    if constexpr (NT) __builtin_nontemporal_store(r, c + i);
+    else c[i] = r;
+  }
+}
+
 template <bool NT>
 __global__ __launch_bounds__(256) void stream_triad_kernel(dbl2* __restrict__ c,
                                                            const dbl2* __restrict__ a,
@@ -282,11 +306,17 @@ void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int6
 void stream_copy_gpu(double* b, const double* a, int64_t n, int nt, int blocks, stream_t stream) {
   RMA_CHECK_ARG(n % 2 == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0,
                 "stream_copy needs even n and 16-byte aligned buffers");
-  const unsigned g = blocks > 0 ? blocks : 256 * 16;
-  if (nt)
-    stream_copy_kernel<true><<<g, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
-  else
-    stream_copy_kernel<false><<<g, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
+  if (blocks <= 0) {  // flat: one element per thread
+    const unsigned g = (unsigned)((n / 2 + 255) / 256);
+    if (nt)
+      stream_copy_flat<true><<<g, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
+    else
+      stream_copy_flat<false><<<g, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
+  } else if (nt) {
+    stream_copy_kernel<true><<<blocks, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
+  } else {
+    stream_copy_kernel<false><<<blocks, 256, 0, as_stream(stream)>>>((dbl2*)b, (const dbl2*)a, n / 2);
+  }
   RMA_HIP_LAUNCH_CHECK();
 }
 
@@ -295,13 +325,21 @@ void stream_triad_gpu(double* c, const double* a, const double* b, double s, int
   RMA_CHECK_ARG(n % 2 == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
                                 reinterpret_cast<uintptr_t>(c)) & 15) == 0,
                 "stream_triad needs even n and 16-byte aligned buffers");
-  const unsigned g = blocks > 0 ? blocks : 256 * 16;
-  if (nt)
-    stream_triad_kernel<true><<<g, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
+  if (blocks <= 0) {
+    const unsigned g = (unsigned)((n / 2 + 255) / 256);
+    if (nt)
+      stream_triad_flat<true><<<g, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
                                                                  (const dbl2*)b, s, n / 2);
-  else
-    stream_triad_kernel<false><<<g, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
+    else
+      stream_triad_flat<false><<<g, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
                                                                   (const dbl2*)b, s, n / 2);
+  } else if (nt) {
+    stream_triad_kernel<true><<<blocks, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
+                                                                      (const dbl2*)b, s, n / 2);
+  } else {
+    stream_triad_kernel<false><<<blocks, 256, 0, as_stream(stream)>>>((dbl2*)c, (const dbl2*)a,
+                                                                       (const dbl2*)b, s, n / 2);
+  }
   RMA_HIP_LAUNCH_CHECK();
 }
 

@@ -129,7 +129,7 @@ __device__ __forceinline__ void row_update(double (&res)[V], const double (&up)[
   }
 }
 
-template <int V, bool NT, int kUnroll, bool NTL>
+template <int V, bool NT, int kUnroll, bool NTL, bool NTT = false>
 __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restrict__ T2,
                                                                const double* __restrict__ T,
                                                                const double* __restrict__ iCp,
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restric
     double ed[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      load_row<V>(rows[u + 2], T + (y + u + 1) * nx + xl);
+      load_row<V, NTT>(rows[u + 2], T + (y + u + 1) * nx + xl);
       load_row<V, NTL>(ic[u], iCp + (y + u) * nx + xl);
       ed[u] = T[(y + u) * nx + eidx];
     }
@@ -326,16 +326,20 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
     const int u = tune.unroll;
     RMA_CHECK_ARG(u == 2 || u == 4 || u == 8, "unroll must be 2, 4 or 8");
     const bool nts = tune.nontemporal & 1, ntl = (tune.nontemporal >> 1) & 1;
+    const bool ntt = (tune.nontemporal >> 2) & 1;  // bit 2: also T loads (implies 1|2)
 #define RMA_MARCH(VV, UU, NTS, NTL)                                                  \
   stencil_march_kernel<VV, NTS, UU, NTL><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, \
                                                                  tune.chunk_rows)
-#define RMA_MARCH_NT(VV, UU)                 \
-  if (nts) {                                 \
-    if (ntl) RMA_MARCH(VV, UU, true, true);   \
-    else RMA_MARCH(VV, UU, true, false);      \
-  } else {                                   \
-    if (ntl) RMA_MARCH(VV, UU, false, true);  \
-    else RMA_MARCH(VV, UU, false, false);     \
+#define RMA_MARCH_NT(VV, UU)                                                            \
+  if (ntt) {                                                                            \
+    stencil_march_kernel<VV, true, UU, true, true><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, \
+                                                                       tune.chunk_rows); \
+  } else if (nts) {                                                                     \
+    if (ntl) RMA_MARCH(VV, UU, true, true);                                              \
+    else RMA_MARCH(VV, UU, true, false);                                                 \
+  } else {                                                                              \
+    if (ntl) RMA_MARCH(VV, UU, false, true);                                             \
+    else RMA_MARCH(VV, UU, false, false);                                                \
   }
 #define RMA_MARCH_U(VV)                     \
   switch (u) {                              \

@@ -63,8 +63,8 @@ class DiffusionConfig:
     periods: tuple = (0, 0, 0)
     transport: str = "auto"
     device: str | None = None
-    chunk_rows: int = 16
-    nontemporal: int = 1  # bit 0: NT T2 stores, bit 1: NT 1/Cp loads
+    chunk_rows: int = 8
+    nontemporal: int = 3  # bit 0: NT T2 stores, bit 1: NT 1/Cp loads, bit 2: NT T loads
     kernel: str = "march"
     unroll: int = 8
     vec: int = 2

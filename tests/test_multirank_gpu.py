@@ -71,9 +71,10 @@ def test_native_executor_refuses_graph_on_loopback():
     from rocm_mpi_amd._native import native
 
     n = native()
-    hub = n.LoopbackHub(1, 5.0)
+    hub = n.LoopbackHub(2, 5.0)
     ep = n.LoopbackEndpoint(hub, 0)
-    halo = n.HaloExchanger(ep, 0, [[-1, -1], [-1, -1], [-1, -1]])
+    halo = n.HaloExchanger(ep, 0, [[1, 1], [-1, -1], [-1, -1]])
+    assert not halo.capturable()
     T = torch.zeros(64, 64, dtype=torch.float64, device="cuda")
     with pytest.raises(RuntimeError, match="capturable"):
         n.Executor(T.data_ptr(), T.data_ptr(), T.data_ptr(), 64, 64, 0, (-1.0, 1.0, 1.0, 0.1),
