@@ -46,9 +46,9 @@ def parse(argv=None):
     ap.add_argument("--max-tile", type=int, default=0, help="cap auto-sized edge (0 = none)")
     ap.add_argument("--dims", default="0,0", help="process grid dimx,dimy (0 = auto)")
     ap.add_argument("--b-width", default="32,4")
-    ap.add_argument("--chunk-rows", type=int, default=8)
+    ap.add_argument("--chunk-rows", type=int, default=4)
     ap.add_argument("--kernel", default="march", choices=["march", "lds"])
-    ap.add_argument("--unroll", type=int, default=8)
+    ap.add_argument("--unroll", type=int, default=4)
     ap.add_argument("--nontemporal", type=int, default=3,
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")

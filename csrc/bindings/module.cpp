@@ -115,9 +115,9 @@ PYBIND11_MODULE(_C, m) {
         }
       },
       py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"), py::arg("rects"),
-      py::arg("coef"), py::arg("chunk_rows") = 8, py::arg("nontemporal") = 3,
+      py::arg("coef"), py::arg("chunk_rows") = 4, py::arg("nontemporal") = 3,
       py::arg("kernel") = 0, py::arg("stream") = 0, py::arg("gpu") = true,
-      py::arg("unroll") = 8, py::arg("vec") = 2);
+      py::arg("unroll") = 4, py::arg("vec") = 2);
   m.def(
       "stream_copy",
       [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {
@@ -312,11 +312,11 @@ PYBIND11_MODULE(_C, m) {
                                           P<double>(dTdt));
            }),
            py::arg("T"), py::arg("T2"), py::arg("iCp"), py::arg("nx"), py::arg("ny"),
-           py::arg("mode"), py::arg("coef"), py::arg("chunk_rows") = 8,
+           py::arg("mode"), py::arg("coef"), py::arg("chunk_rows") = 4,
            py::arg("nontemporal") = 3, py::arg("kernel") = 0, py::arg("bwx") = 127,
            py::arg("bwy") = 4, py::arg("use_graph") = 0, py::arg("graph_steps") = 0,
            py::arg("halo").none(true) = nullptr, py::arg("qx") = 0, py::arg("qy") = 0,
-           py::arg("dTdt") = 0, py::arg("unroll") = 8, py::arg("vec") = 2,
+           py::arg("dTdt") = 0, py::arg("unroll") = 4, py::arg("vec") = 2,
            py::keep_alive<1, 16>())
       .def(
           "run", [](DiffusionExecutor& e, int64_t n, uintptr_t s) { e.run(n, S(s)); },

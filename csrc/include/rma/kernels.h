@@ -26,10 +26,10 @@ using stream_t = void*;  // hipStream_t
 constexpr int kMaxRects = 8;
 
 struct StencilTuning {
-  int chunk_rows = 8;      // rows marched by one wave-task
+  int chunk_rows = 4;      // rows marched by one wave-task
   int nontemporal = 3;     // bit 0: NT T2 stores; bit 1: NT 1/Cp loads; bit 2: NT T loads
   int kernel = 0;          // 0 = register march (default), 1 = LDS-tiled
-  int unroll = 8;          // rows per march iteration whose loads are issued together
+  int unroll = 4;          // rows per march iteration whose loads are issued together
   int vec = 2;             // cells per lane (2: one 16-B access per row, 4: two)
 };
 

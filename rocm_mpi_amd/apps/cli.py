@@ -66,8 +66,8 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--auto-size", action="store_true",
                     help="size the local tile to fill --hbm-frac of free HBM (288 GB MI355X)")
     ap.add_argument("--hbm-frac", type=float, default=0.80)
-    ap.add_argument("--chunk-rows", type=int, default=8)
-    ap.add_argument("--unroll", type=int, default=8)
+    ap.add_argument("--chunk-rows", type=int, default=4)
+    ap.add_argument("--unroll", type=int, default=4)
     ap.add_argument("--kernel", choices=["march", "lds"], default="march")
     ap.add_argument("--nontemporal", type=int, default=3,
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")

@@ -63,10 +63,10 @@ class DiffusionConfig:
     periods: tuple = (0, 0, 0)
     transport: str = "auto"
     device: str | None = None
-    chunk_rows: int = 8
+    chunk_rows: int = 4
     nontemporal: int = 3  # bit 0: NT T2 stores, bit 1: NT 1/Cp loads, bit 2: NT T loads
     kernel: str = "march"
-    unroll: int = 8
+    unroll: int = 4
     vec: int = 2
     use_graph: bool = False
     graph_steps: int = 0

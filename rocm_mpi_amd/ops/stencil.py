@@ -48,10 +48,10 @@ class StencilTuning:
     lane (2 or 4), and the kernel family ("march" or the "lds" baseline).
     Bit 2 of the non-temporal mask also streams T loads (implies bits 0-1)."""
 
-    chunk_rows: int = 8
+    chunk_rows: int = 4
     nontemporal: int = 3
     kernel: str = "march"
-    unroll: int = 8
+    unroll: int = 4
     vec: int = 2
 
 
