@@ -28,8 +28,12 @@ def main(argv=None):
     ap.add_argument("--chunks", default="4,8,16")
     ap.add_argument("--unrolls", default="4,8")
     ap.add_argument("--vecs", default="2")
-    ap.add_argument("--nts", default="1,3,7")
+    ap.add_argument("--nts", default="1,3")
+    ap.add_argument("--xcds", default="0,1")
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--x0", type=int, default=1, help="interior rect offset (perf_hide-like)")
+    ap.add_argument("--y0", type=int, default=1)
+    ap.add_argument("--no-roof", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -61,18 +65,23 @@ def main(argv=None):
     nts = [int(v) for v in a.nts.split(",")]
     if a.quick:
         vecs, nts = [2], [1]
+    xcds = [int(v) for v in a.xcds.split(",")]
+    rect = [(a.x0, n - 1 - a.x0, a.y0, n - 1 - a.y0)] if (a.x0 > 1 or a.y0 > 1) else None
     for c in chunks:
         for u in unrolls:
             for v in vecs:
                 for nt in nts:
-                    tn = ops.StencilTuning(chunk_rows=c, unroll=u, nontemporal=nt, vec=v)
-                    variants[f"march_c{c}_u{u}_v{v}_nt{nt}"] = (
-                        lambda tn=tn: ops.stencil_step(T2, T, iCp, coef, tuning=tn), bytes_model)
+                    for x in xcds:
+                        tn = ops.StencilTuning(chunk_rows=c, unroll=u, nontemporal=nt, vec=v,
+                                               xcd_remap=x)
+                        variants[f"march_c{c}_u{u}_v{v}_nt{nt}_x{x}"] = (
+                            lambda tn=tn: ops.stencil_step(T2, T, iCp, coef, rect, tuning=tn),
+                            bytes_model)
     variants["lds"] = (lambda: ops.stencil_step(T2, T, iCp, coef,
                                                 tuning=ops.StencilTuning(kernel="lds")),
                        bytes_model)
     nn = n * n
-    for nt in (0, 1):
+    for nt in ((0, 1) if not a.no_roof else ()):
         for blocks in (0, 4096, 16384):
             variants[f"roof_copy_nt{nt}_b{blocks}"] = (
                 lambda nt=nt, b=blocks: nat.stream_copy(T2.data_ptr(), T.data_ptr(), nn, s, nt, b),
@@ -103,13 +112,14 @@ def main(argv=None):
         return max((k for k in res if k.startswith(prefix)), key=lambda k: res[k]["GBps_median"])
 
     best = best_of("march")
-    tri, cop = best_of("roof_triad"), best_of("roof_copy")
     doc = {"n": n, "cells": cells, "rounds": a.rounds, "iters": a.iters, "results": res,
            "best_march": best, "best_march_GBps": res[best]["GBps_median"],
-           "best_triad": tri, "triad_GBps": res[tri]["GBps_median"],
-           "best_copy": cop, "copy_GBps": res[cop]["GBps_median"],
-           "best_vs_triad": res[best]["GBps_median"] / res[tri]["GBps_median"],
            "device": torch.cuda.get_device_name(0)}
+    if not a.no_roof:
+        tri, cop = best_of("roof_triad"), best_of("roof_copy")
+        doc.update({"best_triad": tri, "triad_GBps": res[tri]["GBps_median"],
+                    "best_copy": cop, "copy_GBps": res[cop]["GBps_median"],
+                    "best_vs_triad": res[best]["GBps_median"] / res[tri]["GBps_median"]})
     txt = json.dumps(doc, indent=1)
     print(txt)
     if a.out:

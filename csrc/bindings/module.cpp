@@ -97,7 +97,7 @@ PYBIND11_MODULE(_C, m) {
       "stencil_rects",
       [](uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
          const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
-         int kernel, uintptr_t stream, bool gpu, int unroll, int vec) {
+         int kernel, uintptr_t stream, bool gpu, int unroll, int vec, int xcd_remap) {
         auto r = to_rects(rects);
         StencilTuning tn;
         tn.chunk_rows = chunk_rows;
@@ -105,6 +105,7 @@ PYBIND11_MODULE(_C, m) {
         tn.kernel = kernel;
         tn.unroll = unroll;
         tn.vec = vec;
+        tn.xcd_remap = xcd_remap;
         if (gpu)
           stencil_rects_gpu(P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
                             r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
@@ -117,7 +118,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"), py::arg("rects"),
       py::arg("coef"), py::arg("chunk_rows") = 4, py::arg("nontemporal") = 3,
       py::arg("kernel") = 0, py::arg("stream") = 0, py::arg("gpu") = true,
-      py::arg("unroll") = 4, py::arg("vec") = 2);
+      py::arg("unroll") = 4, py::arg("vec") = 2, py::arg("xcd_remap") = 1);
   m.def(
       "stream_copy",
       [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {

@@ -100,6 +100,22 @@ __device__ __forceinline__ void store_row(double* __restrict__ p, const double (
   }
 }
 
+// XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs
+// (block b runs on XCD b % 8; MI355X_MICROARCH.md §Workgroup dispatch). The
+// march tasks are numbered row-chunk-major, strip-group fastest, so
+// vertically adjacent chunks share a halo row and horizontally adjacent ones
+// share edge cache lines. Giving each XCD a CONTIGUOUS 1/8 of the task range
+// keeps both neighbours on the same XCD (same L2) whatever the strip count.
+// Bijective for any grid size (cdna_hip_programming.md "XCD swizzle must be
+// bijective"). Speed only: any mapping computes the same cells.
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nwg) {
+  constexpr int64_t kXcd = 8;
+  if (nwg < kXcd) return b;
+  const int64_t q = nwg / kXcd, r = nwg % kXcd;
+  const int64_t xcd = b % kXcd, slot = b / kXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
 // The canonical cell update (see rma/common.h StencilCoef). Compiled with
 // -ffp-contract=off: every operation rounds exactly as written, in this order.
 __device__ __forceinline__ double cell(double xl, double c, double xr, double up, double dn,
@@ -134,10 +150,11 @@ __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restric
                                                                const double* __restrict__ T,
                                                                const double* __restrict__ iCp,
                                                                int64_t nx, RectList L,
-                                                               StencilCoef k, int chunk_rows) {
+                                                               StencilCoef k, int chunk_rows,
+                                                               int remap) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t b = blockIdx.x;
+  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   int ri = 0;
   while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;  // wave-uniform, <= 8 steps
   const int64_t bstart = ri ? L.block_end[ri - 1] : 0;
@@ -217,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void stencil_lds_kernel(double* __restrict_
                                                              int64_t nx, RectList L,
                                                              StencilCoef k) {
   __shared__ double tile[kTileY + 2][kTileX + 2];
-  const int64_t b = blockIdx.x;
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
   int ri = 0;
   while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
   const int64_t bstart = ri ? L.block_end[ri - 1] : 0;
@@ -329,11 +346,11 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
     const bool ntt = (tune.nontemporal >> 2) & 1;  // bit 2: also T loads (implies 1|2)
 #define RMA_MARCH(VV, UU, NTS, NTL)                                                  \
   stencil_march_kernel<VV, NTS, UU, NTL><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, \
-                                                                 tune.chunk_rows)
+                                                                 tune.chunk_rows, tune.xcd_remap)
 #define RMA_MARCH_NT(VV, UU)                                                            \
   if (ntt) {                                                                            \
-    stencil_march_kernel<VV, true, UU, true, true><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, \
-                                                                       tune.chunk_rows); \
+    stencil_march_kernel<VV, true, UU, true, true><<<grid, block, 0, s>>>(                \
+        T2, T, iCp, nx, L, c, tune.chunk_rows, tune.xcd_remap);                           \
   } else if (nts) {                                                                     \
     if (ntl) RMA_MARCH(VV, UU, true, true);                                              \
     else RMA_MARCH(VV, UU, true, false);                                                 \

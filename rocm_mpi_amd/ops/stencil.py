@@ -53,6 +53,7 @@ class StencilTuning:
     kernel: str = "march"
     unroll: int = 4
     vec: int = 2
+    xcd_remap: int = 1
 
 
 @dataclass
@@ -155,7 +156,7 @@ def stencil_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: Ste
     if T.is_cuda:
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                tn.chunk_rows, int(tn.nontemporal), KERNELS[tn.kernel],
-                               stream_handle(T), True, tn.unroll, tn.vec)
+                               stream_handle(T), True, tn.unroll, tn.vec, tn.xcd_remap)
     elif _use_native_cpu():
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                64, 0, 0, 0, False)
