@@ -47,6 +47,7 @@ struct RectList {
   int64_t strips[kMaxRects];
   int64_t chunks[kMaxRects];
   int64_t block_end[kMaxRects];  // inclusive prefix sum of blocks per rect
+  int64_t gpad[kMaxRects];       // >0: row-aligned mapping with gpad blocks per chunk row
   int n;
 };
 
@@ -159,11 +160,24 @@ __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restric
   while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;  // wave-uniform, <= 8 steps
   const int64_t bstart = ri ? L.block_end[ri - 1] : 0;
   const int64_t nstrips = L.strips[ri];
-  const int64_t task = (b - bstart) * kWavesPerBlock + wave;
-  if (task >= nstrips * L.chunks[ri]) return;  // whole wave exits together
+  int64_t strip, chunk;
+  if (L.gpad[ri] > 0) {
+    // wide rect: one block row per chunk row, padded to a multiple of 8 blocks so
+    // the chunk below runs on the same XCD (shares its halo row through L2)
+    // while the whole chip still streams one compact band of rows
+    const int64_t lb = b - bstart;
+    chunk = lb / L.gpad[ri];
+    strip = (lb % L.gpad[ri]) * kWavesPerBlock + wave;
+    if (strip >= nstrips) return;  // padding / last partial group
+  } else {
+    // narrow rect (< 4 strips, e.g. perf_hide x-frames): the block's waves take
+    // consecutive chunks so none idles
+    const int64_t task = (b - bstart) * kWavesPerBlock + wave;
+    if (task >= nstrips * L.chunks[ri]) return;  // whole wave exits together
+    strip = task % nstrips;
+    chunk = task / nstrips;
+  }
   const Rect r = L.r[ri];
-  const int64_t strip = task % nstrips;
-  const int64_t chunk = task / nstrips;
   const int64_t xs = L.xa[ri] + strip * (kWave * V);
   const int64_t ya = r.y0 + chunk * chunk_rows;
   const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
@@ -325,7 +339,14 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
       L.xa[n] = r.x0 - (r.x0 % V);
       L.strips[n] = (r.x1 - L.xa[n] + sw - 1) / sw;
       L.chunks[n] = (r.y1 - r.y0 + tune.chunk_rows - 1) / tune.chunk_rows;
-      blocks = (L.strips[n] * L.chunks[n] + kWavesPerBlock - 1) / kWavesPerBlock;
+      if (L.strips[n] >= kWavesPerBlock && !tune.xcd_remap) {
+        const int64_t groups = (L.strips[n] + kWavesPerBlock - 1) / kWavesPerBlock;
+        L.gpad[n] = (groups + 7) / 8 * 8;
+        blocks = L.gpad[n] * L.chunks[n];
+      } else {
+        L.gpad[n] = 0;
+        blocks = (L.strips[n] * L.chunks[n] + kWavesPerBlock - 1) / kWavesPerBlock;
+      }
     }
     total += blocks;
     L.block_end[n] = total;

@@ -53,7 +53,7 @@ class StencilTuning:
     kernel: str = "march"
     unroll: int = 4
     vec: int = 2
-    xcd_remap: int = 1
+    xcd_remap: int = 0
 
 
 @dataclass

@@ -6,7 +6,7 @@ echo "== pytest gpu (kernels only)"
 timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py tests/test_executor_gpu.py -q -x > gpurun_out/pytest_gpu_k.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_gpu_k.log
 case $rc in 0) ;; 1) grep -E "^(FAILED|ERROR)" gpurun_out/pytest_gpu_k.log | head; exit 1;; *) exit $rc;; esac
 echo "== sweep 16k fused + interior-like rect"
-timeout -k 10 300 python bench/stencil_sweep.py --n 16384 --rounds 3 --iters 8 --chunks 4,8 --unrolls 4 --nts 3 --xcds 0,1 --vecs 2,4 --out gpurun_out/sweep16k_xcd.json > gpurun_out/sweep16k_xcd.log 2>&1 || { tail -20 gpurun_out/sweep16k_xcd.log; exit 1; }
+timeout -k 10 300 python bench/stencil_sweep.py --n 16384 --rounds 3 --iters 8 --chunks 4,8 --unrolls 4 --nts 3 --xcds 0,1 --vecs 2 --out gpurun_out/sweep16k_xcd.json > gpurun_out/sweep16k_xcd.log 2>&1 || { tail -20 gpurun_out/sweep16k_xcd.log; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/sweep16k_xcd.json')); r=d['results']; [print(k, round(r[k]['GBps_median'])) for k in sorted(r, key=lambda k:-r[k]['GBps_median'])[:14]]"
 timeout -k 10 300 python bench/stencil_sweep.py --n 16384 --x0 128 --y0 5 --no-roof --rounds 3 --iters 8 --chunks 4,8 --unrolls 4 --nts 3 --xcds 0,1 --vecs 2 --out gpurun_out/sweep16k_int.json > gpurun_out/sweep16k_int.log 2>&1 || { tail -20 gpurun_out/sweep16k_int.log; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/sweep16k_int.json')); r=d['results']; [print('interior', k, round(r[k]['GBps_median'])) for k in sorted(r, key=lambda k:-r[k]['GBps_median'])]"
