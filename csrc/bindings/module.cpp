@@ -118,7 +118,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"), py::arg("rects"),
       py::arg("coef"), py::arg("chunk_rows") = 4, py::arg("nontemporal") = 3,
       py::arg("kernel") = 0, py::arg("stream") = 0, py::arg("gpu") = true,
-      py::arg("unroll") = 4, py::arg("vec") = 2, py::arg("xcd_remap") = 0);
+      py::arg("unroll") = 4, py::arg("vec") = 2, py::arg("xcd_remap") = -1);
   m.def(
       "stream_copy",
       [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {

@@ -31,8 +31,8 @@ struct StencilTuning {
   int kernel = 0;          // 0 = register march (default), 1 = LDS-tiled
   int unroll = 4;          // rows per march iteration whose loads are issued together
   int vec = 2;             // cells per lane (2: one 16-B access per row, 4: two)
-  int xcd_remap = 0;       // 1: each XCD takes a contiguous 1/8 of the tasks; 0 (default):
-                           // chunk rows padded to 8-block multiples (same-XCD neighbours)
+  int xcd_remap = -1;      // 1: each XCD takes a contiguous 1/8 of the tasks; 0: chunk rows
+                           // padded to 8-block multiples (same-XCD neighbours); -1: by size
 };
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,

@@ -320,6 +320,10 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
                        ((reinterpret_cast<uintptr_t>(T2) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
   const int V = aligned ? stencil_vec(nx, tune) : 1;
+  // Block order (measured, profiles/SUMMARY_r1.md): chip-wide row bands with
+  // 8-padded block rows win up to 64K-wide tiles (16384^2: 6.44 vs 6.26 TB/s);
+  // per-XCD contiguous ranges win on the 288 GB tiles (101376^2: 6.25 vs 5.93).
+  const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   const bool lds = tune.kernel == 1;
   RectList L{};
   int64_t total = 0;
@@ -339,7 +343,7 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
       L.xa[n] = r.x0 - (r.x0 % V);
       L.strips[n] = (r.x1 - L.xa[n] + sw - 1) / sw;
       L.chunks[n] = (r.y1 - r.y0 + tune.chunk_rows - 1) / tune.chunk_rows;
-      if (L.strips[n] >= kWavesPerBlock && !tune.xcd_remap) {
+      if (L.strips[n] >= kWavesPerBlock && !remap) {
         const int64_t groups = (L.strips[n] + kWavesPerBlock - 1) / kWavesPerBlock;
         L.gpad[n] = (groups + 7) / 8 * 8;
         blocks = L.gpad[n] * L.chunks[n];
@@ -367,11 +371,11 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
     const bool ntt = (tune.nontemporal >> 2) & 1;  // bit 2: also T loads (implies 1|2)
 #define RMA_MARCH(VV, UU, NTS, NTL)                                                  \
   stencil_march_kernel<VV, NTS, UU, NTL><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c, \
-                                                                 tune.chunk_rows, tune.xcd_remap)
+                                                                 tune.chunk_rows, remap)
 #define RMA_MARCH_NT(VV, UU)                                                            \
   if (ntt) {                                                                            \
     stencil_march_kernel<VV, true, UU, true, true><<<grid, block, 0, s>>>(                \
-        T2, T, iCp, nx, L, c, tune.chunk_rows, tune.xcd_remap);                           \
+        T2, T, iCp, nx, L, c, tune.chunk_rows, remap);                           \
   } else if (nts) {                                                                     \
     if (ntl) RMA_MARCH(VV, UU, true, true);                                              \
     else RMA_MARCH(VV, UU, true, false);                                                 \

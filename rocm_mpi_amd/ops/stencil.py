@@ -53,7 +53,7 @@ class StencilTuning:
     kernel: str = "march"
     unroll: int = 4
     vec: int = 2
-    xcd_remap: int = 0
+    xcd_remap: int = -1  # -1: chosen by tile width (see csrc/kernels/stencil.hip)
 
 
 @dataclass
