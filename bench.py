@@ -45,7 +45,7 @@ def parse(argv=None):
                     help="fraction of free HBM for T, T2, 1/Cp when auto-sizing")
     ap.add_argument("--max-tile", type=int, default=0, help="cap auto-sized edge (0 = none)")
     ap.add_argument("--dims", default="0,0", help="process grid dimx,dimy (0 = auto)")
-    ap.add_argument("--b-width", default="32,4")
+    ap.add_argument("--b-width", default="1,1")
     ap.add_argument("--chunk-rows", type=int, default=4)
     ap.add_argument("--kernel", default="march", choices=["march", "lds"])
     ap.add_argument("--unroll", type=int, default=4)

@@ -314,8 +314,8 @@ PYBIND11_MODULE(_C, m) {
            }),
            py::arg("T"), py::arg("T2"), py::arg("iCp"), py::arg("nx"), py::arg("ny"),
            py::arg("mode"), py::arg("coef"), py::arg("chunk_rows") = 4,
-           py::arg("nontemporal") = 3, py::arg("kernel") = 0, py::arg("bwx") = 127,
-           py::arg("bwy") = 4, py::arg("use_graph") = 0, py::arg("graph_steps") = 0,
+           py::arg("nontemporal") = 3, py::arg("kernel") = 0, py::arg("bwx") = 1,
+           py::arg("bwy") = 1, py::arg("use_graph") = 0, py::arg("graph_steps") = 0,
            py::arg("halo").none(true) = nullptr, py::arg("qx") = 0, py::arg("qy") = 0,
            py::arg("dTdt") = 0, py::arg("unroll") = 4, py::arg("vec") = 2,
            py::keep_alive<1, 16>())

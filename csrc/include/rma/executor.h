@@ -33,7 +33,7 @@ struct ExecParams {
   Mode mode = Mode::kPerf;
   StencilCoef coef{};
   StencilTuning tune{};
-  int64_t bwx = 127, bwy = 4;  // perf_hide frame widths (x rounded to a strip)
+  int64_t bwx = 1, bwy = 1;    // perf_hide frame widths (cells beyond the boundary)
   int use_graph = 0;           // capture steps into a hipGraph and replay
   int graph_steps = 0;         // steps per captured graph (even; 0 = auto)
 };

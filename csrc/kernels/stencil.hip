@@ -39,6 +39,7 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int64_t kColMaxWidth = 8;  // rects at most this wide run in column mode
 typedef double dbl2 __attribute__((ext_vector_type(2)));  // native 16-byte vector
 
 struct RectList {
@@ -47,7 +48,8 @@ struct RectList {
   int64_t strips[kMaxRects];
   int64_t chunks[kMaxRects];
   int64_t block_end[kMaxRects];  // inclusive prefix sum of blocks per rect
-  int64_t gpad[kMaxRects];       // >0: row-aligned mapping with gpad blocks per chunk row
+  int64_t gpad[kMaxRects];       // >0: row-aligned mapping with gpad blocks per chunk row,
+                                 // 0: linear task mapping, -1: column mode (thin rects)
   int n;
 };
 
@@ -159,6 +161,26 @@ __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restric
   int ri = 0;
   while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;  // wave-uniform, <= 8 steps
   const int64_t bstart = ri ? L.block_end[ri - 1] : 0;
+  if (L.gpad[ri] < 0) {
+    // column mode for thin rects (perf_hide x-frames, a few cells wide): one
+    // thread per row, scalar loads; a 128-cell wave strip would load 64x the
+    // bytes it updates. The whole block takes this branch (uniform).
+    const Rect r = L.r[ri];
+    const int64_t y = r.y0 + (b - bstart) * kBlock + threadIdx.x;
+    if (y >= r.y1) return;
+    const double* up = T + (y - 1) * nx;
+    const double* cu = T + y * nx;
+    const double* dn = T + (y + 1) * nx;
+    for (int64_t xx = r.x0; xx < r.x1; ++xx) {
+      const double v = cell(cu[xx - 1], cu[xx], cu[xx + 1], up[xx], dn[xx], iCp[y * nx + xx], k);
+      if constexpr (NT) {
+        __builtin_nontemporal_store(v, T2 + y * nx + xx);
+      } else {
+        T2[y * nx + xx] = v;
+      }
+    }
+    return;
+  }
   const int64_t nstrips = L.strips[ri];
   int64_t strip, chunk;
   if (L.gpad[ri] > 0) {
@@ -343,7 +365,10 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
       L.xa[n] = r.x0 - (r.x0 % V);
       L.strips[n] = (r.x1 - L.xa[n] + sw - 1) / sw;
       L.chunks[n] = (r.y1 - r.y0 + tune.chunk_rows - 1) / tune.chunk_rows;
-      if (L.strips[n] >= kWavesPerBlock && !remap) {
+      if (r.x1 - r.x0 <= kColMaxWidth && r.y1 - r.y0 > r.x1 - r.x0) {
+        L.gpad[n] = -1;  // thin column: one thread per row
+        blocks = (r.y1 - r.y0 + kBlock - 1) / kBlock;
+      } else if (L.strips[n] >= kWavesPerBlock && !remap) {
         const int64_t groups = (L.strips[n] + kWavesPerBlock - 1) / kWavesPerBlock;
         L.gpad[n] = (groups + 7) / 8 * 8;
         blocks = L.gpad[n] * L.chunks[n];

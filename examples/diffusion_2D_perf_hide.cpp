@@ -96,7 +96,7 @@ int main(int argc, char** argv) {
   CK(rma_init_gaussian(g, T, n, n, dx, dy, lx, ly, s));
   HK(hipMemcpyAsync(T2, T, bytes, hipMemcpyDeviceToDevice, s));
   rma_executor* ex = nullptr;
-  CK(rma_executor_create(g, mode, T, T2, iCp, n, n, coef, 32, 4, nullptr, nullptr, nullptr, &ex));
+  CK(rma_executor_create(g, mode, T, T2, iCp, n, n, coef, 1, 1, nullptr, nullptr, nullptr, &ex));
   if (me == 0)
     std::printf("Global grid: %ldx%ldx1 (nprocs: %d, dims: %dx%dx%d)\n", (long)rma_nx_g(g),
                 (long)rma_ny_g(g), size, dims[0], dims[1], dims[2]);

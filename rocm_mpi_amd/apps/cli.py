@@ -19,9 +19,9 @@ DEFAULTS = {
     "ap": dict(nx=128, ny=128, nt=1000, do_vis=True),                      # ap.jl:15-16
     "kp": dict(nx=128, ny=128, nt=1000, do_vis=True),                      # kp.jl:62-65
     "perf": dict(nx=12 * 1024, ny=12 * 1024, nt=1000, do_vis=False),       # perf.jl:21-25
-    "perf_hide": dict(nx=12 * 1024, ny=12 * 1024, nt=100, b_width=(32, 4),  # perf_hide.jl:37-43
+    "perf_hide": dict(nx=12 * 1024, ny=12 * 1024, nt=100,                   # perf_hide.jl:37-43
                       do_vis=False),
-    "perf_hide_prof": dict(nx=8 * 1024, ny=8 * 1024, nt=300, b_width=(32, 8),  # _prof.jl:71-77
+    "perf_hide_prof": dict(nx=8 * 1024, ny=8 * 1024, nt=300,               # _prof.jl:71-77
                            do_vis=False, profile=True),
 }
 
@@ -50,7 +50,8 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--ny", type=int, default=d["ny"])
     ap.add_argument("--nt", type=int, default=d["nt"], help="time steps (first 10 untimed)")
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--b-width", type=_pair, default=d.get("b_width", (32, 4)))
+    ap.add_argument("--b-width", type=_pair, default=d.get("b_width", (1, 1)),
+                    help="perf_hide frame width in cells (reference default 32,4)")
     ap.add_argument("--dims", type=_pair, default=(0, 0), help="process grid dimx,dimy")
     ap.add_argument("--periods", type=_pair, default=(0, 0))
     ap.add_argument("--init", choices=["gaussian", "random"], default="gaussian")

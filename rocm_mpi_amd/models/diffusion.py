@@ -55,7 +55,7 @@ class DiffusionConfig:
     ly: float = 10.0
     lam: float = 1.0
     Cp0: float = 1.0
-    b_width: tuple = (32, 4)  # perf_hide frame widths (x rounded up to a wave-strip)
+    b_width: tuple = (1, 1)  # perf_hide frame widths (the send planes need 1)
     init: str = "gaussian"  # gaussian | random
     init_on: str = "auto"  # auto | device | host
     seed: int = 1234

@@ -177,15 +177,15 @@ def hide_rects(nx: int, ny: int, bwx: int, bwy: int,
                vec: int = 2) -> tuple[list[Rect], Rect | None]:
     """Frame rects and interior rect of the boundary/interior split.
 
-    The x-frame is rounded up so the interior starts on a wave-strip boundary
-    (the reference's b_width=(32,4), perf_hide.jl:42, is a thread-block
-    multiple; ours is a wave-strip multiple). Mirrors DiffusionExecutor.
+    The frame holds the send planes (x = 1, nx-2; y = 1, ny-2): width 1 is
+    enough. The reference uses b_width=(32,4) (perf_hide.jl:42) because its
+    masks run on whole thread blocks; thin x-frames here run in the kernel's
+    column mode. Mirrors DiffusionExecutor. ``vec`` is accepted for API
+    stability (the split no longer depends on the strip width).
     """
     if bwx < 1 or bwy < 1:
         raise ValueError("b_width must be >= 1 so the send planes are computed first")
-    s = strip_cells(nx, vec)
-    xi0 = -(-(1 + bwx) // s) * s
-    xi1 = (nx - 1 - bwx) // s * s
+    xi0, xi1 = 1 + bwx, nx - 1 - bwx
     yi0, yi1 = 1 + bwy, ny - 1 - bwy
     full = interior_rect(nx, ny)
     if xi0 >= xi1 or yi0 >= yi1:

@@ -57,6 +57,20 @@ def test_stencil_variants_and_rect_lists(kernel, nt):
     assert torch.equal(full.cpu(), ref)
 
 
+@pytest.mark.parametrize("w", [1, 2, 3, 8, 9])
+def test_stencil_thin_column_rects(w):
+    """Rects at most 8 cells wide run in column mode (one thread per row)."""
+    ny, nx = 700, 300
+    T = rand((ny, nx), 11)
+    iCp = rand((ny, nx), 12) + 0.5
+    rects = [(1, 1 + w, 2, ny - 2), (nx - 1 - w, nx - 1, 3, ny - 1), (150, 150 + w, 1, 40)]
+    out = torch.zeros_like(T)
+    ops.stencil_step(out, T, iCp, coef(), rects)
+    ref = torch.zeros((ny, nx), dtype=torch.float64)
+    ops.stencil_torch(ref, T.cpu(), iCp.cpu(), coef(), rects)
+    assert torch.equal(out.cpu(), ref)
+
+
 def test_stencil_unaligned_pointer_path():
     # a view starting one element in: 8-byte aligned only -> scalar (V=1) path
     base = rand(64 * 200 + 1, 5)
