@@ -1,0 +1,130 @@
+"""Entry points, launcher, checkpoint/resume, PNG output, C ABI (CPU side)."""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+import golden
+from helpers import ROOT, run_loopback
+from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+from rocm_mpi_amd.parallel import implicit_grid as gg
+from rocm_mpi_amd.utils import checkpoint, vis
+
+
+def run(cmd, timeout=300, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
+
+
+def test_app_ap_cpu_writes_png_and_reference_line(tmp_path):
+    r = run([sys.executable, "-m", "rocm_mpi_amd.apps.diffusion_2D_ap", "--device", "cpu",
+             "--nt", "60", "--outdir", str(tmp_path), "--json"])
+    assert r.returncode == 0, r.stderr
+    assert "Executed 60 steps in = " in r.stdout and "GB/s" in r.stdout
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["variant"] == "ap" and rec["timed_steps"] == 50
+    png = tmp_path / "Temp_ap_1_128_128.png"
+    data = png.read_bytes()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+
+
+def test_launcher_runs_four_ranks_and_matches_oracle(tmp_path):
+    r = run([sys.executable, "-m", "rocm_mpi_amd.launch", "-n", "4", "-m",
+             "rocm_mpi_amd.apps.diffusion_2D_perf", "--", "--nx", "128", "--ny", "128",
+             "--device", "cpu", "--transport", "gloo", "--vis", "--outdir", str(tmp_path)],
+            timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "maximum(T_v) = 0.39786473026690" in r.stdout
+    assert (tmp_path / "Temp_perf_4_254_254.png").exists()
+
+
+def test_launcher_kills_job_when_a_rank_fails():
+    code = "import os,sys,time; r=int(os.environ['RANK']); time.sleep(0.2 if r==1 else 30); sys.exit(3 if r==1 else 0)"
+    script = os.path.join(ROOT, "build", "fail_rank.py")
+    os.makedirs(os.path.dirname(script), exist_ok=True)
+    open(script, "w").write(code)
+    r = run([sys.executable, "-m", "rocm_mpi_amd.launch", "-n", "3", script], timeout=60)
+    assert r.returncode == 3
+    assert "terminating the job" in r.stderr
+
+
+def test_presets_and_cli_flags():
+    from rocm_mpi_amd.apps import cli
+
+    p = cli.build_parser("perf_hide")
+    a = p.parse_args([])
+    assert (a.nx, a.ny, a.nt) == (12288, 12288, 100)  # perf_hide.jl:37-43
+    a = cli.build_parser("perf_hide_prof").parse_args([])
+    assert (a.nx, a.nt, a.profile) == (8192, 300, True)
+    assert set(cli.PRESETS) == {"ap256_cpu", "kp16k", "perf_2x1", "hide_2x2", "hide_4x2_288GB"}
+
+
+def test_checkpoint_resume_is_bitwise(tmp_path):
+    cfg = dict(variant="perf", nx=40, ny=30, nt=10, quiet=True, init="random", device="cpu")
+    m = Diffusion2D(DiffusionConfig(**cfg))
+    m.step(10)
+    checkpoint.save_checkpoint(m, str(tmp_path / "ck"))
+    m.step(7)
+    want = m.field.clone()
+    m.close()
+    m2 = Diffusion2D(DiffusionConfig(**cfg))
+    meta = checkpoint.load_checkpoint(m2, str(tmp_path / "ck"))
+    assert meta["steps_done"] == 10 and m2.steps_done == 10
+    m2.step(7)
+    assert torch.equal(m2.field, want)
+    m2.close()
+    m3 = Diffusion2D(DiffusionConfig(**dict(cfg, nx=42)))
+    with pytest.raises(ValueError):
+        checkpoint.load_checkpoint(m3, str(tmp_path / "ck"))
+    m3.close()
+
+
+def test_vis_png_roundtrip(tmp_path):
+    f = torch.linspace(0, 1, 50 * 80, dtype=torch.float64).reshape(50, 80)
+    info = vis.heatmap_png(f, str(tmp_path / "a.png"))
+    raw = (tmp_path / "a.png").read_bytes()
+    assert raw[12:16] == b"IHDR"
+    w, h = int.from_bytes(raw[16:20], "big"), int.from_bytes(raw[20:24], "big")
+    assert h == 50 and w > 80
+    assert info["min"] == 0.0 and info["max"] == 1.0
+
+
+def test_nan_guard_raises():
+    m = Diffusion2D(DiffusionConfig(variant="perf", nx=20, ny=20, nt=5, quiet=True, device="cpu",
+                                    check_every=2))
+    m.field[5, 5] = float("nan")
+    with pytest.raises(FloatingPointError):
+        m._advance(4)
+    m.close()
+
+
+def test_c_abi_topology_and_geometry():
+    """The C ABI of librma_core.so (what the Julia shim calls), single rank."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "rocm_mpi_amd", "librma_core.so"))
+    assert lib is not None
+    lib.rma_nx_g.restype = ctypes.c_int64
+    lib.rma_x_g.restype = ctypes.c_double
+    lib.rma_x_g.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_int64]
+    lib.rma_last_error.restype = ctypes.c_char_p
+    # init needs a device (hipSetDevice); on a CPU-only host it must fail cleanly
+    g = ctypes.c_void_p()
+    me = ctypes.c_int()
+    dims = (ctypes.c_int * 3)()
+    coords = (ctypes.c_int * 3)()
+    rc = lib.rma_init_global_grid(10, 8, 1, None, None, None, None, 1, 0, None, 0,
+                                  ctypes.byref(g), ctypes.byref(me), dims, coords)
+    if torch.cuda.is_available():
+        assert rc == 0
+        assert lib.rma_nx_g(g) == 10 and list(dims) == [1, 1, 1]
+        assert lib.rma_x_g(g, 3, 0.5, 10) == 1.5
+        assert lib.rma_finalize_global_grid(g) == 0
+    else:
+        assert rc != 0 and b"HIP" in lib.rma_last_error()

@@ -140,3 +140,26 @@ def spmd_nohalo(rank, hub):
 
 def test_field_without_halo_is_rejected():
     assert all(run_loopback(4, spmd_nohalo))
+
+
+def spmd_dead_peer(rank, hub):
+    gg.init_global_grid(9, 7, 1, dimx=2, quiet=True, loopback=(hub, rank), select_device=False)
+    try:
+        if rank == 1:
+            return "died"  # never joins the exchange
+        A = torch.zeros(7, 9, dtype=torch.float64)
+        try:
+            update_halo_(A)
+        except RuntimeError as e:
+            return str(e)
+        return "no error"
+    finally:
+        gg.finalize_global_grid()
+
+
+def test_dead_peer_times_out_instead_of_hanging():
+    """Failure detection: a missing peer raises after the
+    transport timeout rather than blocking forever."""
+    out = run_loopback(2, spmd_dead_peer, timeout=2)
+    assert out[1] == "died"
+    assert "no message from 1" in out[0]
