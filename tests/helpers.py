@@ -35,7 +35,7 @@ def run_loopback(n, fn, *args, timeout=120, **kw):
     for t in th:
         t.start()
     for t in th:
-        t.join(timeout)
+        t.join(timeout + 60)
     if err:
         r, e, tb = err[0]
         raise AssertionError(f"rank {r} failed: {e}\n{tb}")
