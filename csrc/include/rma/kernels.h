@@ -48,18 +48,24 @@ int stencil_strip_cells(int64_t nx, const StencilTuning& tune);
 
 // ---------------------------------------------------------------------------
 // kp: the three-kernel formulation (K1-K3; scripts/diffusion_2D_kp.jl:16-54).
-//   qx: (ny-2, nx-1)  qy: (ny-1, nx-2)  dTdt: (ny-2, nx-2)
+// QX, QY, D are full (ny, nx) buffers indexed like T (see kp.hip):
+//   QX[y][x] = reference qx[y-1][x]   (rows 1..ny-2, cols 0..nx-2)
+//   QY[y][x] = reference qy[y][x-1]   (rows 0..ny-2, cols 1..nx-2)
+//   D [y][x] = reference dTdt[y-1][x-1] (interior)
+// The GPU versions use 16-byte accesses for even nx and aligned buffers and a
+// scalar path otherwise.
 // ---------------------------------------------------------------------------
-void flux_gpu(double* qx, double* qy, const double* T, int64_t nx, int64_t ny, double mlam,
+void flux_gpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,
               double rdx, double rdy, stream_t stream);
-void residual_gpu(double* dTdt, const double* qx, const double* qy, const double* iCp, int64_t nx,
+void residual_gpu(double* D, const double* QX, const double* QY, const double* iCp, int64_t nx,
                   int64_t ny, double rdx, double rdy, stream_t stream);
-void update_gpu(double* T, const double* dTdt, int64_t nx, int64_t ny, double dt, stream_t stream);
-void flux_cpu(double* qx, double* qy, const double* T, int64_t nx, int64_t ny, double mlam,
+void update_gpu(double* T, const double* D, int64_t nx, int64_t ny, double dt, stream_t stream);
+void flux_cpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,
               double rdx, double rdy);
-void residual_cpu(double* dTdt, const double* qx, const double* qy, const double* iCp, int64_t nx,
+void residual_cpu(double* D, const double* QX, const double* QY, const double* iCp, int64_t nx,
                   int64_t ny, double rdx, double rdy);
-void update_cpu(double* T, const double* dTdt, int64_t nx, int64_t ny, double dt);
+void update_cpu(double* T, const double* D, int64_t nx, int64_t ny, double dt);
+bool kp_native_layout_ok(int64_t nx);
 
 // ---------------------------------------------------------------------------
 // Initial conditions (K9/K10). Device-side so a 288 GB tile never touches the

@@ -44,34 +44,34 @@ void stencil_rects_cpu(double* T2, const double* T, const double* iCp, int64_t n
   }
 }
 
-void flux_cpu(double* qx, double* qy, const double* T, int64_t nx, int64_t ny, double mlam,
+void flux_cpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,
               double rdx, double rdy) {
-  parallel_for(0, ny - 1, 64, [&](int64_t j) {
-    if (j < ny - 2) {
-      const double* r = T + (j + 1) * nx;
-      for (int64_t i = 0; i < nx - 1; ++i) qx[j * (nx - 1) + i] = (mlam * (r[i + 1] - r[i])) * rdx;
-    }
-    for (int64_t i = 0; i < nx - 2; ++i)
-      qy[j * (nx - 2) + i] = (mlam * (T[(j + 1) * nx + i + 1] - T[j * nx + i + 1])) * rdy;
+  parallel_for(0, ny - 1, 64, [&](int64_t y) {
+    const double* r0 = T + y * nx;
+    const double* r1 = r0 + nx;
+    for (int64_t x = 1; x < nx - 1; ++x) QY[y * nx + x] = (mlam * (r1[x] - r0[x])) * rdy;
+    if (y >= 1)
+      for (int64_t x = 0; x < nx - 1; ++x) QX[y * nx + x] = (mlam * (r0[x + 1] - r0[x])) * rdx;
   });
 }
 
-void residual_cpu(double* dTdt, const double* qx, const double* qy, const double* iCp, int64_t nx,
+void residual_cpu(double* D, const double* QX, const double* QY, const double* iCp, int64_t nx,
                   int64_t ny, double rdx, double rdy) {
-  parallel_for(0, ny - 2, 64, [&](int64_t j) {
-    for (int64_t i = 0; i < nx - 2; ++i) {
-      const double ddx = (qx[j * (nx - 1) + i + 1] - qx[j * (nx - 1) + i]) * rdx;
-      const double ddy = (qy[(j + 1) * (nx - 2) + i] - qy[j * (nx - 2) + i]) * rdy;
-      dTdt[j * (nx - 2) + i] = iCp[(j + 1) * nx + i + 1] * (-(ddx + ddy));
+  parallel_for(1, ny - 1, 64, [&](int64_t y) {
+    for (int64_t x = 1; x < nx - 1; ++x) {
+      const int64_t o = y * nx + x;
+      const double ddx = (QX[o] - QX[o - 1]) * rdx;
+      const double ddy = (QY[o] - QY[o - nx]) * rdy;
+      D[o] = iCp[o] * (-(ddx + ddy));
     }
   });
 }
 
-void update_cpu(double* T, const double* dTdt, int64_t nx, int64_t ny, double dt) {
-  parallel_for(0, ny - 2, 64, [&](int64_t j) {
-    for (int64_t i = 0; i < nx - 2; ++i) {
-      double* p = T + (j + 1) * nx + i + 1;
-      *p = *p + dt * dTdt[j * (nx - 2) + i];
+void update_cpu(double* T, const double* D, int64_t nx, int64_t ny, double dt) {
+  parallel_for(1, ny - 1, 64, [&](int64_t y) {
+    for (int64_t x = 1; x < nx - 1; ++x) {
+      double* p = T + y * nx + x;
+      *p = *p + dt * D[y * nx + x];
     }
   });
 }

@@ -122,11 +122,16 @@ class Diffusion2D:
         self.T2 = None
         if cfg.variant in ("perf", "perf_hide"):
             self.T2 = self.T.clone()  # perf.jl:36 T2 = copy(T)
-        if cfg.variant in ("kp", "ap"):
+        if cfg.variant == "ap":  # the reference's arrays (ap.jl:22-24), preallocated
             self.qx = torch.zeros((ny - 2, nx - 1), **f64)
-            self.qy = torch.zeros((ny - 2 + 1, nx - 2), **f64)
+            self.qy = torch.zeros((ny - 1, nx - 2), **f64)
             self.dTdt = torch.zeros((ny - 2, nx - 2), **f64)
             self._tmp = torch.zeros((ny - 2, nx - 2), **f64)
+        elif cfg.variant == "kp":  # T-indexed flux/residual buffers (csrc/kernels/kp.hip)
+            self.QX = torch.zeros((ny, nx), **f64)
+            self.QY = torch.zeros((ny, nx), **f64)
+            self.D = torch.zeros((ny, nx), **f64)
+            self.qx, self.qy, self.dTdt = ops.kp_views(self.QX, self.QY, self.D)
         self.parity = 0
         self.steps_done = 0
         self.executor = None
@@ -150,9 +155,9 @@ class Diffusion2D:
                 self.iCp.data_ptr(), nx, ny, _MODE[cfg.variant], tuple(self.coef),
                 cfg.chunk_rows, int(cfg.nontemporal), ops.KERNELS[cfg.kernel], int(bwx), int(bwy),
                 int(use_graph), int(cfg.graph_steps), g.halo,
-                self.qx.data_ptr() if cfg.variant == "kp" else 0,
-                self.qy.data_ptr() if cfg.variant == "kp" else 0,
-                self.dTdt.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
+                self.QX.data_ptr() if cfg.variant == "kp" else 0,
+                self.QY.data_ptr() if cfg.variant == "kp" else 0,
+                self.D.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
                 int(cfg.vec))
         if cfg.variant == "perf_hide":
             self.frame_rects, self.interior = ops.hide_rects(nx, ny, *cfg.b_width, vec=cfg.vec)
@@ -212,9 +217,9 @@ class Diffusion2D:
             if v == "ap":
                 self._step_ap()
             elif v == "kp":
-                ops.flux(self.qx, self.qy, self.T, self.coef.mlam, self.coef.rdx, self.coef.rdy)
-                ops.residual(self.dTdt, self.qx, self.qy, self.iCp, self.coef.rdx, self.coef.rdy)
-                ops.update(self.T, self.dTdt, self.coef.dt)
+                ops.flux(self.QX, self.QY, self.T, self.coef.mlam, self.coef.rdx, self.coef.rdy)
+                ops.residual(self.D, self.QX, self.QY, self.iCp, self.coef.rdx, self.coef.rdy)
+                ops.update(self.T, self.D, self.coef.dt)
                 update_halo_(self.T)
             else:
                 Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)

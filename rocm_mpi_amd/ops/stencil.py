@@ -196,44 +196,53 @@ def hide_rects(nx: int, ny: int, bwx: int, bwy: int,
 
 
 # --------------------------------------------------------------------------
-# kp kernels
+# kp kernels: QX, QY, D are (ny, nx) buffers indexed like T (csrc/kernels/kp.hip)
 # --------------------------------------------------------------------------
-def flux(qx, qy, T, mlam: float, rdx: float, rdy: float) -> None:
+def kp_views(QX: torch.Tensor, QY: torch.Tensor, D: torch.Tensor):
+    """The reference-shaped arrays qx (ny-2, nx-1), qy (ny-1, nx-2), dTdt
+    (ny-2, nx-2) of kp.jl:72-74 as views of the T-indexed buffers."""
+    return QX[1:-1, :-1], QY[:-1, 1:-1], D[1:-1, 1:-1]
+
+
+def _kp_native(t: torch.Tensor) -> bool:
+    return t.is_cuda or _use_native_cpu()
+
+
+def flux(QX, QY, T, mlam: float, rdx: float, rdy: float) -> None:
     check_field("T", T)
     ny, nx = T.shape
-    check_field("qx", qx, (ny - 2, nx - 1), T.device)
-    check_field("qy", qy, (ny - 1, nx - 2), T.device)
-    if T.is_cuda or _use_native_cpu():
-        native().flux(_ptr(qx), _ptr(qy), _ptr(T), nx, ny, mlam, rdx, rdy, stream_handle(T),
+    check_field("QX", QX, (ny, nx), T.device)
+    check_field("QY", QY, (ny, nx), T.device)
+    if _kp_native(T):
+        native().flux(_ptr(QX), _ptr(QY), _ptr(T), nx, ny, mlam, rdx, rdy, stream_handle(T),
                       T.is_cuda)
     else:
-        qx.copy_((mlam * (T[1:-1, 1:] - T[1:-1, :-1])) * rdx)
-        qy.copy_((mlam * (T[1:, 1:-1] - T[:-1, 1:-1])) * rdy)
+        QX[1:-1, :-1] = (mlam * (T[1:-1, 1:] - T[1:-1, :-1])) * rdx
+        QY[:-1, 1:-1] = (mlam * (T[1:, 1:-1] - T[:-1, 1:-1])) * rdy
 
 
-def residual(dTdt, qx, qy, iCp, rdx: float, rdy: float) -> None:
+def residual(D, QX, QY, iCp, rdx: float, rdy: float) -> None:
     check_field("iCp", iCp)
     ny, nx = iCp.shape
-    check_field("dTdt", dTdt, (ny - 2, nx - 2), iCp.device)
-    check_field("qx", qx, (ny - 2, nx - 1), iCp.device)
-    check_field("qy", qy, (ny - 1, nx - 2), iCp.device)
-    if iCp.is_cuda or _use_native_cpu():
-        native().residual(_ptr(dTdt), _ptr(qx), _ptr(qy), _ptr(iCp), nx, ny, rdx, rdy,
+    for name, a in (("D", D), ("QX", QX), ("QY", QY)):
+        check_field(name, a, (ny, nx), iCp.device)
+    if _kp_native(iCp):
+        native().residual(_ptr(D), _ptr(QX), _ptr(QY), _ptr(iCp), nx, ny, rdx, rdy,
                           stream_handle(iCp), iCp.is_cuda)
     else:
-        ddx = (qx[:, 1:] - qx[:, :-1]) * rdx
-        ddy = (qy[1:, :] - qy[:-1, :]) * rdy
-        dTdt.copy_(iCp[1:-1, 1:-1] * (-(ddx + ddy)))
+        ddx = (QX[1:-1, 1:-1] - QX[1:-1, :-2]) * rdx
+        ddy = (QY[1:-1, 1:-1] - QY[:-2, 1:-1]) * rdy
+        D[1:-1, 1:-1] = iCp[1:-1, 1:-1] * (-(ddx + ddy))
 
 
-def update(T, dTdt, dt: float) -> None:
+def update(T, D, dt: float) -> None:
     check_field("T", T)
     ny, nx = T.shape
-    check_field("dTdt", dTdt, (ny - 2, nx - 2), T.device)
-    if T.is_cuda or _use_native_cpu():
-        native().update(_ptr(T), _ptr(dTdt), nx, ny, dt, stream_handle(T), T.is_cuda)
+    check_field("D", D, (ny, nx), T.device)
+    if _kp_native(T):
+        native().update(_ptr(T), _ptr(D), nx, ny, dt, stream_handle(T), T.is_cuda)
     else:
-        T[1:-1, 1:-1] = T[1:-1, 1:-1] + dt * dTdt
+        T[1:-1, 1:-1] = T[1:-1, 1:-1] + dt * D[1:-1, 1:-1]
 
 
 # --------------------------------------------------------------------------

@@ -92,7 +92,7 @@ def test_stencil_rejects_bad_rect():
                                tuple(coef()), 64, 0, 0, 0, True)
 
 
-@pytest.mark.parametrize("ny,nx", [(3, 3), (67, 131), (256, 1024)])
+@pytest.mark.parametrize("ny,nx", [(3, 4), (3, 3), (67, 132), (67, 131), (256, 1024), (101, 514)])
 def test_kp_kernels_bitwise(ny, nx):
     c = coef()
     T = rand((ny, nx), 6)
@@ -100,18 +100,21 @@ def test_kp_kernels_bitwise(ny, nx):
     res = {}
     for dev in (DEV, "cpu"):
         Td, iCpd = T.to(dev).clone(), iCp.to(dev)
-        qx = torch.zeros((ny - 2, nx - 1), dtype=torch.float64, device=dev)
-        qy = torch.zeros((ny - 1, nx - 2), dtype=torch.float64, device=dev)
-        d = torch.zeros((ny - 2, nx - 2), dtype=torch.float64, device=dev)
-        ops.flux(qx, qy, Td, c.mlam, c.rdx, c.rdy)
-        ops.residual(d, qx, qy, iCpd, c.rdx, c.rdy)
-        ops.update(Td, d, c.dt)
-        res[dev] = (qx.cpu(), qy.cpu(), d.cpu(), Td.cpu())
+        QX, QY, D = (torch.zeros((ny, nx), dtype=torch.float64, device=dev) for _ in range(3))
+        ops.flux(QX, QY, Td, c.mlam, c.rdx, c.rdy)
+        ops.residual(D, QX, QY, iCpd, c.rdx, c.rdy)
+        ops.update(Td, D, c.dt)
+        res[dev] = tuple(v.cpu().clone() for v in ops.kp_views(QX, QY, D)) + (Td.cpu(),)
     for a, b in zip(res[DEV], res["cpu"]):
         assert torch.equal(a, b)
+    # the reference-shaped views match the plain formulas of kp.jl:16-54
+    Tc = T.cpu()
+    qx = (c.mlam * (Tc[1:-1, 1:] - Tc[1:-1, :-1])) * c.rdx
+    qy = (c.mlam * (Tc[1:, 1:-1] - Tc[:-1, 1:-1])) * c.rdy
+    assert torch.equal(res[DEV][0], qx) and torch.equal(res[DEV][1], qy)
     # kp == fused stencil
-    fused = T.cpu().clone()
-    ops.stencil_torch(fused, T.cpu(), iCp.cpu(), c, [ops.interior_rect(nx, ny)])
+    fused = Tc.clone()
+    ops.stencil_torch(fused, Tc, iCp.cpu(), c, [ops.interior_rect(nx, ny)])
     assert torch.equal(res[DEV][3], fused)
 
 
