@@ -190,6 +190,11 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
     elif tname == "self":
         comm = C.SelfComm()
     elif tname == "rccl":
+        if local_size == comm_size and "NCCL_SOCKET_IFNAME" not in os.environ:
+            # single node: RCCL only bootstraps over sockets (data moves over
+            # xGMI); pin the bootstrap to loopback so odd container interfaces
+            # cannot stall ncclCommInitRank
+            os.environ["NCCL_SOCKET_IFNAME"] = "lo"
         try:
             comm = C.RcclComm(dev, timeout_s=timeout_s)
         except RuntimeError as e:
