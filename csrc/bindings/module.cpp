@@ -237,12 +237,14 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<std::shared_ptr<LoopbackHub>, int>(), py::arg("hub"), py::arg("rank"));
   py::class_<RcclComm, P2PTransport>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
-      .def(py::init([](int nranks, int rank, py::bytes uid, int device) {
+      .def(py::init([](int nranks, int rank, py::bytes uid, int device, double init_timeout_s) {
              std::string s = uid;
              py::gil_scoped_release nogil;
-             return new RcclComm(nranks, rank, s, device);
+             return new RcclComm(nranks, rank, s, device, init_timeout_s);
            }),
-           py::arg("nranks"), py::arg("rank"), py::arg("uid"), py::arg("device"))
+           py::arg("nranks"), py::arg("rank"), py::arg("uid"), py::arg("device"),
+           py::arg("init_timeout_s") = 0.0)
+      .def_property_readonly("nonblocking", &RcclComm::nonblocking)
       .def_property_readonly("device", &RcclComm::device)
       .def("allreduce",
            [](RcclComm& c, uintptr_t sb, uintptr_t rb, size_t count, DType dt, RedOp op,

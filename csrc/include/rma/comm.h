@@ -9,7 +9,12 @@
 // Failure detection: every RCCL/HIP return code is checked and
 // turned into rma::Error carrying the rank; wait() polls the stream together
 // with ncclCommGetAsyncError and aborts the communicator after a timeout, so a
-// dead peer produces an exception instead of a hang.
+// dead peer produces an exception instead of a hang. With init_timeout_s > 0
+// the communicator is created non-blocking (ncclConfig_t::blocking = 0): the
+// constructor polls ncclCommGetAsyncError and aborts after the timeout, so a
+// rank that never joins cannot hang the others inside ncclCommInitRank; every
+// later RCCL call is settled (polled until it left ncclInProgress) before
+// anything else is enqueued on its stream.
 #pragma once
 
 #include <cstddef>
@@ -28,7 +33,8 @@ enum class RedOp : int { kSum = 0, kMax = 1, kMin = 2, kProd = 3 };
 class RcclComm : public P2PTransport {
  public:
   static std::string unique_id();  // 128 opaque bytes, generate on ONE rank
-  RcclComm(int nranks, int rank, const std::string& uid, int device);
+  RcclComm(int nranks, int rank, const std::string& uid, int device,
+           double init_timeout_s = 0.0);
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -60,12 +66,18 @@ class RcclComm : public P2PTransport {
   void check_async();
   void abort();
   bool aborted() const { return aborted_; }
+  bool nonblocking() const { return nonblocking_; }
 
  private:
+  // Non-blocking communicators: wait until the last call left ncclInProgress.
+  void settle(const char* what);
   int nranks_, rank_, device_;
   void* comm_ = nullptr;  // ncclComm_t
   double* scratch_ = nullptr;  // 2 doubles of device memory for barrier()
   bool aborted_ = false;
+  bool nonblocking_ = false;
+  double timeout_s_ = 0.0;
+  int group_depth_ = 0;  // settle only outside ncclGroupStart/End
 };
 
 int rccl_version();

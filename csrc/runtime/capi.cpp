@@ -7,6 +7,7 @@
 #include <array>
 #include <chrono>
 #include <cstring>
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -98,7 +99,13 @@ int rma_init_global_grid(int nx, int ny, int nz, const int dims[3], const int pe
     RMA_HIP_CHECK(hipSetDevice(device));
     if (nprocs > 1) {
       RMA_CHECK_ARG(unique_id != nullptr, "unique_id required when nprocs > 1");
-      g->comm = std::make_unique<rma::RcclComm>(nprocs, rank, std::string(unique_id, 128), device);
+      // non-blocking init with a timeout (RMA_COMM_TIMEOUT s, default 300)
+      // unless RMA_RCCL_BLOCKING=1
+      const char* tb = std::getenv("RMA_RCCL_BLOCKING");
+      const char* to = std::getenv("RMA_COMM_TIMEOUT");
+      const double init_timeout = (tb && tb[0] == '1') ? 0.0 : (to ? std::atof(to) : 300.0);
+      g->comm = std::make_unique<rma::RcclComm>(nprocs, rank, std::string(unique_id, 128), device,
+                                                init_timeout);
     }
     rma::set_rank_for_errors(rank);
     g->halo = std::make_unique<rma::HaloExchanger>(g->comm.get(), rank, g->topo->neighbors(rank));

@@ -59,7 +59,8 @@ std::string RcclComm::unique_id() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-RcclComm::RcclComm(int nranks, int rank, const std::string& uid, int device)
+RcclComm::RcclComm(int nranks, int rank, const std::string& uid, int device,
+                   double init_timeout_s)
     : nranks_(nranks), rank_(rank), device_(device) {
   RMA_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "rank " << rank << "/" << nranks);
   RMA_CHECK_ARG(uid.size() == sizeof(ncclUniqueId),
@@ -67,10 +68,45 @@ RcclComm::RcclComm(int nranks, int rank, const std::string& uid, int device)
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   RMA_HIP_CHECK(hipSetDevice(device));
-  ncclComm_t c;
-  RMA_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
-  comm_ = c;
+  ncclComm_t c = nullptr;
+  if (init_timeout_s > 0) {
+    nonblocking_ = true;
+    timeout_s_ = init_timeout_s;
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    RMA_NCCL_CHECK(ncclCommInitRankConfig(&c, nranks, id, rank, &cfg));
+    comm_ = c;
+    settle("ncclCommInitRankConfig (did every rank join?)");
+  } else {
+    RMA_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+    comm_ = c;
+  }
   RMA_HIP_CHECK(hipMalloc(&scratch_, 2 * sizeof(double)));
+}
+
+void RcclComm::settle(const char* what) {
+  if (!nonblocking_) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  for (;;) {
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t r = ncclCommGetAsyncError(C(comm_), &st);
+    if (r != ncclSuccess) st = r;
+    if (st == ncclSuccess) return;
+    if (st != ncclInProgress) {
+      abort();
+      throw_error("RCCL asynchronous error", __FILE__, __LINE__,
+                  std::string(what) + ": " + ncclGetErrorString(st));
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > timeout_s_) {
+      abort();
+      throw_error("RCCL timeout", __FILE__, __LINE__,
+                  std::string(what) + " still in progress after " + std::to_string(timeout_s_) +
+                      " s; communicator aborted");
+    }
+    if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
 }
 
 RcclComm::~RcclComm() {
@@ -86,29 +122,40 @@ bool RcclComm::capturable() const {
   return v && v[0] == '1';
 }
 
-void RcclComm::group_start() { RMA_NCCL_CHECK(ncclGroupStart()); }
-void RcclComm::group_end() { RMA_NCCL_CHECK(ncclGroupEnd()); }
+void RcclComm::group_start() {
+  RMA_NCCL_CHECK(ncclGroupStart());
+  ++group_depth_;
+}
+void RcclComm::group_end() {
+  --group_depth_;
+  RMA_NCCL_CHECK(ncclGroupEnd());
+  if (group_depth_ == 0) settle("ncclGroupEnd");
+}
 
 void RcclComm::send(const void* buf, size_t bytes, int peer, stream_t stream) {
   RMA_CHECK_ARG(peer >= 0 && peer < nranks_, "peer " << peer);
   RMA_NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, C(comm_), as_stream(stream)));
+  if (group_depth_ == 0) settle("ncclSend");
 }
 
 void RcclComm::recv(void* buf, size_t bytes, int peer, stream_t stream) {
   RMA_CHECK_ARG(peer >= 0 && peer < nranks_, "peer " << peer);
   RMA_NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, C(comm_), as_stream(stream)));
+  if (group_depth_ == 0) settle("ncclRecv");
 }
 
 void RcclComm::allreduce(const void* sendbuf, void* recvbuf, size_t count, DType dt, RedOp op,
                          stream_t stream) {
   RMA_NCCL_CHECK(
       ncclAllReduce(sendbuf, recvbuf, count, to_nccl(dt), to_nccl(op), C(comm_), as_stream(stream)));
+  settle("ncclAllReduce");
 }
 
 void RcclComm::broadcast(const void* sendbuf, void* recvbuf, size_t count, DType dt, int root,
                          stream_t stream) {
   RMA_NCCL_CHECK(
       ncclBroadcast(sendbuf, recvbuf, count, to_nccl(dt), root, C(comm_), as_stream(stream)));
+  settle("ncclBroadcast");
 }
 
 void RcclComm::gather(const void* sendbuf, void* recvbuf, size_t bytes, int root,
@@ -128,12 +175,14 @@ void RcclComm::gather(const void* sendbuf, void* recvbuf, size_t bytes, int root
     RMA_NCCL_CHECK(ncclSend(sendbuf, bytes, ncclUint8, root, C(comm_), s));
   }
   RMA_NCCL_CHECK(ncclGroupEnd());
+  settle("gather");
 }
 
 void RcclComm::barrier(stream_t stream, double timeout_s) {
   hipStream_t s = as_stream(stream);
   RMA_HIP_CHECK(hipMemsetAsync(scratch_, 0, sizeof(double), s));
   RMA_NCCL_CHECK(ncclAllReduce(scratch_, scratch_ + 1, 1, ncclFloat64, ncclSum, C(comm_), s));
+  settle("barrier");
   wait(stream, timeout_s);
 }
 

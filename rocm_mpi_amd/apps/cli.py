@@ -66,6 +66,7 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--profile", action="store_true", default=d.get("profile", False))
     ap.add_argument("--auto-size", action="store_true",
                     help="size the local tile to fill --hbm-frac of free HBM (288 GB MI355X)")
+    ap.add_argument("--no-auto-size", dest="auto_size", action="store_false")
     ap.add_argument("--hbm-frac", type=float, default=0.80)
     ap.add_argument("--chunk-rows", type=int, default=4)
     ap.add_argument("--unroll", type=int, default=4)
@@ -96,20 +97,25 @@ def run_variant(variant: str, argv=None) -> int:
     from ..parallel import comm as C
     from ..utils import checkpoint as ckpt
 
-    a = build_parser(variant).parse_args(argv)
     base = "perf_hide" if variant == "perf_hide_prof" else variant
+    parser = build_parser(variant)
+    pre, _ = parser.parse_known_args(argv)
+    if pre.preset:  # a preset supplies defaults; explicit flags still win
+        p = dict(PRESETS[pre.preset])
+        pv = p.pop("variant")
+        if pv != base:
+            parser.error(f"preset {pre.preset} is a {pv} configuration, not {base}")
+        if "dims" in p:
+            p["dims"] = tuple(p["dims"][:2])
+        parser.set_defaults(**p)
+    a = parser.parse_args(argv)
     opts = dict(variant=base, nx=a.nx, ny=a.ny, nt=a.nt, warmup=a.warmup, b_width=a.b_width,
                 init=a.init, init_on=a.init_on, seed=a.seed, dims=tuple(a.dims) + (0,),
                 periods=tuple(a.periods) + (0,), transport=a.transport, device=a.device,
                 chunk_rows=a.chunk_rows, unroll=a.unroll, vec=a.vec, kernel=a.kernel,
                 nontemporal=a.nontemporal, use_graph=a.graph, do_vis=a.do_vis, outdir=a.outdir,
                 profile=a.profile, check_every=a.check_every, quiet=a.quiet)
-    auto = a.auto_size
-    if a.preset:
-        p = dict(PRESETS[a.preset])
-        auto = p.pop("auto_size", False) or auto
-        opts.update(p)
-    if auto:
+    if a.auto_size:
         rank, size, _ = C.env_world()
         if size > 1:
             C.init_distributed()

@@ -215,7 +215,10 @@ class RcclComm(Communicator):
             else:
                 uid = store.get(key)
         n.set_rank_for_errors(self.rank)
-        self._c = n.RcclComm(self.size, self.rank, bytes(uid), self.device.index or 0)
+        # non-blocking init + timeout unless RMA_RCCL_BLOCKING=1
+        nb = os.environ.get("RMA_RCCL_BLOCKING", "0") != "1"
+        self._c = n.RcclComm(self.size, self.rank, bytes(uid), self.device.index or 0,
+                             init_timeout_s=timeout_s if nb else 0.0)
         self._scratch = torch.zeros(2, dtype=torch.float64, device=self.device)
 
     @property

@@ -67,6 +67,18 @@ def test_presets_and_cli_flags():
     assert set(cli.PRESETS) == {"ap256_cpu", "kp16k", "perf_2x1", "hide_2x2", "hide_4x2_288GB"}
 
 
+def test_preset_supplies_defaults_flags_win(capsys):
+    from rocm_mpi_amd.apps import cli
+
+    assert cli.run_variant("ap", ["--preset", "ap256_cpu", "--nt", "20", "--nx", "40", "--ny",
+                                  "36", "--quiet", "--no-vis", "--json"]) == 0
+    rec = json.loads([l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1])
+    assert (rec["variant"], rec["nx"], rec["ny"], rec["nt"], rec["device"]) == \
+        ("ap", 40, 36, 20, "cpu")
+    with pytest.raises(SystemExit):  # a perf preset on the kp entry point
+        cli.run_variant("kp", ["--preset", "perf_2x1"])
+
+
 def test_checkpoint_resume_is_bitwise(tmp_path):
     cfg = dict(variant="perf", nx=40, ny=30, nt=10, quiet=True, init="random", device="cpu")
     m = Diffusion2D(DiffusionConfig(**cfg))

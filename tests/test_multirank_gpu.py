@@ -102,9 +102,14 @@ def test_rccl_self_send_periodic(graph):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_rccl_single_rank_collectives():
+@pytest.mark.parametrize("blocking", [False, True])
+def test_rccl_single_rank_collectives(blocking, monkeypatch):
+    """Non-blocking init (default: ncclCommInitRankConfig blocking=0 + polled
+    timeout) and the blocking communicator give the same results."""
+    monkeypatch.setenv("RMA_RCCL_BLOCKING", "1" if blocking else "0")
     me, dims, n, coords, comm = gg.init_global_grid(64, 64, 1, quiet=True, transport="rccl")
     assert comm.name == "rccl"
+    assert comm.native.nonblocking == (not blocking)
     comm.barrier()
     assert comm.allreduce(3.5, "sum") == 3.5
     t = torch.arange(10, dtype=torch.float64, device="cuda")
