@@ -135,6 +135,7 @@ class Diffusion2D:
         self.parity = 0
         self.steps_done = 0
         self.executor = None
+        self.use_graph = False
         use_native = cfg.executor == "native" or (
             cfg.executor == "auto" and dev.type == "cuda" and g.halo is not None)
         if use_native and cfg.variant != "ap":
@@ -159,6 +160,17 @@ class Diffusion2D:
                 self.QY.data_ptr() if cfg.variant == "kp" else 0,
                 self.D.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
                 int(cfg.vec))
+        self._ap_graph = None
+        if cfg.variant == "ap" and cfg.use_graph:
+            # ap on a GPU is ~11 small torch launches per step: replay them from
+            # a captured hipGraph (torch.cuda.CUDAGraph) when the halo exchange
+            # is capturable (1 rank or self copies; RCCL/staged are not)
+            self.use_graph = dev.type == "cuda" and g.halo is not None and g.halo.capturable()
+            if not self.use_graph:
+                import warnings
+
+                warnings.warn(f"hipGraph replay disabled for ap ({dev.type}, {g.transport} "
+                              "transport)", RuntimeWarning, stacklevel=2)
         if cfg.variant == "perf_hide":
             self.frame_rects, self.interior = ops.hide_rects(nx, ny, *cfg.b_width, vec=cfg.vec)
         self.tuning = ops.StencilTuning(cfg.chunk_rows, int(cfg.nontemporal), cfg.kernel,
@@ -213,6 +225,12 @@ class Diffusion2D:
             self.steps_done += n
             return
         v = self.cfg.variant
+        if v == "ap" and getattr(self, "use_graph", False):
+            k = self._ap_graph_len()
+            for _ in range(n // k):
+                self._ap_graph.replay()
+            self.steps_done += n - n % k
+            n %= k
         for _ in range(n):
             if v == "ap":
                 self._step_ap()
@@ -234,6 +252,25 @@ class Diffusion2D:
                                          self.tuning)
                 self.parity ^= 1
             self.steps_done += 1
+
+    def _ap_graph_len(self) -> int:
+        """Capture graph_steps ap steps once (capture does not execute them)."""
+        if self._ap_graph is None:
+            k = max(1, int(self.cfg.graph_steps) or 20)
+            cur = torch.cuda.current_stream(self.device)
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(cur)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side):
+                graph.capture_begin()
+                try:
+                    for _ in range(k):
+                        self._step_ap()
+                finally:
+                    graph.capture_end()
+            cur.wait_stream(side)
+            self._ap_graph, self._ap_graph_steps = graph, k
+        return self._ap_graph_steps
 
     def _step_ap(self) -> None:
         """ap.jl:38-42 as torch expressions (canonical operation order)."""
@@ -316,15 +353,31 @@ class Diffusion2D:
         T_nh = self.field[1:-1, 1:-1].contiguous()
         return gather_(T_nh, None, root)
 
-    def visualise(self) -> dict | None:
+    def visualise(self, max_pixels: int = 2048) -> dict | None:
+        """Gather + heatmap PNG on rank 0 (ap.jl:45-47). Above ``max_pixels``
+        per side (e.g. the 288 GB tiles: ~80 GB of interior per rank) every
+        rank subsamples its interior with the same stride before the gather
+        (SURVEY.md §2.5); maximum(T_v) stays exact (a device reduction)."""
         from ..utils import vis
 
-        T_v = self.gather_interior()
-        if self.g.me != 0:
+        g = self.g
+        inner = self.field[1:-1, 1:-1]
+        extent = max(inner.shape[1] * g.dims[0], inner.shape[0] * g.dims[1])
+        stride = max(1, -(-extent // max_pixels))
+        if stride == 1:
+            T_v = self.gather_interior()
+            tmax = None
+        else:
+            T_v = gather_(inner[::stride, ::stride].contiguous(), None, 0)
+            tmax = g.comm.allreduce(float(inner.amax()), "max")
+        if g.me != 0:
             return None
         name = {"perf_hide": "hide"}.get(self.cfg.variant, self.cfg.variant)
         path = vis.output_name(name, self.g.nprocs, gg.nx_g(), gg.ny_g(), self.cfg.outdir)
         info = vis.heatmap_png(T_v, path)
+        info["stride"] = stride
+        if tmax is not None:
+            info["max"] = tmax
         if not self.cfg.quiet:
             print(f"maximum(T_v) = {info['max']}", flush=True)  # perf_hide.jl:115
         return info
@@ -332,5 +385,6 @@ class Diffusion2D:
     def close(self) -> None:
         self.synchronize()
         self.executor = None
+        self._ap_graph = None
         if self._owns_grid:
             gg.finalize_global_grid()

@@ -109,6 +109,22 @@ def test_vis_png_roundtrip(tmp_path):
     assert info["min"] == 0.0 and info["max"] == 1.0
 
 
+def test_visualise_subsamples_large_tiles(tmp_path):
+    """Above max_pixels per side every rank subsamples before the gather; the
+    printed maximum stays the exact maximum over the full interior."""
+    m = Diffusion2D(DiffusionConfig(variant="perf", nx=130, ny=70, nt=3, quiet=True,
+                                    device="cpu", init="random", outdir=str(tmp_path)))
+    m.step(3)
+    exact = float(m.field[1:-1, 1:-1].max())
+    full = m.visualise()
+    sub = m.visualise(max_pixels=40)
+    m.close()
+    assert full["stride"] == 1 and sub["stride"] == 4
+    assert full["max"] == exact and sub["max"] == exact
+    raw = (tmp_path / "Temp_perf_1_130_70.png").read_bytes()
+    assert int.from_bytes(raw[20:24], "big") == 17  # ceil(68 / 4) rows
+
+
 def test_nan_guard_raises():
     m = Diffusion2D(DiffusionConfig(variant="perf", nx=20, ny=20, nt=5, quiet=True, device="cpu",
                                     check_every=2))

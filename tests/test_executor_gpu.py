@@ -41,14 +41,22 @@ def test_variants_agree_on_gpu():
         assert torch.equal(run(v, "cuda:0", nx=514, ny=260), ref)
 
 
-def test_ap_on_gpu_matches_cpu():
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("periods", [(0, 0, 0), (1, 1, 0)])
+def test_ap_on_gpu_matches_cpu(graph, periods):
+    """ap as torch ops on the GPU (eager, or replayed from a captured hipGraph in
+    blocks of 7 steps + an eager remainder) == the CPU run, bitwise."""
     g = Diffusion2D(DiffusionConfig(variant="ap", nx=130, ny=131, nt=25, device="cuda:0",
-                                    quiet=True, init="random"))
-    g.step(25)
+                                    quiet=True, init="random", use_graph=graph, graph_steps=7,
+                                    periods=periods))
+    assert g.use_graph == graph
+    g.step(11)
+    g.step(14)
+    assert g.steps_done == 25
     fg = g.field.cpu().clone()
     g.close()
     c = Diffusion2D(DiffusionConfig(variant="ap", nx=130, ny=131, nt=25, device="cpu",
-                                    quiet=True, init="random"))
+                                    quiet=True, init="random", periods=periods))
     c.step(25)
     fc = c.field.clone()
     c.close()
