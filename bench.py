@@ -53,6 +53,11 @@ def parse(argv=None):
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
+    ap.add_argument("--temporal", type=int, default=1, choices=[1, 2],
+                    help="2: two time steps per kernel pass (register temporal blocking, "
+                         "bitwise identical), width-2 halo exchange per pass, grid overlap 4")
+    ap.add_argument("--chunk2", type=int, default=16, help="two-step kernel rows per wave-task")
+    ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -110,8 +115,8 @@ def main(argv=None) -> int:
     cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup,
                           warmup=a.warmup, init="random", b_width=bw, dims=dims,
                           chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
-                          unroll=a.unroll, vec=a.vec,
-                          use_graph=a.graph, quiet=True)
+                          unroll=a.unroll, vec=a.vec, temporal=a.temporal, chunk2=a.chunk2,
+                          unroll2=a.unroll2, use_graph=a.graph, quiet=True)
     t_setup = time.perf_counter()
     model = Diffusion2D(cfg)
     g = model.g
@@ -168,6 +173,8 @@ def main(argv=None) -> int:
             "nontemporal": a.nontemporal,
             "b_width": list(bw),
             "hipgraph": bool(a.graph),
+            "temporal_blocking": a.temporal,
+            "overlap": list(g.overlaps[:2]),
             "setup_s": round(setup_s, 3),
             "nonfinite_cells_sampled": int(bad),
         },

@@ -34,6 +34,10 @@ def main(argv=None):
     ap.add_argument("--x0", type=int, default=1, help="interior rect offset (perf_hide-like)")
     ap.add_argument("--y0", type=int, default=1)
     ap.add_argument("--no-roof", action="store_true")
+    ap.add_argument("--tb-chunks", default="", help="two-step kernel chunk_rows list")
+    ap.add_argument("--tb-unrolls", default="2,4")
+    ap.add_argument("--tb-xcds", default="0,1")
+    ap.add_argument("--no-march", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -77,6 +81,17 @@ def main(argv=None):
                         variants[f"march_c{c}_u{u}_v{v}_nt{nt}_x{x}"] = (
                             lambda tn=tn: ops.stencil_step(T2, T, iCp, coef, rect, tuning=tn),
                             bytes_model)
+    if a.no_march:
+        variants.clear()
+    # two steps per call: T_eff-equivalent bytes = 2 x 24 B/cell (the metric's
+    # per-step A_eff; the kernel itself moves 24 B/cell per call)
+    for c in [int(v) for v in a.tb_chunks.split(",") if v]:
+        for u in [int(v) for v in a.tb_unrolls.split(",")]:
+            for x in [int(v) for v in a.tb_xcds.split(",")]:
+                tn = ops.StencilTuning(chunk_rows=c, unroll=u, nontemporal=3, xcd_remap=x)
+                variants[f"tb2_c{c}_u{u}_x{x}"] = (
+                    lambda tn=tn: ops.stencil2_step(T2, T, iCp, coef, rect, tuning=tn),
+                    2 * bytes_model)
     variants["lds"] = (lambda: ops.stencil_step(T2, T, iCp, coef,
                                                 tuning=ops.StencilTuning(kernel="lds")),
                        bytes_model)
@@ -111,10 +126,13 @@ def main(argv=None):
     def best_of(prefix):
         return max((k for k in res if k.startswith(prefix)), key=lambda k: res[k]["GBps_median"])
 
-    best = best_of("march")
+    best = best_of("march") if any(k.startswith("march") for k in res) else best_of("tb2")
     doc = {"n": n, "cells": cells, "rounds": a.rounds, "iters": a.iters, "results": res,
            "best_march": best, "best_march_GBps": res[best]["GBps_median"],
            "device": torch.cuda.get_device_name(0)}
+    if any(k.startswith("tb2") for k in res):
+        tb = best_of("tb2")
+        doc.update({"best_tb2": tb, "best_tb2_GBps_equiv": res[tb]["GBps_median"]})
     if not a.no_roof:
         tri, cop = best_of("roof_triad"), best_of("roof_copy")
         doc.update({"best_triad": tri, "triad_GBps": res[tri]["GBps_median"],

@@ -120,6 +120,30 @@ PYBIND11_MODULE(_C, m) {
       py::arg("kernel") = 0, py::arg("stream") = 0, py::arg("gpu") = true,
       py::arg("unroll") = 4, py::arg("vec") = 2, py::arg("xcd_remap") = -1);
   m.def(
+      "stencil2_rects",
+      [](uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
+         const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
+         uintptr_t stream, bool gpu, int unroll, int xcd_remap) {
+        auto r = to_rects(rects);
+        StencilTuning tn;
+        tn.chunk_rows = chunk_rows;
+        tn.nontemporal = nontemporal;
+        tn.unroll = unroll;
+        tn.xcd_remap = xcd_remap;
+        if (gpu)
+          stencil2_rects_gpu(P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
+                             r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
+        else {
+          py::gil_scoped_release nogil;
+          stencil2_rects_cpu(P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
+                             r.data(), (int)r.size(), to_coef(coef));
+        }
+      },
+      py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"), py::arg("rects"),
+      py::arg("coef"), py::arg("chunk_rows") = 8, py::arg("nontemporal") = 3,
+      py::arg("stream") = 0, py::arg("gpu") = true, py::arg("unroll") = 2,
+      py::arg("xcd_remap") = -1);
+  m.def(
       "stream_copy",
       [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {
         stream_copy_gpu(P<double>(b), P<const double>(a), n, nt, blocks, S(s));
@@ -297,8 +321,15 @@ PYBIND11_MODULE(_C, m) {
                        const Coef4& coef, int chunk_rows, int nontemporal, int kernel,
                        int64_t bwx, int64_t bwy, int use_graph, int graph_steps,
                        HaloExchanger* halo, uintptr_t qx, uintptr_t qy, uintptr_t dTdt,
-                       int unroll, int vec) {
+                       int unroll, int vec, int temporal, int64_t olx, int64_t oly,
+                       int chunk2, int unroll2) {
              ExecParams p;
+             p.temporal = temporal;
+             p.olx = olx;
+             p.oly = oly;
+             p.tune2.chunk_rows = chunk2;
+             p.tune2.unroll = unroll2;
+             p.tune2.nontemporal = nontemporal & 3;
              p.mode = static_cast<Mode>(mode);
              p.coef = to_coef(coef);
              p.tune.chunk_rows = chunk_rows;
@@ -320,7 +351,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("bwy") = 1, py::arg("use_graph") = 0, py::arg("graph_steps") = 0,
            py::arg("halo").none(true) = nullptr, py::arg("qx") = 0, py::arg("qy") = 0,
            py::arg("dTdt") = 0, py::arg("unroll") = 4, py::arg("vec") = 2,
-           py::keep_alive<1, 16>())
+           py::arg("temporal") = 1, py::arg("olx") = 2, py::arg("oly") = 2,
+           py::arg("chunk2") = 16, py::arg("unroll2") = 2, py::keep_alive<1, 16>())
       .def(
           "run", [](DiffusionExecutor& e, int64_t n, uintptr_t s) { e.run(n, S(s)); },
           py::arg("nsteps"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())

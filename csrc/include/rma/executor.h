@@ -12,6 +12,9 @@
 //           join both, swap. This is the reference's intended variant (3)
 //           with exact frame/interior grids.
 //   kKp   : [flux] -> [residual] -> [update T in place] -> [halo(T)]
+//   temporal=2 (kPerf/kHide): each pass advances TWO steps with the two-step
+//           kernel on the "owned" rect (cells next to a neighbour's halo are
+//           left to the width-2 exchange), then one exchange of width 2.
 //
 // Python never waits inside the loop; run() returns as soon as n steps are
 // enqueued, ordered after the caller's stream and before its next work.
@@ -36,6 +39,12 @@ struct ExecParams {
   int64_t bwx = 1, bwy = 1;    // perf_hide frame widths (cells beyond the boundary)
   int use_graph = 0;           // capture steps into a hipGraph and replay
   int graph_steps = 0;         // steps per captured graph (even; 0 = auto)
+  // Temporal blocking (kPerf/kHide): 2 = two time steps per kernel pass
+  // (stencil2_rects_gpu) and one halo exchange of width 2 per pass; needs a
+  // grid overlap >= 4 in every dimension with a neighbour. 1 = one step.
+  int temporal = 1;
+  int64_t olx = 2, oly = 2;    // grid overlaps of the field (IGG overlaps)
+  StencilTuning tune2{16, 3, 0, 2, 2, -1};  // two-step kernel: 16-row chunks, unroll 2
 };
 
 class DiffusionExecutor {
@@ -60,7 +69,10 @@ class DiffusionExecutor {
 
  private:
   void enqueue_step(double* Tin, double* Tout);
+  void enqueue_step2(double* Tin, double* Tout);  // temporal=2: two steps
   void exchange(double* A, stream_t s);
+  void split(const Rect& out, int64_t bwx, int64_t bwy, std::vector<Rect>& frame,
+             Rect& interior) const;
   void build_graph(int64_t steps);
   void run_eager(int64_t nsteps);
 
@@ -73,6 +85,9 @@ class DiffusionExecutor {
   double *qx_, *qy_, *dTdt_;
   Rect full_{}, interior_{};
   std::vector<Rect> frame_;
+  Rect out2_{}, interior2_{};  // temporal=2: owned rect and its interior
+  std::vector<Rect> frame2_;
+  int64_t hwx_ = 1, hwy_ = 1;
   void* s_hi_ = nullptr;  // hipStream_t
   void* s_lo_ = nullptr;
   void* e_hi_ = nullptr;  // hipEvent_t

@@ -41,6 +41,16 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
 void stencil_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
                        const Rect* rects, int nrects, const StencilCoef& c);
 
+// Two steps per pass (temporal blocking, stencil_tb.hip): T2[r] = f(f(T))[r],
+// where the intermediate step is f(T) on the interior [1,nx-1)x[1,ny-1) and T
+// elsewhere. Bitwise equal to two one-step launches. T2 != T; unroll 2 or 4;
+// no column mode (every rect is marched in 64*V-cell strips).
+void stencil2_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                        const Rect* rects, int nrects, const StencilCoef& c,
+                        const StencilTuning& tune, stream_t stream);
+void stencil2_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                        const Rect* rects, int nrects, const StencilCoef& c);
+
 // Width (in cells) of one wave's x-strip in the march kernel; perf_hide rounds
 // its x-frame so the interior rect starts on a strip boundary.
 int stencil_vec(int64_t nx, const StencilTuning& tune);

@@ -8,6 +8,8 @@
 #include <cstring>
 #include <limits>
 
+#include <vector>
+
 #include "rma/kernels.h"
 #include "rma/parallel_for.h"
 
@@ -42,6 +44,15 @@ void stencil_rects_cpu(double* T2, const double* T, const double* iCp, int64_t n
         out[x] = cell(cu[x - 1], cu[x], cu[x + 1], up[x], dn[x], ic[x], c);
     });
   }
+}
+
+void stencil2_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                        const Rect* rects, int nrects, const StencilCoef& c) {
+  RMA_CHECK_ARG(T2 != T, "two-step update cannot run in place");
+  std::vector<double> S1(T, T + nx * ny);  // step 1 on the interior, T elsewhere
+  const Rect interior{1, nx - 1, 1, ny - 1};
+  stencil_rects_cpu(S1.data(), T, iCp, nx, ny, &interior, 1, c);
+  stencil_rects_cpu(T2, S1.data(), iCp, nx, ny, rects, nrects, c);
 }
 
 void flux_cpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,

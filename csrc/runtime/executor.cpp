@@ -27,27 +27,42 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   RMA_CHECK_ARG(!p.use_graph || !halo || halo->capturable(),
                 "hipGraph replay needs a capturable halo transport (RCCL or none); the loopback "
                 "transport synchronises on the host");
+  RMA_CHECK_ARG(p.temporal == 1 || p.temporal == 2, "temporal must be 1 or 2");
+  RMA_CHECK_ARG(p.temporal == 1 || p.mode != Mode::kKp,
+                "temporal blocking applies to perf / perf_hide, not kp");
+  RMA_CHECK_ARG(p.olx >= 2 && p.oly >= 2, "overlaps must be >= 2");
+  hwx_ = hwy_ = p.temporal;  // halo width = steps per exchange
+  std::array<std::array<int, 2>, 3> nbr{{{-1, -1}, {-1, -1}, {-1, -1}}};
+  if (halo) nbr = halo->neighbors();
+  const int64_t ol[2] = {p.olx, p.oly};
+  for (int d = 0; d < 2; ++d)
+    RMA_CHECK_ARG((nbr[d][0] < 0 && nbr[d][1] < 0) || ol[d] >= 2 * p.temporal,
+                  "temporal=" << p.temporal << " needs a grid overlap >= " << 2 * p.temporal
+                              << " along dim " << d << " (init_global_grid overlaps=4, "
+                              << "halowidths=2), got " << ol[d]);
   full_ = {1, nx - 1, 1, ny - 1};
+  // perf_hide: the frame must contain the send planes [ol-hw, ol) of every
+  // side, so it is at least ol-1 cells wide (the reference's b_width >= overlap
+  // invariant); minimal frames otherwise (width 1 for ol=2:
+  // thin x-frames run in the kernel's column mode, profiles/).
   if (p.mode == Mode::kHide) {
     RMA_CHECK_ARG(p.bwx >= 1 && p.bwy >= 1,
                   "b_width must be >= 1 so the send planes belong to the boundary kernel");
-    // Minimal frames: the send planes are x = 1, nx-2 and y = 1, ny-2, so a
-    // frame of width 1 suffices; thin x-frames run in the kernel's column
-    // mode and the interior keeps 98-99.99% of the cells (profiles/).
-    const int64_t xi0 = 1 + p.bwx, xi1 = nx - 1 - p.bwx;
-    const int64_t yi0 = 1 + p.bwy, yi1 = ny - 1 - p.bwy;
-    if (xi0 >= xi1 || yi0 >= yi1) {
-      interior_ = {0, 0, 0, 0};
-      frame_ = {full_};
-    } else {
-      interior_ = {xi0, xi1, yi0, yi1};
-      frame_ = {{1, nx - 1, 1, yi0},
-                {1, nx - 1, yi1, ny - 1},
-                {1, xi0, yi0, yi1},
-                {xi1, nx - 1, yi0, yi1}};
-    }
+    split(full_, std::max(p.bwx, p.olx - 1), std::max(p.bwy, p.oly - 1), frame_, interior_);
   } else {
     interior_ = full_;
+  }
+  if (p.temporal == 2) {
+    // owned rect of a two-step pass: next to a neighbour the cell at index 1
+    // is halo (width 2) and only the exchange refreshes it
+    out2_ = {nbr[0][0] >= 0 ? 2 : 1, nx - (nbr[0][1] >= 0 ? 2 : 1),
+             nbr[1][0] >= 0 ? 2 : 1, ny - (nbr[1][1] >= 0 ? 2 : 1)};
+    RMA_CHECK_ARG(!out2_.empty(), "tile too small for temporal blocking: " << nx << "x" << ny);
+    if (p.mode == Mode::kHide)
+      split(out2_, std::max(p.bwx, p.olx - out2_.x0), std::max(p.bwy, p.oly - out2_.y0),
+            frame2_, interior2_);
+    else
+      interior2_ = out2_;
   }
   int least = 0, greatest = 0;
   RMA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -74,15 +89,38 @@ DiffusionExecutor::~DiffusionExecutor() {
   if (s_lo_) (void)hipStreamDestroy(S(s_lo_));
 }
 
-void DiffusionExecutor::exchange(double* A, stream_t s) {
-  if (!halo_) return;
+void DiffusionExecutor::split(const Rect& out, int64_t bwx, int64_t bwy,
+                              std::vector<Rect>& frame, Rect& interior) const {
+  const int64_t xi0 = out.x0 + bwx, xi1 = out.x1 - bwx;
+  const int64_t yi0 = out.y0 + bwy, yi1 = out.y1 - bwy;
+  if (xi0 >= xi1 || yi0 >= yi1) {
+    interior = {0, 0, 0, 0};
+    frame = {out};
+  } else {
+    interior = {xi0, xi1, yi0, yi1};
+    frame = {{out.x0, out.x1, out.y0, yi0},
+             {out.x0, out.x1, yi1, out.y1},
+             {out.x0, xi0, yi0, yi1},
+             {xi1, out.x1, yi0, yi1}};
+  }
+}
+
+namespace {
+HaloField field_of(double* A, int64_t nx, int64_t ny, int64_t olx, int64_t oly, int64_t hwx,
+                   int64_t hwy) {
   HaloField f;
   f.ptr = A;
-  f.size = {nx_, ny_, 1};
+  f.size = {nx, ny, 1};
   f.elem_bytes = 8;
-  f.ol = {2, 2, 2};
-  f.hw = {1, 1, 1};
-  halo_->exchange({f}, s, 3);
+  f.ol = {olx, oly, 2};
+  f.hw = {hwx, hwy, 1};
+  return f;
+}
+}  // namespace
+
+void DiffusionExecutor::exchange(double* A, stream_t s) {
+  if (!halo_) return;
+  halo_->exchange({field_of(A, nx_, ny_, p_.olx, p_.oly, hwx_, hwy_)}, s, 3);
 }
 
 void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
@@ -129,17 +167,58 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
   }
 }
 
+void DiffusionExecutor::enqueue_step2(double* Tin, double* Tout) {
+  const StencilCoef& c = p_.coef;
+  if (p_.mode == Mode::kPerf) {
+    TraceRange tr("rma.step2.perf");
+    stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out2_, 1, c, p_.tune2, s_lo_);
+    exchange(Tout, s_lo_);
+    return;
+  }
+  TraceRange tr("rma.step2.hide");
+  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
+  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+  StencilTuning ft = p_.tune2;
+  ft.chunk_rows = std::min(ft.chunk_rows, 16);
+  {
+    TraceRange tb("rma.boundary");
+    stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, frame2_.data(), (int)frame2_.size(), c, ft,
+                       s_hi_);
+  }
+  {
+    TraceRange th("rma.halo");
+    exchange(Tout, s_hi_);
+  }
+  RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
+  if (!interior2_.empty()) {
+    TraceRange ti("rma.interior");
+    stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &interior2_, 1, c, p_.tune2, s_lo_);
+  }
+  RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+}
+
 void DiffusionExecutor::run_eager(int64_t nsteps) {
-  for (int64_t i = 0; i < nsteps; ++i) {
+  for (int64_t i = 0; i < nsteps;) {
     if (p_.mode == Mode::kKp) {
       enqueue_step(T_, nullptr);
-    } else {
-      double* Tin = parity_ ? T2_ : T_;
-      double* Tout = parity_ ? T_ : T2_;
-      enqueue_step(Tin, Tout);
-      parity_ ^= 1;
+      ++steps_;
+      ++i;
+      continue;
     }
-    ++steps_;
+    double* Tin = parity_ ? T2_ : T_;
+    double* Tout = parity_ ? T_ : T2_;
+    if (p_.temporal == 2 && nsteps - i >= 2) {
+      enqueue_step2(Tin, Tout);
+      steps_ += 2;
+      i += 2;
+    } else {
+      // one step (also the odd remainder of a temporal run: with overlap 4 and
+      // halo width 2 the single-step update + exchange stays consistent)
+      enqueue_step(Tin, Tout);
+      ++steps_;
+      ++i;
+    }
+    parity_ ^= 1;
   }
 }
 
@@ -148,12 +227,8 @@ void DiffusionExecutor::build_graph(int64_t steps) {
     (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec_));
     graph_exec_ = nullptr;
   }
-  if (halo_) {  // pack buffers must exist before capture (no hipMalloc inside)
-    HaloField f;
-    f.ptr = T_;
-    f.size = {nx_, ny_, 1};
-    halo_->prepare({f}, 3);
-  }
+  if (halo_)  // pack buffers must exist before capture (no hipMalloc inside)
+    halo_->prepare({field_of(T_, nx_, ny_, p_.olx, p_.oly, hwx_, hwy_)}, 3);
   hipStream_t lo = S(s_lo_), hi = S(s_hi_);
   const int saved_parity = parity_;
   const int64_t saved_steps = steps_;
@@ -203,7 +278,9 @@ void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
   int64_t left = nsteps;
   if (p_.use_graph) {
     int64_t gl = p_.graph_steps > 0 ? p_.graph_steps : 20;
-    if (gl % 2) ++gl;  // keep the buffer parity of a replay neutral
+    // keep the buffer parity of a replay neutral (temporal=2: 2 steps per swap)
+    const int64_t q = p_.temporal == 2 ? 4 : 2;
+    gl = (gl + q - 1) / q * q;
     if (left >= gl) {
       if (!graph_exec_ || graph_len_ != gl) build_graph(gl);
       while (left >= gl) {

@@ -93,7 +93,8 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
     BUILD.mkdir(parents=True, exist_ok=True)
-    newest_header = max((p.stat().st_mtime for p in INC.rglob("*.h")), default=0.0)
+    headers = list(INC.rglob("*.h")) + list((CSRC / "kernels").glob("*.h"))
+    newest_header = max((p.stat().st_mtime for p in headers), default=0.0)
     jobs = jobs or min(16, os.cpu_count() or 4)
     todo = []
     objs = []

@@ -75,6 +75,11 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
+    ap.add_argument("--temporal", type=int, default=1, choices=[1, 2],
+                    help="perf/perf_hide: 2 = two steps per kernel pass + width-2 halos "
+                         "(grid overlap 4); bitwise identical to 1")
+    ap.add_argument("--chunk2", type=int, default=16)
+    ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
     ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf guard period")
     ap.add_argument("--checkpoint", default="", help="save the final state to this directory")
     ap.add_argument("--resume", default="", help="start from a checkpoint directory")
@@ -114,7 +119,8 @@ def run_variant(variant: str, argv=None) -> int:
                 periods=tuple(a.periods) + (0,), transport=a.transport, device=a.device,
                 chunk_rows=a.chunk_rows, unroll=a.unroll, vec=a.vec, kernel=a.kernel,
                 nontemporal=a.nontemporal, use_graph=a.graph, do_vis=a.do_vis, outdir=a.outdir,
-                profile=a.profile, check_every=a.check_every, quiet=a.quiet)
+                profile=a.profile, check_every=a.check_every, quiet=a.quiet,
+                temporal=a.temporal, chunk2=a.chunk2, unroll2=a.unroll2)
     if a.auto_size:
         rank, size, _ = C.env_world()
         if size > 1:

@@ -76,6 +76,11 @@ class DiffusionConfig:
     profile: bool = False
     check_every: int = 0  # NaN/Inf guard period (0 = off)
     quiet: bool = False
+    # temporal blocking (perf / perf_hide): 2 = two steps per kernel pass and
+    # one width-2 halo exchange per pass (grid overlap 4); bitwise identical
+    temporal: int = 1
+    chunk2: int = 16  # two-step kernel tuning
+    unroll2: int = 2
 
     def validate(self) -> None:
         if self.variant not in VARIANTS:
@@ -86,6 +91,10 @@ class DiffusionConfig:
             raise ValueError("init must be gaussian or random")
         if self.nx < 3 or self.ny < 3:
             raise ValueError("nx, ny >= 3 required")
+        if self.temporal not in (1, 2):
+            raise ValueError("temporal must be 1 or 2")
+        if self.temporal == 2 and self.variant not in ("perf", "perf_hide"):
+            raise ValueError("temporal blocking applies to the perf and perf_hide variants")
 
 
 class Diffusion2D:
@@ -97,6 +106,9 @@ class Diffusion2D:
         kw = dict(grid_kwargs or {})
         if not gg.grid_is_initialized():
             kw.setdefault("quiet", cfg.quiet)
+            if cfg.temporal == 2:  # width-2 halos need overlap 4 (IGG: ol >= 2*hw)
+                kw.setdefault("overlaps", (4, 4, 2))
+                kw.setdefault("halowidths", (2, 2, 1))
             gg.init_global_grid(cfg.nx, cfg.ny, 1, dimx=cfg.dims[0], dimy=cfg.dims[1],
                                 periodx=cfg.periods[0], periody=cfg.periods[1],
                                 transport=cfg.transport, device=cfg.device, **kw)
@@ -159,7 +171,8 @@ class Diffusion2D:
                 self.QX.data_ptr() if cfg.variant == "kp" else 0,
                 self.QY.data_ptr() if cfg.variant == "kp" else 0,
                 self.D.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
-                int(cfg.vec))
+                int(cfg.vec), int(cfg.temporal), int(g.overlaps[0]), int(g.overlaps[1]),
+                int(cfg.chunk2), int(cfg.unroll2))
         self._ap_graph = None
         if cfg.variant == "ap" and cfg.use_graph:
             # ap on a GPU is ~11 small torch launches per step: replay them from
@@ -171,8 +184,17 @@ class Diffusion2D:
 
                 warnings.warn(f"hipGraph replay disabled for ap ({dev.type}, {g.transport} "
                               "transport)", RuntimeWarning, stacklevel=2)
+        if cfg.temporal == 2:
+            nb = g.neighbors
+            if any(max(nb[d]) >= 0 and g.overlaps[d] < 4 for d in (0, 1)):
+                raise ValueError("temporal=2 needs grid overlaps >= 4 (init_global_grid("
+                                 "overlaps=(4,4,2), halowidths=(2,2,1)))")
+            self.out2 = (2 if nb[0][0] >= 0 else 1, nx - (2 if nb[0][1] >= 0 else 1),
+                         2 if nb[1][0] >= 0 else 1, ny - (2 if nb[1][1] >= 0 else 1))
         if cfg.variant == "perf_hide":
-            self.frame_rects, self.interior = ops.hide_rects(nx, ny, *cfg.b_width, vec=cfg.vec)
+            # the frame holds the send planes [ol-hw, ol): at least ol-1 wide
+            bw = (max(cfg.b_width[0], g.overlaps[0] - 1), max(cfg.b_width[1], g.overlaps[1] - 1))
+            self.frame_rects, self.interior = ops.hide_rects(nx, ny, *bw, vec=cfg.vec)
         self.tuning = ops.StencilTuning(cfg.chunk_rows, int(cfg.nontemporal), cfg.kernel,
                                         cfg.unroll, cfg.vec)
 
@@ -231,7 +253,8 @@ class Diffusion2D:
                 self._ap_graph.replay()
             self.steps_done += n - n % k
             n %= k
-        for _ in range(n):
+        done = 0
+        while done < n:
             if v == "ap":
                 self._step_ap()
             elif v == "kp":
@@ -239,6 +262,16 @@ class Diffusion2D:
                 ops.residual(self.D, self.QX, self.QY, self.iCp, self.coef.rdx, self.coef.rdy)
                 ops.update(self.T, self.D, self.coef.dt)
                 update_halo_(self.T)
+            elif self.cfg.temporal == 2 and n - done >= 2:
+                # two steps per pass (the native executor splits frame/interior;
+                # this reference loop runs the owned rect, then the exchange)
+                Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
+                ops.stencil2_step(Tout, Tin, self.iCp, self.coef, [self.out2])
+                update_halo_(Tout)
+                self.parity ^= 1
+                self.steps_done += 2
+                done += 2
+                continue
             else:
                 Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
                 if v == "perf":
@@ -252,6 +285,7 @@ class Diffusion2D:
                                          self.tuning)
                 self.parity ^= 1
             self.steps_done += 1
+            done += 1
 
     def _ap_graph_len(self) -> int:
         """Capture graph_steps ap steps once (capture does not execute them)."""

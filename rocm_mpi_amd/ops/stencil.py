@@ -164,6 +164,35 @@ def stencil_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: Ste
         stencil_torch(T2, T, iCp, coef, rects)
 
 
+def stencil2_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: StencilCoef,
+                  rects: Sequence[Rect] | None = None, tuning: StencilTuning | None = None) -> None:
+    """Two time steps in one pass (temporal blocking, csrc/kernels/stencil_tb.hip):
+    T2[r] = f(f(T))[r] for every rect r, where the intermediate step is f(T) on
+    the interior and T on the boundary/halo cells. Bitwise equal to two
+    ``stencil_step`` calls. Default tuning: 8-row chunks, unroll 2."""
+    check_field("T", T)
+    ny, nx = T.shape
+    check_field("T2", T2, (ny, nx), T.device)
+    check_field("iCp", iCp, (ny, nx), T.device)
+    if T2.data_ptr() == T.data_ptr():
+        raise ValueError("T2 must not alias T (double buffering)")
+    rects = validate_rects(rects if rects is not None else [interior_rect(nx, ny)], nx, ny)
+    if not rects:
+        return
+    tn = tuning or StencilTuning(chunk_rows=8, unroll=2)
+    if T.is_cuda:
+        native().stencil2_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
+                                tn.chunk_rows, int(tn.nontemporal), stream_handle(T), True,
+                                tn.unroll, tn.xcd_remap)
+    elif _use_native_cpu():
+        native().stencil2_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
+                                8, 0, 0, False)
+    else:
+        S1 = T.clone()
+        stencil_torch(S1, T, iCp, coef, [interior_rect(nx, ny)])
+        stencil_torch(T2, S1, iCp, coef, rects)
+
+
 def strip_cells(nx: int, vec: int = 2) -> int:
     """x-width of one wave-strip of the march kernel (perf_hide frame rounding)."""
     if has_native():

@@ -12,6 +12,7 @@ import torch
 
 import golden
 from helpers import run_loopback
+from rocm_mpi_amd import ops
 from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
 from rocm_mpi_amd.parallel import implicit_grid as gg
 
@@ -72,3 +73,38 @@ def test_periodic_decomposition_invariance():
     ta, tb = a[0], b[0]
     assert ta.shape == tb.shape == (14, 36)
     np.testing.assert_array_equal(ta, tb)
+
+
+def spmd_tiles(rank, hub, variant, nx, ny, nt, dims, temporal, periods=(0, 0, 0)):
+    """Every rank returns (coords, full local field incl. halo, global sizes)."""
+    ol = 4 if temporal == 2 else 2
+    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], periodx=periods[0],
+                        periody=periods[1], overlaps=(ol, ol, 2),
+                        halowidths=(ol // 2, ol // 2, 1), quiet=True, loopback=(hub, rank),
+                        select_device=False)
+    m = Diffusion2D(DiffusionConfig(variant=variant, nx=nx, ny=ny, nt=nt, init="random",
+                                    quiet=True, dims=dims, periods=periods, temporal=temporal,
+                                    b_width=(1, 1)))
+    m.step(nt)
+    out = (m.g.coords, m.field.numpy().copy(), m.g.nxyz_g, m.g.overlaps)
+    gg.finalize_global_grid()
+    return out
+
+
+@pytest.mark.parametrize("variant", ["perf", "perf_hide"])
+@pytest.mark.parametrize("P,dims", [(1, (1, 1)), (2, (2, 1)), (3, (1, 3)), (4, (2, 2))])
+@pytest.mark.parametrize("nt", [20, 13])
+def test_temporal_blocking_equals_golden(variant, P, dims, nt):
+    """Two steps per pass + width-2 halos on an overlap-4 grid: every local
+    tile (halo included) equals its window of the global golden model after
+    an even or odd number of steps."""
+    nx, ny = 37, 30
+    res = run_loopback(P, spmd_tiles, variant, nx, ny, nt, dims, 2)
+    nxg, nyg, _ = res[0][2]
+    assert (nxg, nyg) == (dims[0] * (nx - 4) + 4, dims[1] * (ny - 4) + 4)
+    T0 = torch.empty((nyg, nxg), dtype=torch.float64)  # the global random field
+    ops.init_random_(T0, ops.TileGeometry(0, 0, nxg, nyg, 1.0, 1.0), seed=1234)
+    G = golden.run(nxg, nyg, nt, T0=T0.numpy())
+    for coords, T, _, ol in res:
+        gx0, gy0 = coords[0] * (nx - ol[0]), coords[1] * (ny - ol[1])
+        assert np.array_equal(T, G[gy0:gy0 + ny, gx0:gx0 + nx])

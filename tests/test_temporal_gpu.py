@@ -1,0 +1,80 @@
+"""Two-step (temporal blocking) kernel vs two one-step launches and the C++
+CPU twin: bitwise, over odd/tiny shapes, chunk/unroll choices, rect lists,
+unaligned views (scalar path) and both block orders."""
+import pytest
+import torch
+
+from rocm_mpi_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def rand(shape, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(shape, generator=g, dtype=torch.float64)
+
+
+def coef():
+    return ops.StencilCoef(-1.3, 1 / 0.037, 1 / 0.041, 0.00031)
+
+
+def two_steps_cpu(T, iCp, rects, fill=-5.0):
+    S1 = T.clone()
+    ops.stencil_step(S1, T, iCp, coef())
+    out = torch.full_like(T, fill)
+    ops.stencil_step(out, S1, iCp, coef(), rects)
+    return out
+
+
+SHAPES = [(3, 3), (4, 5), (5, 4), (66, 130), (130, 66), (389, 515), (257, 1024), (100, 2050),
+          (31, 4097), (300, 129), (9, 260)]
+
+
+@pytest.mark.parametrize("ny,nx", SHAPES)
+@pytest.mark.parametrize("chunk,unroll", [(1, 2), (8, 2), (6, 4), (13, 4), (64, 2)])
+def test_two_step_bitwise(ny, nx, chunk, unroll):
+    T, iCp = rand((ny, nx), 1), rand((ny, nx), 2) + 0.5
+    ref = two_steps_cpu(T, iCp, [ops.interior_rect(nx, ny)])
+    out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+    ops.stencil2_step(out, T.to(DEV), iCp.to(DEV), coef(),
+                      tuning=ops.StencilTuning(chunk_rows=chunk, unroll=unroll))
+    assert torch.equal(out.cpu(), ref)
+    cpu = torch.full_like(T, -5.0)  # the C++ twin
+    ops.stencil2_step(cpu, T, iCp, coef())
+    assert torch.equal(cpu, ref)
+
+
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_two_step_rect_lists(xcd):
+    """Frame + interior rects (as the multi-rank executor issues them)."""
+    ny, nx = 301, 700
+    T, iCp = rand((ny, nx), 3), rand((ny, nx), 4) + 0.5
+    rects = [(2, nx - 2, 2, 4), (2, nx - 2, ny - 4, ny - 2), (2, 4, 4, ny - 4),
+             (nx - 4, nx - 2, 4, ny - 4)]
+    interior = (4, nx - 4, 4, ny - 4)
+    ref = two_steps_cpu(T, iCp, rects + [interior])
+    out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+    Td, iCpd = T.to(DEV), iCp.to(DEV)
+    tn = ops.StencilTuning(chunk_rows=8, unroll=2, xcd_remap=xcd)
+    ops.stencil2_step(out, Td, iCpd, coef(), rects, tn)
+    ops.stencil2_step(out, Td, iCpd, coef(), [interior], tn)
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_two_step_unaligned_view():
+    base = rand(64 * 200 + 1, 5).to(DEV)
+    T = base[1:].view(200, 64)  # 8-byte aligned only -> V=1 path
+    iCp = torch.ones((200, 64), dtype=torch.float64, device=DEV)
+    out = torch.zeros((200, 64), dtype=torch.float64, device=DEV)
+    ops.stencil2_step(out, T, iCp, coef())
+    ref = two_steps_cpu(T.cpu(), iCp.cpu(), [ops.interior_rect(64, 200)], fill=0.0)
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_two_step_rejects_in_place_and_bad_rects():
+    T = rand((10, 10), 6).to(DEV)
+    with pytest.raises(ValueError):
+        ops.stencil2_step(T, T, T, coef())
+    with pytest.raises(ValueError):
+        ops.stencil2_step(torch.empty_like(T), T, T, coef(), [(0, 5, 1, 5)])
