@@ -27,6 +27,20 @@ ops.fill_(iCp, 1.0)
 c = ops.StencilCoef(-1.0, 1.0, 1.0, 0.2)
 s = torch.cuda.current_stream().cuda_stream
 nat = native()
+which = os.environ.get("RMA_PROBE_SET", "all")
+if which in ("all", "tbk"):  # multi-step kernels (temporal blocking)
+    for K, ch in ((2, 16), (3, 128), (4, 128)):
+        for _ in range(reps):
+            ops.stencilk_step(K, T2, T, iCp, c, tuning=ops.StencilTuning(chunk_rows=ch,
+                                                                        xcd_remap=1))
+    for _ in range(reps):
+        ops.stencil2_step(T2, T, iCp, c)
+    if which == "tbk":
+        for _ in range(reps):
+            ops.stencil_step(T2, T, iCp, c)
+        torch.cuda.synchronize()
+        print(f"probe done n={n} reps={reps} set={which}")
+        sys.exit(0)
 for _ in range(reps):
     ops.stencil_step(T2, T, iCp, c)
 for _ in range(reps):

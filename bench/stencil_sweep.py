@@ -38,6 +38,10 @@ def main(argv=None):
     ap.add_argument("--tb-unrolls", default="2,4")
     ap.add_argument("--tb-xcds", default="0,1")
     ap.add_argument("--no-march", action="store_true")
+    ap.add_argument("--tbk", default="", help="K-step kernel: K list, e.g. 2,3,4")
+    ap.add_argument("--tbk-chunks", default="16")
+    ap.add_argument("--tbk-xcds", default="0")
+    ap.add_argument("--tbk-vecs", default="2")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -92,6 +96,14 @@ def main(argv=None):
                 variants[f"tb2_c{c}_u{u}_x{x}"] = (
                     lambda tn=tn: ops.stencil2_step(T2, T, iCp, coef, rect, tuning=tn),
                     2 * bytes_model)
+    for K in [int(v) for v in a.tbk.split(",") if v]:
+        for c in [int(v) for v in a.tbk_chunks.split(",")]:
+            for x, vv in [(int(x), int(vv)) for x in a.tbk_xcds.split(",")
+                          for vv in a.tbk_vecs.split(",")]:
+                tn = ops.StencilTuning(chunk_rows=c, nontemporal=3, xcd_remap=x, vec=vv)
+                variants[f"tbk{K}_c{c}_x{x}_v{vv}"] = (
+                    lambda K=K, tn=tn: ops.stencilk_step(K, T2, T, iCp, coef, rect, tuning=tn),
+                    K * bytes_model)
     variants["lds"] = (lambda: ops.stencil_step(T2, T, iCp, coef,
                                                 tuning=ops.StencilTuning(kernel="lds")),
                        bytes_model)
@@ -130,6 +142,9 @@ def main(argv=None):
     doc = {"n": n, "cells": cells, "rounds": a.rounds, "iters": a.iters, "results": res,
            "best_march": best, "best_march_GBps": res[best]["GBps_median"],
            "device": torch.cuda.get_device_name(0)}
+    for K in [int(v) for v in a.tbk.split(",") if v]:
+        bk = best_of(f"tbk{K}_")
+        doc.update({f"best_tbk{K}": bk, f"best_tbk{K}_GBps_equiv": res[bk]["GBps_median"]})
     if any(k.startswith("tb2") for k in res):
         tb = best_of("tb2")
         doc.update({"best_tb2": tb, "best_tb2_GBps_equiv": res[tb]["GBps_median"]})

@@ -144,6 +144,30 @@ PYBIND11_MODULE(_C, m) {
       py::arg("stream") = 0, py::arg("gpu") = true, py::arg("unroll") = 2,
       py::arg("xcd_remap") = -1);
   m.def(
+      "stencilk_rects",
+      [](int K, uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
+         const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
+         uintptr_t stream, bool gpu, int xcd_remap, int vec) {
+        auto r = to_rects(rects);
+        StencilTuning tn;
+        tn.chunk_rows = chunk_rows;
+        tn.nontemporal = nontemporal;
+        tn.xcd_remap = xcd_remap;
+        tn.vec = vec;
+        if (gpu)
+          stencilk_rects_gpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
+                             r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
+        else {
+          py::gil_scoped_release nogil;
+          stencilk_rects_cpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
+                             r.data(), (int)r.size(), to_coef(coef));
+        }
+      },
+      py::arg("K"), py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"),
+      py::arg("rects"), py::arg("coef"), py::arg("chunk_rows") = 16, py::arg("nontemporal") = 3,
+      py::arg("stream") = 0, py::arg("gpu") = true, py::arg("xcd_remap") = -1,
+      py::arg("vec") = 2);
+  m.def(
       "stream_copy",
       [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {
         stream_copy_gpu(P<double>(b), P<const double>(a), n, nt, blocks, S(s));

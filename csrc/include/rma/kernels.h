@@ -51,6 +51,16 @@ void stencil2_rects_gpu(double* T2, const double* T, const double* iCp, int64_t 
 void stencil2_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
                         const Rect* rects, int nrects, const StencilCoef& c);
 
+// K steps per pass (K = 2..4, stencil_tbk.hip): T2[r] = f^K(T)[r], the
+// intermediate levels being f on the interior and T elsewhere; face fluxes
+// shared between neighbouring cells (same rounding). Bitwise equal to K
+// one-step launches.
+void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                        int64_t ny, const Rect* rects, int nrects, const StencilCoef& c,
+                        const StencilTuning& tune, stream_t stream);
+void stencilk_rects_cpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                        int64_t ny, const Rect* rects, int nrects, const StencilCoef& c);
+
 // Width (in cells) of one wave's x-strip in the march kernel; perf_hide rounds
 // its x-frame so the interior rect starts on a strip boundary.
 int stencil_vec(int64_t nx, const StencilTuning& tune);

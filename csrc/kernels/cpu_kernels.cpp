@@ -55,6 +55,19 @@ void stencil2_rects_cpu(double* T2, const double* T, const double* iCp, int64_t 
   stencil_rects_cpu(T2, S1.data(), iCp, nx, ny, rects, nrects, c);
 }
 
+void stencilk_rects_cpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                        int64_t ny, const Rect* rects, int nrects, const StencilCoef& c) {
+  RMA_CHECK_ARG(K >= 1, "K=" << K);
+  RMA_CHECK_ARG(T2 != T, "multi-step update cannot run in place");
+  std::vector<double> a(T, T + nx * ny), b(a);
+  const Rect interior{1, nx - 1, 1, ny - 1};
+  for (int j = 1; j < K; ++j) {  // levels 1..K-1 on the interior, T elsewhere
+    stencil_rects_cpu(b.data(), a.data(), iCp, nx, ny, &interior, 1, c);
+    a.swap(b);
+  }
+  stencil_rects_cpu(T2, a.data(), iCp, nx, ny, rects, nrects, c);
+}
+
 void flux_cpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,
               double rdx, double rdy) {
   parallel_for(0, ny - 1, 64, [&](int64_t y) {

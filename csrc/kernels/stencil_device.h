@@ -127,8 +127,12 @@ __device__ __forceinline__ void row_update(double (&res)[V], const double (&up)[
 
 // Host planner: strips/chunks/blocks per rect (see stencil.hip for the block
 // orders). `column_mode` enables the thin-rect column path (one-step only).
+// halo > 0 (overlapped strips of the multi-step kernel): a strip loads 64V
+// columns starting at a multiple of V and outputs `step` = (64V - 2*halo)
+// rounded down to a multiple of V columns from position halo on;
+// consecutive strips advance by step.
 inline int64_t plan_rects(RectList& L, const Rect* rects, int nrects, int V, int chunk_rows,
-                          int remap, bool column_mode) {
+                          int remap, bool column_mode, int halo = 0) {
   L = RectList{};
   int64_t total = 0;
   for (int i = 0; i < nrects; ++i) {
@@ -140,8 +144,17 @@ inline int64_t plan_rects(RectList& L, const Rect* rects, int nrects, int V, int
     // strips start on multiples of the strip width (1 KiB of a row for V=2),
     // whatever the rect's x0: a rect starting at x=2 would otherwise make
     // every wave access straddle one extra 128-B line (measured -9%, r1)
-    L.xa[n] = r.x0 - (r.x0 % sw);
-    L.strips[n] = (r.x1 - L.xa[n] + sw - 1) / sw;
+    if (halo > 0) {
+      // strip origins on multiples of V: a lane's V cells never straddle the
+      // array edge (clamped loads) and 16-B accesses stay aligned
+      const int64_t step = (sw - 2 * halo) / V * V;
+      const int64_t x0 = r.x0 - halo;
+      L.xa[n] = x0 - (((x0 % V) + V) % V);
+      L.strips[n] = (r.x1 - (L.xa[n] + halo) + step - 1) / step;
+    } else {
+      L.xa[n] = r.x0 - (r.x0 % sw);
+      L.strips[n] = (r.x1 - L.xa[n] + sw - 1) / sw;
+    }
     L.chunks[n] = (r.y1 - r.y0 + chunk_rows - 1) / chunk_rows;
     int64_t blocks;
     if (column_mode && r.x1 - r.x0 <= kColMaxWidth && r.y1 - r.y0 > r.x1 - r.x0) {

@@ -40,7 +40,7 @@ template <int V, bool NT, bool NTL, int U>
 __global__ __launch_bounds__(kBlock) void stencil2_march_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
     int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   int ri = 0;

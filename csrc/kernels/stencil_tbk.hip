@@ -1,0 +1,199 @@
+// K explicit-Euler steps per pass (K = 2, 3, 4, 6, 8): deep temporal
+// blocking in registers, overlapped strips, face-flux reuse.
+//
+// The one-step kernel moves the minimum 24 B/cell of a step at the HBM
+// roofline; the only way to go faster per step is to touch HBM once per K
+// steps. A wave marching down its strip keeps, for every time level
+// j = 0..K-1, two rows in registers and computes level j+1 of row i-j one row
+// behind level j (a skewed wavefront in y). HBM sees 24 B/cell per K steps,
+// so from K ~ 3 on the kernel is VALU-bound and the instruction count is what
+// matters (measured: profiles/SUMMARY_r1.md):
+//   * overlapped strips: a wave loads 64V columns and every lane updates its
+//     V cells at every level; level j is valid on strip positions [j, 64V-j)
+//     (strip-edge garbage moves in one column per level), so a strip outputs
+//     its inner columns and consecutive strips overlap by ~2K columns. (A
+//     variant with dedicated edge lanes computing the outside columns cost
+//     one extra evaluation per lane and level: 15.5 vs 19.5 TB/s at K=4.)
+//   * face fluxes are computed once and shared by the two cells of a face —
+//     x-faces with the left lane (one shuffle of the flux instead of the
+//     value), y-faces with the next row (the lower face flux of row r is the
+//     upper one of row r-1, kept in a register). Same expressions, same
+//     rounding as rma/common.h, so the result is bitwise equal to K one-step
+//     launches: 14 fp64 ops per cell update instead of 21.
+//   * no per-level selects: 1/Cp is kept in a K-row register window, zeroed
+//     outside the interior, so boundary/halo cells compute c + dt*(0*...) == c.
+//   * two-row windows alternate slots with the iteration parity (loop
+//     unrolled by two): no copies; the next T and 1/Cp rows are prefetched one
+//     iteration ahead.
+// Step-j values outside the interior [1,nx-1)x[1,ny-1) stay T (fixed
+// boundary / halo cells). Multi-rank use: halo width K, overlap 2K.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "rma/hip_check.h"
+#include "rma/kernels.h"
+#include "stencil_device.h"
+
+namespace rma {
+namespace {
+using namespace march;
+
+__device__ __forceinline__ double face(double lv, double rv, double mlam, double rd) {
+  return (mlam * (rv - lv)) * rd;  // flux lv -> rv: qxR of the left cell == qxL of the right one
+}
+
+
+template <int K, int V, bool NT>
+__global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
+    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
+    int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
+  constexpr int W = kWave * V;
+  constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_rects)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  int ri = 0;
+  while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
+  int64_t strip, chunk;
+  if (!locate_task(L, ri, b, wave, strip, chunk)) return;  // whole wave exits
+  const Rect r = L.r[ri];
+  const int64_t xs = L.xa[ri] + strip * kStep;  // first loaded column
+  const int64_t ya = r.y0 + chunk * chunk_rows;
+  const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
+
+  const int64_t x = xs + (int64_t)lane * V;
+  bool m[V], cin[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int p = lane * V + v;
+    m[v] = p >= K && p < K + kStep && x + v >= r.x0 && x + v < r.x1;
+    cin[v] = (x + v >= 1) && (x + v <= nx - 2);
+  }
+  const int64_t xl = min(max(x, (int64_t)0), nx - V);
+
+  // w[j][s]: level j rows (slot parity alternates per iteration: new row ->
+  // slot P, previous -> 1-P); fy[j]: upper face flux of the previous
+  // level-(j+1) row (== lower face flux of the current one); gic[j]: 1/Cp of
+  // the row level j+1 updates, ZEROED outside the interior (boundary rows and
+  // columns): the canonical update then returns c + dt*(0*(...)) == c for
+  // them, bitwise, without a select per level (all values are finite).
+  double w[K][2][V], fy[K][V], gic[K][V], pT[V], pC[V];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) w[j][0][v] = w[j][1][v] = fy[j][v] = gic[j][v] = 0.0;
+  }
+  int64_t i = ya - K;
+  const int64_t iend = yb + K - 2;
+  auto rowc = [&](int64_t y) { return min(max(y, (int64_t)0), ny - 1); };
+  load_row<V>(w[0][1], T + rowc(i) * nx + xl);
+  load_row<V>(pT, T + rowc(i + 1) * nx + xl);
+  load_row<V>(pC, iCp + rowc(i) * nx + xl);
+
+  auto iter = [&](auto Pc) {
+    constexpr int P = decltype(Pc)::value;
+    // level 0 <- prefetched T row i+1; 1/Cp window <- prefetched row i (masked)
+    const bool rin1 = i >= 1 && i <= ny - 2;  // row of level 1 (wave-uniform)
+#pragma unroll
+    for (int v = 0; v < V; ++v) w[0][P][v] = pT[v];
+#pragma unroll
+    for (int j = K - 1; j > 0; --j) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) gic[j][v] = gic[j - 1][v];
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) gic[0][v] = (rin1 && cin[v]) ? pC[v] : 0.0;
+    load_row<V>(pT, T + rowc(i + 2) * nx + xl);
+    load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
+#pragma unroll
+    for (int j = 1; j <= K; ++j) {
+      const int64_t row = i - (j - 1);
+      const double(&c)[V] = w[j - 1][1 - P];
+      const double(&dn)[V] = w[j - 1][P];
+      const double rn = __shfl_down(c[0], 1);  // lane 63: garbage (invalid column)
+      double qr[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) qr[v] = face(c[v], v + 1 < V ? c[v + 1] : rn, k.mlam, k.rdx);
+      const double ql0 = __shfl_up(qr[V - 1], 1);  // lane 0: garbage
+      double res[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const double qU = face(c[v], dn[v], k.mlam, k.rdy);
+        const double qD = fy[j - 1][v];
+        fy[j - 1][v] = qU;
+        const double qL = v == 0 ? ql0 : qr[v - 1];
+        res[v] = c[v] + k.dt * (gic[j - 1][v] * ((-(qr[v] - qL)) * k.rdx - (qU - qD) * k.rdy));
+      }
+      if (j < K) {
+        const int jj = j < K ? j : K - 1;
+#pragma unroll
+        for (int v = 0; v < V; ++v) w[jj][P][v] = res[v];
+      } else if (row >= ya && row < yb) {
+        store_row<V, NT>(T2 + row * nx + x, res, m);
+      }
+    }
+  };
+  for (;;) {
+    iter(std::integral_constant<int, 0>{});
+    if (++i > iend) break;
+    iter(std::integral_constant<int, 1>{});
+    if (++i > iend) break;
+  }
+}
+
+}  // namespace
+
+void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                        int64_t ny, const Rect* rects, int nrects, const StencilCoef& c,
+                        const StencilTuning& tune, stream_t stream) {
+  RMA_CHECK_ARG(K == 2 || K == 3 || K == 4 || K == 6 || K == 8,
+                "steps per pass must be 2, 3, 4, 6 or 8, got " << K);
+  RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
+  RMA_CHECK_ARG(nx >= 3 && ny >= 3, "grid too small: nx=" << nx << " ny=" << ny);
+  RMA_CHECK_ARG(T2 != T, "multi-step kernel cannot run in place");
+  for (int i = 0; i < nrects; ++i) {
+    const Rect& r = rects[i];
+    if (r.empty()) continue;
+    RMA_CHECK_ARG(r.x0 >= 1 && r.x1 <= nx - 1 && r.y0 >= 1 && r.y1 <= ny - 1,
+                  "rect " << i << " outside the interior of " << nx << "x" << ny);
+  }
+  RMA_CHECK_ARG(tune.chunk_rows >= 1, "chunk_rows=" << tune.chunk_rows);
+  const bool aligned = ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
+                       ((reinterpret_cast<uintptr_t>(T2) & 15) == 0) &&
+                       ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
+  int V = 1;
+  if (aligned && nx % 2 == 0) V = (tune.vec == 4 && nx % 4 == 0) ? 4 : 2;
+  const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
+  RectList L;
+  const int64_t total = plan_rects(L, rects, nrects, V, tune.chunk_rows, remap, false, K);
+  if (L.n == 0) return;
+  RMA_CHECK_ARG(total < (int64_t(1) << 31), "grid too large: " << total << " blocks");
+  const dim3 grid((unsigned)total), block(kBlock);
+  hipStream_t s = as_stream(stream);
+  const bool nts = tune.nontemporal & 1;
+#define RMA_TBK(KK, VV, NTS)                                                      \
+  stencilk_ovl_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c, \
+                                                          tune.chunk_rows, remap)
+#define RMA_TBK_V(KK)                                   \
+  if (V == 4) {                                         \
+    if (nts) { RMA_TBK(KK, 4, true); } else { RMA_TBK(KK, 4, false); } \
+  } else if (V == 2) {                                  \
+    if (nts) { RMA_TBK(KK, 2, true); } else { RMA_TBK(KK, 2, false); } \
+  } else {                                              \
+    if (nts) { RMA_TBK(KK, 1, true); } else { RMA_TBK(KK, 1, false); } \
+  }
+  switch (K) {
+    case 2: RMA_TBK_V(2) break;
+    case 3: RMA_TBK_V(3) break;
+    case 4: RMA_TBK_V(4) break;
+    case 6: RMA_TBK_V(6) break;
+    default: RMA_TBK_V(8) break;
+  }
+#undef RMA_TBK_V
+#undef RMA_TBK
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+}  // namespace rma

@@ -193,6 +193,41 @@ def stencil2_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: St
         stencil_torch(T2, S1, iCp, coef, rects)
 
 
+def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
+                  coef: StencilCoef, rects: Sequence[Rect] | None = None,
+                  tuning: StencilTuning | None = None) -> None:
+    """K time steps in one pass (K = 2, 3, 4, 6, 8; csrc/kernels/stencil_tbk.hip):
+    T2[r] = f^K(T)[r], the intermediate levels being f on the interior and T
+    on boundary/halo cells. Bitwise equal to K ``stencil_step`` calls. Default
+    tuning: 16-row chunks."""
+    if int(K) not in (2, 3, 4, 6, 8):
+        raise ValueError(f"K must be 2, 3, 4, 6 or 8, got {K}")
+    check_field("T", T)
+    ny, nx = T.shape
+    check_field("T2", T2, (ny, nx), T.device)
+    check_field("iCp", iCp, (ny, nx), T.device)
+    if T2.data_ptr() == T.data_ptr():
+        raise ValueError("T2 must not alias T (double buffering)")
+    rects = validate_rects(rects if rects is not None else [interior_rect(nx, ny)], nx, ny)
+    if not rects:
+        return
+    tn = tuning or StencilTuning(chunk_rows=16)
+    if T.is_cuda:
+        native().stencilk_rects(int(K), _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
+                                tn.chunk_rows, int(tn.nontemporal), stream_handle(T), True,
+                                tn.xcd_remap, tn.vec)
+    elif _use_native_cpu():
+        native().stencilk_rects(int(K), _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
+                                16, 0, 0, False)
+    else:
+        a = T.clone()
+        for _ in range(int(K) - 1):
+            b = a.clone()
+            stencil_torch(b, a, iCp, coef, [interior_rect(nx, ny)])
+            a = b
+        stencil_torch(T2, a, iCp, coef, rects)
+
+
 def strip_cells(nx: int, vec: int = 2) -> int:
     """x-width of one wave-strip of the march kernel (perf_hide frame rounding)."""
     if has_native():

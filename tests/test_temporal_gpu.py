@@ -78,3 +78,55 @@ def test_two_step_rejects_in_place_and_bad_rects():
         ops.stencil2_step(T, T, T, coef())
     with pytest.raises(ValueError):
         ops.stencil2_step(torch.empty_like(T), T, T, coef(), [(0, 5, 1, 5)])
+
+
+def k_steps_cpu(K, T, iCp, rects, fill=-5.0):
+    a = T.clone()
+    for _ in range(K - 1):
+        b = a.clone()
+        ops.stencil_step(b, a, iCp, coef())
+        a = b
+    out = torch.full_like(T, fill)
+    ops.stencil_step(out, a, iCp, coef(), rects)
+    return out
+
+
+@pytest.mark.parametrize("K", [2, 3, 4, 6, 8])
+@pytest.mark.parametrize("ny,nx", SHAPES)
+@pytest.mark.parametrize("chunk,vec", [(1, 2), (5, 4), (16, 2), (16, 4), (64, 2)])
+def test_k_step_bitwise(K, ny, nx, chunk, vec):
+    """K-step kernel with face-flux reuse == K one-step launches, bitwise."""
+    T, iCp = rand((ny, nx), 7), rand((ny, nx), 8) + 0.5
+    ref = k_steps_cpu(K, T, iCp, [ops.interior_rect(nx, ny)])
+    out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+    ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(),
+                      tuning=ops.StencilTuning(chunk_rows=chunk, vec=vec))
+    assert torch.equal(out.cpu(), ref)
+    cpu = torch.full_like(T, -5.0)  # the C++ twin
+    ops.stencilk_step(K, cpu, T, iCp, coef())
+    assert torch.equal(cpu, ref)
+
+
+@pytest.mark.parametrize("K", [3, 4, 6, 8])
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_k_step_rect_lists_and_unaligned(K, xcd):
+    ny, nx = 203, 900
+    T, iCp = rand((ny, nx), 9), rand((ny, nx), 10) + 0.5
+    w = K
+    rects = [(w, nx - w, w, 2 * w), (w, nx - w, ny - 2 * w, ny - w), (w, 2 * w, 2 * w, ny - 2 * w),
+             (nx - 2 * w, nx - w, 2 * w, ny - 2 * w)]
+    interior = (2 * w, nx - 2 * w, 2 * w, ny - 2 * w)
+    ref = k_steps_cpu(K, T, iCp, rects + [interior])
+    out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+    tn = ops.StencilTuning(chunk_rows=16, xcd_remap=xcd)
+    Td, iCpd = T.to(DEV), iCp.to(DEV)
+    ops.stencilk_step(K, out, Td, iCpd, coef(), rects, tn)
+    ops.stencilk_step(K, out, Td, iCpd, coef(), [interior], tn)
+    assert torch.equal(out.cpu(), ref)
+    base = rand(64 * 150 + 1, 11).to(DEV)  # 8-byte aligned view -> V=1 path
+    Tu = base[1:].view(150, 64)
+    ones = torch.ones((150, 64), dtype=torch.float64, device=DEV)
+    o2 = torch.zeros_like(ones)
+    ops.stencilk_step(K, o2, Tu, ones, coef(), tuning=tn)
+    assert torch.equal(o2.cpu(), k_steps_cpu(K, Tu.cpu(), ones.cpu(),
+                                             [ops.interior_rect(64, 150)], fill=0.0))
