@@ -53,11 +53,17 @@ def parse(argv=None):
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
-    ap.add_argument("--temporal", type=int, default=1, choices=[1, 2],
-                    help="2: two time steps per kernel pass (register temporal blocking, "
-                         "bitwise identical), width-2 halo exchange per pass, grid overlap 4")
-    ap.add_argument("--chunk2", type=int, default=16, help="two-step kernel rows per wave-task")
+    ap.add_argument("--temporal", type=int, default=6, choices=[1, 2, 3, 4, 6, 8],
+                    help="K: K time steps per kernel pass (register temporal blocking, "
+                         "bitwise identical), width-K halo exchange per pass, grid overlap 2K")
+    ap.add_argument("--chunk2", type=int, default=0,
+                    help="K-step kernel rows per wave-task (0: 16 for K=2, else 128)")
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="grid overlap (0: 2 x steps-per-pass, the minimum)")
+    ap.add_argument("--single-step-steps", type=int, default=100,
+                    help="after the timed run, also time this many steps of the one-step "
+                         "kernel on the same tile (reported in config; 0 = skip)")
     ap.add_argument("--json-out", default="")
     return ap.parse_args(argv)
 
@@ -118,7 +124,11 @@ def main(argv=None) -> int:
                           unroll=a.unroll, vec=a.vec, temporal=a.temporal, chunk2=a.chunk2,
                           unroll2=a.unroll2, use_graph=a.graph, quiet=True)
     t_setup = time.perf_counter()
-    model = Diffusion2D(cfg)
+    gkw = {}
+    if a.overlap:
+        gkw = {"overlaps": (a.overlap, a.overlap, 2),
+               "halowidths": (max(1, a.temporal), max(1, a.temporal), 1)}
+    model = Diffusion2D(cfg, grid_kwargs=gkw)
     g = model.g
     comm = g.comm
     model.synchronize()
@@ -138,6 +148,22 @@ def main(argv=None) -> int:
     wall = comm.allreduce(local_s, "max")
     bad = float(model.field[:: max(1, ny // 64), :: max(1, nx // 64)].isfinite().logical_not().sum())
     bad = comm.allreduce(bad, "sum")
+
+    # secondary: the one-step kernel (24 B/cell/step at the HBM roofline) on the
+    # same tile, so the temporal-blocking gain is visible in one record
+    single = None
+    if a.single_step_steps > 0 and a.temporal > 1:
+        model.set_temporal(1)
+        model.step(2)
+        model.synchronize()
+        comm.barrier()
+        torch.cuda.synchronize()
+        s0 = time.perf_counter()
+        model.step(a.single_step_steps)
+        torch.cuda.synchronize()
+        comm.barrier()
+        s1 = comm.allreduce(time.perf_counter() - s0, "max")
+        single = 3 * nx * ny * 8 / 1e9 / (s1 / a.single_step_steps)
 
     t_it = wall / a.steps
     teff_gpu = 3 * nx * ny * 8 / 1e9 / t_it
@@ -174,6 +200,14 @@ def main(argv=None) -> int:
             "b_width": list(bw),
             "hipgraph": bool(a.graph),
             "temporal_blocking": a.temporal,
+            "steps_per_kernel_pass": a.temporal,
+            "teff_note": ("T_eff = A_eff/t_step with A_eff = 3*nx*ny*8 B (reference "
+                          "perf.jl:55-58). With temporal blocking every step of every cell "
+                          "is still computed (bitwise equal to one-step updates) but HBM is "
+                          f"read/written once per {a.temporal} steps, so T_eff exceeds the "
+                          "HBM bandwidth; teff_single_step_kernel_GBps is the one-step "
+                          "kernel on the same tile") if a.temporal > 1 else "",
+            "teff_single_step_kernel_GBps": round(single, 2) if single else None,
             "overlap": list(g.overlaps[:2]),
             "setup_s": round(setup_s, 3),
             "nonfinite_cells_sampled": int(bad),

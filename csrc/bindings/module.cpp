@@ -353,6 +353,7 @@ PYBIND11_MODULE(_C, m) {
              p.oly = oly;
              p.tune2.chunk_rows = chunk2;
              p.tune2.unroll = unroll2;
+             p.tune2.xcd_remap = temporal > 2 ? 1 : -1;  // measured: sweep_tbk_16k
              p.tune2.nontemporal = nontemporal & 3;
              p.mode = static_cast<Mode>(mode);
              p.coef = to_coef(coef);

@@ -12,9 +12,10 @@
 //           join both, swap. This is the reference's intended variant (3)
 //           with exact frame/interior grids.
 //   kKp   : [flux] -> [residual] -> [update T in place] -> [halo(T)]
-//   temporal=2 (kPerf/kHide): each pass advances TWO steps with the two-step
-//           kernel on the "owned" rect (cells next to a neighbour's halo are
-//           left to the width-2 exchange), then one exchange of width 2.
+//   temporal=K>1 (kPerf/kHide): each pass advances K steps with the K-step
+//           kernel (stencil_tb.hip for K=2, stencil_tbk.hip otherwise) on the
+//           "owned" rect (the K cells next to a neighbour are left to the
+//           width-K exchange), then one exchange of width K (overlap 2K).
 //
 // Python never waits inside the loop; run() returns as soon as n steps are
 // enqueued, ordered after the caller's stream and before its next work.
@@ -39,12 +40,12 @@ struct ExecParams {
   int64_t bwx = 1, bwy = 1;    // perf_hide frame widths (cells beyond the boundary)
   int use_graph = 0;           // capture steps into a hipGraph and replay
   int graph_steps = 0;         // steps per captured graph (even; 0 = auto)
-  // Temporal blocking (kPerf/kHide): 2 = two time steps per kernel pass
-  // (stencil2_rects_gpu) and one halo exchange of width 2 per pass; needs a
-  // grid overlap >= 4 in every dimension with a neighbour. 1 = one step.
+  // Temporal blocking (kPerf/kHide): K = 2, 3, 4, 6, 8 time steps per kernel
+  // pass and one halo exchange of width K per pass; needs a grid overlap
+  // >= 2K in every dimension with a neighbour. 1 = one step per pass.
   int temporal = 1;
   int64_t olx = 2, oly = 2;    // grid overlaps of the field (IGG overlaps)
-  StencilTuning tune2{16, 3, 0, 2, 2, -1};  // two-step kernel: 16-row chunks, unroll 2
+  StencilTuning tune2{16, 3, 0, 2, 2, -1};  // K-step kernel tuning (K=2: 16-row chunks)
 };
 
 class DiffusionExecutor {
@@ -69,7 +70,9 @@ class DiffusionExecutor {
 
  private:
   void enqueue_step(double* Tin, double* Tout);
-  void enqueue_step2(double* Tin, double* Tout);  // temporal=2: two steps
+  void enqueue_step2(double* Tin, double* Tout);  // temporal=K: one K-step pass
+  void multi_step(double* Tin, double* Tout, const Rect* rects, int n, const StencilTuning& tn,
+                  void* stream);
   void exchange(double* A, stream_t s);
   void split(const Rect& out, int64_t bwx, int64_t bwy, std::vector<Rect>& frame,
              Rect& interior) const;
@@ -85,7 +88,7 @@ class DiffusionExecutor {
   double *qx_, *qy_, *dTdt_;
   Rect full_{}, interior_{};
   std::vector<Rect> frame_;
-  Rect out2_{}, interior2_{};  // temporal=2: owned rect and its interior
+  Rect out2_{}, interior2_{};  // temporal=K: owned rect and its interior
   std::vector<Rect> frame2_;
   int64_t hwx_ = 1, hwy_ = 1;
   void* s_hi_ = nullptr;  // hipStream_t

@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <array>
 #include <utility>
 
 #include "rma/hip_check.h"
@@ -27,7 +31,9 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   RMA_CHECK_ARG(!p.use_graph || !halo || halo->capturable(),
                 "hipGraph replay needs a capturable halo transport (RCCL or none); the loopback "
                 "transport synchronises on the host");
-  RMA_CHECK_ARG(p.temporal == 1 || p.temporal == 2, "temporal must be 1 or 2");
+  RMA_CHECK_ARG(p.temporal == 1 || p.temporal == 2 || p.temporal == 3 || p.temporal == 4 ||
+                    p.temporal == 6 || p.temporal == 8,
+                "temporal (steps per pass) must be 1, 2, 3, 4, 6 or 8, got " << p.temporal);
   RMA_CHECK_ARG(p.temporal == 1 || p.mode != Mode::kKp,
                 "temporal blocking applies to perf / perf_hide, not kp");
   RMA_CHECK_ARG(p.olx >= 2 && p.oly >= 2, "overlaps must be >= 2");
@@ -38,8 +44,8 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   for (int d = 0; d < 2; ++d)
     RMA_CHECK_ARG((nbr[d][0] < 0 && nbr[d][1] < 0) || ol[d] >= 2 * p.temporal,
                   "temporal=" << p.temporal << " needs a grid overlap >= " << 2 * p.temporal
-                              << " along dim " << d << " (init_global_grid overlaps=4, "
-                              << "halowidths=2), got " << ol[d]);
+                              << " along dim " << d << " (init_global_grid overlaps=2K, "
+                              << "halowidths=K), got " << ol[d]);
   full_ = {1, nx - 1, 1, ny - 1};
   // perf_hide: the frame must contain the send planes [ol-hw, ol) of every
   // side, so it is at least ol-1 cells wide (the reference's b_width >= overlap
@@ -52,11 +58,13 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   } else {
     interior_ = full_;
   }
-  if (p.temporal == 2) {
-    // owned rect of a two-step pass: next to a neighbour the cell at index 1
-    // is halo (width 2) and only the exchange refreshes it
-    out2_ = {nbr[0][0] >= 0 ? 2 : 1, nx - (nbr[0][1] >= 0 ? 2 : 1),
-             nbr[1][0] >= 0 ? 2 : 1, ny - (nbr[1][1] >= 0 ? 2 : 1)};
+  if (p.temporal > 1) {
+    // owned rect of a K-step pass: next to a neighbour the K cells [0,K) are
+    // halo and only the exchange refreshes them (level j is valid from
+    // column j on, so the pass outputs from column K)
+    const int64_t K = p.temporal;
+    out2_ = {nbr[0][0] >= 0 ? K : 1, nx - (nbr[0][1] >= 0 ? K : 1),
+             nbr[1][0] >= 0 ? K : 1, ny - (nbr[1][1] >= 0 ? K : 1)};
     RMA_CHECK_ARG(!out2_.empty(), "tile too small for temporal blocking: " << nx << "x" << ny);
     if (p.mode == Mode::kHide)
       split(out2_, std::max(p.bwx, p.olx - out2_.x0), std::max(p.bwy, p.oly - out2_.y0),
@@ -67,8 +75,27 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   int least = 0, greatest = 0;
   RMA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   hipStream_t hi, lo;
-  RMA_HIP_CHECK(hipStreamCreateWithPriority(&hi, hipStreamNonBlocking, greatest));
-  RMA_HIP_CHECK(hipStreamCreateWithPriority(&lo, hipStreamNonBlocking, least));
+  // Create the low-priority (interior) stream FIRST. Measured on MI355X /
+  // ROCm 7 (bench/probe_set_temporal.py, profiles/SUMMARY_r1.md): creating the
+  // high-priority stream first left every second executor of a process with
+  // a low-priority stream running the stencil ~25% slower (4.6 vs 6.2 TB/s);
+  // low-first (or unprioritised streams) is fast for every instance.
+  // RMA_EXEC_STREAMS=plain|hifirst selects the alternatives for diagnostics.
+  const char* sm = std::getenv("RMA_EXEC_STREAMS");
+  const std::string mode = sm ? sm : "lofirst";
+  if (mode == "plain") {
+    RMA_HIP_CHECK(hipStreamCreateWithFlags(&lo, hipStreamNonBlocking));
+    RMA_HIP_CHECK(hipStreamCreateWithFlags(&hi, hipStreamNonBlocking));
+  } else if (mode == "hifirst") {
+    RMA_HIP_CHECK(hipStreamCreateWithPriority(&hi, hipStreamNonBlocking, greatest));
+    RMA_HIP_CHECK(hipStreamCreateWithPriority(&lo, hipStreamNonBlocking, least));
+  } else {
+    RMA_HIP_CHECK(hipStreamCreateWithPriority(&lo, hipStreamNonBlocking, least));
+    RMA_HIP_CHECK(hipStreamCreateWithPriority(&hi, hipStreamNonBlocking, greatest));
+  }
+  if (std::getenv("RMA_EXEC_VERBOSE"))
+    fprintf(stderr, "[executor] priority range least=%d greatest=%d mode=%s hi=%p lo=%p\n", least,
+            greatest, mode.c_str(), (void*)hi, (void*)lo);
   s_hi_ = hi;
   s_lo_ = lo;
   hipEvent_t a, b, c;
@@ -167,23 +194,29 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
   }
 }
 
+void DiffusionExecutor::multi_step(double* Tin, double* Tout, const Rect* rects, int n,
+                                   const StencilTuning& tn, void* stream) {
+  if (p_.temporal == 2)  // dedicated two-step kernel: aligned strips, faster at K=2
+    stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, rects, n, p_.coef, tn, stream);
+  else
+    stencilk_rects_gpu(p_.temporal, Tout, Tin, iCp_, nx_, ny_, rects, n, p_.coef, tn, stream);
+}
+
 void DiffusionExecutor::enqueue_step2(double* Tin, double* Tout) {
-  const StencilCoef& c = p_.coef;
   if (p_.mode == Mode::kPerf) {
-    TraceRange tr("rma.step2.perf");
-    stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out2_, 1, c, p_.tune2, s_lo_);
+    TraceRange tr("rma.stepK.perf");
+    multi_step(Tin, Tout, &out2_, 1, p_.tune2, s_lo_);
     exchange(Tout, s_lo_);
     return;
   }
-  TraceRange tr("rma.step2.hide");
+  TraceRange tr("rma.stepK.hide");
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
   StencilTuning ft = p_.tune2;
-  ft.chunk_rows = std::min(ft.chunk_rows, 16);
+  ft.chunk_rows = std::min(ft.chunk_rows, 64);
   {
     TraceRange tb("rma.boundary");
-    stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, frame2_.data(), (int)frame2_.size(), c, ft,
-                       s_hi_);
+    multi_step(Tin, Tout, frame2_.data(), (int)frame2_.size(), ft, s_hi_);
   }
   {
     TraceRange th("rma.halo");
@@ -192,7 +225,7 @@ void DiffusionExecutor::enqueue_step2(double* Tin, double* Tout) {
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
   if (!interior2_.empty()) {
     TraceRange ti("rma.interior");
-    stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &interior2_, 1, c, p_.tune2, s_lo_);
+    multi_step(Tin, Tout, &interior2_, 1, p_.tune2, s_lo_);
   }
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
 }
@@ -207,13 +240,45 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
     }
     double* Tin = parity_ ? T2_ : T_;
     double* Tout = parity_ ? T_ : T2_;
-    if (p_.temporal == 2 && nsteps - i >= 2) {
+    const int64_t left = nsteps - i;
+    if (p_.temporal > 1 && left >= p_.temporal) {
       enqueue_step2(Tin, Tout);
-      steps_ += 2;
-      i += 2;
+      steps_ += p_.temporal;
+      i += p_.temporal;
+    } else if (p_.temporal > 1 && left >= 2) {
+      // remainder: one shorter pass (K' < K steps; the width-K exchange then
+      // rewrites [K', K) with the identical values the neighbour owns)
+      const int kr = left >= 6 ? 6 : left >= 4 ? 4 : left >= 3 ? 3 : 2;
+      TraceRange tr("rma.stepK.rest");
+      if (p_.mode == Mode::kHide) {  // previous pass done on both streams
+        RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+      }
+      Rect out = out2_;
+      const auto& nb = halo_ ? halo_->neighbors() : std::array<std::array<int, 2>, 3>{};
+      if (halo_) {
+        out = {nb[0][0] >= 0 ? kr : 1, nx_ - (nb[0][1] >= 0 ? kr : 1), nb[1][0] >= 0 ? kr : 1,
+               ny_ - (nb[1][1] >= 0 ? kr : 1)};
+      }
+      StencilTuning tn = p_.tune2;
+      if (kr == 2) {
+        tn.chunk_rows = 16;
+        tn.xcd_remap = -1;
+        stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
+      } else {
+        tn.xcd_remap = 1;
+        stencilk_rects_gpu(kr, Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
+      }
+      exchange(Tout, s_lo_);
+      if (p_.mode == Mode::kHide) {
+        RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+        RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
+        RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
+      }
+      steps_ += kr;
+      i += kr;
     } else {
-      // one step (also the odd remainder of a temporal run: with overlap 4 and
-      // halo width 2 the single-step update + exchange stays consistent)
+      // one step (also the remainder of a temporal run: with overlap 2K and
+      // halo width K the single-step update + exchange stays consistent)
       enqueue_step(Tin, Tout);
       ++steps_;
       ++i;
@@ -278,8 +343,8 @@ void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
   int64_t left = nsteps;
   if (p_.use_graph) {
     int64_t gl = p_.graph_steps > 0 ? p_.graph_steps : 20;
-    // keep the buffer parity of a replay neutral (temporal=2: 2 steps per swap)
-    const int64_t q = p_.temporal == 2 ? 4 : 2;
+    // keep the buffer parity of a replay neutral (K steps per swap)
+    const int64_t q = 2 * p_.temporal;
     gl = (gl + q - 1) / q * q;
     if (left >= gl) {
       if (!graph_exec_ || graph_len_ != gl) build_graph(gl);

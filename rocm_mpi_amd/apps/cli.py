@@ -75,10 +75,10 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
-    ap.add_argument("--temporal", type=int, default=1, choices=[1, 2],
-                    help="perf/perf_hide: 2 = two steps per kernel pass + width-2 halos "
-                         "(grid overlap 4); bitwise identical to 1")
-    ap.add_argument("--chunk2", type=int, default=16)
+    ap.add_argument("--temporal", type=int, default=1, choices=[1, 2, 3, 4, 6, 8],
+                    help="perf/perf_hide: K steps per kernel pass + width-K halos "
+                         "(grid overlap 2K); bitwise identical to 1")
+    ap.add_argument("--chunk2", type=int, default=0)
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
     ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf guard period")
     ap.add_argument("--checkpoint", default="", help="save the final state to this directory")

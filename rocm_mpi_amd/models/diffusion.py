@@ -40,6 +40,7 @@ from ..parallel.halo import gather_, update_halo_
 from ..utils import metrics
 from ..utils import profiling as prof
 
+TEMPORAL = (1, 2, 3, 4, 6, 8)
 VARIANTS = ("ap", "kp", "perf", "perf_hide")
 _MODE = {"perf": 0, "perf_hide": 1, "kp": 2}
 
@@ -76,10 +77,11 @@ class DiffusionConfig:
     profile: bool = False
     check_every: int = 0  # NaN/Inf guard period (0 = off)
     quiet: bool = False
-    # temporal blocking (perf / perf_hide): 2 = two steps per kernel pass and
-    # one width-2 halo exchange per pass (grid overlap 4); bitwise identical
+    # temporal blocking (perf / perf_hide): K = 2, 3, 4, 6, 8 steps per kernel
+    # pass and one width-K halo exchange per pass (grid overlap 2K); bitwise
+    # identical to K single steps
     temporal: int = 1
-    chunk2: int = 16  # two-step kernel tuning
+    chunk2: int = 0  # K-step kernel rows per wave-task (0: 16 for K=2, else 128)
     unroll2: int = 2
 
     def validate(self) -> None:
@@ -91,9 +93,9 @@ class DiffusionConfig:
             raise ValueError("init must be gaussian or random")
         if self.nx < 3 or self.ny < 3:
             raise ValueError("nx, ny >= 3 required")
-        if self.temporal not in (1, 2):
-            raise ValueError("temporal must be 1 or 2")
-        if self.temporal == 2 and self.variant not in ("perf", "perf_hide"):
+        if self.temporal not in TEMPORAL:
+            raise ValueError(f"temporal must be one of {TEMPORAL}")
+        if self.temporal > 1 and self.variant not in ("perf", "perf_hide"):
             raise ValueError("temporal blocking applies to the perf and perf_hide variants")
 
 
@@ -103,12 +105,14 @@ class Diffusion2D:
     def __init__(self, cfg: DiffusionConfig, grid_kwargs: dict | None = None):
         cfg.validate()
         self.cfg = cfg
+        self.chunk2 = cfg.chunk2 or (16 if cfg.temporal == 2 else 128)
         kw = dict(grid_kwargs or {})
         if not gg.grid_is_initialized():
             kw.setdefault("quiet", cfg.quiet)
-            if cfg.temporal == 2:  # width-2 halos need overlap 4 (IGG: ol >= 2*hw)
-                kw.setdefault("overlaps", (4, 4, 2))
-                kw.setdefault("halowidths", (2, 2, 1))
+            if cfg.temporal > 1:  # width-K halos need overlap 2K (IGG: ol >= 2*hw)
+                K = cfg.temporal
+                kw.setdefault("overlaps", (2 * K, 2 * K, 2))
+                kw.setdefault("halowidths", (K, K, 1))
             gg.init_global_grid(cfg.nx, cfg.ny, 1, dimx=cfg.dims[0], dimy=cfg.dims[1],
                                 periodx=cfg.periods[0], periody=cfg.periods[1],
                                 transport=cfg.transport, device=cfg.device, **kw)
@@ -153,7 +157,6 @@ class Diffusion2D:
         if use_native and cfg.variant != "ap":
             if dev.type != "cuda" or g.halo is None:
                 raise RuntimeError("native executor needs a GPU and the rccl/self transport")
-            bwx, bwy = cfg.b_width
             use_graph = bool(cfg.use_graph)
             if use_graph and not g.halo.capturable():
                 import warnings
@@ -163,16 +166,7 @@ class Diffusion2D:
                               RuntimeWarning, stacklevel=2)
                 use_graph = False
             self.use_graph = use_graph
-            self.executor = native().Executor(
-                self.T.data_ptr(), self.T2.data_ptr() if self.T2 is not None else 0,
-                self.iCp.data_ptr(), nx, ny, _MODE[cfg.variant], tuple(self.coef),
-                cfg.chunk_rows, int(cfg.nontemporal), ops.KERNELS[cfg.kernel], int(bwx), int(bwy),
-                int(use_graph), int(cfg.graph_steps), g.halo,
-                self.QX.data_ptr() if cfg.variant == "kp" else 0,
-                self.QY.data_ptr() if cfg.variant == "kp" else 0,
-                self.D.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
-                int(cfg.vec), int(cfg.temporal), int(g.overlaps[0]), int(g.overlaps[1]),
-                int(cfg.chunk2), int(cfg.unroll2))
+            self.executor = self._build_executor()
         self._ap_graph = None
         if cfg.variant == "ap" and cfg.use_graph:
             # ap on a GPU is ~11 small torch launches per step: replay them from
@@ -184,19 +178,58 @@ class Diffusion2D:
 
                 warnings.warn(f"hipGraph replay disabled for ap ({dev.type}, {g.transport} "
                               "transport)", RuntimeWarning, stacklevel=2)
-        if cfg.temporal == 2:
+        if cfg.temporal > 1:
+            K = cfg.temporal
             nb = g.neighbors
-            if any(max(nb[d]) >= 0 and g.overlaps[d] < 4 for d in (0, 1)):
-                raise ValueError("temporal=2 needs grid overlaps >= 4 (init_global_grid("
-                                 "overlaps=(4,4,2), halowidths=(2,2,1)))")
-            self.out2 = (2 if nb[0][0] >= 0 else 1, nx - (2 if nb[0][1] >= 0 else 1),
-                         2 if nb[1][0] >= 0 else 1, ny - (2 if nb[1][1] >= 0 else 1))
+            if any(max(nb[d]) >= 0 and g.overlaps[d] < 2 * K for d in (0, 1)):
+                raise ValueError(f"temporal={K} needs grid overlaps >= {2 * K} "
+                                 f"(init_global_grid(overlaps=({2 * K},{2 * K},2), "
+                                 f"halowidths=({K},{K},1)))")
+            # owned rect of a K-step pass (the K cells next to a neighbour are halo)
+            self.out2 = (K if nb[0][0] >= 0 else 1, nx - (K if nb[0][1] >= 0 else 1),
+                         K if nb[1][0] >= 0 else 1, ny - (K if nb[1][1] >= 0 else 1))
         if cfg.variant == "perf_hide":
             # the frame holds the send planes [ol-hw, ol): at least ol-1 wide
             bw = (max(cfg.b_width[0], g.overlaps[0] - 1), max(cfg.b_width[1], g.overlaps[1] - 1))
             self.frame_rects, self.interior = ops.hide_rects(nx, ny, *bw, vec=cfg.vec)
         self.tuning = ops.StencilTuning(cfg.chunk_rows, int(cfg.nontemporal), cfg.kernel,
                                         cfg.unroll, cfg.vec)
+
+    def _build_executor(self):
+        cfg, g = self.cfg, self.g
+        nx, ny = cfg.nx, cfg.ny
+        bwx, bwy = cfg.b_width
+        return native().Executor(
+            self.T.data_ptr(), self.T2.data_ptr() if self.T2 is not None else 0,
+            self.iCp.data_ptr(), nx, ny, _MODE[cfg.variant], tuple(self.coef),
+            cfg.chunk_rows, int(cfg.nontemporal), ops.KERNELS[cfg.kernel], int(bwx), int(bwy),
+            int(self.use_graph), int(cfg.graph_steps), g.halo,
+            self.QX.data_ptr() if cfg.variant == "kp" else 0,
+            self.QY.data_ptr() if cfg.variant == "kp" else 0,
+            self.D.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
+            int(cfg.vec), int(cfg.temporal), int(g.overlaps[0]), int(g.overlaps[1]),
+            int(self.chunk2), int(cfg.unroll2))
+
+    def set_temporal(self, K: int) -> None:
+        """Switch the steps per kernel pass (e.g. to time the one-step kernel on
+        the same tile). The grid overlap must allow it (2K <= overlap)."""
+        cfg, g = self.cfg, self.g
+        if K not in TEMPORAL or (K > 1 and cfg.variant not in ("perf", "perf_hide")):
+            raise ValueError(f"temporal={K} not available for {cfg.variant}")
+        nb = g.neighbors
+        if any(max(nb[d]) >= 0 and g.overlaps[d] < 2 * K for d in (0, 1)):
+            raise ValueError(f"temporal={K} needs grid overlaps >= {2 * K}")
+        self.synchronize()
+        if self.parity:  # make T the current field, then rebuild from parity 0
+            self.T, self.T2 = self.T2, self.T
+            self.parity = 0
+        cfg.temporal = K
+        self.chunk2 = cfg.chunk2 or (16 if K == 2 else 128)
+        if K > 1:
+            self.out2 = (K if nb[0][0] >= 0 else 1, cfg.nx - (K if nb[0][1] >= 0 else 1),
+                         K if nb[1][0] >= 0 else 1, cfg.ny - (K if nb[1][1] >= 0 else 1))
+        if self.executor is not None:
+            self.executor = self._build_executor()
 
     # ------------------------------------------------------------------
     def geometry(self, A_shape=None) -> ops.TileGeometry:
@@ -262,15 +295,16 @@ class Diffusion2D:
                 ops.residual(self.D, self.QX, self.QY, self.iCp, self.coef.rdx, self.coef.rdy)
                 ops.update(self.T, self.D, self.coef.dt)
                 update_halo_(self.T)
-            elif self.cfg.temporal == 2 and n - done >= 2:
-                # two steps per pass (the native executor splits frame/interior;
+            elif self.cfg.temporal > 1 and n - done >= self.cfg.temporal:
+                # K steps per pass (the native executor splits frame/interior;
                 # this reference loop runs the owned rect, then the exchange)
+                K = self.cfg.temporal
                 Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
-                ops.stencil2_step(Tout, Tin, self.iCp, self.coef, [self.out2])
+                ops.stencilk_step(K, Tout, Tin, self.iCp, self.coef, [self.out2])
                 update_halo_(Tout)
                 self.parity ^= 1
-                self.steps_done += 2
-                done += 2
+                self.steps_done += K
+                done += K
                 continue
             else:
                 Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)

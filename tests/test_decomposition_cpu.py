@@ -77,10 +77,10 @@ def test_periodic_decomposition_invariance():
 
 def spmd_tiles(rank, hub, variant, nx, ny, nt, dims, temporal, periods=(0, 0, 0)):
     """Every rank returns (coords, full local field incl. halo, global sizes)."""
-    ol = 4 if temporal == 2 else 2
+    ol = 2 * temporal
     gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], periodx=periods[0],
                         periody=periods[1], overlaps=(ol, ol, 2),
-                        halowidths=(ol // 2, ol // 2, 1), quiet=True, loopback=(hub, rank),
+                        halowidths=(temporal, temporal, 1), quiet=True, loopback=(hub, rank),
                         select_device=False)
     m = Diffusion2D(DiffusionConfig(variant=variant, nx=nx, ny=ny, nt=nt, init="random",
                                     quiet=True, dims=dims, periods=periods, temporal=temporal,
@@ -93,15 +93,15 @@ def spmd_tiles(rank, hub, variant, nx, ny, nt, dims, temporal, periods=(0, 0, 0)
 
 @pytest.mark.parametrize("variant", ["perf", "perf_hide"])
 @pytest.mark.parametrize("P,dims", [(1, (1, 1)), (2, (2, 1)), (3, (1, 3)), (4, (2, 2))])
-@pytest.mark.parametrize("nt", [20, 13])
-def test_temporal_blocking_equals_golden(variant, P, dims, nt):
-    """Two steps per pass + width-2 halos on an overlap-4 grid: every local
-    tile (halo included) equals its window of the global golden model after
-    an even or odd number of steps."""
+@pytest.mark.parametrize("nt,K", [(20, 2), (13, 2), (23, 3), (26, 4)])
+def test_temporal_blocking_equals_golden(variant, P, dims, nt, K):
+    """K steps per pass + width-K halos on an overlap-2K grid: every local
+    tile (halo included) equals its window of the global golden model, also
+    when nt is not a multiple of K."""
     nx, ny = 37, 30
-    res = run_loopback(P, spmd_tiles, variant, nx, ny, nt, dims, 2)
+    res = run_loopback(P, spmd_tiles, variant, nx, ny, nt, dims, K)
     nxg, nyg, _ = res[0][2]
-    assert (nxg, nyg) == (dims[0] * (nx - 4) + 4, dims[1] * (ny - 4) + 4)
+    assert (nxg, nyg) == (dims[0] * (nx - 2 * K) + 2 * K, dims[1] * (ny - 2 * K) + 2 * K)
     T0 = torch.empty((nyg, nxg), dtype=torch.float64)  # the global random field
     ops.init_random_(T0, ops.TileGeometry(0, 0, nxg, nyg, 1.0, 1.0), seed=1234)
     G = golden.run(nxg, nyg, nt, T0=T0.numpy())

@@ -46,14 +46,14 @@ def test_loopback_gpu_equals_golden(variant, P, dims):
     assert np.array_equal(Tv, G[1:-1, 1:-1])
 
 
-def spmd_tiles(rank, hub, variant, nx, ny, nt, dims, periods=(0, 0, 0), graph=False):
-    """temporal=2 on an overlap-4 grid; returns (coords, local field, global sizes)."""
+def spmd_tiles(rank, hub, variant, nx, ny, nt, dims, K=2, periods=(0, 0, 0), graph=False):
+    """temporal=K on an overlap-2K grid; returns (coords, local field, global sizes)."""
     gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], periodx=periods[0],
-                        periody=periods[1], overlaps=(4, 4, 2), halowidths=(2, 2, 1),
+                        periody=periods[1], overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
                         quiet=True, loopback=(hub, rank))
     m = Diffusion2D(DiffusionConfig(variant=variant, nx=nx, ny=ny, nt=nt, init="random",
-                                    quiet=True, dims=dims, periods=periods, temporal=2,
-                                    use_graph=graph, graph_steps=8))
+                                    quiet=True, dims=dims, periods=periods, temporal=K,
+                                    use_graph=graph, graph_steps=8, chunk2=0))
     assert m.executor is not None
     m.step(nt)
     out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g)
@@ -64,30 +64,30 @@ def spmd_tiles(rank, hub, variant, nx, ny, nt, dims, periods=(0, 0, 0), graph=Fa
 
 @pytest.mark.parametrize("variant", ["perf_hide", "perf"])
 @pytest.mark.parametrize("P,dims", [(1, (1, 1)), (2, (2, 1)), (4, (2, 2)), (8, (4, 2))])
-@pytest.mark.parametrize("nt", [22, 15])
-def test_loopback_gpu_temporal_equals_golden(variant, P, dims, nt):
-    """Native executor, two-step kernel + width-2 exchange (frame on the
+@pytest.mark.parametrize("nt,K", [(22, 2), (15, 2), (27, 4), (40, 6), (19, 8)])
+def test_loopback_gpu_temporal_equals_golden(variant, P, dims, nt, K):
+    """Native executor, K-step kernel + width-K exchange (frame on the
     high-priority stream, interior on the low one): every tile == golden."""
     from rocm_mpi_amd import ops
 
     nx, ny = 300, 134
-    res = run_loopback(P, spmd_tiles, variant, nx, ny, nt, dims, timeout=120)
+    res = run_loopback(P, spmd_tiles, variant, nx, ny, nt, dims, K, timeout=120)
     nxg, nyg, _ = res[0][2]
     T0 = torch.empty((nyg, nxg), dtype=torch.float64)
     ops.init_random_(T0, ops.TileGeometry(0, 0, nxg, nyg, 1.0, 1.0), seed=1234)
     G = golden.run(nxg, nyg, nt, T0=T0.numpy())
     for coords, T, _ in res:
-        gx0, gy0 = coords[0] * (nx - 4), coords[1] * (ny - 4)
+        gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
         assert np.array_equal(T, G[gy0:gy0 + ny, gx0:gx0 + nx])
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_temporal_single_rank_periodic_and_graph(graph):
-    """1 rank, periodic (self exchange of width 2), optional hipGraph replay
-    (8 steps = 4 two-step passes per graph) == the 1-step executor."""
+@pytest.mark.parametrize("graph,K", [(False, 2), (True, 2), (False, 6), (True, 4)])
+def test_temporal_single_rank_periodic_and_graph(graph, K):
+    """1 rank, periodic (self exchange of width K), optional hipGraph replay
+    == the 1-step executor."""
     def run(temporal, g):
-        gg.init_global_grid(258, 130, 1, periodx=1, periody=1, overlaps=(4, 4, 2),
-                            halowidths=(2, 2, 1), quiet=True)
+        gg.init_global_grid(258, 130, 1, periodx=1, periody=1, overlaps=(2 * K, 2 * K, 2),
+                            halowidths=(K, K, 1), quiet=True)
         m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=258, ny=130, nt=1,
                                         init="random", quiet=True, periods=(1, 1, 0),
                                         temporal=temporal, use_graph=g, graph_steps=8))
@@ -96,7 +96,7 @@ def test_temporal_single_rank_periodic_and_graph(graph):
         m.close()
         gg.finalize_global_grid()
         return f
-    assert torch.equal(run(2, graph), run(1, False))
+    assert torch.equal(run(K, graph), run(1, False))
 
 
 def test_loopback_gpu_reference_oracle():
