@@ -53,11 +53,11 @@ def parse(argv=None):
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
-    ap.add_argument("--temporal", type=int, default=6, choices=[1, 2, 3, 4, 6, 8],
+    ap.add_argument("--temporal", type=int, default=8, choices=[1, 2, 3, 4, 6, 8],
                     help="K: K time steps per kernel pass (register temporal blocking, "
                          "bitwise identical), width-K halo exchange per pass, grid overlap 2K")
     ap.add_argument("--chunk2", type=int, default=0,
-                    help="K-step kernel rows per wave-task (0: 16 for K=2, else 128)")
+                    help="K-step kernel rows per wave-task (0: auto, models.diffusion.default_chunk2)")
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
     ap.add_argument("--overlap", type=int, default=0,
                     help="grid overlap (0: 2 x steps-per-pass, the minimum)")
@@ -200,6 +200,7 @@ def main(argv=None) -> int:
             "b_width": list(bw),
             "hipgraph": bool(a.graph),
             "temporal_blocking": a.temporal,
+            "chunk2": model.chunk2,
             "steps_per_kernel_pass": a.temporal,
             "teff_note": ("T_eff = A_eff/t_step with A_eff = 3*nx*ny*8 B (reference "
                           "perf.jl:55-58). With temporal blocking every step of every cell "

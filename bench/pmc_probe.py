@@ -29,7 +29,7 @@ s = torch.cuda.current_stream().cuda_stream
 nat = native()
 which = os.environ.get("RMA_PROBE_SET", "all")
 if which in ("all", "tbk"):  # multi-step kernels (temporal blocking)
-    for K, ch in ((2, 16), (3, 128), (4, 128)):
+    for K, ch in ((2, 16), (3, 128), (4, 128), (6, 128), (8, 128)):
         for _ in range(reps):
             ops.stencilk_step(K, T2, T, iCp, c, tuning=ops.StencilTuning(chunk_rows=ch,
                                                                         xcd_remap=1))

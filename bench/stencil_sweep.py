@@ -42,6 +42,7 @@ def main(argv=None):
     ap.add_argument("--tbk-chunks", default="16")
     ap.add_argument("--tbk-xcds", default="0")
     ap.add_argument("--tbk-vecs", default="2")
+    ap.add_argument("--tbk-kernels", default="march", help="march (1/Cp in registers), lds (LDS ring)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -98,10 +99,11 @@ def main(argv=None):
                     2 * bytes_model)
     for K in [int(v) for v in a.tbk.split(",") if v]:
         for c in [int(v) for v in a.tbk_chunks.split(",")]:
-            for x, vv in [(int(x), int(vv)) for x in a.tbk_xcds.split(",")
-                          for vv in a.tbk_vecs.split(",")]:
-                tn = ops.StencilTuning(chunk_rows=c, nontemporal=3, xcd_remap=x, vec=vv)
-                variants[f"tbk{K}_c{c}_x{x}_v{vv}"] = (
+            for x, vv, kk in [(int(x), int(vv), kk) for x in a.tbk_xcds.split(",")
+                              for vv in a.tbk_vecs.split(",") for kk in a.tbk_kernels.split(",")]:
+                tn = ops.StencilTuning(chunk_rows=c, nontemporal=3, xcd_remap=x, vec=vv,
+                                       kernel=kk)
+                variants[f"tbk{K}_c{c}_x{x}_v{vv}_{kk}"] = (
                     lambda K=K, tn=tn: ops.stencilk_step(K, T2, T, iCp, coef, rect, tuning=tn),
                     K * bytes_model)
     variants["lds"] = (lambda: ops.stencil_step(T2, T, iCp, coef,

@@ -147,13 +147,14 @@ PYBIND11_MODULE(_C, m) {
       "stencilk_rects",
       [](int K, uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
          const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
-         uintptr_t stream, bool gpu, int xcd_remap, int vec) {
+         uintptr_t stream, bool gpu, int xcd_remap, int vec, int kernel) {
         auto r = to_rects(rects);
         StencilTuning tn;
         tn.chunk_rows = chunk_rows;
         tn.nontemporal = nontemporal;
         tn.xcd_remap = xcd_remap;
         tn.vec = vec;
+        tn.kernel = kernel;
         if (gpu)
           stencilk_rects_gpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
                              r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
@@ -166,7 +167,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("K"), py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"),
       py::arg("rects"), py::arg("coef"), py::arg("chunk_rows") = 16, py::arg("nontemporal") = 3,
       py::arg("stream") = 0, py::arg("gpu") = true, py::arg("xcd_remap") = -1,
-      py::arg("vec") = 2);
+      py::arg("vec") = 2, py::arg("kernel") = 0);
   m.def(
       "stream_copy",
       [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {
@@ -354,6 +355,7 @@ PYBIND11_MODULE(_C, m) {
              p.tune2.chunk_rows = chunk2;
              p.tune2.unroll = unroll2;
              p.tune2.xcd_remap = temporal > 2 ? 1 : -1;  // measured: sweep_tbk_16k
+             p.tune2.kernel = temporal > 2 ? 1 : 0;      // LDS 1/Cp ring (occupancy at K=8)
              p.tune2.nontemporal = nontemporal & 3;
              p.mode = static_cast<Mode>(mode);
              p.coef = to_coef(coef);

@@ -45,7 +45,9 @@ __device__ __forceinline__ double face(double lv, double rv, double mlam, double
 }
 
 
-template <int K, int V, bool NT>
+// kLds: keep the masked 1/Cp window in an LDS ring (per wave, slot = row mod
+// K) instead of K*V registers, for occupancy (kernel=1 of StencilTuning).
+template <int K, int V, bool NT, bool kLds>
 __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
     int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
@@ -92,24 +94,72 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
   load_row<V>(pT, T + rowc(i + 1) * nx + xl);
   load_row<V>(pC, iCp + rowc(i) * nx + xl);
 
+  // LDS ring of masked 1/Cp rows: [wave][slot][lane*V + v] (16-B per lane)
+  __shared__ double ring[kLds ? kWavesPerBlock * K * W : 1];
+  double* myring = ring + (kLds ? wave * K * W + lane * V : 0);
+  int slot = 0;  // ring slot of the current level-1 row (iteration count mod K)
+  if constexpr (kLds) {  // slots read before their first write feed only discarded rows
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int v = 0; v < V; ++v) myring[j * W + v] = 0.0;
+  }
+
   auto iter = [&](auto Pc) {
     constexpr int P = decltype(Pc)::value;
     // level 0 <- prefetched T row i+1; 1/Cp window <- prefetched row i (masked)
     const bool rin1 = i >= 1 && i <= ny - 2;  // row of level 1 (wave-uniform)
 #pragma unroll
     for (int v = 0; v < V; ++v) w[0][P][v] = pT[v];
+    if constexpr (kLds) {
+      double g[V];
 #pragma unroll
-    for (int j = K - 1; j > 0; --j) {
+      for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? pC[v] : 0.0;
+      double* dst = myring + slot * W;
+      if constexpr (V == 1) {
+        dst[0] = g[0];
+      } else {
 #pragma unroll
-      for (int v = 0; v < V; ++v) gic[j][v] = gic[j - 1][v];
+        for (int h = 0; h < V / 2; ++h) {
+          dbl2 t2;
+          t2.x = g[2 * h];
+          t2.y = g[2 * h + 1];
+          reinterpret_cast<dbl2*>(dst)[h] = t2;
+        }
+      }
+
+    } else {
+#pragma unroll
+      for (int j = K - 1; j > 0; --j) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) gic[j][v] = gic[j - 1][v];
+      }
+#pragma unroll
+      for (int v = 0; v < V; ++v) gic[0][v] = (rin1 && cin[v]) ? pC[v] : 0.0;
     }
-#pragma unroll
-    for (int v = 0; v < V; ++v) gic[0][v] = (rin1 && cin[v]) ? pC[v] : 0.0;
     load_row<V>(pT, T + rowc(i + 2) * nx + xl);
     load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
 #pragma unroll
     for (int j = 1; j <= K; ++j) {
       const int64_t row = i - (j - 1);
+      double icl[V];  // masked 1/Cp of `row` (written j-1 iterations ago)
+      if constexpr (kLds) {
+        const int sl = slot - (j - 1) < 0 ? slot - (j - 1) + K : slot - (j - 1);
+        const double* src = myring + sl * W;
+        if constexpr (V == 1) {
+          icl[0] = src[0];
+        } else {
+#pragma unroll
+          for (int h = 0; h < V / 2; ++h) {
+            const dbl2 t2 = reinterpret_cast<const dbl2*>(src)[h];
+            icl[2 * h] = t2.x;
+            icl[2 * h + 1] = t2.y;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) icl[v] = gic[j - 1][v];
+      }
       const double(&c)[V] = w[j - 1][1 - P];
       const double(&dn)[V] = w[j - 1][P];
       const double rn = __shfl_down(c[0], 1);  // lane 63: garbage (invalid column)
@@ -124,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
         const double qD = fy[j - 1][v];
         fy[j - 1][v] = qU;
         const double qL = v == 0 ? ql0 : qr[v - 1];
-        res[v] = c[v] + k.dt * (gic[j - 1][v] * ((-(qr[v] - qL)) * k.rdx - (qU - qD) * k.rdy));
+        res[v] = c[v] + k.dt * (icl[v] * ((-(qr[v] - qL)) * k.rdx - (qU - qD) * k.rdy));
       }
       if (j < K) {
         const int jj = j < K ? j : K - 1;
@@ -134,6 +184,7 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
         store_row<V, NT>(T2 + row * nx + x, res, m);
       }
     }
+    if constexpr (kLds) slot = slot + 1 == K ? 0 : slot + 1;
   };
   for (;;) {
     iter(std::integral_constant<int, 0>{});
@@ -173,9 +224,13 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
   const dim3 grid((unsigned)total), block(kBlock);
   hipStream_t s = as_stream(stream);
   const bool nts = tune.nontemporal & 1;
-#define RMA_TBK(KK, VV, NTS)                                                      \
-  stencilk_ovl_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c, \
-                                                          tune.chunk_rows, remap)
+#define RMA_TBK(KK, VV, NTS)                                                              \
+  if (tune.kernel == 1)                                                                     \
+    stencilk_ovl_kernel<KK, VV, NTS, true><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,  \
+                                                                  tune.chunk_rows, remap);  \
+  else                                                                                      \
+    stencilk_ovl_kernel<KK, VV, NTS, false><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c, \
+                                                                   tune.chunk_rows, remap)
 #define RMA_TBK_V(KK)                                   \
   if (V == 4) {                                         \
     if (nts) { RMA_TBK(KK, 4, true); } else { RMA_TBK(KK, 4, false); } \

@@ -266,6 +266,7 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
         stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       } else {
         tn.xcd_remap = 1;
+        tn.kernel = 1;
         stencilk_rects_gpu(kr, Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       }
       exchange(Tout, s_lo_);

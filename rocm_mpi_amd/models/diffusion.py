@@ -41,6 +41,18 @@ from ..utils import metrics
 from ..utils import profiling as prof
 
 TEMPORAL = (1, 2, 3, 4, 6, 8)
+
+
+def default_chunk2(K: int, ny: int) -> int:
+    """Rows per wave-task of the K-step kernels (profiles/SUMMARY_r1.md sweeps):
+    16 for the two-step kernel; longer chunks amortise the 2K-1 rows a chunk
+    recomputes at its edges: 128-256 up to 32K-row tiles, 512-1024 beyond
+    (101376^2, K=6: c128 28.1, c256 29.0, c512 29.4 TB/s; K=8: c1024 30.7)."""
+    if K == 2:
+        return 16
+    if ny >= 32768:
+        return 1024 if K >= 8 else 512
+    return 128 if K >= 8 else 256
 VARIANTS = ("ap", "kp", "perf", "perf_hide")
 _MODE = {"perf": 0, "perf_hide": 1, "kp": 2}
 
@@ -81,7 +93,7 @@ class DiffusionConfig:
     # pass and one width-K halo exchange per pass (grid overlap 2K); bitwise
     # identical to K single steps
     temporal: int = 1
-    chunk2: int = 0  # K-step kernel rows per wave-task (0: 16 for K=2, else 128)
+    chunk2: int = 0  # K-step kernel rows per wave-task (0: default_chunk2)
     unroll2: int = 2
 
     def validate(self) -> None:
@@ -105,7 +117,7 @@ class Diffusion2D:
     def __init__(self, cfg: DiffusionConfig, grid_kwargs: dict | None = None):
         cfg.validate()
         self.cfg = cfg
-        self.chunk2 = cfg.chunk2 or (16 if cfg.temporal == 2 else 128)
+        self.chunk2 = cfg.chunk2 or default_chunk2(cfg.temporal, cfg.ny)
         kw = dict(grid_kwargs or {})
         if not gg.grid_is_initialized():
             kw.setdefault("quiet", cfg.quiet)
@@ -224,7 +236,7 @@ class Diffusion2D:
             self.T, self.T2 = self.T2, self.T
             self.parity = 0
         cfg.temporal = K
-        self.chunk2 = cfg.chunk2 or (16 if K == 2 else 128)
+        self.chunk2 = cfg.chunk2 or default_chunk2(K, cfg.ny)
         if K > 1:
             self.out2 = (K if nb[0][0] >= 0 else 1, cfg.nx - (K if nb[0][1] >= 0 else 1),
                          K if nb[1][0] >= 0 else 1, cfg.ny - (K if nb[1][1] >= 0 else 1))

@@ -215,7 +215,7 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
     if T.is_cuda:
         native().stencilk_rects(int(K), _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                 tn.chunk_rows, int(tn.nontemporal), stream_handle(T), True,
-                                tn.xcd_remap, tn.vec)
+                                tn.xcd_remap, tn.vec, KERNELS[tn.kernel])
     elif _use_native_cpu():
         native().stencilk_rects(int(K), _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                 16, 0, 0, False)

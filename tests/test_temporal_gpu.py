@@ -93,14 +93,16 @@ def k_steps_cpu(K, T, iCp, rects, fill=-5.0):
 
 @pytest.mark.parametrize("K", [2, 3, 4, 6, 8])
 @pytest.mark.parametrize("ny,nx", SHAPES)
-@pytest.mark.parametrize("chunk,vec", [(1, 2), (5, 4), (16, 2), (16, 4), (64, 2)])
-def test_k_step_bitwise(K, ny, nx, chunk, vec):
+@pytest.mark.parametrize("chunk,vec,kern", [(1, 2, "march"), (5, 4, "march"), (16, 2, "march"),
+                                            (16, 4, "march"), (64, 2, "march"), (3, 2, "lds"),
+                                            (16, 4, "lds"), (64, 2, "lds")])
+def test_k_step_bitwise(K, ny, nx, chunk, vec, kern):
     """K-step kernel with face-flux reuse == K one-step launches, bitwise."""
     T, iCp = rand((ny, nx), 7), rand((ny, nx), 8) + 0.5
     ref = k_steps_cpu(K, T, iCp, [ops.interior_rect(nx, ny)])
     out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
     ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(),
-                      tuning=ops.StencilTuning(chunk_rows=chunk, vec=vec))
+                      tuning=ops.StencilTuning(chunk_rows=chunk, vec=vec, kernel=kern))
     assert torch.equal(out.cpu(), ref)
     cpu = torch.full_like(T, -5.0)  # the C++ twin
     ops.stencilk_step(K, cpu, T, iCp, coef())
