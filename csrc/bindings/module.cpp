@@ -352,10 +352,9 @@ PYBIND11_MODULE(_C, m) {
              p.temporal = temporal;
              p.olx = olx;
              p.oly = oly;
-             p.tune2.chunk_rows = chunk2;
-             p.tune2.unroll = unroll2;
-             p.tune2.xcd_remap = temporal > 2 ? 1 : -1;  // measured: sweep_tbk_16k
-             p.tune2.kernel = temporal > 2 ? 1 : 0;      // LDS 1/Cp ring (occupancy at K=8)
+             p.tune2 = default_tune_k(temporal, ny);  // measured defaults
+             if (chunk2 > 0) p.tune2.chunk_rows = chunk2;
+             if (temporal == 2) p.tune2.unroll = unroll2;
              p.tune2.nontemporal = nontemporal & 3;
              p.mode = static_cast<Mode>(mode);
              p.coef = to_coef(coef);

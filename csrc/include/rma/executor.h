@@ -48,6 +48,12 @@ struct ExecParams {
   StencilTuning tune2{16, 3, 0, 2, 2, -1};  // K-step kernel tuning (K=2: 16-row chunks)
 };
 
+// Measured defaults of the K-step kernels (profiles/SUMMARY_r1.md): K=2 uses
+// the aligned two-step kernel with 16-row chunks; K>=3 the overlapped-strip
+// kernel with the LDS 1/Cp ring, per-XCD task ranges and chunks growing with
+// the tile height (they amortise the 2K-1 rows recomputed per chunk).
+StencilTuning default_tune_k(int K, int64_t ny);
+
 class DiffusionExecutor {
  public:
   // T, T2, iCp: (ny, nx) device fields; qx/qy/dTdt only for kKp.

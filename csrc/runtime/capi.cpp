@@ -241,21 +241,32 @@ int rma_fill(double* A, int64_t n, double value, void* stream) {
   return guard([&] { rma::fill_gpu(A, n, value, stream); });
 }
 
-int rma_executor_create(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
-                        int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
-                        double* qx, double* qy, double* dTdt, rma_executor** out) {
+int rma_executor_create_k(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
+                          int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
+                          int steps_per_pass, double* qx, double* qy, double* dTdt,
+                          rma_executor** out) {
   return guard([&] {
-    RMA_CHECK_ARG(out && mode >= 0 && mode <= 2, "bad executor arguments");
+    RMA_CHECK_ARG(g && out && mode >= 0 && mode <= 2, "bad executor arguments");
     rma::ExecParams p;
     p.mode = static_cast<rma::Mode>(mode);
     p.coef = {coef[0], coef[1], coef[2], coef[3]};
     p.bwx = bwx;
     p.bwy = bwy;
+    p.temporal = steps_per_pass;
+    p.olx = g->overlaps[0];
+    p.oly = g->overlaps[1];
+    p.tune2 = rma::default_tune_k(steps_per_pass, ny);
     auto e = std::make_unique<rma_executor>();
     e->ex = std::make_unique<rma::DiffusionExecutor>(T, T2, iCp, nx, ny, p, g->halo.get(), qx, qy,
                                                      dTdt);
     *out = e.release();
   });
+}
+
+int rma_executor_create(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
+                        int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
+                        double* qx, double* qy, double* dTdt, rma_executor** out) {
+  return rma_executor_create_k(g, mode, T, T2, iCp, nx, ny, coef, bwx, bwy, 1, qx, qy, dTdt, out);
 }
 
 int rma_executor_run(rma_executor* e, int64_t nsteps, void* stream) {

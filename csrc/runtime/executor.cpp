@@ -19,6 +19,20 @@ hipStream_t S(void* p) { return reinterpret_cast<hipStream_t>(p); }
 hipEvent_t E(void* p) { return reinterpret_cast<hipEvent_t>(p); }
 }  // namespace
 
+StencilTuning default_tune_k(int K, int64_t ny) {
+  StencilTuning t;
+  t.nontemporal = 3;
+  if (K <= 2) {
+    t.chunk_rows = 16;
+    t.unroll = 2;
+    return t;
+  }
+  t.kernel = 1;
+  t.xcd_remap = 1;
+  t.chunk_rows = ny >= 32768 ? (K >= 8 ? 1024 : 512) : (K >= 8 ? 128 : 256);
+  return t;
+}
+
 DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, int64_t nx,
                                      int64_t ny, const ExecParams& p, HaloExchanger* halo,
                                      double* qx, double* qy, double* dTdt)

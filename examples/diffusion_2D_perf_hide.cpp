@@ -2,7 +2,8 @@
 // reference scripts/diffusion_2D_perf_hide.jl's intended overlap variant,
 // written against the C ABI of librma_core.so (rma/capi.h).
 //
-//   ./build/examples/diffusion_2D_perf_hide [nx] [nt] [mode]        # 1 GPU
+//   ./build/examples/diffusion_2D_perf_hide [nx] [nt] [mode] [K]    # 1 GPU
+//   (mode 0 perf, 1 perf_hide; K = time steps per kernel pass, 1/2/3/4/6/8)
 //   python -m rocm_mpi_amd.launch -n 8 ./build/examples/diffusion_2D_perf_hide 16384 1000
 //
 // Ranks come from RANK / WORLD_SIZE / LOCAL_RANK (torchrun or our launcher);
@@ -46,6 +47,7 @@ int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? std::atoll(argv[1]) : 16384;
   const int nt = argc > 2 ? std::atoi(argv[2]) : 1000;
   const int mode = argc > 3 ? std::atoi(argv[3]) : 1;  // 0 perf, 1 perf_hide
+  const int K = argc > 4 ? std::atoi(argv[4]) : 1;     // steps per kernel pass
   const int rank = env_int("RANK", 0), size = env_int("WORLD_SIZE", 1);
   const int local = env_int("LOCAL_RANK", rank);
   int ndev = 0;
@@ -79,7 +81,10 @@ int main(int argc, char** argv) {
   rma_grid* g = nullptr;
   int me = 0, dims[3], coords[3];
   const int dims_in[3] = {0, 0, 1};
-  CK(rma_init_global_grid((int)n, (int)n, 1, dims_in, nullptr, nullptr, nullptr, size, rank,
+  // temporal blocking: K steps per kernel pass need overlap 2K and halo width K
+  const int ol[3] = {2 * std::max(1, K), 2 * std::max(1, K), 2};
+  const int hw[3] = {std::max(1, K), std::max(1, K), 1};
+  CK(rma_init_global_grid((int)n, (int)n, 1, dims_in, nullptr, ol, hw, size, rank,
                           size > 1 ? uid : nullptr, dev, &g, &me, dims, coords));
   const double lx = 10, ly = 10, lam = 1, Cp0 = 1;
   const double dx = lx / rma_nx_g(g), dy = ly / rma_ny_g(g);
@@ -96,7 +101,8 @@ int main(int argc, char** argv) {
   CK(rma_init_gaussian(g, T, n, n, dx, dy, lx, ly, s));
   HK(hipMemcpyAsync(T2, T, bytes, hipMemcpyDeviceToDevice, s));
   rma_executor* ex = nullptr;
-  CK(rma_executor_create(g, mode, T, T2, iCp, n, n, coef, 1, 1, nullptr, nullptr, nullptr, &ex));
+  CK(rma_executor_create_k(g, mode, T, T2, iCp, n, n, coef, 1, 1, K, nullptr, nullptr, nullptr,
+                           &ex));
   if (me == 0)
     std::printf("Global grid: %ldx%ldx1 (nprocs: %d, dims: %dx%dx%d)\n", (long)rma_nx_g(g),
                 (long)rma_ny_g(g), size, dims[0], dims[1], dims[2]);

@@ -64,3 +64,21 @@ def diffusion_gpu(rank, world, outdir, variant, nx, ny, nt, dims):
         with open(os.path.join(outdir, "meta.txt"), "w") as f:
             f.write(f"{g.nxyz_g[0]} {g.nxyz_g[1]} {g.transport}")
     m.close()
+
+
+def diffusion_tiles(rank, world, outdir, variant, nx, ny, nt, dims, temporal, device="cpu"):
+    """Each rank saves its full local field (halo incl.) and coords: temporal
+    blocking uses overlap 2K, so tiles are compared with golden windows."""
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    m = Diffusion2D(DiffusionConfig(variant=variant, nx=nx, ny=ny, nt=nt, dims=tuple(dims) + (0,),
+                                    quiet=True, init="random", device=device,
+                                    temporal=temporal))
+    m.step(nt)
+    g = gg.global_grid()
+    np.save(os.path.join(outdir, f"tile{g.me}.npy"), m.field.cpu().numpy())
+    with open(os.path.join(outdir, f"meta{g.me}.txt"), "w") as f:
+        f.write(f"{g.coords[0]} {g.coords[1]} {g.nxyz_g[0]} {g.nxyz_g[1]} {g.overlaps[0]} "
+                f"{g.overlaps[1]} {g.transport}")
+    m.close()

@@ -37,3 +37,26 @@ def test_collectives_and_timers(tmp_path):
     for r in range(2):
         s, mx, t, n, d0, d1, d2 = np.load(tmp_path / f"coll{r}.npy")
         assert s == 3 and mx == 1 and t >= 0 and n == 2 and (d0, d1, d2) == (2, 1, 1)
+
+
+@pytest.mark.parametrize("variant,K", [("perf_hide", 3), ("perf", 4)])
+def test_gloo_temporal_blocking_tiles(tmp_path, variant, K):
+    """2 processes over gloo, K steps per pass with width-K halos (overlap
+    2K): every tile equals its window of the global golden model."""
+    import torch
+
+    from rocm_mpi_amd import ops
+
+    nx, ny, nt = 40, 31, 23
+    run_procs(2, "mp_targets:diffusion_tiles", str(tmp_path), variant, nx, ny, nt, (2, 1), K)
+    metas = [open(tmp_path / f"meta{r}.txt").read().split() for r in range(2)]
+    nxg, nyg = int(metas[0][2]), int(metas[0][3])
+    assert (nxg, nyg) == (2 * (nx - 2 * K) + 2 * K, ny) and metas[0][6] == "gloo"
+    T0 = torch.empty((nyg, nxg), dtype=torch.float64)
+    ops.init_random_(T0, ops.TileGeometry(0, 0, nxg, nyg, 1.0, 1.0), seed=1234)
+    G = golden.run(nxg, nyg, nt, T0=T0.numpy())
+    for r in range(2):
+        cx, cy, ol = int(metas[r][0]), int(metas[r][1]), int(metas[r][4])
+        T = np.load(tmp_path / f"tile{r}.npy")
+        gx0, gy0 = cx * (nx - ol), cy * (ny - ol)
+        assert np.array_equal(T, G[gy0:gy0 + ny, gx0:gx0 + nx])
