@@ -22,7 +22,7 @@ DEFAULTS = {
     "perf_hide": dict(nx=12 * 1024, ny=12 * 1024, nt=100,                   # perf_hide.jl:37-43
                       do_vis=False),
     "perf_hide_prof": dict(nx=8 * 1024, ny=8 * 1024, nt=300,               # _prof.jl:71-77
-                           do_vis=False, profile=True),
+                           do_vis=False, profile=True, threads=(32, 4)),
 }
 
 # BASELINE.json "configs", in order.
@@ -50,6 +50,10 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--ny", type=int, default=d["ny"])
     ap.add_argument("--nt", type=int, default=d["nt"], help="time steps (first 10 untimed)")
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--threads", type=_pair, default=d.get("threads", (32, 8)),
+                    help="accepted for compatibility with the reference's work-group shape "
+                         "(perf.jl:23); the gfx950 kernels use 4 waves of 64 lanes marching "
+                         "row chunks (tune with --chunk-rows / --vec) and record it only")
     ap.add_argument("--b-width", type=_pair, default=d.get("b_width", (1, 1)),
                     help="perf_hide frame width in cells (reference default 32,4)")
     ap.add_argument("--dims", type=_pair, default=(0, 0), help="process grid dimx,dimy")
@@ -146,6 +150,8 @@ def run_variant(variant: str, argv=None) -> int:
     res = model.run()
     if a.checkpoint:
         ckpt.save_checkpoint(model, a.checkpoint)
+    res.extra["threads_requested"] = list(a.threads)
+    res.extra["temporal"] = a.temporal
     if a.json and model.g.me == 0:
         print(res.to_json(), flush=True)
     model.close()

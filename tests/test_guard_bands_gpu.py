@@ -1,0 +1,104 @@
+"""Out-of-bounds write detection for every device kernel.
+
+GPU AddressSanitizer is not available on the MI355X pool, so each kernel runs
+on a field carved out of a larger allocation whose leading and trailing guard
+bands hold a canary bit pattern; after the launch the guards must be intact
+and every cell outside the kernel's output region unchanged. Writes past a
+row end inside the field are caught by the "untouched outside" checks, writes
+before/after the array by the guards. (Reads are checked indirectly: the
+results are compared bitwise with the CPU twins elsewhere.)
+"""
+import pytest
+import torch
+
+from rocm_mpi_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+G = 4096  # guard elements on each side (multiple of 2: keeps 16-B alignment)
+CANARY = -1.2345678901234567e300
+
+
+def guarded(ny, nx, seed, lo=0.0):
+    buf = torch.full((G + ny * nx + G,), CANARY, dtype=torch.float64, device=DEV)
+    f = buf[G:G + ny * nx].view(ny, nx)
+    g = torch.Generator().manual_seed(seed)
+    f.copy_(torch.rand((ny, nx), generator=g, dtype=torch.float64) + lo)
+    return buf, f
+
+
+def guards_intact(buf):
+    torch.cuda.synchronize()
+    return bool((buf[:G] == CANARY).all()) and bool((buf[-G:] == CANARY).all())
+
+
+def coef():
+    return ops.StencilCoef(-1.3, 1 / 0.037, 1 / 0.041, 0.00031)
+
+
+SHAPES = [(3, 3), (5, 4), (67, 131), (130, 258), (257, 1024), (31, 4097)]
+
+
+def check_stencil(fn, ny, nx, rects):
+    bT, T = guarded(ny, nx, 1)
+    bC, iCp = guarded(ny, nx, 2, 0.5)
+    bO, out = guarded(ny, nx, 3)
+    before = out.clone()
+    fn(out, T, iCp, rects)
+    assert guards_intact(bT) and guards_intact(bC) and guards_intact(bO)
+    mask = torch.ones((ny, nx), dtype=torch.bool, device=DEV)
+    for (x0, x1, y0, y1) in rects:
+        mask[y0:y1, x0:x1] = False
+    assert torch.equal(out[mask], before[mask]), "write outside the output rects"
+
+
+@pytest.mark.parametrize("ny,nx", SHAPES)
+@pytest.mark.parametrize("kernel", ["march", "lds"])
+def test_one_step_kernels_stay_in_bounds(ny, nx, kernel):
+    rects = [ops.interior_rect(nx, ny)]
+    tn = ops.StencilTuning(chunk_rows=7, kernel=kernel)
+    check_stencil(lambda o, t, c, r: ops.stencil_step(o, t, c, coef(), r, tn), ny, nx, rects)
+    if nx > 20 and ny > 20:  # perf_hide frames incl. thin column rects
+        frame, interior = ops.hide_rects(nx, ny, 1, 1)
+        check_stencil(lambda o, t, c, r: ops.stencil_step(o, t, c, coef(), r, tn), ny, nx,
+                      frame)
+
+
+@pytest.mark.parametrize("ny,nx", SHAPES)
+@pytest.mark.parametrize("K", [2, 3, 4, 6, 8])
+def test_multi_step_kernels_stay_in_bounds(ny, nx, K):
+    rects = [ops.interior_rect(nx, ny)]
+    for kern in ("march", "lds"):
+        tn = ops.StencilTuning(chunk_rows=5, kernel=kern)
+        check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny, nx,
+                      rects)
+    if K == 2:
+        check_stencil(lambda o, t, c, r: ops.stencil2_step(o, t, c, coef(), r), ny, nx, rects)
+
+
+@pytest.mark.parametrize("ny,nx", SHAPES)
+def test_kp_kernels_stay_in_bounds(ny, nx):
+    c = coef()
+    bufs = [guarded(ny, nx, s) for s in range(5)]
+    (bT, T), (bC, iCp), (bX, QX), (bY, QY), (bD, D) = bufs
+    ops.flux(QX, QY, T, c.mlam, c.rdx, c.rdy)
+    ops.residual(D, QX, QY, iCp, c.rdx, c.rdy)
+    ops.update(T, D, c.dt)
+    assert all(guards_intact(b) for b, _ in bufs)
+
+
+def test_copy_init_fill_reduce_stay_in_bounds():
+    ny, nx = 77, 130
+    b, A = guarded(ny, nx, 4)
+    geom = ops.TileGeometry(0, 0, nx, ny, 1.0, 1.0)
+    ops.init_random_(A, geom, seed=3)
+    ops.init_gaussian_(A, geom, 10.0, 10.0)
+    ops.fill_(A, 0.25)
+    float(ops.reduce(A, "sum"))
+    assert guards_intact(b)
+    # strided plane pack / unpack (halo x-planes)
+    bB, B = guarded(ny, 8, 5)
+    ops.copy_plane(B[:, 2:5], A[:, 10:13])
+    ops.copy_plane(A[:, 120:123], B[:, 2:5])
+    assert guards_intact(b) and guards_intact(bB)
+    assert torch.equal(A[:, 120:123], A[:, 10:13])
