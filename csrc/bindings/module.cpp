@@ -341,6 +341,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("bytes_sent_last", &HaloExchanger::bytes_sent_last);
 
   // ---------------- executor ----------------
+  m.def("default_chunk_k", [](int K, int64_t ny) { return default_tune_k(K, ny).chunk_rows; },
+        py::arg("K"), py::arg("ny"));
   py::class_<DiffusionExecutor>(m, "Executor")
       .def(py::init([](uintptr_t T, uintptr_t T2, uintptr_t iCp, int64_t nx, int64_t ny, int mode,
                        const Coef4& coef, int chunk_rows, int nontemporal, int kernel,

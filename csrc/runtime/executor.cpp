@@ -29,7 +29,14 @@ StencilTuning default_tune_k(int K, int64_t ny) {
   }
   t.kernel = 1;
   t.xcd_remap = 1;
-  t.chunk_rows = ny >= 32768 ? (K >= 8 ? 1024 : 512) : (K >= 8 ? 128 : 256);
+  // rows per wave-task: long chunks amortise the 2K-1 rows a chunk recomputes,
+  // short ones give small tiles enough waves (sweeps at 2048^2..101376^2,
+  // profiles/SUMMARY_r1.md)
+  if (ny < 3072) t.chunk_rows = 16;
+  else if (ny < 6144) t.chunk_rows = 32;
+  else if (ny < 12288) t.chunk_rows = 64;
+  else if (ny < 32768) t.chunk_rows = K >= 8 ? 128 : 256;
+  else t.chunk_rows = K >= 8 ? 1024 : 512;
   return t;
 }
 

@@ -44,15 +44,23 @@ TEMPORAL = (1, 2, 3, 4, 6, 8)
 
 
 def default_chunk2(K: int, ny: int) -> int:
-    """Rows per wave-task of the K-step kernels (profiles/SUMMARY_r1.md sweeps):
-    16 for the two-step kernel; longer chunks amortise the 2K-1 rows a chunk
-    recomputes at its edges: 128-256 up to 32K-row tiles, 512-1024 beyond
-    (101376^2, K=6: c128 28.1, c256 29.0, c512 29.4 TB/s; K=8: c1024 30.7)."""
-    if K == 2:
+    """Rows per wave-task of the K-step kernels: the native executor's measured
+    table (csrc/runtime/executor.cpp default_tune_k; 16 for the two-step kernel,
+    16..1024 growing with the tile height for K >= 3)."""
+    from .._native import has_native, native
+
+    if has_native():
+        return int(native().default_chunk_k(int(K), int(ny)))
+    if K <= 2:
         return 16
-    if ny >= 32768:
-        return 1024 if K >= 8 else 512
-    return 128 if K >= 8 else 256
+    for lim, c in ((3072, 16), (6144, 32), (12288, 64)):
+        if ny < lim:
+            return c
+    if ny < 32768:
+        return 128 if K >= 8 else 256
+    return 1024 if K >= 8 else 512
+
+
 VARIANTS = ("ap", "kp", "perf", "perf_hide")
 _MODE = {"perf": 0, "perf_hide": 1, "kp": 2}
 
@@ -190,6 +198,12 @@ class Diffusion2D:
 
                 warnings.warn(f"hipGraph replay disabled for ap ({dev.type}, {g.transport} "
                               "transport)", RuntimeWarning, stacklevel=2)
+        if cfg.temporal > 1 and nx * ny < 1_500_000 and not cfg.quiet:
+            import warnings
+
+            warnings.warn(f"temporal={cfg.temporal} on a {nx}x{ny} tile: too few wave-tasks to "
+                          "fill the GPU (measured slower than one step per pass below ~1.5M "
+                          "cells, e.g. 1024^2: 1.2 vs 1.6 TB/s)", RuntimeWarning, stacklevel=2)
         if cfg.temporal > 1:
             K = cfg.temporal
             nb = g.neighbors
