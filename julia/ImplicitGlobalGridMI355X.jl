@@ -12,12 +12,16 @@
 # world size must be 1. NOTE: Julia is not installed in this repository's CI;
 # this shim is untested here (the C ABI itself is exercised by
 # examples/diffusion_2D_perf_hide.cpp and tests/test_capi_gpu.py).
+#
+# The native time loop is exposed too: `ex = DiffusionExecutor(T, T2, iCp,
+# coef; mode=1, steps_per_pass=8)`, `run!(ex, n)` — K steps per kernel pass
+# need init_global_grid(...; overlaps=(2K,2K,2), halowidths=(K,K,1)).
 module ImplicitGlobalGridMI355X
 
 using Libdl
 
 export init_global_grid, finalize_global_grid, update_halo!, gather!, nx_g, ny_g, nz_g,
-       x_g, y_g, z_g, tic, toc
+       x_g, y_g, z_g, tic, toc, DiffusionExecutor, run!, current_field
 
 const LIB = Ref{Ptr{Cvoid}}(C_NULL)
 const GRID = Ref{Ptr{Cvoid}}(C_NULL)
@@ -99,5 +103,33 @@ function toc(; stream::Ptr{Cvoid}=C_NULL)
     check(ccall(sym(:rma_toc), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Float64}), GRID[], stream, t))
     return t[]
 end
+
+# Native executor (mode 0 perf, 1 perf_hide, 2 kp; coef = (-lam, 1/dx, 1/dy, dt)).
+mutable struct DiffusionExecutor
+    ptr::Ptr{Cvoid}
+    T::Any
+    T2::Any
+end
+
+function DiffusionExecutor(T, T2, iCp, coef::NTuple{4,Float64}; mode::Integer=1,
+                           steps_per_pass::Integer=1, b_width=(1, 1))
+    out = Ref{Ptr{Cvoid}}(C_NULL)
+    c = collect(coef)
+    nx, ny = size(T, 1), size(T, 2)
+    check(ccall(sym(:rma_executor_create_k), Cint,
+                (Ptr{Cvoid}, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Ptr{Float64},
+                 Int64, Int64, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                GRID[], mode, pointer(T), pointer(T2), pointer(iCp), nx, ny, c, b_width[1],
+                b_width[2], steps_per_pass, C_NULL, C_NULL, C_NULL, out))
+    ex = DiffusionExecutor(out[], T, T2)
+    finalizer(e -> ccall(sym(:rma_executor_destroy), Cint, (Ptr{Cvoid},), e.ptr), ex)
+    return ex
+end
+
+run!(ex::DiffusionExecutor, n::Integer; stream::Ptr{Cvoid}=C_NULL) =
+    check(ccall(sym(:rma_executor_run), Cint, (Ptr{Cvoid}, Int64, Ptr{Cvoid}), ex.ptr, n, stream))
+
+current_field(ex::DiffusionExecutor) =
+    ccall(sym(:rma_executor_parity), Cint, (Ptr{Cvoid},), ex.ptr) == 0 ? ex.T : ex.T2
 
 end # module
