@@ -40,6 +40,31 @@ namespace rma {
 namespace {
 using namespace march;
 
+// Cross-lane moves by one lane. kDpp: DPP wave shifts (VALU, a few cycles of
+// latency); otherwise ds_bpermute (LDS pipe, ~100+ cycles round trip). The
+// lane that has no source (63 for next, 0 for prev) gets garbage: those strip
+// positions are invalid at every level anyway.
+template <bool kDpp>
+__device__ __forceinline__ double from_next_lane(double v) {
+  if constexpr (kDpp) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);  // wave_shl:1 -> lane i gets lane i+1
+  } else {
+    return __shfl_down(v, 1);
+  }
+}
+template <bool kDpp>
+__device__ __forceinline__ double from_prev_lane(double v) {
+  if constexpr (kDpp) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);  // wave_shr:1 -> lane i gets lane i-1
+  } else {
+    return __shfl_up(v, 1);
+  }
+}
+
 __device__ __forceinline__ double face(double lv, double rv, double mlam, double rd) {
   return (mlam * (rv - lv)) * rd;  // flux lv -> rv: qxR of the left cell == qxL of the right one
 }
@@ -47,7 +72,7 @@ __device__ __forceinline__ double face(double lv, double rv, double mlam, double
 
 // kLds: keep the masked 1/Cp window in an LDS ring (per wave, slot = row mod
 // K) instead of K*V registers, for occupancy (kernel=1 of StencilTuning).
-template <int K, int V, bool NT, bool kLds>
+template <int K, int V, bool NT, bool kLds, bool kDpp>
 __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
     int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
@@ -162,11 +187,11 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
       }
       const double(&c)[V] = w[j - 1][1 - P];
       const double(&dn)[V] = w[j - 1][P];
-      const double rn = __shfl_down(c[0], 1);  // lane 63: garbage (invalid column)
+      const double rn = from_next_lane<kDpp>(c[0]);  // lane 63: garbage (invalid column)
       double qr[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) qr[v] = face(c[v], v + 1 < V ? c[v + 1] : rn, k.mlam, k.rdx);
-      const double ql0 = __shfl_up(qr[V - 1], 1);  // lane 0: garbage
+      const double ql0 = from_prev_lane<kDpp>(qr[V - 1]);  // lane 0: garbage
       double res[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
@@ -224,13 +249,24 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
   const dim3 grid((unsigned)total), block(kBlock);
   hipStream_t s = as_stream(stream);
   const bool nts = tune.nontemporal & 1;
-#define RMA_TBK(KK, VV, NTS)                                                              \
-  if (tune.kernel == 1)                                                                     \
-    stencilk_ovl_kernel<KK, VV, NTS, true><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,  \
-                                                                  tune.chunk_rows, remap);  \
-  else                                                                                      \
-    stencilk_ovl_kernel<KK, VV, NTS, false><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c, \
-                                                                   tune.chunk_rows, remap)
+#define RMA_TBK(KK, VV, NTS)                                                                 \
+  switch (tune.kernel) {                                                                       \
+    case 1:                                                                                    \
+      stencilk_ovl_kernel<KK, VV, NTS, true, false><<<grid, block, 0, s>>>(                     \
+          T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
+      break;                                                                                   \
+    case 2:                                                                                    \
+      stencilk_ovl_kernel<KK, VV, NTS, false, true><<<grid, block, 0, s>>>(                     \
+          T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
+      break;                                                                                   \
+    case 3:                                                                                    \
+      stencilk_ovl_kernel<KK, VV, NTS, true, true><<<grid, block, 0, s>>>(                      \
+          T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
+      break;                                                                                   \
+    default:                                                                                   \
+      stencilk_ovl_kernel<KK, VV, NTS, false, false><<<grid, block, 0, s>>>(                    \
+          T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
+  }
 #define RMA_TBK_V(KK)                                   \
   if (V == 4) {                                         \
     if (nts) { RMA_TBK(KK, 4, true); } else { RMA_TBK(KK, 4, false); } \

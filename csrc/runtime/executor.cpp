@@ -27,7 +27,7 @@ StencilTuning default_tune_k(int K, int64_t ny) {
     t.unroll = 2;
     return t;
   }
-  t.kernel = 1;
+  t.kernel = 3;  // LDS 1/Cp ring + DPP lane shifts (sweep_tbk_dpp_*: +6% over bpermute)
   t.xcd_remap = 1;
   // rows per wave-task: long chunks amortise the 2K-1 rows a chunk recomputes,
   // short ones give small tiles enough waves (sweeps at 2048^2..101376^2,
@@ -287,7 +287,7 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
         stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       } else {
         tn.xcd_remap = 1;
-        tn.kernel = 1;
+        tn.kernel = 3;
         stencilk_rects_gpu(kr, Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       }
       exchange(Tout, s_lo_);

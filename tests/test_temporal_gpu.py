@@ -95,7 +95,8 @@ def k_steps_cpu(K, T, iCp, rects, fill=-5.0):
 @pytest.mark.parametrize("ny,nx", SHAPES)
 @pytest.mark.parametrize("chunk,vec,kern", [(1, 2, "march"), (5, 4, "march"), (16, 2, "march"),
                                             (16, 4, "march"), (64, 2, "march"), (3, 2, "lds"),
-                                            (16, 4, "lds"), (64, 2, "lds")])
+                                            (16, 4, "lds"), (64, 2, "lds"), (7, 2, "dpp"),
+                                            (16, 4, "dpp"), (5, 2, "lds_dpp"), (64, 2, "lds_dpp")])
 def test_k_step_bitwise(K, ny, nx, chunk, vec, kern):
     """K-step kernel with face-flux reuse == K one-step launches, bitwise."""
     T, iCp = rand((ny, nx), 7), rand((ny, nx), 8) + 0.5
