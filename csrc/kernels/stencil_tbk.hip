@@ -47,8 +47,9 @@ using namespace march;
 template <bool kDpp>
 __device__ __forceinline__ double from_next_lane(double v) {
   if constexpr (kDpp) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+    // bound_ctrl: lanes without a source read 0 (no `old` register to set up)
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);  // wave_shl:1 -> lane i gets lane i+1
   } else {
     return __shfl_down(v, 1);
@@ -57,8 +58,8 @@ __device__ __forceinline__ double from_next_lane(double v) {
 template <bool kDpp>
 __device__ __forceinline__ double from_prev_lane(double v) {
   if constexpr (kDpp) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);  // wave_shr:1 -> lane i gets lane i-1
   } else {
     return __shfl_up(v, 1);

@@ -199,7 +199,7 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
     """K time steps in one pass (K = 2, 3, 4, 6, 8; csrc/kernels/stencil_tbk.hip):
     T2[r] = f^K(T)[r], the intermediate levels being f on the interior and T
     on boundary/halo cells. Bitwise equal to K ``stencil_step`` calls. Default
-    tuning: 16-row chunks."""
+    tuning: the native executor's (chunk by tile height, LDS 1/Cp ring, DPP)."""
     if int(K) not in (2, 3, 4, 6, 8):
         raise ValueError(f"K must be 2, 3, 4, 6 or 8, got {K}")
     check_field("T", T)
@@ -211,7 +211,10 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
     rects = validate_rects(rects if rects is not None else [interior_rect(nx, ny)], nx, ny)
     if not rects:
         return
-    tn = tuning or StencilTuning(chunk_rows=16)
+    if tuning is None:  # the executor's measured defaults (default_tune_k)
+        ch = native().default_chunk_k(int(K), ny) if has_native() else 16
+        tuning = StencilTuning(chunk_rows=ch, kernel="lds_dpp", xcd_remap=1)
+    tn = tuning
     if T.is_cuda:
         native().stencilk_rects(int(K), _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                 tn.chunk_rows, int(tn.nontemporal), stream_handle(T), True,
