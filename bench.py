@@ -59,6 +59,11 @@ def parse(argv=None):
     ap.add_argument("--chunk2", type=int, default=0,
                     help="K-step kernel rows per wave-task (0: auto, models.diffusion.default_chunk2)")
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
+    ap.add_argument("--fast-math", dest="fast_math", action="store_true", default=True,
+                    help="K-step passes with reassociated fp64 arithmetic (FMAs, folded "
+                         "constants): same scheme, not bitwise equal to the canonical update "
+                         "(default; the canonical K-step and one-step kernels are timed too)")
+    ap.add_argument("--no-fast-math", dest="fast_math", action="store_false")
     ap.add_argument("--overlap", type=int, default=0,
                     help="grid overlap (0: 2 x steps-per-pass, the minimum)")
     ap.add_argument("--single-step-steps", type=int, default=100,
@@ -122,7 +127,8 @@ def main(argv=None) -> int:
                           warmup=a.warmup, init="random", b_width=bw, dims=dims,
                           chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
                           unroll=a.unroll, vec=a.vec, temporal=a.temporal, chunk2=a.chunk2,
-                          unroll2=a.unroll2, use_graph=a.graph, quiet=True)
+                          unroll2=a.unroll2, use_graph=a.graph, quiet=True,
+                          fast_math=a.fast_math and a.temporal > 1)
     t_setup = time.perf_counter()
     gkw = {}
     if a.overlap:
@@ -151,19 +157,25 @@ def main(argv=None) -> int:
 
     # secondary: the one-step kernel (24 B/cell/step at the HBM roofline) on the
     # same tile, so the temporal-blocking gain is visible in one record
-    single = None
-    if a.single_step_steps > 0 and a.temporal > 1:
-        model.set_temporal(1)
-        model.step(2)
+    def side_teff(K, fast, steps):
+        model.set_temporal(K, fast_math=fast)
+        model.step(2 * K)
         model.synchronize()
         comm.barrier()
         torch.cuda.synchronize()
         s0 = time.perf_counter()
-        model.step(a.single_step_steps)
+        model.step(steps)
         torch.cuda.synchronize()
         comm.barrier()
         s1 = comm.allreduce(time.perf_counter() - s0, "max")
-        single = 3 * nx * ny * 8 / 1e9 / (s1 / a.single_step_steps)
+        return 3 * nx * ny * 8 / 1e9 / (s1 / steps)
+
+    single = canonical = None
+    if a.single_step_steps > 0 and a.temporal > 1:
+        if a.fast_math:  # the bitwise-canonical K-step kernel on the same tile
+            canonical = side_teff(a.temporal, False, max(a.temporal, a.single_step_steps
+                                                         // a.temporal * a.temporal))
+        single = side_teff(1, False, a.single_step_steps)
 
     t_it = wall / a.steps
     teff_gpu = 3 * nx * ny * 8 / 1e9 / t_it
@@ -207,8 +219,15 @@ def main(argv=None) -> int:
                           "is still computed (bitwise equal to one-step updates) but HBM is "
                           f"read/written once per {a.temporal} steps, so T_eff exceeds the "
                           "HBM bandwidth; teff_single_step_kernel_GBps is the one-step "
-                          "kernel on the same tile") if a.temporal > 1 else "",
+                          "kernel on the same tile. fast_math: the K-step passes use "
+                          "reassociated fp64 arithmetic (differences, folded constants, FMA; "
+                          "max deviation from the canonical update ~1e-15 relative, "
+                          "tests/test_temporal_gpu.py); teff_bitwise_kstep_GBps is the "
+                          "bitwise-canonical K-step kernel on the same tile")
+                         if a.temporal > 1 else "",
             "teff_single_step_kernel_GBps": round(single, 2) if single else None,
+            "fast_math": bool(a.fast_math and a.temporal > 1),
+            "teff_bitwise_kstep_GBps": round(canonical, 2) if canonical else None,
             "overlap": list(g.overlaps[:2]),
             "setup_s": round(setup_s, 3),
             "nonfinite_cells_sampled": int(bad),

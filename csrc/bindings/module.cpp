@@ -349,8 +349,9 @@ PYBIND11_MODULE(_C, m) {
                        int64_t bwx, int64_t bwy, int use_graph, int graph_steps,
                        HaloExchanger* halo, uintptr_t qx, uintptr_t qy, uintptr_t dTdt,
                        int unroll, int vec, int temporal, int64_t olx, int64_t oly,
-                       int chunk2, int unroll2) {
+                       int chunk2, int unroll2, int fast_math) {
              ExecParams p;
+             p.fast_math = fast_math;
              p.temporal = temporal;
              p.olx = olx;
              p.oly = oly;
@@ -380,7 +381,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("halo").none(true) = nullptr, py::arg("qx") = 0, py::arg("qy") = 0,
            py::arg("dTdt") = 0, py::arg("unroll") = 4, py::arg("vec") = 2,
            py::arg("temporal") = 1, py::arg("olx") = 2, py::arg("oly") = 2,
-           py::arg("chunk2") = 16, py::arg("unroll2") = 2, py::keep_alive<1, 16>())
+           py::arg("chunk2") = 16, py::arg("unroll2") = 2, py::arg("fast_math") = 0,
+           py::keep_alive<1, 16>())
       .def(
           "run", [](DiffusionExecutor& e, int64_t n, uintptr_t s) { e.run(n, S(s)); },
           py::arg("nsteps"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())

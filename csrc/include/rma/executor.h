@@ -46,6 +46,10 @@ struct ExecParams {
   int temporal = 1;
   int64_t olx = 2, oly = 2;    // grid overlaps of the field (IGG overlaps)
   StencilTuning tune2{16, 3, 0, 2, 2, -1};  // K-step kernel tuning (K=2: 16-row chunks)
+  // fast_math: K-step passes use the reassociated arithmetic (differences,
+  // folded constants, FMAs; stencil_tbk.hip kernel 4): same scheme in fp64,
+  // not bitwise equal to the canonical expression (~1e-15 relative).
+  int fast_math = 0;
 };
 
 // Measured defaults of the K-step kernels (profiles/SUMMARY_r1.md): K=2 uses

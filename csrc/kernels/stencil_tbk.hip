@@ -73,7 +73,11 @@ __device__ __forceinline__ double face(double lv, double rv, double mlam, double
 
 // kLds: keep the masked 1/Cp window in an LDS ring (per wave, slot = row mod
 // K) instead of K*V registers, for occupancy (kernel=1 of StencilTuning).
-template <int K, int V, bool NT, bool kLds, bool kDpp>
+// kFast: the same scheme with reassociated arithmetic (NOT bitwise equal to
+// the canonical expression): differences instead of fluxes, the constants
+// folded (ax = lam/dx^2, ay = lam/dy^2, g = dt/Cp) and FMAs:
+//   T2 = fma(g, fma(ay, dU - dD, ax * (dR - dL)), c)   — 7 fp64 ops per cell.
+template <int K, int V, bool NT, bool kLds, bool kDpp, bool kFast = false>
 __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
     int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
@@ -120,6 +124,8 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
   load_row<V>(pT, T + rowc(i + 1) * nx + xl);
   load_row<V>(pC, iCp + rowc(i) * nx + xl);
 
+  const double ax = (-k.mlam) * k.rdx * k.rdx;  // kFast only
+  const double ay = (-k.mlam) * k.rdy * k.rdy;
   // LDS ring of masked 1/Cp rows: [wave][slot][lane*V + v] (16-B per lane)
   __shared__ double ring[kLds ? kWavesPerBlock * K * W : 1];
   double* myring = ring + (kLds ? wave * K * W + lane * V : 0);
@@ -140,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
     if constexpr (kLds) {
       double g[V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? pC[v] : 0.0;
+      for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? (kFast ? k.dt * pC[v] : pC[v]) : 0.0;
       double* dst = myring + slot * W;
       if constexpr (V == 1) {
         dst[0] = g[0];
@@ -161,7 +167,8 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
         for (int v = 0; v < V; ++v) gic[j][v] = gic[j - 1][v];
       }
 #pragma unroll
-      for (int v = 0; v < V; ++v) gic[0][v] = (rin1 && cin[v]) ? pC[v] : 0.0;
+      for (int v = 0; v < V; ++v)
+        gic[0][v] = (rin1 && cin[v]) ? (kFast ? k.dt * pC[v] : pC[v]) : 0.0;
     }
     load_row<V>(pT, T + rowc(i + 2) * nx + xl);
     load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
@@ -191,16 +198,22 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
       const double rn = from_next_lane<kDpp>(c[0]);  // lane 63: garbage (invalid column)
       double qr[V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) qr[v] = face(c[v], v + 1 < V ? c[v + 1] : rn, k.mlam, k.rdx);
+      for (int v = 0; v < V; ++v) {
+        const double rv = v + 1 < V ? c[v + 1] : rn;
+        qr[v] = kFast ? rv - c[v] : face(c[v], rv, k.mlam, k.rdx);
+      }
       const double ql0 = from_prev_lane<kDpp>(qr[V - 1]);  // lane 0: garbage
       double res[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        const double qU = face(c[v], dn[v], k.mlam, k.rdy);
+        const double qU = kFast ? dn[v] - c[v] : face(c[v], dn[v], k.mlam, k.rdy);
         const double qD = fy[j - 1][v];
         fy[j - 1][v] = qU;
         const double qL = v == 0 ? ql0 : qr[v - 1];
-        res[v] = c[v] + k.dt * (icl[v] * ((-(qr[v] - qL)) * k.rdx - (qU - qD) * k.rdy));
+        if constexpr (kFast)
+          res[v] = __builtin_fma(icl[v], __builtin_fma(ay, qU - qD, ax * (qr[v] - qL)), c[v]);
+        else
+          res[v] = c[v] + k.dt * (icl[v] * ((-(qr[v] - qL)) * k.rdx - (qU - qD) * k.rdy));
       }
       if (j < K) {
         const int jj = j < K ? j : K - 1;
@@ -262,6 +275,10 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
       break;                                                                                   \
     case 3:                                                                                    \
       stencilk_ovl_kernel<KK, VV, NTS, true, true><<<grid, block, 0, s>>>(                      \
+          T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
+      break;                                                                                   \
+    case 4:                                                                                    \
+      stencilk_ovl_kernel<KK, VV, NTS, true, true, true><<<grid, block, 0, s>>>(                \
           T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
       break;                                                                                   \
     default:                                                                                   \

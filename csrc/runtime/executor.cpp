@@ -59,6 +59,7 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
                 "temporal blocking applies to perf / perf_hide, not kp");
   RMA_CHECK_ARG(p.olx >= 2 && p.oly >= 2, "overlaps must be >= 2");
   hwx_ = hwy_ = p.temporal;  // halo width = steps per exchange
+  if (p_.fast_math && p.temporal > 1) p_.tune2.kernel = 4;
   std::array<std::array<int, 2>, 3> nbr{{{-1, -1}, {-1, -1}, {-1, -1}}};
   if (halo) nbr = halo->neighbors();
   const int64_t ol[2] = {p.olx, p.oly};
@@ -217,7 +218,7 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
 
 void DiffusionExecutor::multi_step(double* Tin, double* Tout, const Rect* rects, int n,
                                    const StencilTuning& tn, void* stream) {
-  if (p_.temporal == 2)  // dedicated two-step kernel: aligned strips, faster at K=2
+  if (p_.temporal == 2 && !p_.fast_math)  // dedicated two-step kernel: faster at K=2
     stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, rects, n, p_.coef, tn, stream);
   else
     stencilk_rects_gpu(p_.temporal, Tout, Tin, iCp_, nx_, ny_, rects, n, p_.coef, tn, stream);
@@ -281,13 +282,13 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
                ny_ - (nb[1][1] >= 0 ? kr : 1)};
       }
       StencilTuning tn = p_.tune2;
-      if (kr == 2) {
+      if (kr == 2 && !p_.fast_math) {
         tn.chunk_rows = 16;
         tn.xcd_remap = -1;
         stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       } else {
         tn.xcd_remap = 1;
-        tn.kernel = 3;
+        tn.kernel = p_.fast_math ? 4 : 3;
         stencilk_rects_gpu(kr, Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       }
       exchange(Tout, s_lo_);

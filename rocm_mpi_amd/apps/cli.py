@@ -84,6 +84,9 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
                          "(grid overlap 2K); bitwise identical to 1")
     ap.add_argument("--chunk2", type=int, default=0)
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
+    ap.add_argument("--fast-math", action="store_true",
+                    help="K-step passes with reassociated fp64 arithmetic (FMAs, folded "
+                         "constants): same scheme, not bitwise equal to the canonical update")
     ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf guard period")
     ap.add_argument("--checkpoint", default="", help="save the final state to this directory")
     ap.add_argument("--resume", default="", help="start from a checkpoint directory")
@@ -124,7 +127,8 @@ def run_variant(variant: str, argv=None) -> int:
                 chunk_rows=a.chunk_rows, unroll=a.unroll, vec=a.vec, kernel=a.kernel,
                 nontemporal=a.nontemporal, use_graph=a.graph, do_vis=a.do_vis, outdir=a.outdir,
                 profile=a.profile, check_every=a.check_every, quiet=a.quiet,
-                temporal=a.temporal, chunk2=a.chunk2, unroll2=a.unroll2)
+                temporal=a.temporal, chunk2=a.chunk2, unroll2=a.unroll2,
+                fast_math=a.fast_math)
     if a.auto_size:
         rank, size, _ = C.env_world()
         if size > 1:

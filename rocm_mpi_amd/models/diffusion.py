@@ -103,6 +103,10 @@ class DiffusionConfig:
     temporal: int = 1
     chunk2: int = 0  # K-step kernel rows per wave-task (0: default_chunk2)
     unroll2: int = 2
+    # reassociated fp64 arithmetic in the K-step passes (differences, folded
+    # constants, FMAs): same scheme, not bitwise equal to the canonical
+    # expression (GPU executor only; the CPU path stays canonical)
+    fast_math: bool = False
 
     def validate(self) -> None:
         if self.variant not in VARIANTS:
@@ -234,11 +238,12 @@ class Diffusion2D:
             self.QY.data_ptr() if cfg.variant == "kp" else 0,
             self.D.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
             int(cfg.vec), int(cfg.temporal), int(g.overlaps[0]), int(g.overlaps[1]),
-            int(self.chunk2), int(cfg.unroll2))
+            int(self.chunk2), int(cfg.unroll2), int(bool(cfg.fast_math)))
 
-    def set_temporal(self, K: int) -> None:
+    def set_temporal(self, K: int, fast_math: bool | None = None) -> None:
         """Switch the steps per kernel pass (e.g. to time the one-step kernel on
-        the same tile). The grid overlap must allow it (2K <= overlap)."""
+        the same tile) and optionally the fast-math arithmetic. The grid
+        overlap must allow it (2K <= overlap)."""
         cfg, g = self.cfg, self.g
         if K not in TEMPORAL or (K > 1 and cfg.variant not in ("perf", "perf_hide")):
             raise ValueError(f"temporal={K} not available for {cfg.variant}")
@@ -250,6 +255,8 @@ class Diffusion2D:
             self.T, self.T2 = self.T2, self.T
             self.parity = 0
         cfg.temporal = K
+        if fast_math is not None:
+            cfg.fast_math = bool(fast_math)
         self.chunk2 = cfg.chunk2 or default_chunk2(K, cfg.ny)
         if K > 1:
             self.out2 = (K if nb[0][0] >= 0 else 1, cfg.nx - (K if nb[0][1] >= 0 else 1),

@@ -24,7 +24,8 @@ from .._native import has_native, native
 
 Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 
-KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3}  # 2/3: K-step kernels only
+# K-step kernels also: 2 = dpp, 3 = lds_dpp (default), 4 = fast (reassociated, FMA; not bitwise)
+KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4}
 
 
 class StencilCoef(NamedTuple):

@@ -181,3 +181,32 @@ def test_staged_transport_two_processes(tmp_path):
     nxg, nyg, transport = open(tmp_path / "meta.txt").read().split()[:3]
     assert transport == "staged"
     assert np.array_equal(Tv, golden.run(int(nxg), int(nyg), 25)[1:-1, 1:-1])
+
+
+def spmd_fast(rank, hub, nx, ny, nt, dims, K, fast):
+    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], overlaps=(2 * K, 2 * K, 2),
+                        halowidths=(K, K, 1), quiet=True, loopback=(hub, rank))
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=nt, init="random",
+                                    quiet=True, dims=dims, temporal=K, fast_math=fast))
+    m.step(nt)
+    out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g)
+    m.close()
+    gg.finalize_global_grid()
+    return out
+
+
+@pytest.mark.parametrize("K,nt", [(8, 21), (4, 13), (2, 9)])
+def test_fast_math_decomposition_invariant_and_close(K, nt):
+    """fast_math: 4 ranks (2x2) == 1 rank on the same global grid, bitwise
+    (same reassociated expression everywhere), and within 1e-13 of the
+    canonical arithmetic."""
+    nx, ny = 300, 134
+    res = run_loopback(4, spmd_fast, nx, ny, nt, (2, 2), K, True, timeout=120)
+    nxg, nyg, _ = res[0][2]
+    one = run_loopback(1, spmd_fast, nxg, nyg, nt, (1, 1), K, True, timeout=120)[0][1]
+    can = run_loopback(1, spmd_fast, nxg, nyg, nt, (1, 1), K, False, timeout=120)[0][1]
+    for coords, T, _ in res:
+        gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
+        assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx])
+    np.testing.assert_allclose(one, can, rtol=1e-13, atol=1e-13)
+    assert not np.array_equal(one, can)  # it really is the other arithmetic

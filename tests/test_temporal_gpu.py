@@ -133,3 +133,19 @@ def test_k_step_rect_lists_and_unaligned(K, xcd):
     ops.stencilk_step(K, o2, Tu, ones, coef(), tuning=tn)
     assert torch.equal(o2.cpu(), k_steps_cpu(K, Tu.cpu(), ones.cpu(),
                                              [ops.interior_rect(64, 150)], fill=0.0))
+
+
+@pytest.mark.parametrize("K", [2, 4, 8])
+@pytest.mark.parametrize("ny,nx", [(67, 131), (257, 1024), (300, 129)])
+def test_k_step_fast_variant_close(K, ny, nx):
+    """kernel='fast' reassociates the update (differences, folded constants,
+    FMAs): not bitwise, but within a few ulp of the canonical K steps, and
+    boundary cells stay exactly fixed."""
+    T, iCp = rand((ny, nx), 12), rand((ny, nx), 13) + 0.5
+    ref = k_steps_cpu(K, T, iCp, [ops.interior_rect(nx, ny)])
+    out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+    ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(),
+                      tuning=ops.StencilTuning(chunk_rows=16, kernel="fast"))
+    o = out.cpu()
+    assert torch.equal(o[0], ref[0]) and torch.equal(o[:, 0], ref[:, 0])
+    torch.testing.assert_close(o, ref, rtol=1e-13, atol=1e-13)
