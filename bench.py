@@ -135,6 +135,7 @@ def main(argv=None) -> int:
         gkw = {"overlaps": (a.overlap, a.overlap, 2),
                "halowidths": (max(1, a.temporal), max(1, a.temporal), 1)}
     model = Diffusion2D(cfg, grid_kwargs=gkw)
+    chunk2_main = model.chunk2
     g = model.g
     comm = g.comm
     model.synchronize()
@@ -212,7 +213,7 @@ def main(argv=None) -> int:
             "b_width": list(bw),
             "hipgraph": bool(a.graph),
             "temporal_blocking": a.temporal,
-            "chunk2": model.chunk2,
+            "chunk2": chunk2_main,
             "steps_per_kernel_pass": a.temporal,
             "teff_note": ("T_eff = A_eff/t_step with A_eff = 3*nx*ny*8 B (reference "
                           "perf.jl:55-58). With temporal blocking every step of every cell "
