@@ -78,9 +78,9 @@ __device__ __forceinline__ double face(double lv, double rv, double mlam, double
 // folded (ax = lam/dx^2, ay = lam/dy^2, g = dt/Cp) and FMAs:
 //   T2 = fma(g, fma(ay, dU - dD, ax * (dR - dL)), c)   — 7 fp64 ops per cell.
 template <int K, int V, bool NT, bool kLds, bool kDpp, bool kFast = false>
-__global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
+__device__ __forceinline__ void stencilk_body(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
-    int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
+    int64_t nx, int64_t ny, const RectList& L, const StencilCoef& k, int chunk_rows, int remap) {
   constexpr int W = kWave * V;
   constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_rects)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
@@ -231,6 +231,13 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
     iter(std::integral_constant<int, 1>{});
     if (++i > iend) break;
   }
+}
+
+template <int K, int V, bool NT, bool kLds, bool kDpp, bool kFast = false>
+__global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
+    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
+    int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
+  stencilk_body<K, V, NT, kLds, kDpp, kFast>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
 }
 
 }  // namespace

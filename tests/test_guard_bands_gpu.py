@@ -68,7 +68,7 @@ def test_one_step_kernels_stay_in_bounds(ny, nx, kernel):
 @pytest.mark.parametrize("K", [2, 3, 4, 6, 8])
 def test_multi_step_kernels_stay_in_bounds(ny, nx, K):
     rects = [ops.interior_rect(nx, ny)]
-    for kern in ("march", "lds", "dpp", "lds_dpp"):
+    for kern in ("march", "lds", "dpp", "lds_dpp", "fast"):
         tn = ops.StencilTuning(chunk_rows=5, kernel=kern)
         check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny, nx,
                       rects)
