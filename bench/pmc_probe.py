@@ -28,6 +28,16 @@ c = ops.StencilCoef(-1.0, 1.0, 1.0, 0.2)
 s = torch.cuda.current_stream().cuda_stream
 nat = native()
 which = os.environ.get("RMA_PROBE_SET", "all")
+if which == "fast":  # fast-math K-step kernels at the executor's tuning (bench default)
+    K = int(os.environ.get("RMA_PROBE_K", "8"))
+    ch = nat.default_chunk_k(K, n)
+    for kern in os.environ.get("RMA_PROBE_KERNELS", "fast,fast5").split(","):
+        for _ in range(reps):
+            ops.stencilk_step(K, T2, T, iCp, c, tuning=ops.StencilTuning(chunk_rows=ch, xcd_remap=1,
+                                                                        kernel=kern))
+    torch.cuda.synchronize()
+    print(f"probe done n={n} reps={reps} set={which} K={K} chunk={ch}")
+    sys.exit(0)
 if which in ("all", "tbk"):  # multi-step kernels (temporal blocking)
     for K, ch in ((2, 16), (3, 128), (4, 128), (6, 128), (8, 128)):
         for _ in range(reps):

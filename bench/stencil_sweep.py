@@ -42,7 +42,9 @@ def main(argv=None):
     ap.add_argument("--tbk-chunks", default="16")
     ap.add_argument("--tbk-xcds", default="0")
     ap.add_argument("--tbk-vecs", default="2")
-    ap.add_argument("--tbk-kernels", default="march", help="march (1/Cp in registers), lds (LDS ring)")
+    ap.add_argument("--tbk-kernels", default="march",
+                    help="comma list of ops.KERNELS names: march, lds, dpp, lds_dpp, fast, fast5, "
+                         "fast5s")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -140,9 +142,10 @@ def main(argv=None):
     def best_of(prefix):
         return max((k for k in res if k.startswith(prefix)), key=lambda k: res[k]["GBps_median"])
 
-    best = best_of("march") if any(k.startswith("march") for k in res) else best_of("tb2")
+    best = (best_of("march") if any(k.startswith("march") for k in res)
+            else best_of("tb2") if any(k.startswith("tb2") for k in res) else None)
     doc = {"n": n, "cells": cells, "rounds": a.rounds, "iters": a.iters, "results": res,
-           "best_march": best, "best_march_GBps": res[best]["GBps_median"],
+           "best_march": best, "best_march_GBps": res[best]["GBps_median"] if best else None,
            "device": torch.cuda.get_device_name(0)}
     for K in [int(v) for v in a.tbk.split(",") if v]:
         bk = best_of(f"tbk{K}_")
@@ -154,7 +157,8 @@ def main(argv=None):
         tri, cop = best_of("roof_triad"), best_of("roof_copy")
         doc.update({"best_triad": tri, "triad_GBps": res[tri]["GBps_median"],
                     "best_copy": cop, "copy_GBps": res[cop]["GBps_median"],
-                    "best_vs_triad": res[best]["GBps_median"] / res[tri]["GBps_median"]})
+                    "best_vs_triad": (res[best]["GBps_median"] / res[tri]["GBps_median"]
+                                      if best else None)})
     txt = json.dumps(doc, indent=1)
     print(txt)
     if a.out:

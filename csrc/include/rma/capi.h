@@ -73,13 +73,19 @@ typedef struct rma_executor rma_executor;
 int rma_executor_create(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
                         int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
                         double* qx, double* qy, double* dTdt, rma_executor** out);
-// Same with temporal blocking: `steps_per_pass` = 1, 2, 3, 4, 6 or 8 time steps
+// Same with temporal blocking: `steps_per_pass` = 1, 2, 3, 4, 6, 8 (12, 16: fast_math) time steps
 // per kernel pass (needs a grid created with overlaps >= 2*steps_per_pass and
 // halowidths = steps_per_pass along every dimension with a neighbour).
 int rma_executor_create_k(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
                           int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
                           int steps_per_pass, double* qx, double* qy, double* dTdt,
                           rma_executor** out);
+// Same with `fast_math` != 0: the K-step passes use the 5-point-sum arithmetic
+// (not bitwise equal to the canonical update; required for 12 and 16 steps per pass).
+int rma_executor_create_kf(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
+                           int64_t nx, int64_t ny, const double coef[4], int64_t bwx,
+                           int64_t bwy, int steps_per_pass, int fast_math, double* qx,
+                           double* qy, double* dTdt, rma_executor** out);
 int rma_executor_run(rma_executor* e, int64_t nsteps, void* stream);
 int rma_executor_parity(const rma_executor* e);
 int rma_executor_destroy(rma_executor* e);

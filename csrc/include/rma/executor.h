@@ -40,15 +40,17 @@ struct ExecParams {
   int64_t bwx = 1, bwy = 1;    // perf_hide frame widths (cells beyond the boundary)
   int use_graph = 0;           // capture steps into a hipGraph and replay
   int graph_steps = 0;         // steps per captured graph (even; 0 = auto)
-  // Temporal blocking (kPerf/kHide): K = 2, 3, 4, 6, 8 time steps per kernel
-  // pass and one halo exchange of width K per pass; needs a grid overlap
-  // >= 2K in every dimension with a neighbour. 1 = one step per pass.
+  // Temporal blocking (kPerf/kHide): K = 2, 3, 4, 6, 8 (12, 16 with fast_math)
+  // time steps per kernel pass and one halo exchange of width K per pass;
+  // needs a grid overlap >= 2K in every dimension with a neighbour. 1 = one
+  // step per pass.
   int temporal = 1;
   int64_t olx = 2, oly = 2;    // grid overlaps of the field (IGG overlaps)
   StencilTuning tune2{16, 3, 0, 2, 2, -1};  // K-step kernel tuning (K=2: 16-row chunks)
-  // fast_math: K-step passes use the reassociated arithmetic (differences,
-  // folded constants, FMAs; stencil_tbk.hip kernel 4): same scheme in fp64,
-  // not bitwise equal to the canonical expression (~1e-15 relative).
+  // fast_math: K-step passes use the 5-point-sum arithmetic with one folded
+  // per-cell factor (stencil_tbk.hip kernel 5; kernel 4 if lam == 0): same
+  // scheme in fp64, not bitwise equal to the canonical expression (rounding
+  // level, tests/test_temporal_gpu.py).
   int fast_math = 0;
 };
 

@@ -60,6 +60,12 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                         const StencilTuning& tune, stream_t stream);
 void stencilk_rects_cpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
                         int64_t ny, const Rect* rects, int nrects, const StencilCoef& c);
+// StencilTuning::kernel of the K-step launcher: 0 march, 1 LDS 1/Cp ring, 2 DPP,
+// 3 LDS ring + DPP (bitwise default), 4 fast (reassociated fluxes, 7 fp64 ops
+// per cell update), 5 fast5 (5-point sum, constants folded into one per-cell
+// factor, 5 ops). 4 and 5 are not bitwise equal to the canonical update.
+// fast5_ok: kernel 5 divides by lam/dx^2, so it needs lam != 0.
+bool fast5_ok(const StencilCoef& c);
 
 // Width (in cells) of one wave's x-strip in the march kernel; perf_hide rounds
 // its x-frame so the interior rect starts on a strip boundary.

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 #include "rma/hip_check.h"
@@ -233,6 +234,311 @@ __device__ __forceinline__ void stencilk_body(
   }
 }
 
+// kernel=5 ("fast5"): the 5-point sum form with every constant folded into one
+// per-cell coefficient, 5 fp64 operations per cell update (kFast: 7):
+//   T2 = fma(g, fma(r, U + D, fma(-kc, c, R + L)), c)
+//   g = dt*(lam/dx^2)/Cp (LDS ring, ZERO outside the interior), r = dy^-2/dx^-2,
+//   kc = 2*(1 + r).
+// No face fluxes are carried: a level keeps three rows (up, centre, down) in a
+// 3-slot rotation (loop unrolled by three), the same register count as two
+// rows + one flux row. Both lane moves read the centre row only, so they issue
+// at the start of a level instead of in the middle of its dependency chain.
+template <int K, int V, bool NT>
+__device__ __forceinline__ void stencilk5_body(
+    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
+    int64_t nx, int64_t ny, const RectList& L, const StencilCoef& k, int chunk_rows, int remap) {
+  constexpr int W = kWave * V;
+  constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_rects)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  int ri = 0;
+  while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
+  int64_t strip, chunk;
+  if (!locate_task(L, ri, b, wave, strip, chunk)) return;  // whole wave exits
+  const Rect r = L.r[ri];
+  const int64_t xs = L.xa[ri] + strip * kStep;
+  const int64_t ya = r.y0 + chunk * chunk_rows;
+  const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
+
+  const int64_t x = xs + (int64_t)lane * V;
+  bool m[V], cin[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int p = lane * V + v;
+    m[v] = p >= K && p < K + kStep && x + v >= r.x0 && x + v < r.x1;
+    cin[v] = (x + v >= 1) && (x + v <= nx - 2);
+  }
+  const int64_t xl = min(max(x, (int64_t)0), nx - V);
+
+  const double ax = (-k.mlam) * k.rdx * k.rdx;  // lam/dx^2
+  const double ay = (-k.mlam) * k.rdy * k.rdy;
+  const double ry = ay / ax;                    // host guarantees ax != 0, ry finite
+  const double mkc = -2.0 * (1.0 + ry);
+  const double gs = k.dt * ax;
+
+  // w[j][s]: level-j rows; at iteration t the new row goes to slot t%3, the
+  // centre row is slot (t+2)%3 and the upper row slot (t+1)%3.
+  double w[K][3][V], pT[V], pC[V];
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int v = 0; v < V; ++v) w[j][s][v] = 0.0;
+  int64_t i = ya - K;
+  const int64_t iend = yb + K - 2;
+  auto rowc = [&](int64_t y) { return min(max(y, (int64_t)0), ny - 1); };
+  load_row<V>(w[0][2], T + rowc(i) * nx + xl);
+  load_row<V>(pT, T + rowc(i + 1) * nx + xl);
+  load_row<V>(pC, iCp + rowc(i) * nx + xl);
+
+  __shared__ double ring[kWavesPerBlock * K * W];
+  double* myring = ring + wave * K * W + lane * V;
+  int slot = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int v = 0; v < V; ++v) myring[j * W + v] = 0.0;
+
+  auto iter = [&](auto Pc) {
+    constexpr int P = decltype(Pc)::value;       // new row
+    constexpr int PC = (P + 2) % 3, PU = (P + 1) % 3;  // centre, up
+    const bool rin1 = i >= 1 && i <= ny - 2;
+#pragma unroll
+    for (int v = 0; v < V; ++v) w[0][P][v] = pT[v];
+    {
+      double g[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? gs * pC[v] : 0.0;
+      double* dst = myring + slot * W;
+      if constexpr (V == 1) {
+        dst[0] = g[0];
+      } else {
+#pragma unroll
+        for (int h = 0; h < V / 2; ++h) {
+          dbl2 t2;
+          t2.x = g[2 * h];
+          t2.y = g[2 * h + 1];
+          reinterpret_cast<dbl2*>(dst)[h] = t2;
+        }
+      }
+    }
+    load_row<V>(pT, T + rowc(i + 2) * nx + xl);
+    load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
+#pragma unroll
+    for (int j = 1; j <= K; ++j) {
+      const int64_t row = i - (j - 1);
+      double gl[V];
+      {
+        const int sl = slot - (j - 1) < 0 ? slot - (j - 1) + K : slot - (j - 1);
+        const double* src = myring + sl * W;
+        if constexpr (V == 1) {
+          gl[0] = src[0];
+        } else {
+#pragma unroll
+          for (int h = 0; h < V / 2; ++h) {
+            const dbl2 t2 = reinterpret_cast<const dbl2*>(src)[h];
+            gl[2 * h] = t2.x;
+            gl[2 * h + 1] = t2.y;
+          }
+        }
+      }
+      const double(&up)[V] = w[j - 1][PU];
+      const double(&c)[V] = w[j - 1][PC];
+      const double(&dn)[V] = w[j - 1][P];
+      const double rn = from_next_lane<true>(c[0]);      // lane 63: 0 (invalid column)
+      const double ln = from_prev_lane<true>(c[V - 1]);  // lane 0: 0 (invalid column)
+      double res[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const double rv = v + 1 < V ? c[v + 1] : rn;
+        const double lv = v > 0 ? c[v - 1] : ln;
+        const double sx = rv + lv;
+        const double sy = up[v] + dn[v];
+        res[v] = __builtin_fma(gl[v], __builtin_fma(ry, sy, __builtin_fma(mkc, c[v], sx)), c[v]);
+      }
+      if (j < K) {
+        const int jj = j < K ? j : K - 1;
+#pragma unroll
+        for (int v = 0; v < V; ++v) w[jj][P][v] = res[v];
+      } else if (row >= ya && row < yb) {
+        store_row<V, NT>(T2 + row * nx + x, res, m);
+      }
+    }
+    slot = slot + 1 == K ? 0 : slot + 1;
+  };
+  for (;;) {
+    iter(std::integral_constant<int, 0>{});
+    if (++i > iend) break;
+    iter(std::integral_constant<int, 1>{});
+    if (++i > iend) break;
+    iter(std::integral_constant<int, 2>{});
+    if (++i > iend) break;
+  }
+}
+
+template <int K, int V, bool NT>
+__global__ __launch_bounds__(kBlock) void stencilk5_kernel(
+    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
+    int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
+  stencilk5_body<K, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
+}
+
+// kernel=6 ("fast5s"): kernel 5's arithmetic with TWO carried values per level
+// and cell instead of three rows. When the down neighbour dn of row r arrives
+// (level j-1 of row r+1), row r is finished with
+//   T2(r) = fma(g, fma(r_y, dn, A(r)), c(r))
+// and the state advances to row r+1:
+//   A(r+1) = fma(r_y, c(r), fma(-kc, dn, L(dn) + R(dn))),  c(r+1) = dn,
+// so the critical path per level is two FMAs (the lane moves and partial sums
+// of A feed only the next iteration) and a level holds 2V doubles: 2/3 of the
+// registers, which is what lets K = 12 / 16 levels fit at 3 waves per SIMD.
+// Rounding: c + g*(r_y*dn + (r_y*up + (-kc*c + (L+R)))) — same class as kernel
+// 5, not bitwise equal to it.
+template <int K, int V, bool NT, bool kPin = true>
+__device__ __forceinline__ void stencilk5s_body(
+    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
+    int64_t nx, int64_t ny, const RectList& L, const StencilCoef& k, int chunk_rows, int remap) {
+  constexpr int W = kWave * V;
+  constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_rects)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  int ri = 0;
+  while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
+  int64_t strip, chunk;
+  if (!locate_task(L, ri, b, wave, strip, chunk)) return;  // whole wave exits
+  const Rect r = L.r[ri];
+  const int64_t xs = L.xa[ri] + strip * kStep;
+  const int64_t ya = r.y0 + chunk * chunk_rows;
+  const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
+
+  const int64_t x = xs + (int64_t)lane * V;
+  bool m[V], cin[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int p = lane * V + v;
+    m[v] = p >= K && p < K + kStep && x + v >= r.x0 && x + v < r.x1;
+    cin[v] = (x + v >= 1) && (x + v <= nx - 2);
+  }
+  const int64_t xl = min(max(x, (int64_t)0), nx - V);
+
+  const double ax = (-k.mlam) * k.rdx * k.rdx;  // lam/dx^2
+  const double ay = (-k.mlam) * k.rdy * k.rdy;
+  const double ry = ay / ax;                    // host guarantees ax != 0, ry finite
+  const double mkc = -2.0 * (1.0 + ry);
+  const double gs = k.dt * ax;
+
+  // cc[j]: level-j row r (the centre of the next level-(j+1) update), aa[j]:
+  // its partial sum A(r). Rows outside the validity cone start from zeros:
+  // finite garbage that no output depends on.
+  double cc[K][V], aa[K][V], pT[V], pC[V];
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int v = 0; v < V; ++v) cc[j][v] = aa[j][v] = 0.0;
+  int64_t i = ya - K;
+  const int64_t iend = yb + K - 2;
+  auto rowc = [&](int64_t y) { return min(max(y, (int64_t)0), ny - 1); };
+  load_row<V>(cc[0], T + rowc(i) * nx + xl);
+  load_row<V>(pT, T + rowc(i + 1) * nx + xl);
+  load_row<V>(pC, iCp + rowc(i) * nx + xl);
+
+  __shared__ double ring[kWavesPerBlock * K * W];
+  double* myring = ring + wave * K * W + lane * V;
+  int slot = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int v = 0; v < V; ++v) myring[j * W + v] = 0.0;
+
+  for (;;) {
+    const bool rin1 = i >= 1 && i <= ny - 2;
+    double dn[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) dn[v] = pT[v];
+    {
+      double g[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? gs * pC[v] : 0.0;
+      double* dst = myring + slot * W;
+      if constexpr (V == 1) {
+        dst[0] = g[0];
+      } else {
+#pragma unroll
+        for (int h = 0; h < V / 2; ++h) {
+          dbl2 t2;
+          t2.x = g[2 * h];
+          t2.y = g[2 * h + 1];
+          reinterpret_cast<dbl2*>(dst)[h] = t2;
+        }
+      }
+    }
+    load_row<V>(pT, T + rowc(i + 2) * nx + xl);
+    load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
+    // ring reads pipelined one level ahead behind compiler fences: left to
+    // itself the scheduler hoists all K reads to the top of the iteration and
+    // keeps 2KV more VGPRs live (measured: 184 instead of ~140 at K=12)
+    auto ring_read = [&](int j, double (&g)[V]) {
+      const int sl = slot - (j - 1) < 0 ? slot - (j - 1) + K : slot - (j - 1);
+      const double* src = myring + sl * W;
+      if constexpr (V == 1) {
+        g[0] = src[0];
+      } else {
+#pragma unroll
+        for (int h = 0; h < V / 2; ++h) {
+          const dbl2 t2 = reinterpret_cast<const dbl2*>(src)[h];
+          g[2 * h] = t2.x;
+          g[2 * h + 1] = t2.y;
+        }
+      }
+    };
+    double gl[V];
+    ring_read(1, gl);
+#pragma unroll
+    for (int j = 1; j <= K; ++j) {
+      const int64_t row = i - (j - 1);
+      double gn[V];
+      if (j < K) ring_read(j + 1, gn);
+      if constexpr (kPin) asm volatile("" ::: "memory");
+      double res[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        res[v] = __builtin_fma(gl[v], __builtin_fma(ry, dn[v], aa[j - 1][v]), cc[j - 1][v]);
+      // advance level j-1 to row+1 (= dn)
+      const double rn = from_next_lane<true>(dn[0]);      // lane 63: 0 (invalid column)
+      const double ln = from_prev_lane<true>(dn[V - 1]);  // lane 0: 0 (invalid column)
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const double rv = v + 1 < V ? dn[v + 1] : rn;
+        const double lv = v > 0 ? dn[v - 1] : ln;
+        aa[j - 1][v] = __builtin_fma(ry, cc[j - 1][v], __builtin_fma(mkc, dn[v], rv + lv));
+        cc[j - 1][v] = dn[v];
+        if constexpr (kPin) asm volatile("" : "+v"(aa[j - 1][v]), "+v"(cc[j - 1][v]));
+      }
+      if (j < K) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          dn[v] = res[v];
+          gl[v] = gn[v];
+        }
+      } else if (row >= ya && row < yb) {
+        store_row<V, NT>(T2 + row * nx + x, res, m);
+      }
+    }
+    slot = slot + 1 == K ? 0 : slot + 1;
+    if (++i > iend) break;
+  }
+}
+
+template <int K, int V, bool NT>
+__global__ __launch_bounds__(kBlock) void stencilk5s_kernel(
+    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
+    int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
+  stencilk5s_body<K, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
+}
+
 template <int K, int V, bool NT, bool kLds, bool kDpp, bool kFast = false>
 __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
@@ -242,11 +548,20 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
 
 }  // namespace
 
+bool fast5_ok(const StencilCoef& c) {
+  const double ax = (-c.mlam) * c.rdx * c.rdx, ay = (-c.mlam) * c.rdy * c.rdy;
+  return ax != 0.0 && std::isfinite(ax) && std::isfinite(ay) && std::isfinite(ay / ax) &&
+         std::isfinite(c.dt * ax);
+}
+
 void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
                         int64_t ny, const Rect* rects, int nrects, const StencilCoef& c,
                         const StencilTuning& tune, stream_t stream) {
-  RMA_CHECK_ARG(K == 2 || K == 3 || K == 4 || K == 6 || K == 8,
-                "steps per pass must be 2, 3, 4, 6 or 8, got " << K);
+  RMA_CHECK_ARG(K == 2 || K == 3 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16,
+                "steps per pass must be 2, 3, 4, 6, 8, 12 or 16, got " << K);
+  RMA_CHECK_ARG(K <= 8 || tune.kernel == 5 || tune.kernel == 6,
+                "12 or 16 steps per pass need the fast5 kernels (kernel 5 or 6), got kernel "
+                    << tune.kernel);
   RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
   RMA_CHECK_ARG(nx >= 3 && ny >= 3, "grid too small: nx=" << nx << " ny=" << ny);
   RMA_CHECK_ARG(T2 != T, "multi-step kernel cannot run in place");
@@ -257,11 +572,14 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                   "rect " << i << " outside the interior of " << nx << "x" << ny);
   }
   RMA_CHECK_ARG(tune.chunk_rows >= 1, "chunk_rows=" << tune.chunk_rows);
+  RMA_CHECK_ARG((tune.kernel != 5 && tune.kernel != 6) || fast5_ok(c),
+                "kernel 5 folds dy^-2/dx^-2 into one factor: needs lam != 0 and finite "
+                "coefficients");
   const bool aligned = ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(T2) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
   int V = 1;
-  if (aligned && nx % 2 == 0) V = (tune.vec == 4 && nx % 4 == 0) ? 4 : 2;
+  if (aligned && nx % 2 == 0) V = (tune.vec == 4 && nx % 4 == 0 && K <= 8) ? 4 : 2;
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   RectList L;
   const int64_t total = plan_rects(L, rects, nrects, V, tune.chunk_rows, remap, false, K);
@@ -288,6 +606,14 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
       stencilk_ovl_kernel<KK, VV, NTS, true, true, true><<<grid, block, 0, s>>>(                \
           T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
       break;                                                                                   \
+    case 5:                                                                                    \
+      stencilk5_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,           \
+                                                            tune.chunk_rows, remap);          \
+      break;                                                                                   \
+    case 6:                                                                                    \
+      stencilk5s_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,          \
+                                                             tune.chunk_rows, remap);         \
+      break;                                                                                   \
     default:                                                                                   \
       stencilk_ovl_kernel<KK, VV, NTS, false, false><<<grid, block, 0, s>>>(                    \
           T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
@@ -300,13 +626,31 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
   } else {                                              \
     if (nts) { RMA_TBK(KK, 1, true); } else { RMA_TBK(KK, 1, false); } \
   }
+  // 12 / 16 levels: fast5 kernels only, V <= 2 (register budget)
+#define RMA_TBK_DEEP(KK, VV, NTS)                                                           \
+  if (tune.kernel == 5)                                                                       \
+    stencilk5_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,            \
+                                                         tune.chunk_rows, remap);             \
+  else                                                                                        \
+    stencilk5s_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,           \
+                                                          tune.chunk_rows, remap);
+#define RMA_TBK_DEEP_V(KK)                                                                  \
+  if (V == 2) {                                                                               \
+    if (nts) { RMA_TBK_DEEP(KK, 2, true) } else { RMA_TBK_DEEP(KK, 2, false) }                \
+  } else {                                                                                    \
+    if (nts) { RMA_TBK_DEEP(KK, 1, true) } else { RMA_TBK_DEEP(KK, 1, false) }                \
+  }
   switch (K) {
     case 2: RMA_TBK_V(2) break;
     case 3: RMA_TBK_V(3) break;
     case 4: RMA_TBK_V(4) break;
     case 6: RMA_TBK_V(6) break;
-    default: RMA_TBK_V(8) break;
+    case 8: RMA_TBK_V(8) break;
+    case 12: RMA_TBK_DEEP_V(12) break;
+    default: RMA_TBK_DEEP_V(16) break;
   }
+#undef RMA_TBK_DEEP_V
+#undef RMA_TBK_DEEP
 #undef RMA_TBK_V
 #undef RMA_TBK
   RMA_HIP_LAUNCH_CHECK();

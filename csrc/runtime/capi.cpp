@@ -245,6 +245,14 @@ int rma_executor_create_k(rma_grid* g, int mode, double* T, double* T2, const do
                           int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
                           int steps_per_pass, double* qx, double* qy, double* dTdt,
                           rma_executor** out) {
+  return rma_executor_create_kf(g, mode, T, T2, iCp, nx, ny, coef, bwx, bwy, steps_per_pass, 0,
+                                qx, qy, dTdt, out);
+}
+
+int rma_executor_create_kf(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
+                           int64_t nx, int64_t ny, const double coef[4], int64_t bwx,
+                           int64_t bwy, int steps_per_pass, int fast_math, double* qx,
+                           double* qy, double* dTdt, rma_executor** out) {
   return guard([&] {
     RMA_CHECK_ARG(g && out && mode >= 0 && mode <= 2, "bad executor arguments");
     rma::ExecParams p;
@@ -256,6 +264,7 @@ int rma_executor_create_k(rma_grid* g, int mode, double* T, double* T2, const do
     p.olx = g->overlaps[0];
     p.oly = g->overlaps[1];
     p.tune2 = rma::default_tune_k(steps_per_pass, ny);
+    p.fast_math = fast_math ? 1 : 0;
     auto e = std::make_unique<rma_executor>();
     e->ex = std::make_unique<rma::DiffusionExecutor>(T, T2, iCp, nx, ny, p, g->halo.get(), qx, qy,
                                                      dTdt);

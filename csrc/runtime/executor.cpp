@@ -35,7 +35,7 @@ StencilTuning default_tune_k(int K, int64_t ny) {
   if (ny < 3072) t.chunk_rows = 16;
   else if (ny < 6144) t.chunk_rows = 32;
   else if (ny < 12288) t.chunk_rows = 64;
-  else if (ny < 32768) t.chunk_rows = K >= 8 ? 128 : 256;
+  else if (ny < 32768) t.chunk_rows = K == 8 ? 128 : 256;  // K=12/16: c256 (fast5s sweep)
   else t.chunk_rows = K >= 8 ? 1024 : 512;
   return t;
 }
@@ -53,13 +53,19 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
                 "hipGraph replay needs a capturable halo transport (RCCL or none); the loopback "
                 "transport synchronises on the host");
   RMA_CHECK_ARG(p.temporal == 1 || p.temporal == 2 || p.temporal == 3 || p.temporal == 4 ||
-                    p.temporal == 6 || p.temporal == 8,
-                "temporal (steps per pass) must be 1, 2, 3, 4, 6 or 8, got " << p.temporal);
+                    p.temporal == 6 || p.temporal == 8 || p.temporal == 12 || p.temporal == 16,
+                "temporal (steps per pass) must be 1, 2, 3, 4, 6, 8, 12 or 16, got "
+                    << p.temporal);
+  RMA_CHECK_ARG(p.temporal <= 8 || (p.fast_math && fast5_ok(p.coef)),
+                "12 or 16 steps per pass run on the fast5 kernel only: needs fast_math and "
+                "lam != 0");
   RMA_CHECK_ARG(p.temporal == 1 || p.mode != Mode::kKp,
                 "temporal blocking applies to perf / perf_hide, not kp");
   RMA_CHECK_ARG(p.olx >= 2 && p.oly >= 2, "overlaps must be >= 2");
   hwx_ = hwy_ = p.temporal;  // halo width = steps per exchange
-  if (p_.fast_math && p.temporal > 1) p_.tune2.kernel = 4;
+  // fast_math: the 5-point-sum kernel (5 fp64 ops per cell update) unless the
+  // coefficients cannot be folded (lam == 0), then the reassociated-flux one
+  if (p_.fast_math && p.temporal > 1) p_.tune2.kernel = fast5_ok(p.coef) ? 5 : 4;
   std::array<std::array<int, 2>, 3> nbr{{{-1, -1}, {-1, -1}, {-1, -1}}};
   if (halo) nbr = halo->neighbors();
   const int64_t ol[2] = {p.olx, p.oly};
@@ -270,7 +276,8 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
     } else if (p_.temporal > 1 && left >= 2) {
       // remainder: one shorter pass (K' < K steps; the width-K exchange then
       // rewrites [K', K) with the identical values the neighbour owns)
-      const int kr = left >= 6 ? 6 : left >= 4 ? 4 : left >= 3 ? 3 : 2;
+      const int kr = left >= 12 ? 12 : left >= 8 ? 8 : left >= 6 ? 6 : left >= 4 ? 4
+                     : left >= 3 ? 3 : 2;
       TraceRange tr("rma.stepK.rest");
       if (p_.mode == Mode::kHide) {  // previous pass done on both streams
         RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
@@ -288,7 +295,7 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
         stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       } else {
         tn.xcd_remap = 1;
-        tn.kernel = p_.fast_math ? 4 : 3;
+        tn.kernel = p_.fast_math ? p_.tune2.kernel : 3;
         stencilk_rects_gpu(kr, Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       }
       exchange(Tout, s_lo_);

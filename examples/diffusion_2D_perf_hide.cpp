@@ -2,7 +2,7 @@
 // reference scripts/diffusion_2D_perf_hide.jl's intended overlap variant,
 // written against the C ABI of librma_core.so (rma/capi.h).
 //
-//   ./build/examples/diffusion_2D_perf_hide [nx] [nt] [mode] [K]    # 1 GPU
+//   ./build/examples/diffusion_2D_perf_hide [nx] [nt] [mode] [K] [fast]    # 1 GPU
 //   (mode 0 perf, 1 perf_hide; K = time steps per kernel pass, 1/2/3/4/6/8)
 //   python -m rocm_mpi_amd.launch -n 8 ./build/examples/diffusion_2D_perf_hide 16384 1000
 //
@@ -48,6 +48,7 @@ int main(int argc, char** argv) {
   const int nt = argc > 2 ? std::atoi(argv[2]) : 1000;
   const int mode = argc > 3 ? std::atoi(argv[3]) : 1;  // 0 perf, 1 perf_hide
   const int K = argc > 4 ? std::atoi(argv[4]) : 1;     // steps per kernel pass
+  const int fast = argc > 5 ? std::atoi(argv[5]) : 0;  // 1: fast-math K-step passes
   const int rank = env_int("RANK", 0), size = env_int("WORLD_SIZE", 1);
   const int local = env_int("LOCAL_RANK", rank);
   int ndev = 0;
@@ -101,8 +102,8 @@ int main(int argc, char** argv) {
   CK(rma_init_gaussian(g, T, n, n, dx, dy, lx, ly, s));
   HK(hipMemcpyAsync(T2, T, bytes, hipMemcpyDeviceToDevice, s));
   rma_executor* ex = nullptr;
-  CK(rma_executor_create_k(g, mode, T, T2, iCp, n, n, coef, 1, 1, K, nullptr, nullptr, nullptr,
-                           &ex));
+  CK(rma_executor_create_kf(g, mode, T, T2, iCp, n, n, coef, 1, 1, K, fast, nullptr, nullptr,
+                            nullptr, &ex));
   if (me == 0)
     std::printf("Global grid: %ldx%ldx1 (nprocs: %d, dims: %dx%dx%d)\n", (long)rma_nx_g(g),
                 (long)rma_ny_g(g), size, dims[0], dims[1], dims[2]);

@@ -40,7 +40,8 @@ from ..parallel.halo import gather_, update_halo_
 from ..utils import metrics
 from ..utils import profiling as prof
 
-TEMPORAL = (1, 2, 3, 4, 6, 8)
+TEMPORAL = (1, 2, 3, 4, 6, 8, 12, 16)
+DEEP_TEMPORAL = (12, 16)  # fast-math (kernel fast5) only on the GPU
 
 
 def default_chunk2(K: int, ny: int) -> int:
@@ -57,7 +58,7 @@ def default_chunk2(K: int, ny: int) -> int:
         if ny < lim:
             return c
     if ny < 32768:
-        return 128 if K >= 8 else 256
+        return 128 if K == 8 else 256
     return 1024 if K >= 8 else 512
 
 
@@ -99,13 +100,13 @@ class DiffusionConfig:
     quiet: bool = False
     # temporal blocking (perf / perf_hide): K = 2, 3, 4, 6, 8 steps per kernel
     # pass and one width-K halo exchange per pass (grid overlap 2K); bitwise
-    # identical to K single steps
+    # identical to K single steps. K = 12, 16: fast_math only (GPU).
     temporal: int = 1
     chunk2: int = 0  # K-step kernel rows per wave-task (0: default_chunk2)
     unroll2: int = 2
-    # reassociated fp64 arithmetic in the K-step passes (differences, folded
-    # constants, FMAs): same scheme, not bitwise equal to the canonical
-    # expression (GPU executor only; the CPU path stays canonical)
+    # fast-math fp64 arithmetic in the K-step passes (5-point sum with one
+    # folded per-cell factor, FMAs; kernel fast5): same scheme, not bitwise
+    # equal to the canonical expression (GPU only; the CPU path stays canonical)
     fast_math: bool = False
 
     def validate(self) -> None:
@@ -121,6 +122,9 @@ class DiffusionConfig:
             raise ValueError(f"temporal must be one of {TEMPORAL}")
         if self.temporal > 1 and self.variant not in ("perf", "perf_hide"):
             raise ValueError("temporal blocking applies to the perf and perf_hide variants")
+        if self.temporal in DEEP_TEMPORAL and not self.fast_math and self.device != "cpu":
+            raise ValueError(f"temporal={self.temporal} runs on the fast5 kernel only: set "
+                             "fast_math=True (or use K <= 8)")
 
 
 class Diffusion2D:
@@ -247,6 +251,9 @@ class Diffusion2D:
         cfg, g = self.cfg, self.g
         if K not in TEMPORAL or (K > 1 and cfg.variant not in ("perf", "perf_hide")):
             raise ValueError(f"temporal={K} not available for {cfg.variant}")
+        fm = cfg.fast_math if fast_math is None else bool(fast_math)
+        if K in DEEP_TEMPORAL and not fm and self.device.type != "cpu":
+            raise ValueError(f"temporal={K} needs fast_math")
         nb = g.neighbors
         if any(max(nb[d]) >= 0 and g.overlaps[d] < 2 * K for d in (0, 1)):
             raise ValueError(f"temporal={K} needs grid overlaps >= {2 * K}")
@@ -333,7 +340,11 @@ class Diffusion2D:
                 # this reference loop runs the owned rect, then the exchange)
                 K = self.cfg.temporal
                 Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
-                ops.stencilk_step(K, Tout, Tin, self.iCp, self.coef, [self.out2])
+                tn = None
+                if self.cfg.fast_math and Tin.is_cuda:
+                    tn = ops.StencilTuning(chunk_rows=self.chunk2, xcd_remap=1,
+                                           kernel="fast5" if ops.fast5_ok(self.coef) else "fast")
+                ops.stencilk_step(K, Tout, Tin, self.iCp, self.coef, [self.out2], tn)
                 update_halo_(Tout)
                 self.parity ^= 1
                 self.steps_done += K

@@ -68,8 +68,9 @@ def test_one_step_kernels_stay_in_bounds(ny, nx, kernel):
 @pytest.mark.parametrize("K", [2, 3, 4, 6, 8])
 def test_multi_step_kernels_stay_in_bounds(ny, nx, K):
     rects = [ops.interior_rect(nx, ny)]
-    for kern in ("march", "lds", "dpp", "lds_dpp", "fast"):
-        tn = ops.StencilTuning(chunk_rows=5, kernel=kern)
+    for kern, vec in (("march", 2), ("lds", 2), ("dpp", 2), ("lds_dpp", 2), ("fast", 2),
+                      ("fast5", 2), ("fast5", 4), ("fast5s", 2)):
+        tn = ops.StencilTuning(chunk_rows=5, kernel=kern, vec=vec)
         check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny, nx,
                       rects)
     if K == 2:

@@ -195,16 +195,18 @@ def spmd_fast(rank, hub, nx, ny, nt, dims, K, fast):
     return out
 
 
-@pytest.mark.parametrize("K,nt", [(8, 21), (4, 13), (2, 9)])
+@pytest.mark.parametrize("K,nt", [(16, 37), (12, 29), (8, 21), (4, 13), (2, 9)])
 def test_fast_math_decomposition_invariant_and_close(K, nt):
     """fast_math: 4 ranks (2x2) == 1 rank on the same global grid, bitwise
-    (same reassociated expression everywhere), and within 1e-13 of the
-    canonical arithmetic."""
+    (same fast-math expression everywhere), and within 1e-13 of the
+    canonical arithmetic (canonical K-step passes go up to K=8; one rank's
+    global grid does not depend on the overlap)."""
     nx, ny = 300, 134
     res = run_loopback(4, spmd_fast, nx, ny, nt, (2, 2), K, True, timeout=120)
     nxg, nyg, _ = res[0][2]
     one = run_loopback(1, spmd_fast, nxg, nyg, nt, (1, 1), K, True, timeout=120)[0][1]
-    can = run_loopback(1, spmd_fast, nxg, nyg, nt, (1, 1), K, False, timeout=120)[0][1]
+    can = run_loopback(1, spmd_fast, nxg, nyg, nt, (1, 1), min(K, 8), False,
+                       timeout=120)[0][1]
     for coords, T, _ in res:
         gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx])

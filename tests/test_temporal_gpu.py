@@ -135,17 +135,52 @@ def test_k_step_rect_lists_and_unaligned(K, xcd):
                                              [ops.interior_rect(64, 150)], fill=0.0))
 
 
-@pytest.mark.parametrize("K", [2, 4, 8])
-@pytest.mark.parametrize("ny,nx", [(67, 131), (257, 1024), (300, 129)])
-def test_k_step_fast_variant_close(K, ny, nx):
+@pytest.mark.parametrize("K", [2, 3, 4, 6, 8])
+@pytest.mark.parametrize("ny,nx", [(3, 3), (67, 131), (257, 1024), (300, 129), (31, 4097)])
+@pytest.mark.parametrize("kern,vec,chunk", [("fast", 2, 16), ("fast5", 2, 16), ("fast5", 4, 5),
+                                            ("fast5s", 2, 7), ("fast5s", 2, 64), ("fast5", 2, 1)])
+def test_k_step_fast_variant_close(K, ny, nx, kern, vec, chunk):
     """kernel='fast' reassociates the update (differences, folded constants,
-    FMAs): not bitwise, but within a few ulp of the canonical K steps, and
-    boundary cells stay exactly fixed."""
+    FMAs) and 'fast5' / 'fast5s' evaluate the 5-point sum with one folded
+    per-cell factor: not bitwise, but within a few ulp of the canonical K
+    steps, and boundary cells stay exactly fixed."""
     T, iCp = rand((ny, nx), 12), rand((ny, nx), 13) + 0.5
     ref = k_steps_cpu(K, T, iCp, [ops.interior_rect(nx, ny)])
     out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
     ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(),
-                      tuning=ops.StencilTuning(chunk_rows=16, kernel="fast"))
+                      tuning=ops.StencilTuning(chunk_rows=chunk, kernel=kern, vec=vec))
     o = out.cpu()
     assert torch.equal(o[0], ref[0]) and torch.equal(o[:, 0], ref[:, 0])
     torch.testing.assert_close(o, ref, rtol=1e-13, atol=1e-13)
+
+
+def test_fast5_rejects_zero_lambda():
+    """kernel 5 divides by lam/dx^2: lam == 0 is refused before any launch."""
+    T = rand((40, 40), 14).to(DEV)
+    with pytest.raises(ValueError):
+        ops.stencilk_step(4, torch.empty_like(T), T, torch.ones_like(T),
+                          ops.StencilCoef(0.0, 10.0, 10.0, 1e-3),
+                          tuning=ops.StencilTuning(chunk_rows=16, kernel="fast5"))
+
+
+@pytest.mark.parametrize("K", [12, 16])
+@pytest.mark.parametrize("ny,nx", [(3, 3), (67, 131), (257, 1024), (300, 129), (41, 4097)])
+@pytest.mark.parametrize("kern,chunk", [("fast5", 16), ("fast5s", 16), ("fast5s", 1), ("fast5s", 50)])
+def test_deep_k_step_fast5_close(K, ny, nx, kern, chunk):
+    """12 / 16 steps per pass (fast5 kernels only): within rounding of the
+    canonical K steps, boundary cells fixed."""
+    T, iCp = rand((ny, nx), 15), rand((ny, nx), 16) + 0.5
+    ref = k_steps_cpu(K, T, iCp, [ops.interior_rect(nx, ny)])
+    out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+    ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(),
+                      tuning=ops.StencilTuning(chunk_rows=chunk, kernel=kern))
+    o = out.cpu()
+    assert torch.equal(o[0], ref[0]) and torch.equal(o[:, 0], ref[:, 0])
+    torch.testing.assert_close(o, ref, rtol=1e-13, atol=1e-13)
+
+
+def test_deep_k_needs_fast5():
+    T = rand((40, 40), 17).to(DEV)
+    with pytest.raises(ValueError):
+        ops.stencilk_step(12, torch.empty_like(T), T, torch.ones_like(T), coef(),
+                          tuning=ops.StencilTuning(chunk_rows=16, kernel="fast"))
