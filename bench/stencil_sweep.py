@@ -43,8 +43,7 @@ def main(argv=None):
     ap.add_argument("--tbk-xcds", default="0")
     ap.add_argument("--tbk-vecs", default="2")
     ap.add_argument("--tbk-kernels", default="march",
-                    help="comma list of ops.KERNELS names: march, lds, dpp, lds_dpp, fast, fast5, "
-                         "fast5s")
+                    help="comma list of ops.KERNELS names: march, lds, dpp, lds_dpp, fast, fast5")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 

@@ -23,8 +23,9 @@
 //   * no per-level selects: 1/Cp is kept in a K-row register window, zeroed
 //     outside the interior, so boundary/halo cells compute c + dt*(0*...) == c.
 //   * two-row windows alternate slots with the iteration parity (loop
-//     unrolled by two): no copies; the next T and 1/Cp rows are prefetched one
-//     iteration ahead.
+//     unrolled by two): no copies; the T and 1/Cp rows are prefetched two
+//     iterations ahead (one ahead made every iteration wait for the previous
+//     iteration's store as well: its vmcnt count is path-dependent).
 // Step-j values outside the interior [1,nx-1)x[1,ny-1) stay T (fixed
 // boundary / halo cells). Multi-rank use: halo width K, overlap 2K.
 #include <hip/hip_runtime.h>
@@ -112,7 +113,7 @@ __device__ __forceinline__ void stencilk_body(
   // the row level j+1 updates, ZEROED outside the interior (boundary rows and
   // columns): the canonical update then returns c + dt*(0*(...)) == c for
   // them, bitwise, without a select per level (all values are finite).
-  double w[K][2][V], fy[K][V], gic[K][V], pT[V], pC[V];
+  double w[K][2][V], fy[K][V], gic[K][V], pT[V], pC[V], qT[V], qC[V];  // q: 2 rows ahead
 #pragma unroll
   for (int j = 0; j < K; ++j) {
 #pragma unroll
@@ -124,6 +125,8 @@ __device__ __forceinline__ void stencilk_body(
   load_row<V>(w[0][1], T + rowc(i) * nx + xl);
   load_row<V>(pT, T + rowc(i + 1) * nx + xl);
   load_row<V>(pC, iCp + rowc(i) * nx + xl);
+  load_row<V>(qT, T + rowc(i + 2) * nx + xl);
+  load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
 
   const double ax = (-k.mlam) * k.rdx * k.rdx;  // kFast only
   const double ay = (-k.mlam) * k.rdy * k.rdy;
@@ -171,8 +174,13 @@ __device__ __forceinline__ void stencilk_body(
       for (int v = 0; v < V; ++v)
         gic[0][v] = (rin1 && cin[v]) ? (kFast ? k.dt * pC[v] : pC[v]) : 0.0;
     }
-    load_row<V>(pT, T + rowc(i + 2) * nx + xl);
-    load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {  // see stencilk5_body: two rows of prefetch
+      pT[v] = qT[v];
+      pC[v] = qC[v];
+    }
+    load_row<V>(qT, T + rowc(i + 3) * nx + xl);
+    load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
 #pragma unroll
     for (int j = 1; j <= K; ++j) {
       const int64_t row = i - (j - 1);
@@ -279,7 +287,11 @@ __device__ __forceinline__ void stencilk5_body(
 
   // w[j][s]: level-j rows; at iteration t the new row goes to slot t%3, the
   // centre row is slot (t+2)%3 and the upper row slot (t+1)%3.
-  double w[K][3][V], pT[V], pC[V];
+  // prefetch two rows ahead: (pT, pC) are consumed this iteration, (qT, qC)
+  // arrive for the next one. With one row of prefetch the wait at the top of
+  // an iteration also covered the previous iteration's (conditional) store:
+  // its vmcnt count differs between paths, so the compiler waited for all.
+  double w[K][3][V], pT[V], pC[V], qT[V], qC[V];
 #pragma unroll
   for (int j = 0; j < K; ++j)
 #pragma unroll
@@ -292,6 +304,8 @@ __device__ __forceinline__ void stencilk5_body(
   load_row<V>(w[0][2], T + rowc(i) * nx + xl);
   load_row<V>(pT, T + rowc(i + 1) * nx + xl);
   load_row<V>(pC, iCp + rowc(i) * nx + xl);
+  load_row<V>(qT, T + rowc(i + 2) * nx + xl);
+  load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
 
   __shared__ double ring[kWavesPerBlock * K * W];
   double* myring = ring + wave * K * W + lane * V;
@@ -324,8 +338,13 @@ __device__ __forceinline__ void stencilk5_body(
         }
       }
     }
-    load_row<V>(pT, T + rowc(i + 2) * nx + xl);
-    load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      pT[v] = qT[v];
+      pC[v] = qC[v];
+    }
+    load_row<V>(qT, T + rowc(i + 3) * nx + xl);
+    load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
 #pragma unroll
     for (int j = 1; j <= K; ++j) {
       const int64_t row = i - (j - 1);
@@ -385,160 +404,6 @@ __global__ __launch_bounds__(kBlock) void stencilk5_kernel(
   stencilk5_body<K, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
 }
 
-// kernel=6 ("fast5s"): kernel 5's arithmetic with TWO carried values per level
-// and cell instead of three rows. When the down neighbour dn of row r arrives
-// (level j-1 of row r+1), row r is finished with
-//   T2(r) = fma(g, fma(r_y, dn, A(r)), c(r))
-// and the state advances to row r+1:
-//   A(r+1) = fma(r_y, c(r), fma(-kc, dn, L(dn) + R(dn))),  c(r+1) = dn,
-// so the critical path per level is two FMAs (the lane moves and partial sums
-// of A feed only the next iteration) and a level holds 2V doubles: 2/3 of the
-// registers, which is what lets K = 12 / 16 levels fit at 3 waves per SIMD.
-// Rounding: c + g*(r_y*dn + (r_y*up + (-kc*c + (L+R)))) — same class as kernel
-// 5, not bitwise equal to it.
-template <int K, int V, bool NT, bool kPin = true>
-__device__ __forceinline__ void stencilk5s_body(
-    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
-    int64_t nx, int64_t ny, const RectList& L, const StencilCoef& k, int chunk_rows, int remap) {
-  constexpr int W = kWave * V;
-  constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_rects)
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  int ri = 0;
-  while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
-  int64_t strip, chunk;
-  if (!locate_task(L, ri, b, wave, strip, chunk)) return;  // whole wave exits
-  const Rect r = L.r[ri];
-  const int64_t xs = L.xa[ri] + strip * kStep;
-  const int64_t ya = r.y0 + chunk * chunk_rows;
-  const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
-
-  const int64_t x = xs + (int64_t)lane * V;
-  bool m[V], cin[V];
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    const int p = lane * V + v;
-    m[v] = p >= K && p < K + kStep && x + v >= r.x0 && x + v < r.x1;
-    cin[v] = (x + v >= 1) && (x + v <= nx - 2);
-  }
-  const int64_t xl = min(max(x, (int64_t)0), nx - V);
-
-  const double ax = (-k.mlam) * k.rdx * k.rdx;  // lam/dx^2
-  const double ay = (-k.mlam) * k.rdy * k.rdy;
-  const double ry = ay / ax;                    // host guarantees ax != 0, ry finite
-  const double mkc = -2.0 * (1.0 + ry);
-  const double gs = k.dt * ax;
-
-  // cc[j]: level-j row r (the centre of the next level-(j+1) update), aa[j]:
-  // its partial sum A(r). Rows outside the validity cone start from zeros:
-  // finite garbage that no output depends on.
-  double cc[K][V], aa[K][V], pT[V], pC[V];
-#pragma unroll
-  for (int j = 0; j < K; ++j)
-#pragma unroll
-    for (int v = 0; v < V; ++v) cc[j][v] = aa[j][v] = 0.0;
-  int64_t i = ya - K;
-  const int64_t iend = yb + K - 2;
-  auto rowc = [&](int64_t y) { return min(max(y, (int64_t)0), ny - 1); };
-  load_row<V>(cc[0], T + rowc(i) * nx + xl);
-  load_row<V>(pT, T + rowc(i + 1) * nx + xl);
-  load_row<V>(pC, iCp + rowc(i) * nx + xl);
-
-  __shared__ double ring[kWavesPerBlock * K * W];
-  double* myring = ring + wave * K * W + lane * V;
-  int slot = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j)
-#pragma unroll
-    for (int v = 0; v < V; ++v) myring[j * W + v] = 0.0;
-
-  for (;;) {
-    const bool rin1 = i >= 1 && i <= ny - 2;
-    double dn[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) dn[v] = pT[v];
-    {
-      double g[V];
-#pragma unroll
-      for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? gs * pC[v] : 0.0;
-      double* dst = myring + slot * W;
-      if constexpr (V == 1) {
-        dst[0] = g[0];
-      } else {
-#pragma unroll
-        for (int h = 0; h < V / 2; ++h) {
-          dbl2 t2;
-          t2.x = g[2 * h];
-          t2.y = g[2 * h + 1];
-          reinterpret_cast<dbl2*>(dst)[h] = t2;
-        }
-      }
-    }
-    load_row<V>(pT, T + rowc(i + 2) * nx + xl);
-    load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
-    // ring reads pipelined one level ahead behind compiler fences: left to
-    // itself the scheduler hoists all K reads to the top of the iteration and
-    // keeps 2KV more VGPRs live (measured: 184 instead of ~140 at K=12)
-    auto ring_read = [&](int j, double (&g)[V]) {
-      const int sl = slot - (j - 1) < 0 ? slot - (j - 1) + K : slot - (j - 1);
-      const double* src = myring + sl * W;
-      if constexpr (V == 1) {
-        g[0] = src[0];
-      } else {
-#pragma unroll
-        for (int h = 0; h < V / 2; ++h) {
-          const dbl2 t2 = reinterpret_cast<const dbl2*>(src)[h];
-          g[2 * h] = t2.x;
-          g[2 * h + 1] = t2.y;
-        }
-      }
-    };
-    double gl[V];
-    ring_read(1, gl);
-#pragma unroll
-    for (int j = 1; j <= K; ++j) {
-      const int64_t row = i - (j - 1);
-      double gn[V];
-      if (j < K) ring_read(j + 1, gn);
-      if constexpr (kPin) asm volatile("" ::: "memory");
-      double res[V];
-#pragma unroll
-      for (int v = 0; v < V; ++v)
-        res[v] = __builtin_fma(gl[v], __builtin_fma(ry, dn[v], aa[j - 1][v]), cc[j - 1][v]);
-      // advance level j-1 to row+1 (= dn)
-      const double rn = from_next_lane<true>(dn[0]);      // lane 63: 0 (invalid column)
-      const double ln = from_prev_lane<true>(dn[V - 1]);  // lane 0: 0 (invalid column)
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const double rv = v + 1 < V ? dn[v + 1] : rn;
-        const double lv = v > 0 ? dn[v - 1] : ln;
-        aa[j - 1][v] = __builtin_fma(ry, cc[j - 1][v], __builtin_fma(mkc, dn[v], rv + lv));
-        cc[j - 1][v] = dn[v];
-        if constexpr (kPin) asm volatile("" : "+v"(aa[j - 1][v]), "+v"(cc[j - 1][v]));
-      }
-      if (j < K) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          dn[v] = res[v];
-          gl[v] = gn[v];
-        }
-      } else if (row >= ya && row < yb) {
-        store_row<V, NT>(T2 + row * nx + x, res, m);
-      }
-    }
-    slot = slot + 1 == K ? 0 : slot + 1;
-    if (++i > iend) break;
-  }
-}
-
-template <int K, int V, bool NT>
-__global__ __launch_bounds__(kBlock) void stencilk5s_kernel(
-    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
-    int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
-  stencilk5s_body<K, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
-}
-
 template <int K, int V, bool NT, bool kLds, bool kDpp, bool kFast = false>
 __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
@@ -559,8 +424,9 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                         const StencilTuning& tune, stream_t stream) {
   RMA_CHECK_ARG(K == 2 || K == 3 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16,
                 "steps per pass must be 2, 3, 4, 6, 8, 12 or 16, got " << K);
-  RMA_CHECK_ARG(K <= 8 || tune.kernel == 5 || tune.kernel == 6,
-                "12 or 16 steps per pass need the fast5 kernels (kernel 5 or 6), got kernel "
+  RMA_CHECK_ARG(tune.kernel >= 0 && tune.kernel <= 5, "unknown K-step kernel " << tune.kernel);
+  RMA_CHECK_ARG(K <= 8 || tune.kernel == 5,
+                "12 or 16 steps per pass need the fast5 kernel (kernel 5), got kernel "
                     << tune.kernel);
   RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
   RMA_CHECK_ARG(nx >= 3 && ny >= 3, "grid too small: nx=" << nx << " ny=" << ny);
@@ -572,7 +438,7 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                   "rect " << i << " outside the interior of " << nx << "x" << ny);
   }
   RMA_CHECK_ARG(tune.chunk_rows >= 1, "chunk_rows=" << tune.chunk_rows);
-  RMA_CHECK_ARG((tune.kernel != 5 && tune.kernel != 6) || fast5_ok(c),
+  RMA_CHECK_ARG(tune.kernel != 5 || fast5_ok(c),
                 "kernel 5 folds dy^-2/dx^-2 into one factor: needs lam != 0 and finite "
                 "coefficients");
   const bool aligned = ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
@@ -610,10 +476,6 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
       stencilk5_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,           \
                                                             tune.chunk_rows, remap);          \
       break;                                                                                   \
-    case 6:                                                                                    \
-      stencilk5s_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,          \
-                                                             tune.chunk_rows, remap);         \
-      break;                                                                                   \
     default:                                                                                   \
       stencilk_ovl_kernel<KK, VV, NTS, false, false><<<grid, block, 0, s>>>(                    \
           T2, T, iCp, nx, ny, L, c, tune.chunk_rows, remap);                                   \
@@ -626,14 +488,10 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
   } else {                                              \
     if (nts) { RMA_TBK(KK, 1, true); } else { RMA_TBK(KK, 1, false); } \
   }
-  // 12 / 16 levels: fast5 kernels only, V <= 2 (register budget)
+  // 12 / 16 levels: fast5 only, V <= 2 (register budget)
 #define RMA_TBK_DEEP(KK, VV, NTS)                                                           \
-  if (tune.kernel == 5)                                                                       \
-    stencilk5_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,            \
-                                                         tune.chunk_rows, remap);             \
-  else                                                                                        \
-    stencilk5s_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,           \
-                                                          tune.chunk_rows, remap);
+  stencilk5_kernel<KK, VV, NTS><<<grid, block, 0, s>>>(T2, T, iCp, nx, ny, L, c,              \
+                                                       tune.chunk_rows, remap);
 #define RMA_TBK_DEEP_V(KK)                                                                  \
   if (V == 2) {                                                                               \
     if (nts) { RMA_TBK_DEEP(KK, 2, true) } else { RMA_TBK_DEEP(KK, 2, false) }                \

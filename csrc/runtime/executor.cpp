@@ -35,7 +35,7 @@ StencilTuning default_tune_k(int K, int64_t ny) {
   if (ny < 3072) t.chunk_rows = 16;
   else if (ny < 6144) t.chunk_rows = 32;
   else if (ny < 12288) t.chunk_rows = 64;
-  else if (ny < 32768) t.chunk_rows = K == 8 ? 128 : 256;  // K=12/16: c256 (fast5s sweep)
+  else if (ny < 32768) t.chunk_rows = K == 8 ? 128 : 256;  // K=12/16: c256 (profiles/sweep_deepk_16k)
   else t.chunk_rows = K >= 8 ? 1024 : 512;
   return t;
 }

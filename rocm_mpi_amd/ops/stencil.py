@@ -25,9 +25,10 @@ from .._native import has_native, native
 Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 
 # K-step kernels also: 2 = dpp, 3 = lds_dpp (default), 4 = fast (reassociated, FMA; not
-# bitwise), 5 = fast5 (5-point sum with one folded per-cell factor; not bitwise, lam != 0),
-# 6 = fast5s (fast5 arithmetic, two carried values per level: 12 / 16 steps per pass)
-KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4, "fast5": 5, "fast5s": 6}
+# bitwise), 5 = fast5 (5-point sum with one folded per-cell factor; not bitwise, lam != 0;
+# the only kernel for 12 / 16 steps per pass)
+FAST5 = ("fast5",)
+KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4, "fast5": 5}
 
 
 class StencilCoef(NamedTuple):
@@ -199,17 +200,17 @@ def stencil2_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: St
 def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
                   coef: StencilCoef, rects: Sequence[Rect] | None = None,
                   tuning: StencilTuning | None = None) -> None:
-    """K time steps in one pass (K = 2, 3, 4, 6, 8; 12, 16 with the fast5 kernels;
+    """K time steps in one pass (K = 2, 3, 4, 6, 8; 12, 16 with kernel fast5;
     csrc/kernels/stencil_tbk.hip):
     T2[r] = f^K(T)[r], the intermediate levels being f on the interior and T
     on boundary/halo cells. Bitwise equal to K ``stencil_step`` calls (kernels
-    fast / fast5 / fast5s: within rounding). Default tuning: the native
+    fast / fast5: within rounding). Default tuning: the native
     executor's (chunk by tile height, LDS 1/Cp ring, DPP)."""
     if int(K) not in (2, 3, 4, 6, 8, 12, 16):
         raise ValueError(f"K must be 2, 3, 4, 6, 8, 12 or 16, got {K}")
     check_field("T", T)
-    if int(K) > 8 and T.is_cuda and (tuning is None or tuning.kernel not in ("fast5", "fast5s")):
-        raise ValueError("12 or 16 steps per pass need kernel 'fast5' or 'fast5s' on the GPU")
+    if int(K) > 8 and T.is_cuda and (tuning is None or tuning.kernel not in FAST5):
+        raise ValueError("12 or 16 steps per pass need kernel 'fast5' on the GPU")
     ny, nx = T.shape
     check_field("T2", T2, (ny, nx), T.device)
     check_field("iCp", iCp, (ny, nx), T.device)
@@ -222,7 +223,7 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
         ch = native().default_chunk_k(int(K), ny) if has_native() else 16
         tuning = StencilTuning(chunk_rows=ch, kernel="lds_dpp", xcd_remap=1)
     tn = tuning
-    if tn.kernel in ("fast5", "fast5s") and not fast5_ok(coef):
+    if tn.kernel in FAST5 and not fast5_ok(coef):
         raise ValueError("kernel 'fast5' folds dy^-2/dx^-2 into one factor: needs lam != 0 "
                          f"and finite coefficients, got {tuple(coef)}")
     if T.is_cuda:

@@ -1,0 +1,16 @@
+#!/bin/bash
+# fast5 with two-row-ahead prefetch: tests, then K=8/12/16 sweeps (fast5 vs fast5b).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
+OUT=gpurun_out/fast5_pf2; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_temporal_gpu.py tests/test_guard_bands_gpu.py -k "fast or deep or stay_in_bounds" > $OUT/tests.log 2>&1 &&
+echo "tests ok" && tail -1 $OUT/tests.log &&
+timeout -k 10 300 python bench/stencil_sweep.py --n 16384 --rounds 3 --iters 4 --no-march --no-roof \
+    --tbk 8,12,16 --tbk-chunks 128,256 --tbk-xcds 1 --tbk-vecs 2 --tbk-kernels fast5 \
+    --out $OUT/sweep16k.json > $OUT/sweep16k.log 2>&1 &&
+echo "sweep16k ok" &&
+timeout -k 10 500 python bench/stencil_sweep.py --n 101376 --rounds 3 --iters 2 --no-march --no-roof \
+    --tbk 8,12,16 --tbk-chunks 512,1024,2048 --tbk-xcds 1 --tbk-vecs 2 --tbk-kernels fast5 \
+    --out $OUT/sweep101k.json > $OUT/sweep101k.log 2>&1 &&
+echo "sweep101k ok"

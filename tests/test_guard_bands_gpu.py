@@ -69,7 +69,7 @@ def test_one_step_kernels_stay_in_bounds(ny, nx, kernel):
 def test_multi_step_kernels_stay_in_bounds(ny, nx, K):
     rects = [ops.interior_rect(nx, ny)]
     for kern, vec in (("march", 2), ("lds", 2), ("dpp", 2), ("lds_dpp", 2), ("fast", 2),
-                      ("fast5", 2), ("fast5", 4), ("fast5s", 2)):
+                      ("fast5", 2), ("fast5", 4)):
         tn = ops.StencilTuning(chunk_rows=5, kernel=kern, vec=vec)
         check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny, nx,
                       rects)

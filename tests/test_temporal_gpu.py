@@ -138,10 +138,10 @@ def test_k_step_rect_lists_and_unaligned(K, xcd):
 @pytest.mark.parametrize("K", [2, 3, 4, 6, 8])
 @pytest.mark.parametrize("ny,nx", [(3, 3), (67, 131), (257, 1024), (300, 129), (31, 4097)])
 @pytest.mark.parametrize("kern,vec,chunk", [("fast", 2, 16), ("fast5", 2, 16), ("fast5", 4, 5),
-                                            ("fast5s", 2, 7), ("fast5s", 2, 64), ("fast5", 2, 1)])
+                                            ("fast5", 2, 7), ("fast5", 2, 64), ("fast5", 2, 1)])
 def test_k_step_fast_variant_close(K, ny, nx, kern, vec, chunk):
     """kernel='fast' reassociates the update (differences, folded constants,
-    FMAs) and 'fast5' / 'fast5s' evaluate the 5-point sum with one folded
+    FMAs) and 'fast5' evaluates the 5-point sum with one folded
     per-cell factor: not bitwise, but within a few ulp of the canonical K
     steps, and boundary cells stay exactly fixed."""
     T, iCp = rand((ny, nx), 12), rand((ny, nx), 13) + 0.5
@@ -165,15 +165,15 @@ def test_fast5_rejects_zero_lambda():
 
 @pytest.mark.parametrize("K", [12, 16])
 @pytest.mark.parametrize("ny,nx", [(3, 3), (67, 131), (257, 1024), (300, 129), (41, 4097)])
-@pytest.mark.parametrize("kern,chunk", [("fast5", 16), ("fast5s", 16), ("fast5s", 1), ("fast5s", 50)])
-def test_deep_k_step_fast5_close(K, ny, nx, kern, chunk):
-    """12 / 16 steps per pass (fast5 kernels only): within rounding of the
+@pytest.mark.parametrize("chunk,xcd", [(16, 1), (1, 0), (50, 1), (37, 0)])
+def test_deep_k_step_fast5_close(K, ny, nx, chunk, xcd):
+    """12 / 16 steps per pass (fast5 kernel only): within rounding of the
     canonical K steps, boundary cells fixed."""
     T, iCp = rand((ny, nx), 15), rand((ny, nx), 16) + 0.5
     ref = k_steps_cpu(K, T, iCp, [ops.interior_rect(nx, ny)])
     out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
     ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(),
-                      tuning=ops.StencilTuning(chunk_rows=chunk, kernel=kern))
+                      tuning=ops.StencilTuning(chunk_rows=chunk, kernel="fast5", xcd_remap=xcd))
     o = out.cpu()
     assert torch.equal(o[0], ref[0]) and torch.equal(o[:, 0], ref[:, 0])
     torch.testing.assert_close(o, ref, rtol=1e-13, atol=1e-13)
@@ -184,3 +184,21 @@ def test_deep_k_needs_fast5():
     with pytest.raises(ValueError):
         ops.stencilk_step(12, torch.empty_like(T), T, torch.ones_like(T), coef(),
                           tuning=ops.StencilTuning(chunk_rows=16, kernel="fast"))
+
+
+@pytest.mark.parametrize("K", [4, 16])
+def test_fast5_rect_lists(K):
+    """Frame + interior rects as the executor issues them (thin column rects)."""
+    ny, nx = 203, 900
+    T, iCp = rand((ny, nx), 20), rand((ny, nx), 21) + 0.5
+    w = K
+    rects = [(w, nx - w, w, 2 * w), (w, nx - w, ny - 2 * w, ny - w), (w, 2 * w, 2 * w, ny - 2 * w),
+             (nx - 2 * w, nx - w, 2 * w, ny - 2 * w)]
+    interior = (2 * w, nx - 2 * w, 2 * w, ny - 2 * w)
+    out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+    tn = ops.StencilTuning(chunk_rows=16, kernel="fast5", xcd_remap=1)
+    Td, iCpd = T.to(DEV), iCp.to(DEV)
+    ops.stencilk_step(K, out, Td, iCpd, coef(), rects, tn)
+    ops.stencilk_step(K, out, Td, iCpd, coef(), [interior], tn)
+    ref = k_steps_cpu(K, T, iCp, rects + [interior])
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-13, atol=1e-13)
