@@ -71,6 +71,9 @@ def parse(argv=None):
                     help="after the timed run, also time this many steps of the one-step "
                          "kernel on the same tile (reported in config; 0 = skip)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: the same driver on the C++ CPU twins over gloo (tests of the "
+                         "multi-rank bench path; needs --nx; not a benchmark)")
     return ap.parse_args(argv)
 
 
@@ -105,14 +108,22 @@ def main(argv=None) -> int:
     from rocm_mpi_amd.parallel import comm as C
     from rocm_mpi_amd.parallel import implicit_grid as gg
 
-    if not torch.cuda.is_available():
+    gpu = a.device == "cuda"
+    if gpu and not torch.cuda.is_available():
         print("bench.py needs an MI355X (no GPU visible)", file=sys.stderr)
         return 2
+    if not gpu and not a.nx:
+        print("bench.py --device cpu needs --nx", file=sys.stderr)
+        return 2
     if world > 1:
-        C.init_distributed()
+        C.init_distributed(None if gpu else "gloo")
     rank = int(os.environ.get("RANK", "0"))
     local, _ = C.node_local_rank(rank, world)
-    C.select_device(local)
+    dev = str(C.select_device(local)) if gpu else "cpu"
+
+    def sync():
+        if gpu:
+            torch.cuda.synchronize()
 
     nx = a.nx or auto_tile(a.hbm_frac, a.max_tile)
     if world > 1 and not a.nx:
@@ -124,7 +135,7 @@ def main(argv=None) -> int:
     ny = a.ny or nx
     dims = tuple(int(v) for v in a.dims.split(",")) + (0,)
     bw = tuple(int(v) for v in a.b_width.split(","))
-    cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup,
+    cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup, device=dev,
                           warmup=a.warmup, init="random", b_width=bw, dims=dims,
                           chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
                           unroll=a.unroll, vec=a.vec, temporal=a.temporal, chunk2=a.chunk2,
@@ -146,10 +157,10 @@ def main(argv=None) -> int:
     model.step(a.warmup)
     model.synchronize()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     model.step(a.steps)
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
     t1 = time.perf_counter()
     local_s = t1 - t0
@@ -164,10 +175,10 @@ def main(argv=None) -> int:
         model.step(2 * K)
         model.synchronize()
         comm.barrier()
-        torch.cuda.synchronize()
+        sync()
         s0 = time.perf_counter()
         model.step(steps)
-        torch.cuda.synchronize()
+        sync()
         comm.barrier()
         s1 = comm.allreduce(time.perf_counter() - s0, "max")
         return 3 * nx * ny * 8 / 1e9 / (s1 / steps)

@@ -60,3 +60,44 @@ def test_gloo_temporal_blocking_tiles(tmp_path, variant, K):
         T = np.load(tmp_path / f"tile{r}.npy")
         gx0, gy0 = cx * (nx - ol), cy * (ny - ol)
         assert np.array_equal(T, G[gy0:gy0 + ny, gx0:gx0 + nx])
+
+
+@pytest.mark.parametrize("world,extra", [(2, ["--temporal", "4", "--dims", "2,1"]),
+                                         (4, ["--temporal", "16", "--dims", "2,2"])])
+def test_bench_driver_contract_multirank(tmp_path, world, extra):
+    """bench.py's multi-rank path (the driver runs it under torch.distributed.run
+    at N = 2, 4, 8) on the CPU twins over gloo: rank 0 prints ONE JSON line with
+    the contract's keys, n_gpus == WORLD_SIZE, value == N x per-rank T_eff,
+    weak scaling (same local tile), and the global grid of a dims decomposition."""
+    import json
+    import subprocess
+    import sys
+
+    from helpers import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    nx = 72
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(world), "--steps", "20", "--warmup", "3", "--device", "cpu",
+           "--nx", str(nx), "--single-step-steps", "4", *extra]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
+                       env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == world and d["steps"] == 20 and d["warmup"] == 3
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    c = d["config"]
+    assert c["local_grid"] == [nx, nx]
+    K = int(extra[1])
+    dims = [int(v) for v in extra[3].split(",")]
+    assert c["global_grid"] == [dims[0] * (nx - 2 * K) + 2 * K, dims[1] * (nx - 2 * K) + 2 * K]
+    assert abs(d["value"] - world * c["teff_per_gpu_GBps"]) <= 1e-6 * d["value"] + 0.02
+    assert c["nonfinite_cells_sampled"] == 0
