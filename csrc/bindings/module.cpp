@@ -343,6 +343,13 @@ PYBIND11_MODULE(_C, m) {
   // ---------------- executor ----------------
   m.def("default_chunk_k", [](int K, int64_t ny) { return default_tune_k(K, ny).chunk_rows; },
         py::arg("K"), py::arg("ny"));
+  m.def(
+      "fast_kernel_k",
+      [](int K, int64_t ny, const Coef4& coef) {
+        const StencilTuning t = fast_tune_k(K, ny, to_coef(coef));
+        return std::make_tuple(t.kernel, t.vec, t.chunk_rows);
+      },
+      py::arg("K"), py::arg("ny"), py::arg("coef"));
   py::class_<DiffusionExecutor>(m, "Executor")
       .def(py::init([](uintptr_t T, uintptr_t T2, uintptr_t iCp, int64_t nx, int64_t ny, int mode,
                        const Coef4& coef, int chunk_rows, int nontemporal, int kernel,

@@ -59,6 +59,12 @@ struct ExecParams {
 // kernel with the LDS 1/Cp ring, per-XCD task ranges and chunks growing with
 // the tile height (they amortise the 2K-1 rows recomputed per chunk).
 StencilTuning default_tune_k(int K, int64_t ny);
+// The fast-math K-step passes (fast_math, stencil_tbk.hip kernels 5-7; needs
+// fast5_ok): K=16 runs the 4-stage pipelined kernel with 4 cells per lane, K=12
+// the 2-stage one with 4 cells per lane, K<=8 the single-wave kernel 5
+// (measured, profiles/SUMMARY_r1.md). Kernel 4 when the coefficients cannot be
+// folded (lam == 0; K <= 8 only).
+StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c);
 
 class DiffusionExecutor {
  public:

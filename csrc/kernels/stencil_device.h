@@ -174,6 +174,31 @@ inline int64_t plan_rects(RectList& L, const Rect* rects, int nrects, int V, int
   return total;
 }
 
+// Planner of the stage-pipelined K-step kernel (stencil_tbk.hip kernels 6/7):
+// one block per (strip, chunk) task, strips as in plan_rects with halo > 0;
+// block b of a rect is (chunk = lb / strips, strip = lb % strips).
+inline int64_t plan_strip_tasks(RectList& L, const Rect* rects, int nrects, int V,
+                                int chunk_rows, int halo) {
+  L = RectList{};
+  int64_t total = 0;
+  const int64_t sw = (int64_t)kWave * V;
+  const int64_t step = (sw - 2 * halo) / V * V;
+  for (int i = 0; i < nrects; ++i) {
+    const Rect& r = rects[i];
+    if (r.empty()) continue;
+    const int n = L.n++;
+    L.r[n] = r;
+    const int64_t x0 = r.x0 - halo;
+    L.xa[n] = x0 - (((x0 % V) + V) % V);
+    L.strips[n] = (r.x1 - (L.xa[n] + halo) + step - 1) / step;
+    L.chunks[n] = (r.y1 - r.y0 + chunk_rows - 1) / chunk_rows;
+    L.gpad[n] = 0;
+    total += L.strips[n] * L.chunks[n];
+    L.block_end[n] = total;
+  }
+  return total;
+}
+
 // Wave task of block b (wide rects: one block row per chunk row, padded to a
 // multiple of 8 blocks; narrow rects: consecutive chunks per wave). Returns
 // false for padding / idle waves (the whole wave exits together).

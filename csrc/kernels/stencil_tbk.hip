@@ -404,6 +404,183 @@ __global__ __launch_bounds__(kBlock) void stencilk5_kernel(
   stencilk5_body<K, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
 }
 
+// kernel=6/7 ("fast5p2" / "fast5p4"): kernel 5's arithmetic with the K levels
+// of ONE strip split over the S waves of a block (S = 2 / 4 stages of H = K/S
+// levels each). Stage s keeps only its own H three-row windows (K=16, S=4:
+// 48 instead of 192 VGPRs of windows, so 5 waves per SIMD instead of 2 hide
+// the fp64 and LDS latencies). Stage 0 streams T / 1/Cp from HBM and fills
+// the per-strip 1/Cp ring; every other stage reads its input level from an
+// LDS hand-off row written by the previous stage one iteration earlier; the
+// last stage stores. One barrier per row iteration; stage s runs s(H+1) rows
+// behind stage 0 (its new input row at iteration i is i + 1 - s(H+1)).
+// Bitwise equal to kernel 5 (same operations per cell).
+template <int K, int S, int V, bool NT>
+__device__ __forceinline__ void stencilk5p_body(
+    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
+    int64_t nx, int64_t ny, const RectList& L, const StencilCoef& k, int chunk_rows, int remap) {
+  static_assert(K % S == 0, "levels must split evenly over the stages");
+  constexpr int H = K / S;
+  constexpr int W = kWave * V;
+  constexpr int kStep = (W - 2 * K) / V * V;
+  constexpr int R = K + S - 1;  // ring rows: i (newest) .. i + 2 - K - S (oldest read)
+  const int stage = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  int ri = 0;
+  while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
+  // one block = one strip task; every block is a task (the stages meet at barriers)
+  const int64_t lb = b - (ri ? L.block_end[ri - 1] : 0);
+  const int64_t strip = lb % L.strips[ri], chunk = lb / L.strips[ri];
+  const Rect r = L.r[ri];
+  const int64_t xs = L.xa[ri] + strip * kStep;
+  const int64_t ya = r.y0 + chunk * chunk_rows;
+  const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
+
+  const int64_t x = xs + (int64_t)lane * V;
+  bool m[V], cin[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int p = lane * V + v;
+    m[v] = p >= K && p < K + kStep && x + v >= r.x0 && x + v < r.x1;
+    cin[v] = (x + v >= 1) && (x + v <= nx - 2);
+  }
+  const int64_t xl = min(max(x, (int64_t)0), nx - V);
+
+  const double ax = (-k.mlam) * k.rdx * k.rdx;
+  const double ay = (-k.mlam) * k.rdy * k.rdy;
+  const double ry = ay / ax;
+  const double mkc = -2.0 * (1.0 + ry);
+  const double gs = k.dt * ax;
+
+  // w[0]: the stage's input level (T for stage 0, level s*H otherwise),
+  // w[j]: local level s*H + j, j < H; the level-(s+1)*H row is handed off
+  double w[H][3][V], pT[V], pC[V], qT[V], qC[V];
+#pragma unroll
+  for (int j = 0; j < H; ++j)
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int v = 0; v < V; ++v) w[j][t][v] = 0.0;
+  int64_t i = ya - K;
+  const int64_t iend = yb + K - 3 + S;
+  auto rowc = [&](int64_t y) { return min(max(y, (int64_t)0), ny - 1); };
+  if (stage == 0) {
+    load_row<V>(w[0][2], T + rowc(i) * nx + xl);
+    load_row<V>(pT, T + rowc(i + 1) * nx + xl);
+    load_row<V>(pC, iCp + rowc(i) * nx + xl);
+    load_row<V>(qT, T + rowc(i + 2) * nx + xl);
+    load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
+  }
+  __shared__ double ring[R * W];
+  __shared__ double hand[2][S > 1 ? S - 1 : 1][W];
+  for (int t = threadIdx.x; t < R * W; t += S * kWave) ring[t] = 0.0;
+  for (int t = threadIdx.x; t < 2 * (S > 1 ? S - 1 : 1) * W; t += S * kWave) (&hand[0][0][0])[t] = 0.0;
+  __syncthreads();
+  auto rd2 = [&](const double* src, double (&out)[V]) {
+    if constexpr (V == 1) {
+      out[0] = src[0];
+    } else {
+#pragma unroll
+      for (int h = 0; h < V / 2; ++h) {
+        const dbl2 t2 = reinterpret_cast<const dbl2*>(src)[h];
+        out[2 * h] = t2.x;
+        out[2 * h + 1] = t2.y;
+      }
+    }
+  };
+  auto wr2 = [&](double* dst, const double (&in)[V]) {
+    if constexpr (V == 1) {
+      dst[0] = in[0];
+    } else {
+#pragma unroll
+      for (int h = 0; h < V / 2; ++h) {
+        dbl2 t2;
+        t2.x = in[2 * h];
+        t2.y = in[2 * h + 1];
+        reinterpret_cast<dbl2*>(dst)[h] = t2;
+      }
+    }
+  };
+  int slot0 = 0;  // ring slot of row i (stage 0's level-1 row)
+  int par = 0;
+  const int lag = stage * (H + 1);  // rows behind stage 0
+  auto iter = [&](auto Pc) {
+    constexpr int P = decltype(Pc)::value;
+    constexpr int PC = (P + 2) % 3, PU = (P + 1) % 3;
+    if (stage == 0) {
+      const bool rin1 = i >= 1 && i <= ny - 2;
+#pragma unroll
+      for (int v = 0; v < V; ++v) w[0][P][v] = pT[v];
+      double g[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? gs * pC[v] : 0.0;
+      wr2(ring + slot0 * W + lane * V, g);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        pT[v] = qT[v];
+        pC[v] = qC[v];
+      }
+      load_row<V>(qT, T + rowc(i + 3) * nx + xl);
+      load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
+    } else {
+      rd2(&hand[par ^ 1][stage - 1][lane * V], w[0][P]);
+    }
+    // this stage's level-1 row is i - lag: its ring slot
+    int sbase = slot0 - lag;
+    sbase = sbase < 0 ? sbase + R : sbase;
+#pragma unroll
+    for (int j = 1; j <= H; ++j) {
+      const int64_t row = i - lag - (j - 1);
+      double gl[V];
+      {
+        const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
+        rd2(ring + sl * W + lane * V, gl);
+      }
+      const double(&up)[V] = w[j - 1][PU];
+      const double(&c)[V] = w[j - 1][PC];
+      const double(&dn)[V] = w[j - 1][P];
+      const double rn = from_next_lane<true>(c[0]);
+      const double ln = from_prev_lane<true>(c[V - 1]);
+      double res[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const double rv = v + 1 < V ? c[v + 1] : rn;
+        const double lv = v > 0 ? c[v - 1] : ln;
+        const double sx = rv + lv;
+        const double sy = up[v] + dn[v];
+        res[v] = __builtin_fma(gl[v], __builtin_fma(ry, sy, __builtin_fma(mkc, c[v], sx)), c[v]);
+      }
+      if (j < H) {
+        const int jj = j < H ? j : H - 1;
+#pragma unroll
+        for (int v = 0; v < V; ++v) w[jj][P][v] = res[v];
+      } else if (stage < S - 1) {
+        wr2(&hand[par][stage][lane * V], res);
+      } else if (row >= ya && row < yb) {
+        store_row<V, NT>(T2 + row * nx + x, res, m);
+      }
+    }
+    slot0 = slot0 + 1 == R ? 0 : slot0 + 1;
+    par ^= 1;
+    __syncthreads();  // hand-off rows and ring row visible; this iteration's reads done
+  };
+  for (;;) {
+    iter(std::integral_constant<int, 0>{});
+    if (++i > iend) break;
+    iter(std::integral_constant<int, 1>{});
+    if (++i > iend) break;
+    iter(std::integral_constant<int, 2>{});
+    if (++i > iend) break;
+  }
+}
+
+template <int K, int S, int V, bool NT>
+__global__ __launch_bounds__(kWave * S) void stencilk5p_kernel(
+    double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
+    int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
+  stencilk5p_body<K, S, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
+}
+
 template <int K, int V, bool NT, bool kLds, bool kDpp, bool kFast = false>
 __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
@@ -424,9 +601,9 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                         const StencilTuning& tune, stream_t stream) {
   RMA_CHECK_ARG(K == 2 || K == 3 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16,
                 "steps per pass must be 2, 3, 4, 6, 8, 12 or 16, got " << K);
-  RMA_CHECK_ARG(tune.kernel >= 0 && tune.kernel <= 5, "unknown K-step kernel " << tune.kernel);
-  RMA_CHECK_ARG(K <= 8 || tune.kernel == 5,
-                "12 or 16 steps per pass need the fast5 kernel (kernel 5), got kernel "
+  RMA_CHECK_ARG(tune.kernel >= 0 && tune.kernel <= 7, "unknown K-step kernel " << tune.kernel);
+  RMA_CHECK_ARG(K <= 8 || tune.kernel >= 5,
+                "12 or 16 steps per pass need a fast5 kernel (kernel 5, 6 or 7), got kernel "
                     << tune.kernel);
   RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
   RMA_CHECK_ARG(nx >= 3 && ny >= 3, "grid too small: nx=" << nx << " ny=" << ny);
@@ -438,16 +615,53 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                   "rect " << i << " outside the interior of " << nx << "x" << ny);
   }
   RMA_CHECK_ARG(tune.chunk_rows >= 1, "chunk_rows=" << tune.chunk_rows);
-  RMA_CHECK_ARG(tune.kernel != 5 || fast5_ok(c),
+  RMA_CHECK_ARG(tune.kernel < 5 || fast5_ok(c),
                 "kernel 5 folds dy^-2/dx^-2 into one factor: needs lam != 0 and finite "
                 "coefficients");
   const bool aligned = ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(T2) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
   int V = 1;
-  if (aligned && nx % 2 == 0) V = (tune.vec == 4 && nx % 4 == 0 && K <= 8) ? 4 : 2;
+  if (aligned && nx % 2 == 0)
+    V = (tune.vec == 4 && nx % 4 == 0 && (K <= 8 || tune.kernel == 6 || tune.kernel == 7)) ? 4 : 2;
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   RectList L;
+  if (tune.kernel == 6 || tune.kernel == 7) {  // stage-pipelined fast5: 2 or 4 waves per strip
+    const int S = tune.kernel == 6 ? 2 : 4;
+    RMA_CHECK_ARG(K == 8 || K == 12 || K == 16,
+                  "the stage-pipelined kernels run 8, 12 or 16 steps per pass, got " << K);
+    const int64_t ntask = plan_strip_tasks(L, rects, nrects, V, tune.chunk_rows, K);
+    if (L.n == 0) return;
+    RMA_CHECK_ARG(ntask < (int64_t(1) << 31), "grid too large: " << ntask << " blocks");
+    const dim3 g((unsigned)ntask), blk(kWave * S);
+    hipStream_t st = as_stream(stream);
+    const bool nt1 = tune.nontemporal & 1;
+#define RMA_TBKP(KK, SS)                                                                     \
+  if (V == 4) {                                                                               \
+    if (nt1) stencilk5p_kernel<KK, SS, 4, true><<<g, blk, 0, st>>>(T2, T, iCp, nx, ny, L, c,  \
+                                                                    tune.chunk_rows, remap);  \
+    else stencilk5p_kernel<KK, SS, 4, false><<<g, blk, 0, st>>>(T2, T, iCp, nx, ny, L, c,     \
+                                                                 tune.chunk_rows, remap);     \
+  } else if (V == 2) {                                                                        \
+    if (nt1) stencilk5p_kernel<KK, SS, 2, true><<<g, blk, 0, st>>>(T2, T, iCp, nx, ny, L, c,  \
+                                                                    tune.chunk_rows, remap);  \
+    else stencilk5p_kernel<KK, SS, 2, false><<<g, blk, 0, st>>>(T2, T, iCp, nx, ny, L, c,     \
+                                                                 tune.chunk_rows, remap);     \
+  } else {                                                                                    \
+    if (nt1) stencilk5p_kernel<KK, SS, 1, true><<<g, blk, 0, st>>>(T2, T, iCp, nx, ny, L, c,  \
+                                                                    tune.chunk_rows, remap);  \
+    else stencilk5p_kernel<KK, SS, 1, false><<<g, blk, 0, st>>>(T2, T, iCp, nx, ny, L, c,     \
+                                                                 tune.chunk_rows, remap);     \
+  }
+    if (S == 2) {
+      if (K == 8) { RMA_TBKP(8, 2) } else if (K == 12) { RMA_TBKP(12, 2) } else { RMA_TBKP(16, 2) }
+    } else {
+      if (K == 8) { RMA_TBKP(8, 4) } else if (K == 12) { RMA_TBKP(12, 4) } else { RMA_TBKP(16, 4) }
+    }
+#undef RMA_TBKP
+    RMA_HIP_LAUNCH_CHECK();
+    return;
+  }
   const int64_t total = plan_rects(L, rects, nrects, V, tune.chunk_rows, remap, false, K);
   if (L.n == 0) return;
   RMA_CHECK_ARG(total < (int64_t(1) << 31), "grid too large: " << total << " blocks");

@@ -40,6 +40,19 @@ StencilTuning default_tune_k(int K, int64_t ny) {
   return t;
 }
 
+StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c) {
+  StencilTuning t = default_tune_k(K, ny);
+  if (K <= 1) return t;
+  t.xcd_remap = 1;
+  if (!fast5_ok(c)) {
+    t.kernel = 4;
+    return t;
+  }
+  t.kernel = K == 16 ? 7 : K == 12 ? 6 : 5;
+  t.vec = K >= 12 ? 4 : 2;
+  return t;
+}
+
 DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, int64_t nx,
                                      int64_t ny, const ExecParams& p, HaloExchanger* halo,
                                      double* qx, double* qy, double* dTdt)
@@ -63,9 +76,14 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
                 "temporal blocking applies to perf / perf_hide, not kp");
   RMA_CHECK_ARG(p.olx >= 2 && p.oly >= 2, "overlaps must be >= 2");
   hwx_ = hwy_ = p.temporal;  // halo width = steps per exchange
-  // fast_math: the 5-point-sum kernel (5 fp64 ops per cell update) unless the
+  // fast_math: the 5-point-sum kernels (5 fp64 ops per cell update) unless the
   // coefficients cannot be folded (lam == 0), then the reassociated-flux one
-  if (p_.fast_math && p.temporal > 1) p_.tune2.kernel = fast5_ok(p.coef) ? 5 : 4;
+  if (p_.fast_math && p.temporal > 1) {
+    const StencilTuning f = fast_tune_k(p.temporal, ny, p.coef);
+    p_.tune2.kernel = f.kernel;
+    p_.tune2.vec = f.vec;
+    p_.tune2.xcd_remap = f.xcd_remap;
+  }
   std::array<std::array<int, 2>, 3> nbr{{{-1, -1}, {-1, -1}, {-1, -1}}};
   if (halo) nbr = halo->neighbors();
   const int64_t ol[2] = {p.olx, p.oly};
@@ -295,7 +313,12 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
         stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       } else {
         tn.xcd_remap = 1;
-        tn.kernel = p_.fast_math ? p_.tune2.kernel : 3;
+        tn.kernel = 3;
+        if (p_.fast_math) {
+          const StencilTuning f = fast_tune_k(kr, ny_, p_.coef);
+          tn.kernel = f.kernel;
+          tn.vec = f.vec;
+        }
         stencilk_rects_gpu(kr, Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
       }
       exchange(Tout, s_lo_);

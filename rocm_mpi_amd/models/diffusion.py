@@ -341,9 +341,11 @@ class Diffusion2D:
                 K = self.cfg.temporal
                 Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
                 tn = None
-                if self.cfg.fast_math and Tin.is_cuda:
-                    tn = ops.StencilTuning(chunk_rows=self.chunk2, xcd_remap=1,
-                                           kernel="fast5" if ops.fast5_ok(self.coef) else "fast")
+                if self.cfg.fast_math and Tin.is_cuda:  # the executor's fast-math kernel
+                    kern, vec, _ = native().fast_kernel_k(K, self.cfg.ny, tuple(self.coef))
+                    name = {v: k for k, v in ops.KERNELS.items()}[kern]
+                    tn = ops.StencilTuning(chunk_rows=self.chunk2, xcd_remap=1, kernel=name,
+                                           vec=vec)
                 ops.stencilk_step(K, Tout, Tin, self.iCp, self.coef, [self.out2], tn)
                 update_halo_(Tout)
                 self.parity ^= 1

@@ -26,9 +26,11 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 
 # K-step kernels also: 2 = dpp, 3 = lds_dpp (default), 4 = fast (reassociated, FMA; not
 # bitwise), 5 = fast5 (5-point sum with one folded per-cell factor; not bitwise, lam != 0;
-# the only kernel for 12 / 16 steps per pass)
-FAST5 = ("fast5",)
-KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4, "fast5": 5}
+# the only kernel family for 12 / 16 steps per pass); 6 / 7 = fast5p2 / fast5p4: the same
+# arithmetic with the levels of one strip split over 2 / 4 pipelined waves (K = 8, 12, 16)
+FAST5 = ("fast5", "fast5p2", "fast5p4")
+KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4, "fast5": 5, "fast5p2": 6,
+           "fast5p4": 7}
 
 
 class StencilCoef(NamedTuple):
@@ -210,7 +212,7 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
         raise ValueError(f"K must be 2, 3, 4, 6, 8, 12 or 16, got {K}")
     check_field("T", T)
     if int(K) > 8 and T.is_cuda and (tuning is None or tuning.kernel not in FAST5):
-        raise ValueError("12 or 16 steps per pass need kernel 'fast5' on the GPU")
+        raise ValueError("12 or 16 steps per pass need a fast5 kernel (fast5, fast5p2, fast5p4) on the GPU")
     ny, nx = T.shape
     check_field("T2", T2, (ny, nx), T.device)
     check_field("iCp", iCp, (ny, nx), T.device)

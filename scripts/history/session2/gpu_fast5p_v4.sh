@@ -1,0 +1,16 @@
+#!/bin/bash
+# stage-pipelined fast5 with 4 cells per lane: tests, sweeps vs fast5.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
+OUT=gpurun_out/fast5p_v4; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_temporal_gpu.py tests/test_guard_bands_gpu.py -k "pipelined or stay_in_bounds" > $OUT/tests.log 2>&1 &&
+echo "tests ok" && tail -1 $OUT/tests.log &&
+timeout -k 10 300 python bench/stencil_sweep.py --n 16384 --rounds 3 --iters 4 --no-march --no-roof \
+    --tbk 12,16 --tbk-chunks 256 --tbk-xcds 1 --tbk-vecs 2,4 --tbk-kernels fast5,fast5p2,fast5p4 \
+    --out $OUT/sweep16k.json > $OUT/sweep16k.log 2>&1 &&
+echo "sweep16k ok" &&
+timeout -k 10 500 python bench/stencil_sweep.py --n 101376 --rounds 3 --iters 2 --no-march --no-roof \
+    --tbk 12,16 --tbk-chunks 512,1024 --tbk-xcds 1 --tbk-vecs 2,4 --tbk-kernels fast5,fast5p2,fast5p4 \
+    --out $OUT/sweep101k.json > $OUT/sweep101k.log 2>&1 &&
+echo "sweep101k ok"

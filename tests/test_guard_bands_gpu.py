@@ -73,6 +73,11 @@ def test_multi_step_kernels_stay_in_bounds(ny, nx, K):
         tn = ops.StencilTuning(chunk_rows=5, kernel=kern, vec=vec)
         check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny, nx,
                       rects)
+    if K == 8:
+        for kern, vec in (("fast5p2", 2), ("fast5p4", 2), ("fast5p4", 4)):
+            tn = ops.StencilTuning(chunk_rows=5, kernel=kern, vec=vec)
+            check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny,
+                          nx, rects)
     if K == 2:
         check_stencil(lambda o, t, c, r: ops.stencil2_step(o, t, c, coef(), r), ny, nx, rects)
 

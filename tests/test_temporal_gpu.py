@@ -202,3 +202,44 @@ def test_fast5_rect_lists(K):
     ops.stencilk_step(K, out, Td, iCpd, coef(), [interior], tn)
     ref = k_steps_cpu(K, T, iCp, rects + [interior])
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("K", [8, 12, 16])
+@pytest.mark.parametrize("kern", ["fast5p2", "fast5p4"])
+@pytest.mark.parametrize("ny,nx", [(3, 3), (67, 131), (257, 1024), (300, 129), (41, 4097),
+                                   (130, 515), (19, 2000)])
+@pytest.mark.parametrize("chunk,xcd,vec", [(16, 1, 2), (1, 0, 2), (37, 1, 2), (16, 1, 4),
+                                           (5, 0, 4)])
+def test_pipelined_fast5_equals_fast5_bitwise(K, kern, ny, nx, chunk, xcd, vec):
+    """The stage-pipelined kernels (levels of a strip split over 2 / 4 waves,
+    hand-off rows through LDS; 2 or 4 cells per lane) compute exactly kernel
+    fast5's operations."""
+    T, iCp = rand((ny, nx), 18), rand((ny, nx), 19) + 0.5
+    Td, iCpd = T.to(DEV), iCp.to(DEV)
+    outs = []
+    for kn, vv in (("fast5", 2), (kern, vec)):
+        out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+        ops.stencilk_step(K, out, Td, iCpd, coef(),
+                          tuning=ops.StencilTuning(chunk_rows=chunk, kernel=kn, xcd_remap=xcd,
+                                                   vec=vv))
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("kern", ["fast5p2", "fast5p4"])
+def test_pipelined_fast5_rect_lists(kern):
+    K, ny, nx = 16, 203, 900
+    T, iCp = rand((ny, nx), 20), rand((ny, nx), 21) + 0.5
+    w = K
+    rects = [(w, nx - w, w, 2 * w), (w, nx - w, ny - 2 * w, ny - w), (w, 2 * w, 2 * w, ny - 2 * w),
+             (nx - 2 * w, nx - w, 2 * w, ny - 2 * w)]
+    interior = (2 * w, nx - 2 * w, 2 * w, ny - 2 * w)
+    Td, iCpd = T.to(DEV), iCp.to(DEV)
+    outs = []
+    for kn in ("fast5", kern):
+        out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+        tn = ops.StencilTuning(chunk_rows=16, kernel=kn, xcd_remap=1)
+        ops.stencilk_step(K, out, Td, iCpd, coef(), rects, tn)
+        ops.stencilk_step(K, out, Td, iCpd, coef(), [interior], tn)
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
