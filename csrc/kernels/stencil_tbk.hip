@@ -626,7 +626,7 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
     V = (tune.vec == 4 && nx % 4 == 0 && (K <= 8 || tune.kernel == 6 || tune.kernel == 7)) ? 4 : 2;
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   RectList L;
-  if (tune.kernel == 6 || tune.kernel == 7) {  // stage-pipelined fast5: 2 or 4 waves per strip
+  if (tune.kernel >= 6) {  // stage-pipelined fast5: 2 or 4 waves per strip
     const int S = tune.kernel == 6 ? 2 : 4;
     RMA_CHECK_ARG(K == 8 || K == 12 || K == 16,
                   "the stage-pipelined kernels run 8, 12 or 16 steps per pass, got " << K);
