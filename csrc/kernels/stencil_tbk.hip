@@ -1,5 +1,16 @@
-// K explicit-Euler steps per pass (K = 2, 3, 4, 6, 8): deep temporal
-// blocking in registers, overlapped strips, face-flux reuse.
+// K explicit-Euler steps per pass (K = 2, 3, 4, 6, 8; 12, 16 fast-math):
+// deep temporal blocking in registers, overlapped strips.
+//
+// Kernels (StencilTuning::kernel):
+//   0-3  canonical arithmetic, face-flux reuse, bitwise equal to K one-step
+//        launches (1/Cp window in registers or an LDS ring; lane moves by
+//        ds_bpermute or DPP). 3 is the bitwise default.
+//   4    "fast": reassociated fluxes, 7 fp64 ops per cell update.
+//   5    "fast5": 5-point sum with one folded per-cell factor, 5 fp64 ops.
+//   6/7  "fast5p2"/"fast5p4": kernel 5's arithmetic with the K levels of one
+//        strip pipelined over 2 / 4 waves of a block; 4 cells per lane fit,
+//        halving the strip overlap. fast_tune_k picks 7 at K=16, 6 at K=12.
+// The notes below describe the common scheme (written for kernels 0-3).
 //
 // The one-step kernel moves the minimum 24 B/cell of a step at the HBM
 // roofline; the only way to go faster per step is to touch HBM once per K
