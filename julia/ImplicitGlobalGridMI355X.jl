@@ -111,16 +111,18 @@ mutable struct DiffusionExecutor
     T2::Any
 end
 
+# fast_math=true: the K-step passes use the 5-point-sum arithmetic (required
+# for steps_per_pass = 12 or 16; rounding-level difference from the canonical update).
 function DiffusionExecutor(T, T2, iCp, coef::NTuple{4,Float64}; mode::Integer=1,
-                           steps_per_pass::Integer=1, b_width=(1, 1))
+                           steps_per_pass::Integer=1, b_width=(1, 1), fast_math::Bool=false)
     out = Ref{Ptr{Cvoid}}(C_NULL)
     c = collect(coef)
     nx, ny = size(T, 1), size(T, 2)
-    check(ccall(sym(:rma_executor_create_k), Cint,
+    check(ccall(sym(:rma_executor_create_kf), Cint,
                 (Ptr{Cvoid}, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Ptr{Float64},
-                 Int64, Int64, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                 Int64, Int64, Cint, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
                 GRID[], mode, pointer(T), pointer(T2), pointer(iCp), nx, ny, c, b_width[1],
-                b_width[2], steps_per_pass, C_NULL, C_NULL, C_NULL, out))
+                b_width[2], steps_per_pass, Cint(fast_math), C_NULL, C_NULL, C_NULL, out))
     ex = DiffusionExecutor(out[], T, T2)
     finalizer(e -> ccall(sym(:rma_executor_destroy), Cint, (Ptr{Cvoid},), e.ptr), ex)
     return ex

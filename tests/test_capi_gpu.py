@@ -87,6 +87,42 @@ def test_capi_executor_matches_model(mode, K):
     assert np.array_equal(field, G)
 
 
+@pytest.mark.parametrize("mode,K", [(1, 16), (0, 12)])
+def test_capi_fast_math_executor_close(mode, K):
+    """rma_executor_create_kf(fast_math=1): 12 / 16 steps per pass on the
+    fast-math kernels, within rounding of the golden model."""
+    L = lib()
+    nx, ny, nt = 514, 300, 41
+    g = grid(L, nx, ny, K)
+    s = torch.cuda.current_stream().cuda_stream
+    T = torch.from_numpy(golden.initial(nx, ny)).cuda()
+    T2 = T.clone()
+    iCp = torch.ones_like(T)
+    ex = ctypes.c_void_p()
+    ck(L, L.rma_executor_create_kf(g, mode, ctypes.c_void_p(T.data_ptr()),
+                                   ctypes.c_void_p(T2.data_ptr()), ctypes.c_void_p(iCp.data_ptr()),
+                                   ctypes.c_int64(nx), ctypes.c_int64(ny), coef4(L, g, nx, ny),
+                                   ctypes.c_int64(1), ctypes.c_int64(1), K, 1, None, None, None,
+                                   ctypes.byref(ex)))
+    ck(L, L.rma_executor_run(ex, ctypes.c_int64(nt), ctypes.c_void_p(s)))
+    par = L.rma_executor_parity(ex)
+    torch.cuda.synchronize()
+    field = (T2 if par else T).cpu().numpy()
+    ck(L, L.rma_executor_destroy(ex))
+    ck(L, L.rma_finalize_global_grid(g))
+    np.testing.assert_allclose(field, golden.run(nx, ny, nt), rtol=1e-13, atol=1e-13)
+    # without fast_math, 16 steps per pass are refused
+    if K == 16:
+        g = grid(L, nx, ny, K)
+        rc = L.rma_executor_create_kf(g, mode, ctypes.c_void_p(T.data_ptr()),
+                                      ctypes.c_void_p(T2.data_ptr()),
+                                      ctypes.c_void_p(iCp.data_ptr()), ctypes.c_int64(nx),
+                                      ctypes.c_int64(ny), coef4(L, g, nx, ny), ctypes.c_int64(1),
+                                      ctypes.c_int64(1), K, 0, None, None, None, ctypes.byref(ex))
+        assert rc != 0 and b"fast" in L.rma_last_error()
+        ck(L, L.rma_finalize_global_grid(g))
+
+
 def test_capi_update_halo_periodic_and_gather():
     L = lib()
     nx, ny = 130, 67
