@@ -190,6 +190,18 @@ def main(argv=None) -> int:
             canonical = side_teff(kc, False, max(kc, a.single_step_steps // kc * kc))
         single = side_teff(1, False, a.single_step_steps)
 
+    kstep = None  # the K-step kernel the executor runs (csrc/runtime/executor.cpp fast_tune_k)
+    if a.temporal > 1:
+        from rocm_mpi_amd import ops
+        from rocm_mpi_amd._native import native
+
+        if a.fast_math and gpu:
+            kern, kvec, _ = native().fast_kernel_k(a.temporal, ny, tuple(model.coef))
+            kstep = {"kernel": {v: k for k, v in ops.KERNELS.items()}[kern], "vec": kvec,
+                     "chunk_rows": chunk2_main}
+        else:
+            kstep = {"kernel": "canonical", "chunk_rows": chunk2_main}
+
     t_it = wall / a.steps
     teff_gpu = 3 * nx * ny * 8 / 1e9 / t_it
     total = teff_gpu * world
@@ -218,6 +230,7 @@ def main(argv=None) -> int:
             "teff_per_gpu_GBps": round(teff_gpu, 2),
             "a_eff_GB_per_step": round(3 * nx * ny * 8 / 1e9, 6),
             "kernel": a.kernel,
+            "kstep_kernel": kstep,
             "chunk_rows": a.chunk_rows,
             "unroll": a.unroll,
             "vec": a.vec,

@@ -20,9 +20,8 @@ P = os.path.join(ROOT, "profiles")
 
 
 def short(name):
-    n = name.split("(")[0]
-    n = n.replace("rma::(anonymous namespace)::", "").replace("void ", "")
-    return n
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0]
 
 
 def sweep_md(path):
