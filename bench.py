@@ -267,6 +267,11 @@ def main(argv=None) -> int:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
     model.close()
+    if world > 1:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
     return 0 if bad == 0 else 3
 
 
