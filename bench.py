@@ -30,6 +30,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+_TRANSPORT_DESC = {"rccl": "RCCL send/recv over xGMI", "staged": "host-staged copies + gloo",
+                   "self": "single rank, no exchange", "gloo": "gloo (CPU twin)",
+                   "loopback": "in-process loopback"}
+
 METRIC = "T_eff (GB/s) + weak-scaling eff., 2D diffusion 1000 steps at 1/2/4/8 MI355X"
 
 
@@ -223,7 +227,7 @@ def main(argv=None) -> int:
             "global_batch": g.nxyz_g[0] * g.nxyz_g[1],
             "seq_len": None,
             "parallelism": f"2D domain decomposition dims {g.dims[0]}x{g.dims[1]} "
-                           f"(halo: {g.transport} over xGMI"
+                           f"(halo: {_TRANSPORT_DESC.get(g.transport, g.transport)}"
                            + (", boundary/interior overlap)" if a.variant == "perf_hide" else ")"),
             "local_grid": [nx, ny],
             "global_grid": [g.nxyz_g[0], g.nxyz_g[1]],

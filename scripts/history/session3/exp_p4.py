@@ -1,4 +1,7 @@
-"""A/B of fast5p4 experiment bits (RMA_EXP_P) at K=16, interleaved in one process."""
+"""A/B of fast5p4 experiment bits (RMA_EXP_P) at K=16, interleaved in one process.
+
+The RMA_EXP_P hook (stage rotation = 2, stage-0 s_setprio = 4) lived in a scratch
+build of csrc/kernels/stencil_tbk.hip only; results in profiles/pmc_fast5_r1.md."""
 import os, sys, statistics, json
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
 import torch
