@@ -156,3 +156,20 @@ def test_c_abi_topology_and_geometry():
         assert lib.rma_finalize_global_grid(g) == 0
     else:
         assert rc != 0 and b"HIP" in lib.rma_last_error()
+
+
+def test_runme_and_startup_scripts(tmp_path):
+    """scripts/startup.sh (toolchain check, in-tree build, import) and
+    scripts/runme.sh N VARIANT (setenv.sh, launcher, one process per rank) —
+    the counterparts of the reference's startup.sh and scripts/runme.sh."""
+    r = run(["bash", "scripts/startup.sh"], timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ENV setup done" in r.stdout and "native core" in r.stdout and ": OK" in r.stdout
+    r = run(["bash", "scripts/runme.sh", "2", "kp", "--nx", "66", "--ny", "34", "--nt", "30",
+             "--device", "cpu", "--transport", "gloo", "--outdir", str(tmp_path), "--json",
+             "--no-vis"], timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    # the launcher prefixes every line with "[rank] "
+    rec = json.loads([l.split("] ", 1)[1] for l in r.stdout.splitlines()
+                      if l.startswith("[0] {")][-1])
+    assert rec["variant"] == "kp" and rec["nprocs"] == 2 and rec["nxg"] == 2 * (66 - 2) + 2
