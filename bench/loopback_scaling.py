@@ -24,7 +24,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(N: int, n: int, K: int, steps: int, variant: str) -> dict:
+def run(N: int, n: int, K: int, steps: int, variant: str, fast: bool = False) -> dict:
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
@@ -42,7 +42,8 @@ def run(N: int, n: int, K: int, steps: int, variant: str) -> dict:
             gg.init_global_grid(n, n, 1, overlaps=(ol, ol, 2), halowidths=(K, K, 1), quiet=True,
                                 loopback=(hub, r))
             m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=n, nt=steps, quiet=True,
-                                            init="random", temporal=K))
+                                            init="random", temporal=K,
+                                            fast_math=K > 1 and (fast or K > 8)))
             m.step(2 * K)
             m.synchronize()
             go.wait()
@@ -68,6 +69,7 @@ def run(N: int, n: int, K: int, steps: int, variant: str) -> dict:
     agg = N * 3 * n * n * 8 / 1e9 / (wall / steps)
     torch.cuda.empty_cache()
     return {"ranks": N, "dims": list(out[0][1]), "tile": n, "temporal": K, "steps": steps,
+            "fast_math": K > 1 and (fast or K > 8),
             "ms_per_step": wall / steps * 1e3, "aggregate_teff_GBps": agg}
 
 
@@ -78,13 +80,15 @@ def main(argv=None) -> int:
     ap.add_argument("--temporal", default="1,8")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--variant", default="perf_hide")
+    ap.add_argument("--fast-math", action="store_true",
+                    help="fast-math K-step passes (always on for K = 12, 16)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     rows = []
     for K in [int(v) for v in a.temporal.split(",")]:
         base = None
         for N in [int(v) for v in a.ranks.split(",")]:
-            r = run(N, a.n, K, a.steps, a.variant)
+            r = run(N, a.n, K, a.steps, a.variant, a.fast_math)
             base = base or r["aggregate_teff_GBps"]
             r["fraction_of_1_rank"] = r["aggregate_teff_GBps"] / base
             rows.append(r)
