@@ -487,28 +487,33 @@ __device__ __forceinline__ void stencilk5p_body(
   for (int t = threadIdx.x; t < R * W; t += S * kWave) ring[t] = 0.0;
   for (int t = threadIdx.x; t < 2 * (S > 1 ? S - 1 : 1) * W; t += S * kWave) (&hand[0][0][0])[t] = 0.0;
   __syncthreads();
-  auto rd2 = [&](const double* src, double (&out)[V]) {
+  // LDS rows (ring and hand-off) are lane-interleaved: cell pair h of lane l
+  // sits at dbl2 index h * 64 + l, so each ds_read/write_b128 covers 1 KiB
+  // contiguously. The lane-major layout (lane l at l * V) strode 32 B per lane
+  // at V = 4, a 2-way bank conflict on every access (SQ_LDS_BANK_CONFLICT =
+  // half of SQ_LDS_IDX_ACTIVE, profiles/pmc_fast5_r1.md).
+  auto rd2 = [&](const double* row, double (&out)[V]) {
     if constexpr (V == 1) {
-      out[0] = src[0];
+      out[0] = row[lane];
     } else {
 #pragma unroll
       for (int h = 0; h < V / 2; ++h) {
-        const dbl2 t2 = reinterpret_cast<const dbl2*>(src)[h];
+        const dbl2 t2 = reinterpret_cast<const dbl2*>(row)[h * kWave + lane];
         out[2 * h] = t2.x;
         out[2 * h + 1] = t2.y;
       }
     }
   };
-  auto wr2 = [&](double* dst, const double (&in)[V]) {
+  auto wr2 = [&](double* row, const double (&in)[V]) {
     if constexpr (V == 1) {
-      dst[0] = in[0];
+      row[lane] = in[0];
     } else {
 #pragma unroll
       for (int h = 0; h < V / 2; ++h) {
         dbl2 t2;
         t2.x = in[2 * h];
         t2.y = in[2 * h + 1];
-        reinterpret_cast<dbl2*>(dst)[h] = t2;
+        reinterpret_cast<dbl2*>(row)[h * kWave + lane] = t2;
       }
     }
   };
@@ -525,7 +530,7 @@ __device__ __forceinline__ void stencilk5p_body(
       double g[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? gs * pC[v] : 0.0;
-      wr2(ring + slot0 * W + lane * V, g);
+      wr2(ring + slot0 * W, g);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         pT[v] = qT[v];
@@ -534,7 +539,7 @@ __device__ __forceinline__ void stencilk5p_body(
       load_row<V>(qT, T + rowc(i + 3) * nx + xl);
       load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
     } else {
-      rd2(&hand[par ^ 1][stage - 1][lane * V], w[0][P]);
+      rd2(&hand[par ^ 1][stage - 1][0], w[0][P]);
     }
     // this stage's level-1 row is i - lag: its ring slot
     int sbase = slot0 - lag;
@@ -545,7 +550,7 @@ __device__ __forceinline__ void stencilk5p_body(
       double gl[V];
       {
         const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
-        rd2(ring + sl * W + lane * V, gl);
+        rd2(ring + sl * W, gl);
       }
       const double(&up)[V] = w[j - 1][PU];
       const double(&c)[V] = w[j - 1][PC];
@@ -566,7 +571,7 @@ __device__ __forceinline__ void stencilk5p_body(
 #pragma unroll
         for (int v = 0; v < V; ++v) w[jj][P][v] = res[v];
       } else if (stage < S - 1) {
-        wr2(&hand[par][stage][lane * V], res);
+        wr2(&hand[par][stage][0], res);
       } else if (row >= ya && row < yb) {
         store_row<V, NT>(T2 + row * nx + x, res, m);
       }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One-GPU validation + measurement pass (run on the GPU box, e.g.
 #   gpurun --timeout 1200 -- bash scripts/gpu_check.sh):
-# GPU test suite, smoke(), default bench (8 steps/pass at the 288 GB tile, also
+# GPU test suite, smoke(), default bench (16 fast-math steps/pass at the 288 GB tile, also
 # reporting the one-step kernel), the BASELINE presets that fit one GPU, and a
 # rocprofv3 kernel trace of a short bench. Every GPU step has its own time
 # limit; the script stops at the first failure, fault or timeout.

@@ -226,6 +226,37 @@ def test_pipelined_fast5_equals_fast5_bitwise(K, kern, ny, nx, chunk, xcd, vec):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("K,kern,vec", [(16, "fast5p4", 4), (8, "lds_dpp", 2)])
+def test_k_step_int64_indexing(K, kern, vec):
+    """K-step kernels on a tile beyond 2^31 cells (64-bit row offsets, as at the
+    288 GB bench tile): the last rows of the big tile equal the same kernel run
+    on a small copy of those rows (a K-step result depends on K rows around it,
+    so rows >= K away from the copy's top edge agree bitwise)."""
+    free, _ = torch.cuda.mem_get_info()
+    ny, nx = 33000, 65536  # 2.16e9 cells, 17.3 GB per array
+    if free < 3 * ny * nx * 8 * 1.1:
+        pytest.skip("not enough HBM")
+    T = torch.empty((ny, nx), dtype=torch.float64, device=DEV)
+    ops.init_random_(T, ops.TileGeometry(0, 0, nx, ny, 1.0, 1.0), seed=5)
+    iCp = torch.empty_like(T)
+    ops.init_random_(iCp, ops.TileGeometry(0, 0, nx, ny, 1.0, 1.0), seed=6)
+    iCp.add_(0.5)
+    out = torch.zeros_like(T)
+    tn = ops.StencilTuning(chunk_rows=16, kernel=kern, xcd_remap=1, vec=vec)
+    rows = 40
+    ops.stencilk_step(K, out, T, iCp, coef(), [(1, nx - 1, ny - rows, ny - 1)], tn)
+    got = out[ny - rows:ny - 1].cpu()
+    del out
+    h = rows + 2 * K  # the copy: K + rows + K rows, the last one the fixed boundary row
+    Ts, Cs = T[ny - h:].clone(), iCp[ny - h:].clone()
+    del T, iCp
+    small = torch.zeros_like(Ts)
+    ops.stencilk_step(K, small, Ts, Cs, coef(), [(1, nx - 1, h - rows, h - 1)], tn)
+    assert torch.equal(got, small[h - rows:h - 1].cpu())
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("kern", ["fast5p2", "fast5p4"])
 def test_pipelined_fast5_rect_lists(kern):
     K, ny, nx = 16, 203, 900
