@@ -557,15 +557,26 @@ __device__ __forceinline__ void stencilk5p_body(
       const double(&dn)[V] = w[j - 1][P];
       const double rn = from_next_lane<true>(c[0]);
       const double ln = from_prev_lane<true>(c[V - 1]);
-      double res[V];
+      // the V cells' operation chains issued interleaved (sched_barrier keeps
+      // the compiler from serialising each cell's dependent FMA chain):
+      // 64.6 -> 64.2 ms per K=16 pass at 101376^2, same operations, bitwise
+      double res[V], sx[V], sy[V], t[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const double rv = v + 1 < V ? c[v + 1] : rn;
         const double lv = v > 0 ? c[v - 1] : ln;
-        const double sx = rv + lv;
-        const double sy = up[v] + dn[v];
-        res[v] = __builtin_fma(gl[v], __builtin_fma(ry, sy, __builtin_fma(mkc, c[v], sx)), c[v]);
+        sx[v] = rv + lv;
+        sy[v] = up[v] + dn[v];
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int v = 0; v < V; ++v) t[v] = __builtin_fma(mkc, c[v], sx[v]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, sy[v], t[v]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int v = 0; v < V; ++v) res[v] = __builtin_fma(gl[v], t[v], c[v]);
       if (j < H) {
         const int jj = j < H ? j : H - 1;
 #pragma unroll

@@ -24,7 +24,11 @@ res = {v: [] for v in variants}
 ref = None
 for r in range(rounds):
     for v in variants:
-        os.environ["RMA_EXP_P"] = v
+        if "=" in v:  # NAME=VALUE: an environment switch of a scratch build
+            name, val = v.split("=", 1)
+            os.environ[name] = val
+        else:
+            os.environ["RMA_EXP_P"] = v
         ops.stencilk_step(K, T2, T, iCp, c, tuning=tn)
         torch.cuda.synchronize()
         if r == 0:
