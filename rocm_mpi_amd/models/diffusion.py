@@ -59,6 +59,8 @@ def default_chunk2(K: int, ny: int) -> int:
             return c
     if ny < 32768:
         return 128 if K == 8 else 256
+    if K == 16 and ny >= 98304:
+        return 1536
     return 1024 if K >= 8 else 512
 
 
