@@ -82,3 +82,25 @@ def diffusion_tiles(rank, world, outdir, variant, nx, ny, nt, dims, temporal, de
         f.write(f"{g.coords[0]} {g.coords[1]} {g.nxyz_g[0]} {g.nxyz_g[1]} {g.overlaps[0]} "
                 f"{g.overlaps[1]} {g.transport}")
     m.close()
+
+
+def node_local(rank, world, outdir, ranks_per_node):
+    """Fake multi-node placement: no LOCAL_RANK / LOCAL_WORLD_SIZE in the
+    environment, a per-'node' hostname instead (MPI.Comm_split_type analogue,
+    SURVEY.md §4.5); the global grid's device choice follows the local rank."""
+    for k in ("LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        os.environ.pop(k, None)
+    os.environ["RMA_HOSTNAME"] = f"node{rank // ranks_per_node}"
+    from rocm_mpi_amd.parallel import comm as C
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    C.init_distributed("gloo")
+    local, lsize = C.node_local_rank(rank, world)
+    gg.init_global_grid(8, 8, 1, quiet=True, device="cpu", init_dist=False)
+    g = gg.global_grid()
+    np.save(os.path.join(outdir, f"local{rank}.npy"),
+            np.array([local, lsize, g.local_rank, g.local_size]))
+    gg.finalize_global_grid()
+    import torch.distributed as dist
+
+    dist.destroy_process_group()

@@ -101,3 +101,12 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     assert c["global_grid"] == [dims[0] * (nx - 2 * K) + 2 * K, dims[1] * (nx - 2 * K) + 2 * K]
     assert abs(d["value"] - world * c["teff_per_gpu_GBps"]) <= 1e-6 * d["value"] + 0.02
     assert c["nonfinite_cells_sampled"] == 0
+
+
+def test_node_local_rank_from_hostnames(tmp_path):
+    """4 ranks on 2 fake nodes (hostname exchange, no LOCAL_RANK): local ranks
+    restart at 0 on every node — the reference's smoke test instead took the
+    local rank modulo the GLOBAL size (rocmaware_test_selectdevice.jl:12-13)."""
+    run_procs(4, "mp_targets:node_local", str(tmp_path), 2)
+    got = [np.load(tmp_path / f"local{r}.npy").tolist() for r in range(4)]
+    assert got == [[0, 2, 0, 2], [1, 2, 1, 2], [0, 2, 0, 2], [1, 2, 1, 2]]
