@@ -9,7 +9,6 @@ configurations as named presets (``--preset``).
 from __future__ import annotations
 
 import argparse
-import json
 import math
 import os
 import sys

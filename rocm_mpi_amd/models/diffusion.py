@@ -25,10 +25,7 @@ loopback transports) the same steps are issued from Python.
 """
 from __future__ import annotations
 
-import math
-import os
-import time
-from dataclasses import asdict, dataclass, field
+from dataclasses import dataclass
 
 import numpy as np
 import torch

@@ -6,7 +6,6 @@ import os, sys, statistics, json
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
 import torch
 from rocm_mpi_amd import ops
-from rocm_mpi_amd._native import native
 
 n = int(os.environ.get("N", "101376")); K = int(os.environ.get("K", "16"))
 variants = os.environ.get("VARIANTS", "0,2,4,6").split(",")

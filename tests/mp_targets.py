@@ -2,7 +2,6 @@
 import os
 
 import numpy as np
-import torch
 
 
 def diffusion(rank, world, outdir, variant, nx, ny, nt, dims, transport="gloo", init="gaussian"):

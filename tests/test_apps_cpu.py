@@ -4,16 +4,12 @@ import json
 import os
 import subprocess
 import sys
-import zlib
 
-import numpy as np
 import pytest
 import torch
 
-import golden
-from helpers import ROOT, run_loopback
+from helpers import ROOT
 from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
-from rocm_mpi_amd.parallel import implicit_grid as gg
 from rocm_mpi_amd.utils import checkpoint, vis
 
 

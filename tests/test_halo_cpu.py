@@ -5,7 +5,6 @@ halo planes that face a neighbour, update_halo_ must restore exactly the
 global values — for 1-D/2-D/3-D fields, several fields per call, staggered
 fields (size n+-1), halowidth 2 (overlap 4) and periodic dimensions.
 """
-import itertools
 
 import pytest
 import torch
