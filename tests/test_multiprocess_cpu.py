@@ -110,3 +110,12 @@ def test_node_local_rank_from_hostnames(tmp_path):
     run_procs(4, "mp_targets:node_local", str(tmp_path), 2)
     got = [np.load(tmp_path / f"local{r}.npy").tolist() for r in range(4)]
     assert got == [[0, 2, 0, 2], [1, 2, 1, 2], [0, 2, 0, 2], [1, 2, 1, 2]]
+
+
+def test_slurm_style_environment(tmp_path):
+    """Ranks that only see SLURM_PROCID / SLURM_NTASKS / SLURM_LOCALID (srun)
+    bootstrap the grid: world from SLURM, node-local ranks from the hostname
+    exchange, rendezvous on the default loopback address."""
+    run_procs(2, "mp_targets:slurm_env", str(tmp_path))
+    got = [np.load(tmp_path / f"slurm{r}.npy").tolist() for r in range(2)]
+    assert got == [[0, 2, 0, 2, 1.0], [1, 2, 1, 2, 1.0]]
