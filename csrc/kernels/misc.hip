@@ -99,6 +99,15 @@ template <typename E>
 __global__ void copy2d_kernel(E* __restrict__ dst, int64_t dst_ld, const E* __restrict__ src,
                               int64_t src_ld, int64_t n_o, int64_t n_k) {
   const int64_t n = n_o * n_k;
+  if (n < (int64_t(1) << 31)) {  // 32-bit index split (a 64-bit division is a long sequence)
+    const unsigned nk = (unsigned)n_k;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n;
+         i += gridDim.x * blockDim.x) {
+      const unsigned o = i / nk, k = i - o * nk;
+      dst[(int64_t)o * dst_ld + k] = src[(int64_t)o * src_ld + k];
+    }
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t o = i / n_k, k = i - o * n_k;
@@ -280,6 +289,15 @@ void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int6
                 int64_t n_k, int elem_bytes, stream_t stream) {
   if (n_o <= 0 || n_k <= 0) return;
   RMA_CHECK_ARG(dst_ld >= n_k && src_ld >= n_k, "leading dims smaller than row length");
+  // 8-byte planes with even rows and 16-B aligned rows move as 16-byte
+  // elements (a width-K halo of fp64: K/2 dwordx4 per row instead of K dwords)
+  if (elem_bytes == 8 && n_k % 2 == 0 && dst_ld % 2 == 0 && src_ld % 2 == 0 &&
+      ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+    elem_bytes = 16;
+    n_k /= 2;
+    dst_ld /= 2;
+    src_ld /= 2;
+  }
   const unsigned g = grid_stride_blocks(n_o * n_k, 256);
   hipStream_t s = as_stream(stream);
   switch (elem_bytes) {

@@ -153,6 +153,21 @@ def test_copy_plane_strided(elem):
     assert float(B[:, :50].abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("c0,w", [(2, 4), (3, 4), (16, 16), (2, 3)])
+def test_copy_plane_fp64_wide_rows(c0, w):
+    """fp64 planes with even rows, even leading dims and 16-B aligned rows are
+    moved as 16-byte elements (width-K halos); the others element by element."""
+    A = rand((41, 54), 10).to(DEV)
+    col = A[:, c0:c0 + w]
+    buf = torch.empty((41, w), dtype=torch.float64, device=DEV)
+    ops.copy_plane(buf, col)
+    assert torch.equal(buf, col)
+    B = torch.zeros_like(A)
+    ops.copy_plane(B[:, 30:30 + w], buf)
+    assert torch.equal(B[:, 30:30 + w], col)
+    assert float(B[:, :30].abs().sum()) == 0.0 and float(B[:, 30 + w:].abs().sum()) == 0.0
+
+
 @pytest.mark.parametrize("op", ["sum", "max", "min", "maxabs", "nonfinite"])
 def test_reduce(op):
     A = rand((513, 257), 9) - 0.5
