@@ -155,6 +155,27 @@ def test_rccl_self_send_periodic(graph):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("K,fast,nt", [(16, True, 37), (8, False, 19)])
+def test_rccl_self_send_periodic_kstep(K, fast, nt):
+    """The bench's multi-rank message pattern through RCCL on one GPU: a
+    periodic single rank with width-K halos (overlap 2K) sends its packed
+    x-planes and contiguous y-planes to itself through RCCL send/recv once per
+    K-step pass (plus the remainder pass) == the local self-copy path."""
+    outs = []
+    for via in (True, False):
+        gg.init_global_grid(600, 300, 1, periodx=1, periody=1, quiet=True, transport="rccl",
+                            overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
+                            self_via_transport=via)
+        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=600, ny=300, nt=nt, quiet=True,
+                                        init="random", periods=(1, 1, 0), temporal=K,
+                                        fast_math=fast))
+        m.step(nt)
+        outs.append(m.field.cpu().clone())
+        m.close()
+        gg.finalize_global_grid()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("blocking", [False, True])
 def test_rccl_single_rank_collectives(blocking, monkeypatch):
     """Non-blocking init (default: ncclCommInitRankConfig blocking=0 + polled
