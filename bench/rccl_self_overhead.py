@@ -1,0 +1,84 @@
+#!/usr/bin/env python
+"""Multi-rank halo-path overhead with REAL RCCL traffic on one GPU.
+
+RCCL refuses two ranks on one GPU, so the 2-8 GPU weak-scaling run is the
+driver's. This probe runs the production configuration on one MI355X twice:
+  * open boundaries (no neighbour: one launch per K-step pass), and
+  * periodic in x and y with every halo plane routed through RCCL send/recv to
+    self (4 neighbours: frame kernel + x-plane pack/unpack + 4 RCCL messages of
+    K rows/columns per pass, overlapped with the interior on the low-priority
+    stream) -- the message pattern of an interior rank of the 4x2 grid.
+The ratio of the two step times bounds what the distributed path costs per
+rank (xGMI wire time aside: self messages stay on the GPU).
+
+    python bench/rccl_self_overhead.py [--n 0 (auto: 288 GB tile)] [--steps 320]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(n: int, K: int, steps: int, periodic: bool) -> float:
+    import torch
+
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    p = 1 if periodic else 0
+    gg.init_global_grid(n, n, 1, periodx=p, periody=p, quiet=True, transport="rccl",
+                        overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
+                        self_via_transport=periodic)
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=n, ny=n, nt=steps, quiet=True,
+                                    init="random", periods=(p, p, 0), temporal=K,
+                                    fast_math=K > 8))
+    m.step(2 * K)
+    m.synchronize()
+    t0 = time.perf_counter()
+    m.step(steps)
+    m.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    m.close()
+    gg.finalize_global_grid()
+    torch.cuda.empty_cache()
+    return dt
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=0, help="tile edge (0: 80%% of free HBM)")
+    ap.add_argument("--K", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=320)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+    import torch
+
+    n = a.n
+    if not n:
+        free, _ = torch.cuda.mem_get_info()
+        n = int(math.isqrt(int(0.8 * free / 24))) // 256 * 256
+    rows = []
+    for periodic in (False, True, False, True):
+        dt = run(n, a.K, a.steps, periodic)
+        rows.append({"periodic_rccl_self": periodic, "ms_per_step": dt * 1e3,
+                     "teff_GBps": 3 * n * n * 8 / 1e9 / dt})
+        print(json.dumps(rows[-1]), flush=True)
+    op = [r["ms_per_step"] for r in rows if not r["periodic_rccl_self"]]
+    pe = [r["ms_per_step"] for r in rows if r["periodic_rccl_self"]]
+    out = {"tile": n, "K": a.K, "steps": a.steps, "runs": rows,
+           "overhead": min(pe) / min(op) - 1.0}
+    print(json.dumps(out), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
