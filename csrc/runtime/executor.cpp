@@ -263,8 +263,13 @@ void DiffusionExecutor::enqueue_step2(double* Tin, double* Tout) {
   TraceRange tr("rma.stepK.hide");
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+  // frame tuning: the x-frames are ~2K columns wide, so the narrowest strip
+  // (2 cells per lane: 128 columns) wastes the least recomputation, and the
+  // interior's long row chunks keep the launch small; the frame still ends
+  // long before the interior (1.6 of ~64 ms per pass at the 288 GB tile)
   StencilTuning ft = p_.tune2;
   ft.chunk_rows = std::min(ft.chunk_rows, 64);
+  if (ft.kernel >= 6) ft.vec = std::min(ft.vec, 2);
   {
     TraceRange tb("rma.boundary");
     multi_step(Tin, Tout, frame2_.data(), (int)frame2_.size(), ft, s_hi_);
