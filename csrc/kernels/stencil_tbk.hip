@@ -520,10 +520,11 @@ __device__ __forceinline__ void stencilk5p_body(
   int slot0 = 0;  // ring slot of row i (stage 0's level-1 row)
   int par = 0;
   const int lag = stage * (H + 1);  // rows behind stage 0
-  auto iter = [&](auto Pc) {
+  auto iter = [&](auto Pc, auto S0c) {
     constexpr int P = decltype(Pc)::value;
+    constexpr bool S0 = decltype(S0c)::value;
     constexpr int PC = (P + 2) % 3, PU = (P + 1) % 3;
-    if (stage == 0) {
+    if constexpr (S0) {
       const bool rin1 = i >= 1 && i <= ny - 2;
 #pragma unroll
       for (int v = 0; v < V; ++v) w[0][P][v] = pT[v];
@@ -542,11 +543,11 @@ __device__ __forceinline__ void stencilk5p_body(
       rd2(&hand[par ^ 1][stage - 1][0], w[0][P]);
     }
     // this stage's level-1 row is i - lag: its ring slot
-    int sbase = slot0 - lag;
+    int sbase = slot0 - (S0 ? 0 : lag);
     sbase = sbase < 0 ? sbase + R : sbase;
 #pragma unroll
     for (int j = 1; j <= H; ++j) {
-      const int64_t row = i - lag - (j - 1);
+      const int64_t row = i - (S0 ? 0 : lag) - (j - 1);
       double gl[V];
       {
         const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
@@ -581,8 +582,8 @@ __device__ __forceinline__ void stencilk5p_body(
         const int jj = j < H ? j : H - 1;
 #pragma unroll
         for (int v = 0; v < V; ++v) w[jj][P][v] = res[v];
-      } else if (stage < S - 1) {
-        wr2(&hand[par][stage][0], res);
+      } else if (S0 ? S > 1 : stage < S - 1) {
+        wr2(&hand[par][S0 ? 0 : stage][0], res);
       } else if (row >= ya && row < yb) {
         store_row<V, NT>(T2 + row * nx + x, res, m);
       }
@@ -591,14 +592,25 @@ __device__ __forceinline__ void stencilk5p_body(
     par ^= 1;
     __syncthreads();  // hand-off rows and ring row visible; this iteration's reads done
   };
-  for (;;) {
-    iter(std::integral_constant<int, 0>{});
-    if (++i > iend) break;
-    iter(std::integral_constant<int, 1>{});
-    if (++i > iend) break;
-    iter(std::integral_constant<int, 2>{});
-    if (++i > iend) break;
-  }
+  // stage 0 and the other stages run separate copies of the row loop (the
+  // stage is wave-uniform; both copies pass the same barriers). In one shared
+  // loop the merge after the stage branch made every stage carry stage 0's
+  // prefetch registers: 16 v_mov_b64 per row iteration on stages 1..S-1
+  // (1 per cell update, ~11 % of their VALU instructions)
+  auto run = [&](auto S0c) {
+    for (;;) {
+      iter(std::integral_constant<int, 0>{}, S0c);
+      if (++i > iend) break;
+      iter(std::integral_constant<int, 1>{}, S0c);
+      if (++i > iend) break;
+      iter(std::integral_constant<int, 2>{}, S0c);
+      if (++i > iend) break;
+    }
+  };
+  if (stage == 0)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
 }
 
 template <int K, int S, int V, bool NT>
