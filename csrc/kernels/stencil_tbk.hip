@@ -524,11 +524,11 @@ __device__ __forceinline__ void stencilk5p_body(
     constexpr int P = decltype(Pc)::value;
     constexpr bool S0 = decltype(S0c)::value;
     constexpr int PC = (P + 2) % 3, PU = (P + 1) % 3;
+    double g[V];  // stage 0: the new ring row (its level-1 factors)
     if constexpr (S0) {
       const bool rin1 = i >= 1 && i <= ny - 2;
 #pragma unroll
       for (int v = 0; v < V; ++v) w[0][P][v] = pT[v];
-      double g[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? gs * pC[v] : 0.0;
       wr2(ring + slot0 * W, g);
@@ -545,14 +545,27 @@ __device__ __forceinline__ void stencilk5p_body(
     // this stage's level-1 row is i - lag: its ring slot
     int sbase = slot0 - (S0 ? 0 : lag);
     sbase = sbase < 0 ? sbase + R : sbase;
+    auto ring_row = [&](int j) {  // ring row of local level j
+      const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
+      return ring + sl * W;
+    };
+    // level factors read one level ahead, so the LDS latency of level j + 1's
+    // read hides under level j's arithmetic; stage 0's level-1 factors are the
+    // row it just wrote (still in registers)
+    double gn[V];
+    if constexpr (S0) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) gn[v] = g[v];
+    } else {
+      rd2(ring_row(1), gn);
+    }
 #pragma unroll
     for (int j = 1; j <= H; ++j) {
       const int64_t row = i - (S0 ? 0 : lag) - (j - 1);
       double gl[V];
-      {
-        const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
-        rd2(ring + sl * W, gl);
-      }
+#pragma unroll
+      for (int v = 0; v < V; ++v) gl[v] = gn[v];
+      if (j < H) rd2(ring_row(j + 1), gn);
       const double(&up)[V] = w[j - 1][PU];
       const double(&c)[V] = w[j - 1][PC];
       const double(&dn)[V] = w[j - 1][P];
@@ -613,8 +626,10 @@ __device__ __forceinline__ void stencilk5p_body(
     run(std::false_type{});
 }
 
+// 3 waves per SIMD: the 51.2 KB LDS of a K=16, S=4 block allows 3 blocks per
+// CU, so the VGPR budget is 168 (512 / 3, 8-register granules)
 template <int K, int S, int V, bool NT>
-__global__ __launch_bounds__(kWave * S) void stencilk5p_kernel(
+__global__ __launch_bounds__(kWave * S) __attribute__((amdgpu_waves_per_eu(S == 4 ? 3 : 1))) void stencilk5p_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
     int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
   stencilk5p_body<K, S, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
