@@ -456,6 +456,8 @@ __device__ __forceinline__ void stencilk5p_body(
     cin[v] = (x + v >= 1) && (x + v <= nx - 2);
   }
   const int64_t xl = min(max(x, (int64_t)0), nx - V);
+  // every cell of the strip inside the x range 1..nx-2 (so every cin is true)
+  const bool xin = xs >= 1 && xs + W - 1 <= nx - 2;
 
   const double ax = (-k.mlam) * k.rdx * k.rdx;
   const double ay = (-k.mlam) * k.rdy * k.rdy;
@@ -529,8 +531,15 @@ __device__ __forceinline__ void stencilk5p_body(
       const bool rin1 = i >= 1 && i <= ny - 2;
 #pragma unroll
       for (int v = 0; v < V; ++v) w[0][P][v] = pT[v];
+      // rin1 and xin are wave-uniform: strips away from the x edges take a
+      // branch without the per-cell selects (2 v_cndmask_b32 per cell)
+      if (rin1 && xin) {
 #pragma unroll
-      for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? gs * pC[v] : 0.0;
+        for (int v = 0; v < V; ++v) g[v] = gs * pC[v];
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? gs * pC[v] : 0.0;
+      }
       wr2(ring + slot0 * W, g);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
