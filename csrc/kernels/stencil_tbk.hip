@@ -474,9 +474,13 @@ __device__ __forceinline__ void stencilk5p_body(
     for (int t = 0; t < 3; ++t)
 #pragma unroll
       for (int v = 0; v < V; ++v) w[j][t][v] = 0.0;
-  int64_t i = ya - K;
-  const int64_t iend = yb + K - 3 + S;
-  auto rowc = [&](int64_t y) { return min(max(y, (int64_t)0), ny - 1); };
+  // row bookkeeping in 32 bits (the host checks ny < 2^31): gfx950 has no
+  // 64-bit scalar compares, so int64 row tests became VALU v_cmp_*_i64 +
+  // v_mov_b64 copies on every row iteration
+  const int ny32 = (int)ny, ya32 = (int)ya, yb32 = (int)yb;
+  int i = ya32 - K;
+  const int iend = yb32 + K - 3 + S;
+  auto rowc = [&](int y) { return (int64_t)min(max(y, 0), ny32 - 1); };
   if (stage == 0) {
     load_row<V>(w[0][2], T + rowc(i) * nx + xl);
     load_row<V>(pT, T + rowc(i + 1) * nx + xl);
@@ -528,7 +532,7 @@ __device__ __forceinline__ void stencilk5p_body(
     constexpr int PC = (P + 2) % 3, PU = (P + 1) % 3;
     double g[V];  // stage 0: the new ring row (its level-1 factors)
     if constexpr (S0) {
-      const bool rin1 = i >= 1 && i <= ny - 2;
+      const bool rin1 = i >= 1 && i <= ny32 - 2;
 #pragma unroll
       for (int v = 0; v < V; ++v) w[0][P][v] = pT[v];
       // rin1 and xin are wave-uniform: strips away from the x edges take a
@@ -570,7 +574,7 @@ __device__ __forceinline__ void stencilk5p_body(
     }
 #pragma unroll
     for (int j = 1; j <= H; ++j) {
-      const int64_t row = i - (S0 ? 0 : lag) - (j - 1);
+      const int row = i - (S0 ? 0 : lag) - (j - 1);
       double gl[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) gl[v] = gn[v];
@@ -606,8 +610,8 @@ __device__ __forceinline__ void stencilk5p_body(
         for (int v = 0; v < V; ++v) w[jj][P][v] = res[v];
       } else if (S0 ? S > 1 : stage < S - 1) {
         wr2(&hand[par][S0 ? 0 : stage][0], res);
-      } else if (row >= ya && row < yb) {
-        store_row<V, NT>(T2 + row * nx + x, res, m);
+      } else if (row >= ya32 && row < yb32) {
+        store_row<V, NT>(T2 + (int64_t)row * nx + x, res, m);
       }
     }
     slot0 = slot0 + 1 == R ? 0 : slot0 + 1;
@@ -691,6 +695,7 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
   RectList L;
   if (tune.kernel >= 6) {  // stage-pipelined fast5: 2 or 4 waves per strip
     const int S = tune.kernel == 6 ? 2 : 4;
+    RMA_CHECK_ARG(ny < (int64_t(1) << 30), "the stage-pipelined kernels index rows in 32 bits, ny = " << ny);
     RMA_CHECK_ARG(K == 8 || K == 12 || K == 16,
                   "the stage-pipelined kernels run 8, 12 or 16 steps per pass, got " << K);
     const int64_t ntask = plan_strip_tasks(L, rects, nrects, V, tune.chunk_rows, K);
