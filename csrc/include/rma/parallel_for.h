@@ -5,16 +5,31 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <system_error>
 #include <thread>
 #include <vector>
 
 namespace rma {
 
+// Worker count: hardware threads, capped at 16 and at OMP_NUM_THREADS /
+// RMA_NUM_THREADS when set (several ranks share one host in the CPU tests).
+inline int64_t host_threads() {
+  int64_t nt = std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  for (const char* var : {"RMA_NUM_THREADS", "OMP_NUM_THREADS"}) {
+    if (const char* s = std::getenv(var)) {
+      const long v = std::strtol(s, nullptr, 10);
+      if (v > 0) return std::min<int64_t>(nt, v);
+    }
+  }
+  return nt;
+}
+
 template <typename F>
 void parallel_for(int64_t begin, int64_t end, int64_t min_chunk, F&& f) {
   const int64_t n = end - begin;
   if (n <= 0) return;
-  int64_t nt = std::max<int64_t>(1, std::min<int64_t>(std::thread::hardware_concurrency(), 16));
+  int64_t nt = host_threads();
   nt = std::min(nt, std::max<int64_t>(1, n / std::max<int64_t>(1, min_chunk)));
   if (nt <= 1) {
     for (int64_t i = begin; i < end; ++i) f(i);
@@ -22,11 +37,20 @@ void parallel_for(int64_t begin, int64_t end, int64_t min_chunk, F&& f) {
   }
   std::vector<std::thread> th;
   th.reserve(nt);
-  for (int64_t t = 0; t < nt; ++t) {
+  int64_t t = 0;
+  for (; t < nt; ++t) {
     const int64_t a = begin + n * t / nt, b = begin + n * (t + 1) / nt;
-    th.emplace_back([a, b, &f] {
-      for (int64_t i = a; i < b; ++i) f(i);
-    });
+    try {
+      th.emplace_back([a, b, &f] {
+        for (int64_t i = a; i < b; ++i) f(i);
+      });
+    } catch (const std::system_error&) {
+      break;  // out of threads (loaded host): the caller runs the rest itself
+    }
+  }
+  for (; t < nt; ++t) {
+    const int64_t a = begin + n * t / nt, b = begin + n * (t + 1) / nt;
+    for (int64_t i = a; i < b; ++i) f(i);
   }
   for (auto& x : th) x.join();
 }
