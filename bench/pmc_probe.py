@@ -32,7 +32,7 @@ if which == "fast":  # fast-math K-step kernels at the executor's tuning (bench 
     K = int(os.environ.get("RMA_PROBE_K", "8"))
     ch = nat.default_chunk_k(K, n)
     for kern in os.environ.get("RMA_PROBE_KERNELS", "fast,fast5").split(","):
-        vec = 4 if kern in ("fast5p2", "fast5p4") else 2
+        vec = 4 if kern in ("fast5p2", "fast5p4", "fast5p8") else 2
         for _ in range(reps):
             ops.stencilk_step(K, T2, T, iCp, c, tuning=ops.StencilTuning(chunk_rows=ch, xcd_remap=1,
                                                                         kernel=kern, vec=vec))

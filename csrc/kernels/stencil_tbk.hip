@@ -642,7 +642,7 @@ __device__ __forceinline__ void stencilk5p_body(
 // 3 waves per SIMD: the 51.2 KB LDS of a K=16, S=4 block allows 3 blocks per
 // CU, so the VGPR budget is 168 (512 / 3, 8-register granules)
 template <int K, int S, int V, bool NT>
-__global__ __launch_bounds__(kWave * S) __attribute__((amdgpu_waves_per_eu(S == 4 ? 3 : 1))) void stencilk5p_kernel(
+__global__ __launch_bounds__(kWave * S) __attribute__((amdgpu_waves_per_eu(S == 8 ? 4 : S == 4 ? 3 : 1))) void stencilk5p_kernel(
     double* __restrict__ T2, const double* __restrict__ T, const double* __restrict__ iCp,
     int64_t nx, int64_t ny, RectList L, StencilCoef k, int chunk_rows, int remap) {
   stencilk5p_body<K, S, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
@@ -668,9 +668,9 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                         const StencilTuning& tune, stream_t stream) {
   RMA_CHECK_ARG(K == 2 || K == 3 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16,
                 "steps per pass must be 2, 3, 4, 6, 8, 12 or 16, got " << K);
-  RMA_CHECK_ARG(tune.kernel >= 0 && tune.kernel <= 7, "unknown K-step kernel " << tune.kernel);
+  RMA_CHECK_ARG(tune.kernel >= 0 && tune.kernel <= 8, "unknown K-step kernel " << tune.kernel);
   RMA_CHECK_ARG(K <= 8 || tune.kernel >= 5,
-                "12 or 16 steps per pass need a fast5 kernel (kernel 5, 6 or 7), got kernel "
+                "12 or 16 steps per pass need a fast5 kernel (kernel 5, 6, 7 or 8), got kernel "
                     << tune.kernel);
   RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
   RMA_CHECK_ARG(nx >= 3 && ny >= 3, "grid too small: nx=" << nx << " ny=" << ny);
@@ -690,13 +690,13 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                        ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
   int V = 1;
   if (aligned && nx % 2 == 0)
-    V = (tune.vec == 4 && nx % 4 == 0 && (K <= 8 || tune.kernel == 6 || tune.kernel == 7)) ? 4 : 2;
+    V = (tune.vec == 4 && nx % 4 == 0 && (K <= 8 || tune.kernel >= 6)) ? 4 : 2;
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   RectList L;
-  if (tune.kernel >= 6) {  // stage-pipelined fast5: 2 or 4 waves per strip
-    const int S = tune.kernel == 6 ? 2 : 4;
+  if (tune.kernel >= 6) {  // stage-pipelined fast5: 2, 4 or 8 waves per strip
+    const int S = tune.kernel == 6 ? 2 : tune.kernel == 7 ? 4 : 8;
     RMA_CHECK_ARG(ny < (int64_t(1) << 30), "the stage-pipelined kernels index rows in 32 bits, ny = " << ny);
-    RMA_CHECK_ARG(K == 8 || K == 12 || K == 16,
+    RMA_CHECK_ARG(K == 8 || K == 16 || (K == 12 && S < 8),
                   "the stage-pipelined kernels run 8, 12 or 16 steps per pass, got " << K);
     const int64_t ntask = plan_strip_tasks(L, rects, nrects, V, tune.chunk_rows, K);
     if (L.n == 0) return;
@@ -723,8 +723,10 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
   }
     if (S == 2) {
       if (K == 8) { RMA_TBKP(8, 2) } else if (K == 12) { RMA_TBKP(12, 2) } else { RMA_TBKP(16, 2) }
-    } else {
+    } else if (S == 4) {
       if (K == 8) { RMA_TBKP(8, 4) } else if (K == 12) { RMA_TBKP(12, 4) } else { RMA_TBKP(16, 4) }
+    } else {
+      if (K == 8) { RMA_TBKP(8, 8) } else { RMA_TBKP(16, 8) }
     }
 #undef RMA_TBKP
     RMA_HIP_LAUNCH_CHECK();

@@ -26,11 +26,12 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 
 # K-step kernels also: 2 = dpp, 3 = lds_dpp (default), 4 = fast (reassociated, FMA; not
 # bitwise), 5 = fast5 (5-point sum with one folded per-cell factor; not bitwise, lam != 0;
-# the only kernel family for 12 / 16 steps per pass); 6 / 7 = fast5p2 / fast5p4: the same
-# arithmetic with the levels of one strip split over 2 / 4 pipelined waves (K = 8, 12, 16)
-FAST5 = ("fast5", "fast5p2", "fast5p4")
+# the only kernel family for 12 / 16 steps per pass); 6 / 7 / 8 = fast5p2 / fast5p4 / fast5p8: the
+# same arithmetic with the levels of one strip split over 2 / 4 / 8 pipelined waves (K = 8, 12, 16;
+# fast5p8: K = 8, 16)
+FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8")
 KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4, "fast5": 5, "fast5p2": 6,
-           "fast5p4": 7}
+           "fast5p4": 7, "fast5p8": 8}
 
 
 class StencilCoef(NamedTuple):

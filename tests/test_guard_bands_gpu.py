@@ -74,7 +74,7 @@ def test_multi_step_kernels_stay_in_bounds(ny, nx, K):
         check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny, nx,
                       rects)
     if K == 8:
-        for kern, vec in (("fast5p2", 2), ("fast5p4", 2), ("fast5p4", 4)):
+        for kern, vec in (("fast5p2", 2), ("fast5p4", 2), ("fast5p4", 4), ("fast5p8", 4)):
             tn = ops.StencilTuning(chunk_rows=5, kernel=kern, vec=vec)
             check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny,
                           nx, rects)

@@ -205,13 +205,14 @@ def test_fast5_rect_lists(K):
 
 
 @pytest.mark.parametrize("K,kern", [(8, "fast5p2"), (12, "fast5p2"), (16, "fast5p2"),
-                                    (8, "fast5p4"), (12, "fast5p4"), (16, "fast5p4")])
+                                    (8, "fast5p4"), (12, "fast5p4"), (16, "fast5p4"),
+                                    (8, "fast5p8"), (16, "fast5p8")])
 @pytest.mark.parametrize("ny,nx", [(3, 3), (67, 131), (257, 1024), (300, 129), (41, 4097),
                                    (130, 515), (19, 2000)])
 @pytest.mark.parametrize("chunk,xcd,vec", [(16, 1, 2), (1, 0, 2), (37, 1, 2), (16, 1, 4),
                                            (5, 0, 4)])
 def test_pipelined_fast5_equals_fast5_bitwise(K, kern, ny, nx, chunk, xcd, vec):
-    """The stage-pipelined kernels (levels of a strip split over 2 / 4 waves,
+    """The stage-pipelined kernels (levels of a strip split over 2 / 4 / 8 waves,
     hand-off rows through LDS; 2 or 4 cells per lane) compute exactly kernel
     fast5's operations."""
     T, iCp = rand((ny, nx), 18), rand((ny, nx), 19) + 0.5
@@ -257,7 +258,7 @@ def test_k_step_int64_indexing(K, kern, vec):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("kern", ["fast5p2", "fast5p4"])
+@pytest.mark.parametrize("kern", ["fast5p2", "fast5p4", "fast5p8"])
 def test_pipelined_fast5_rect_lists(kern):
     K, ny, nx = 16, 203, 900
     T, iCp = rand((ny, nx), 20), rand((ny, nx), 21) + 0.5
