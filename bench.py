@@ -272,10 +272,7 @@ def main(argv=None) -> int:
                 f.write(line + "\n")
     model.close()
     if world > 1:
-        import torch.distributed as dist
-
-        if dist.is_initialized():
-            dist.destroy_process_group()
+        C.shutdown_distributed()
     return 0 if bad == 0 else 3
 
 

@@ -175,6 +175,26 @@ def _gloo_group():
     return _gloo_pg
 
 
+def shutdown_distributed() -> None:
+    """Destroy the default process group once every rank has reached teardown.
+
+    Without the barrier a rank that finishes first closes its gloo pairs while
+    a peer's last collective is still draining them; the peer's gloo thread
+    then aborts the process ("terminate called without an active exception",
+    seen at 4 and 8 ranks), turning a finished run into a failed one.
+    """
+    global _gloo_pg
+    if not dist.is_initialized():
+        return
+    try:
+        # a CPU all-reduce is a barrier on the gloo side of a "cpu:gloo,cuda:nccl"
+        # group (dist.barrier there would create a torch RCCL communicator)
+        dist.all_reduce(torch.zeros(1), group=_gloo_group())
+    finally:
+        dist.destroy_process_group()
+        _gloo_pg = None
+
+
 _rccl_generation = 0
 
 

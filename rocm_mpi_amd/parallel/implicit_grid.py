@@ -259,9 +259,8 @@ def finalize_global_grid(finalize_dist: bool = True) -> None:
             _tls.grid = None
         else:
             _set_grid(None, False)
-        if g.owns_dist and finalize_dist and torch.distributed.is_initialized():
-            torch.distributed.destroy_process_group()
-            C._gloo_pg = None
+        if g.owns_dist and finalize_dist:
+            C.shutdown_distributed()
 
 
 # ---------------------------------------------------------------------------

@@ -30,10 +30,9 @@ def ring(rank, world, outdir):
 
     vals = app.run(4, transport="gloo", verbose=False)
     np.save(os.path.join(outdir, f"ring{rank}.npy"), np.array(vals))
-    import torch.distributed as dist
+    from rocm_mpi_amd.parallel import comm as C
 
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    C.shutdown_distributed()
 
 
 def collectives(rank, world, outdir):
@@ -100,9 +99,9 @@ def node_local(rank, world, outdir, ranks_per_node):
     np.save(os.path.join(outdir, f"local{rank}.npy"),
             np.array([local, lsize, g.local_rank, g.local_size]))
     gg.finalize_global_grid()
-    import torch.distributed as dist
+    from rocm_mpi_amd.parallel import comm as C
 
-    dist.destroy_process_group()
+    C.shutdown_distributed()
 
 
 def slurm_env(rank, world, outdir):
