@@ -63,12 +63,14 @@ def test_gloo_temporal_blocking_tiles(tmp_path, variant, K):
 
 
 @pytest.mark.parametrize("world,extra", [(2, ["--temporal", "4", "--dims", "2,1"]),
-                                         (4, ["--temporal", "16", "--dims", "2,2"])])
+                                         (4, ["--temporal", "16", "--dims", "2,2"]),
+                                         (8, ["--temporal", "16", "--dims", "4,2"])])
 def test_bench_driver_contract_multirank(tmp_path, world, extra):
     """bench.py's multi-rank path (the driver runs it under torch.distributed.run
     at N = 2, 4, 8) on the CPU twins over gloo: rank 0 prints ONE JSON line with
     the contract's keys, n_gpus == WORLD_SIZE, value == N x per-rank T_eff,
-    weak scaling (same local tile), and the global grid of a dims decomposition."""
+    weak scaling (same local tile), the global grid of a dims decomposition, and
+    exit status 0 on every rank (teardown through comm.shutdown_distributed)."""
     import json
     import subprocess
     import sys
