@@ -7,7 +7,7 @@ sized to 288 GB HBM". One process per GPU (torch.distributed.run), halo
 exchange GPU-direct over RCCL/xGMI overlapped with the interior kernel.
 
     python bench.py                                   # 1 GPU, 1000 steps, 10 warmup
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \\
         --master-addr 127.0.0.1 --master-port 29600 bench.py --gpus 8
 
 T_eff per GPU follows the reference exactly (scripts/diffusion_2D_perf.jl:55-58):
@@ -16,6 +16,20 @@ time per step. W warmup steps run untimed (the reference skips 10); K steps
 are timed between barrier+device-sync pairs; the step time is the MAX over
 ranks; ``value`` is the whole-job aggregate = N x per-GPU T_eff (weak scaling:
 the local tile is the same for every N). Data: synthetic random-init field.
+
+A multi-rank run validates itself:
+* RCCL is mandatory (no fallback to the host-staged transport) and every rank
+  must drive a different physical GPU (PCI bus ids are compared); otherwise
+  the run exits non-zero before timing anything;
+* per-pass HIP-event timings of the frame kernel, the halo exchange (pack +
+  RCCL group + unpack) and the interior give halo ms, the exposed part of the
+  exchange and the overlap fraction, per rank (``config.pass_timing``);
+* each rank then re-times its own tile with the exchange disabled, all ranks
+  concurrently: ``weak_scaling_eff_same_run`` = solo time / multi-rank time;
+* after the timed run a small grid with the same process grid runs fast-math
+  and canonical passes through the same RCCL halo path; the tiles are gathered
+  on rank 0 and compared bitwise with a 1-rank run of the global grid on rank
+  0's GPU (``rccl_halo_bitwise_ok``); a mismatch fails the run.
 """
 from __future__ import annotations
 
@@ -29,10 +43,6 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-_TRANSPORT_DESC = {"rccl": "RCCL send/recv over xGMI", "staged": "host-staged copies + gloo",
-                   "self": "single rank, no exchange", "gloo": "gloo (CPU twin)",
-                   "loopback": "in-process loopback"}
 
 METRIC = "T_eff (GB/s) + weak-scaling eff., 2D diffusion 1000 steps at 1/2/4/8 MI355X"
 
@@ -57,23 +67,36 @@ def parse(argv=None):
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
-    ap.add_argument("--temporal", type=int, default=16, choices=[1, 2, 3, 4, 6, 8, 12, 16],
-                    help="K: K time steps per kernel pass (register temporal blocking), "
-                         "width-K halo exchange per pass, grid overlap 2K (12, 16: fast-math)")
+    ap.add_argument("--temporal", type=int, default=24,
+                    help="K: at most K time steps per kernel pass (1..24); the executor's "
+                         "planner splits the steps into passes of <= K (e.g. 20 -> one "
+                         "20-step pass, 1000 -> 24-step passes); halo width K, overlap 2K")
     ap.add_argument("--chunk2", type=int, default=0,
-                    help="K-step kernel rows per wave-task (0: auto, models.diffusion.default_chunk2)")
+                    help="K-step kernel rows per task (0: per pass depth, executor default)")
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
     ap.add_argument("--fast-math", dest="fast_math", action="store_true", default=True,
-                    help="K-step passes with fast-math fp64 arithmetic (5-point sum, one folded "
+                    help="passes with the fast-math fp64 arithmetic (5-point sum, one folded "
                          "per-cell factor, FMAs): same scheme, not bitwise equal to the "
-                         "canonical update (default; the bitwise K-step (K <= 8) and one-step "
-                         "kernels are timed too)")
+                         "canonical update but bitwise equal to its CPU twin (default; the "
+                         "canonical K-step and one-step kernels are timed too)")
     ap.add_argument("--no-fast-math", dest="fast_math", action="store_false")
     ap.add_argument("--overlap", type=int, default=0,
                     help="grid overlap (0: 2 x steps-per-pass, the minimum)")
     ap.add_argument("--single-step-steps", type=int, default=100,
                     help="after the timed run, also time this many steps of the one-step "
                          "kernel on the same tile (reported in config; 0 = skip)")
+    ap.add_argument("--canonical-steps", type=int, default=0,
+                    help="steps of the canonical (bitwise) K-step passes timed on the same tile "
+                         "(0: 2 x the canonical depth)")
+    ap.add_argument("--solo-steps", type=int, default=-1,
+                    help="steps re-timed with the exchange disabled for the same-run weak-scaling "
+                         "efficiency (-1: = --steps; 0: skip)")
+    ap.add_argument("--check", type=int, default=-1,
+                    help="RCCL halo bitwise check after the run (1 on, 0 off, -1: on if N > 1)")
+    ap.add_argument("--check-nx", type=int, default=0,
+                    help="local tile of the halo check (0: 2050 on GPU, 130 on CPU)")
+    ap.add_argument("--check-self-rccl", action="store_true",
+                    help="one rank: run the halo check periodic with RCCL send/recv to self")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the same driver on the C++ CPU twins over gloo (tests of the "
@@ -92,6 +115,131 @@ def auto_tile(frac: float, cap: int) -> int:
     return max(n, 512)
 
 
+def fail(msg: str, rank: int) -> int:
+    print(f"bench.py rank {rank}: {msg}", file=sys.stderr, flush=True)
+    return 2
+
+
+def gather_obj(obj, world: int):
+    """All-gather a small picklable object over the gloo group."""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+
+    from rocm_mpi_amd.parallel import comm as C
+
+    out: list = [None] * world
+    dist.all_gather_object(out, obj, group=C._gloo_group())
+    return out
+
+
+def gather_to_root(obj, world: int):
+    """Gather a picklable object on rank 0 over the gloo group (others: None)."""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+
+    from rocm_mpi_amd.parallel import comm as C
+
+    out = [None] * world if dist.get_rank() == 0 else None
+    dist.gather_object(obj, out, dst=0, group=C._gloo_group())
+    return out
+
+
+def summarize_timings(ts: list) -> dict:
+    """Mean per-pass frame / halo / interior / exposed-halo ms of one rank."""
+    if not ts:
+        return {}
+    n = len(ts)
+    mean = {k: sum(t[k] for t in ts) / n for k in ("frame_ms", "halo_ms", "interior_ms",
+                                                   "pass_ms", "exposed_halo_ms")}
+    halo = sum(t["halo_ms"] for t in ts)
+    exposed = sum(t["exposed_halo_ms"] for t in ts)
+    mean["passes"] = n
+    mean["depths"] = sorted({int(t["K"]) for t in ts}, reverse=True)
+    mean["overlap_fraction"] = (1.0 - exposed / halo) if halo > 0 else None
+    return mean
+
+
+def halo_check(a, dims, K: int, dev: str, world: int, self_rccl: bool = False) -> tuple[bool, dict]:
+    """Run a small grid with the bench's process grid through the real halo
+    path (fast-math passes, then canonical passes), gather every rank's tile
+    on rank 0 and compare bitwise with a 1-rank run of the global grid on rank
+    0's device. Returns (ok on every rank, info).
+
+    self_rccl (one rank): the check grid is periodic and its halos go through
+    RCCL send/recv to itself; the reference is the same periodic tile with
+    local self copies (exercises this path with real RCCL traffic on 1 GPU)."""
+    import numpy as np
+    import torch
+
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import comm as C
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    n = a.check_nx or (2050 if dev != "cpu" else max(130, 6 * K + 2))
+    n_fast, n_can = 37, 23
+    ol = 2 * K
+    per = 1 if self_rccl else 0
+
+    def run(nx, ny, dims_, loopback=None, device=None, via=False):
+        kw = dict(dimx=dims_[0], dimy=dims_[1], overlaps=(ol, ol, 2), halowidths=(K, K, 1),
+                  quiet=True, periodx=per, periody=per)
+        if loopback is not None:
+            kw.update(loopback=loopback, device=device)
+        elif via:
+            kw.update(transport="rccl", self_via_transport=True)
+        gg.init_global_grid(nx, ny, 1, **kw)
+        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=n_fast + n_can,
+                                        init="random", quiet=True, dims=(*dims_, 0), temporal=K,
+                                        periods=(per, per, 0), fast_math=True, device=device))
+        m.step(n_fast)
+        m.set_temporal(K, fast_math=False)
+        m.step(n_can)
+        m.synchronize()
+        field, coords, nxyz_g, transport = m.field.clone(), m.g.coords, m.g.nxyz_g, m.g.transport
+        plan = m.plan(n_fast)
+        m.close()
+        gg.finalize_global_grid(finalize_dist=False)
+        return field, coords, nxyz_g, transport, plan
+
+    t0 = time.perf_counter()
+    field, coords, nxyz_g, transport, plan = run(n, n, dims, via=self_rccl)
+    if os.environ.get("RMA_BENCH_CHECK_CORRUPT") == "1" and int(os.environ.get("RANK", "0")) == world - 1:
+        field[n // 2, n // 2] += 1e-12  # negative test of the check (tests/test_multiprocess_cpu.py)
+    # tiles to rank 0 (host copies: at most a few hundred MB)
+    tiles = gather_to_root((coords, field.cpu().numpy()), world)
+    ok = True
+    info = {"local_tile": [n, n], "global_grid": list(nxyz_g[:2]), "transport": transport,
+            "steps": [n_fast, n_can], "fast_math_plan": plan, "self_rccl": self_rccl}
+    rank = int(os.environ.get("RANK", "0"))
+    if rank == 0:
+        import torch.cuda as tc
+
+        hub = C.LoopbackHub(1)
+        device = dev if dev == "cpu" else f"cuda:{tc.current_device()}"
+        prev = tc.current_stream() if dev != "cpu" else None
+        rn = (n, n) if self_rccl else (nxyz_g[0], nxyz_g[1])
+        try:
+            ref = run(*rn, (1, 1), loopback=(hub, 0), device=device)[0]
+        finally:
+            if prev is not None:
+                tc.set_stream(prev)
+        ref = ref.cpu().numpy()
+        bad = 0
+        for (cx, cy, _), T in tiles:
+            gx0, gy0 = cx * (n - ol), cy * (n - ol)
+            if not np.array_equal(T, ref[gy0:gy0 + n, gx0:gx0 + n]):
+                bad += 1
+        ok = bad == 0
+        info["tiles_mismatched"] = bad
+    ok = bool(gather_obj(ok, world)[0])
+    info["seconds"] = round(time.perf_counter() - t0, 3)
+    if dev != "cpu":
+        torch.cuda.synchronize()
+    return ok, info
+
+
 def main(argv=None) -> int:
     a = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,28 +250,45 @@ def main(argv=None) -> int:
                os.environ.get("MASTER_PORT", "29613"), os.path.abspath(__file__),
                *(argv if argv is not None else sys.argv[1:])]
         return subprocess.call(cmd)
+    rank = int(os.environ.get("RANK", "0"))
     if world != a.gpus:
-        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr)
-        return 2
+        return fail(f"WORLD_SIZE={world} but --gpus {a.gpus}", rank)
+    if not 1 <= a.temporal <= 24:
+        return fail(f"--temporal must be 1..24, got {a.temporal}", rank)
+
+    gpu = a.device == "cuda"
+    if gpu and world > 1:
+        # a scaling point must never silently run on the host-staged transport
+        os.environ["RMA_RCCL_STRICT"] = "1"
+        os.environ["RMA_TRANSPORT"] = "rccl"
 
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
     from rocm_mpi_amd.parallel import comm as C
-    from rocm_mpi_amd.parallel import implicit_grid as gg
 
-    gpu = a.device == "cuda"
     if gpu and not torch.cuda.is_available():
-        print("bench.py needs an MI355X (no GPU visible)", file=sys.stderr)
-        return 2
+        return fail("needs an MI355X (no GPU visible)", rank)
     if not gpu and not a.nx:
-        print("bench.py --device cpu needs --nx", file=sys.stderr)
-        return 2
+        return fail("--device cpu needs --nx", rank)
     if world > 1:
         C.init_distributed(None if gpu else "gloo")
-    rank = int(os.environ.get("RANK", "0"))
     local, _ = C.node_local_rank(rank, world)
     dev = str(C.select_device(local)) if gpu else "cpu"
+
+    # one rank per PHYSICAL GPU: compare PCI bus ids (shared GPUs would make
+    # the scaling point meaningless)
+    if gpu:
+        from rocm_mpi_amd._native import native
+
+        bus = native().device_pci_bus_id(torch.cuda.current_device())
+    else:
+        bus = f"cpu-rank-{rank}"
+    buses = gather_obj(bus, world)
+    n_gpus = len(set(buses)) if gpu else world
+    if gpu and n_gpus != world:
+        return fail(f"{world} ranks share {n_gpus} physical GPU(s) (PCI bus ids {buses}); "
+                    "a scaling point needs one GPU per rank", rank)
 
     def sync():
         if gpu:
@@ -139,28 +304,32 @@ def main(argv=None) -> int:
     ny = a.ny or nx
     dims = tuple(int(v) for v in a.dims.split(",")) + (0,)
     bw = tuple(int(v) for v in a.b_width.split(","))
+    K = a.temporal if a.variant != "kp" else 1
     cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup, device=dev,
                           warmup=a.warmup, init="random", b_width=bw, dims=dims,
                           chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
-                          unroll=a.unroll, vec=a.vec, temporal=a.temporal, chunk2=a.chunk2,
+                          unroll=a.unroll, vec=a.vec, temporal=K, chunk2=a.chunk2,
                           unroll2=a.unroll2, use_graph=a.graph, quiet=True,
-                          fast_math=a.fast_math and a.temporal > 1)
+                          fast_math=a.fast_math and a.variant != "kp")
     t_setup = time.perf_counter()
     gkw = {}
     if a.overlap:
-        gkw = {"overlaps": (a.overlap, a.overlap, 2),
-               "halowidths": (max(1, a.temporal), max(1, a.temporal), 1)}
+        gkw = {"overlaps": (a.overlap, a.overlap, 2), "halowidths": (K, K, 1)}
     model = Diffusion2D(cfg, grid_kwargs=gkw)
-    chunk2_main = model.chunk2
     g = model.g
     comm = g.comm
+    if gpu and world > 1 and g.transport != "rccl":
+        return fail(f"halo transport is {g.transport!r}, a multi-GPU point needs RCCL", rank)
     model.synchronize()
     comm.barrier()
     setup_s = time.perf_counter() - t_setup
 
+    plan_warm = model.plan(a.warmup)
+    plan_timed = model.plan(a.steps)
     model.step(a.warmup)
     model.synchronize()
     comm.barrier()
+    model.enable_pass_timing(True)  # 5 event records per pass (~us against ~70 ms passes)
     sync()
     t0 = time.perf_counter()
     model.step(a.steps)
@@ -169,14 +338,16 @@ def main(argv=None) -> int:
     t1 = time.perf_counter()
     local_s = t1 - t0
     wall = comm.allreduce(local_s, "max")
+    timings = summarize_timings(model.pass_timings())
+    model.enable_pass_timing(False)
     bad = float(model.field[:: max(1, ny // 64), :: max(1, nx // 64)].isfinite().logical_not().sum())
     bad = comm.allreduce(bad, "sum")
+    a_eff = 3 * nx * ny * 8 / 1e9
+    teff_ranks = gather_obj(a_eff / (local_s / a.steps), world)
 
-    # secondary: the one-step kernel (24 B/cell/step at the HBM roofline) on the
-    # same tile, so the temporal-blocking gain is visible in one record
-    def side_teff(K, fast, steps):
-        model.set_temporal(K, fast_math=fast)
-        model.step(2 * K)
+    def side_teff(Kside, fast, steps):
+        model.set_temporal(Kside, fast_math=fast)
+        model.step(2 * Kside)
         model.synchronize()
         comm.barrier()
         sync()
@@ -185,35 +356,83 @@ def main(argv=None) -> int:
         sync()
         comm.barrier()
         s1 = comm.allreduce(time.perf_counter() - s0, "max")
-        return 3 * nx * ny * 8 / 1e9 / (s1 / steps)
+        return a_eff / (s1 / steps)
 
+    # same-run weak-scaling reference: every rank re-times its tile without
+    # the exchange (one launch per pass), all ranks concurrently
+    solo_steps = a.steps if a.solo_steps < 0 else a.solo_steps
+    solo = None
+    if solo_steps > 0:
+        model.set_solo(True)
+        model.step(a.warmup)
+        model.synchronize()
+        comm.barrier()
+        sync()
+        s0 = time.perf_counter()
+        model.step(solo_steps)
+        sync()
+        comm.barrier()
+        solo = comm.allreduce(time.perf_counter() - s0, "max") / solo_steps
+        model.set_solo(False)
+
+    # side measurements on the same tile: the canonical (bitwise) K-step
+    # passes and the one-step kernel (24 B/cell/step at the HBM roofline)
     single = canonical = None
-    kc = min(a.temporal, 8)  # the canonical K-step kernels go up to 8 steps per pass
-    if a.single_step_steps > 0 and a.temporal > 1:
-        if a.fast_math:  # the bitwise-canonical K-step kernel on the same tile
-            canonical = side_teff(kc, False, max(kc, a.single_step_steps // kc * kc))
+    kc = 1
+    if K > 1:  # the canonical depth <= K with the lowest measured cost per step
+        from rocm_mpi_amd._native import has_native, native
+
+        if has_native():
+            cc = native().default_pass_costs(K, False)
+            kc = min(range(1, K + 1), key=lambda k: cc[k] / k)
+        else:
+            kc = min(K, 8)
+    if a.single_step_steps > 0 and K > 1:
+        if a.fast_math:
+            canonical = side_teff(kc, False, a.canonical_steps or 2 * kc)
         single = side_teff(1, False, a.single_step_steps)
 
-    kstep = None  # the K-step kernel the executor runs (csrc/runtime/executor.cpp fast_tune_k)
-    if a.temporal > 1:
+    kinfo = None
+    if K > 1:
         from rocm_mpi_amd import ops
-        from rocm_mpi_amd._native import native
+        from rocm_mpi_amd._native import has_native, native
 
-        if a.fast_math and gpu:
-            kern, kvec, _ = native().fast_kernel_k(a.temporal, ny, tuple(model.coef))
-            kstep = {"kernel": {v: k for k, v in ops.KERNELS.items()}[kern], "vec": kvec,
-                     "chunk_rows": chunk2_main}
-        else:
-            kstep = {"kernel": "canonical", "chunk_rows": chunk2_main}
+        if has_native():
+            depth = max(plan_timed)
+            if a.fast_math:
+                kern, kvec, kch = native().fast_kernel_k(depth, ny, tuple(model.coef))
+            else:
+                kern, kvec, kch = native().canonical_kernel_k(depth, ny)
+            names = {v: k for k, v in ops.KERNELS.items()}
+            kinfo = {"kernel": names[kern], "vec": kvec, "chunk_rows": a.chunk2 or kch,
+                     "stages": native().pipe_default_stages(depth) if kern >= 9 else None}
+    model.close()
+
+    check_on = a.check == 1 or (a.check < 0 and world > 1)
+    check_ok, check_info = None, None
+    if check_on and a.variant != "kp":
+        check_ok, check_info = halo_check(a, dims[:2], K, dev, world,
+                                          self_rccl=a.check_self_rccl and world == 1 and gpu)
 
     t_it = wall / a.steps
-    teff_gpu = 3 * nx * ny * 8 / 1e9 / t_it
+    teff_gpu = a_eff / t_it
     total = teff_gpu * world
+    nbrs = any(p >= 0 for side in g.neighbors[:2] for p in side)
+    if not nbrs:
+        par = "single rank, no halo exchange (one launch per pass)"
+    else:
+        tdesc = {"rccl": "RCCL send/recv over xGMI", "staged": "host-staged copies + gloo",
+                 "gloo": "gloo (CPU twin)", "loopback": "in-process loopback",
+                 "self": "periodic self copies"}.get(g.transport, g.transport)
+        par = f"halo: {tdesc}" + (", boundary frame + exchange on a high-priority stream "
+                                  "overlapped with the interior" if a.variant == "perf_hide"
+                                  else ", exchange after each pass")
+    eff_same = (solo / t_it) if solo else None
     out = {
         "metric": METRIC,
         "value": round(total, 2),
         "unit": "GB/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(t_it * 1e3, 6),
@@ -226,53 +445,57 @@ def main(argv=None) -> int:
             "model": f"diffusion_2D_{a.variant}",
             "global_batch": g.nxyz_g[0] * g.nxyz_g[1],
             "seq_len": None,
-            "parallelism": f"2D domain decomposition dims {g.dims[0]}x{g.dims[1]} "
-                           f"(halo: {_TRANSPORT_DESC.get(g.transport, g.transport)}"
-                           + (", boundary/interior overlap)" if a.variant == "perf_hide" else ")"),
+            "parallelism": f"2D domain decomposition dims {g.dims[0]}x{g.dims[1]} ({par})",
+            "ranks": world,
             "local_grid": [nx, ny],
             "global_grid": [g.nxyz_g[0], g.nxyz_g[1]],
             "teff_per_gpu_GBps": round(teff_gpu, 2),
-            "a_eff_GB_per_step": round(3 * nx * ny * 8 / 1e9, 6),
-            "kernel": a.kernel,
-            "kstep_kernel": kstep,
-            "chunk_rows": a.chunk_rows,
-            "unroll": a.unroll,
-            "vec": a.vec,
-            "nontemporal": a.nontemporal,
-            "b_width": list(bw),
-            "hipgraph": bool(a.graph),
-            "temporal_blocking": a.temporal,
-            "chunk2": chunk2_main,
-            "steps_per_kernel_pass": a.temporal,
+            "teff_per_gpu_min_GBps": round(min(teff_ranks), 2),
+            "teff_per_gpu_max_GBps": round(max(teff_ranks), 2),
+            "a_eff_GB_per_step": round(a_eff, 6),
+            "max_steps_per_pass": K,
+            "passes_warmup": plan_warm,
+            "passes_timed": plan_timed,
+            "kstep_kernel": kinfo,
+            "fast_math": bool(cfg.fast_math),
+            "pass_timing": timings,
+            "solo_ms_per_step": round(solo * 1e3, 6) if solo else None,
+            "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,
+            "rccl_halo_bitwise_ok": check_ok,
+            "halo_check": check_info,
             "teff_note": ("T_eff = A_eff/t_step with A_eff = 3*nx*ny*8 B (reference "
                           "perf.jl:55-58). With temporal blocking every step of every cell "
-                          "is still computed (bitwise equal to one-step updates) but HBM is "
-                          f"read/written once per {a.temporal} steps, so T_eff exceeds the "
-                          "HBM bandwidth; teff_single_step_kernel_GBps is the one-step "
-                          "kernel on the same tile. fast_math: the K-step passes evaluate "
-                          "the same fp64 update as a 5-point sum with one folded per-cell "
-                          "factor and FMAs (rounding-level deviation from the canonical "
-                          "update, tests/test_temporal_gpu.py); teff_bitwise_kstep_GBps is "
-                          "the bitwise-canonical K-step kernel on the same tile")
-                         if a.temporal > 1 else "",
+                          "is computed, but HBM is read/written once per pass of up to "
+                          f"{K} steps, so T_eff exceeds the HBM bandwidth and is a time per "
+                          "step, not a memory throughput; teff_single_step_kernel_GBps is "
+                          "the one-step kernel on the same tile (the like-for-like memory "
+                          "number). fast_math: the passes evaluate the same fp64 update as "
+                          "a 5-point sum with one folded per-cell factor and FMAs "
+                          "(rounding-level deviation from the canonical update, bitwise "
+                          "equal to its CPU twin, tests/test_pipe_gpu.py); "
+                          "teff_bitwise_kstep_GBps is the canonical K-step kernel on the "
+                          "same tile") if K > 1 else "",
             "teff_single_step_kernel_GBps": round(single, 2) if single else None,
-            "fast_math": bool(a.fast_math and a.temporal > 1),
             "teff_bitwise_kstep_GBps": round(canonical, 2) if canonical else None,
             "bitwise_kstep_steps_per_pass": kc if canonical else None,
             "overlap": list(g.overlaps[:2]),
+            "transport": g.transport,
+            "pci_bus_ids": buses if gpu else None,
+            "hipgraph": bool(a.graph),
             "setup_s": round(setup_s, 3),
             "nonfinite_cells_sampled": int(bad),
         },
     }
-    if g.me == 0:
+    if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    model.close()
     if world > 1:
         C.shutdown_distributed()
+    if check_ok is False:
+        return 4
     return 0 if bad == 0 else 3
 
 

@@ -1,0 +1,141 @@
+#!/usr/bin/env python
+"""Time one kernel pass of every depth K (the executor's pass planner input).
+
+For each configuration (kernel family, K, stage split, chunk rows) one pass of
+K steps over the interior of an n x n fp64 tile is timed with HIP events in
+interleaved rounds (A/B in one process, median reported). The one-step march
+kernel is the unit: ``rel`` = pass time / one-step time, the cost the planner
+(csrc/runtime/plan.cpp default_pass_costs) minimises. Prints one JSON document.
+
+    python bench/pass_sweep.py                       # 288 GB tile (auto), default set
+    python bench/pass_sweep.py --n 16384 --pipe 1-24 --pipec 8,12,16
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def krange(spec: str) -> list[int]:
+    out = []
+    for part in filter(None, spec.split(",")):
+        if "-" in part:
+            a, b = part.split("-")
+            out += list(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=0, help="tile edge (0: auto-size to 80%% of HBM)")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--pipe", default="1-24", help="fast5 pipelined kernel depths")
+    ap.add_argument("--pipec", default="3-12,16", help="canonical pipelined kernel depths")
+    ap.add_argument("--ldsdpp", default="3,4,6,8", help="canonical kernel-3 depths")
+    ap.add_argument("--old", default="fast5p4:16,fast5p2:12,fast5:8", help="fixed-K kernels")
+    ap.add_argument("--alt", default="12:3,16:8,24:8,8:4,8:1", help="pipe K:stages splits")
+    ap.add_argument("--chunk", type=int, default=0, help="rows per task (0: executor default)")
+    ap.add_argument("--chunks", default="", help="pipe K:c1/c2/..., extra chunk-row variants")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from rocm_mpi_amd import ops
+    from rocm_mpi_amd._native import native
+
+    dev = torch.device("cuda", 0)
+    n = a.n
+    if not n:
+        free, _ = torch.cuda.mem_get_info()
+        n = int(math.isqrt(int(0.80 * free / 24))) // 256 * 256
+    f = dict(dtype=torch.float64, device=dev)
+    T = torch.empty((n, n), **f)
+    ops.init_random_(T, ops.TileGeometry(0, 0, n, n, 1.0, 1.0), seed=1)
+    T2 = torch.empty_like(T)
+    T2.copy_(T)
+    iCp = torch.empty_like(T)
+    ops.fill_(iCp, 1.0)
+    dx = 10.0 / n
+    coef = ops.StencilCoef.from_physics(1.0, dx, dx, dx * dx / 4.1)
+    N = native()
+
+    def chunk(K, c=0):
+        return c or a.chunk or N.default_chunk_k(max(K, 3), n)
+
+    cfgs = [("march", 1, 0)]
+    cfgs += [("pipe", K, 0) for K in krange(a.pipe)]
+    cfgs += [("pipec", K, 0) for K in krange(a.pipec)]
+    cfgs += [("lds_dpp", K, 0) for K in krange(a.ldsdpp)]
+    cfgs += [("two_step", 2, 0)]
+    for item in filter(None, a.old.split(",")):
+        k, K = item.split(":")
+        cfgs.append((k, int(K), 0))
+    for item in filter(None, a.alt.split(",")):
+        K, S = item.split(":")
+        cfgs.append(("pipe", int(K), int(S)))
+    for item in filter(None, a.chunks.split(",")):
+        K, cs = item.split(":")
+        for c in cs.split("/"):
+            cfgs.append(("pipe", int(K), 0, int(c)))
+
+    rect = [ops.interior_rect(n, n)]
+
+    def launch(kind, K, S, c=0):
+        if kind == "march":
+            ops.stencil_step(T2, T, iCp, coef, rect, ops.StencilTuning())
+        elif kind == "two_step":
+            ops.stencil2_step(T2, T, iCp, coef, rect, ops.StencilTuning(chunk_rows=16, unroll=2))
+        else:
+            vec = 2 if kind in ("lds_dpp", "fast5") else 4
+            tn = ops.StencilTuning(chunk_rows=chunk(K, c), kernel=kind, vec=vec, xcd_remap=1,
+                                   stages=S)
+            ops.stencilk_step(K, T2, T, iCp, coef, rect, tn)
+
+    times: dict = {c: [] for c in cfgs}
+    for c in cfgs:  # warm every kernel once (first launches)
+        launch(*c)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in cfgs]
+    for r in range(a.rounds):
+        for i, c in enumerate(cfgs):
+            e0, e1 = ev[i]
+            e0.record()
+            launch(*c)
+            e1.record()
+        torch.cuda.synchronize()
+        for i, c in enumerate(cfgs):
+            times[c].append(ev[i][0].elapsed_time(ev[i][1]))
+        print(f"[pass_sweep] round {r + 1}/{a.rounds} done", flush=True)
+    base = statistics.median(times[("march", 1, 0)])
+    rows = []
+    for c in cfgs:
+        kind, K, S = c[:3]
+        med = statistics.median(times[c])
+        rows.append({"kernel": kind, "K": K, "stages": S or (native().pipe_default_stages(K)
+                                                             if kind in ops.PIPE else 0),
+                     "chunk_rows": (chunk(K, c[3] if len(c) > 3 else 0)
+                                    if kind not in ("march", "two_step") else None),
+                     "ms_per_pass": round(med, 3), "ms_min": round(min(times[c]), 3),
+                     "ms_per_step": round(med / K, 4), "rel": round(med / base, 4),
+                     "teff_equiv_GBps": round(K * 24 * n * n / 1e9 / (med / 1e3), 1)})
+    doc = {"tile": n, "rounds": a.rounds, "one_step_ms": round(base, 3), "rows": rows,
+           "note": "rel = pass time / one-step march kernel time (the planner's cost unit)"}
+    s = json.dumps(doc, indent=1)
+    print(s)
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()

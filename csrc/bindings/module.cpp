@@ -18,6 +18,7 @@
 #include "rma/kernels.h"
 #include "rma/loopback.h"
 #include "rma/p2p.h"
+#include "rma/plan.h"
 #include "rma/topology.h"
 #include "rma/trace.h"
 
@@ -83,6 +84,7 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("set_rank_for_errors", &set_rank_for_errors);
   m.def("rccl_version", &rccl_version);
+  m.def("device_pci_bus_id", &device_pci_bus_id, py::arg("device"));
   m.def(
       "stencil_strip_cells",
       [](int64_t nx, int vec) {
@@ -147,7 +149,7 @@ PYBIND11_MODULE(_C, m) {
       "stencilk_rects",
       [](int K, uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
          const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
-         uintptr_t stream, bool gpu, int xcd_remap, int vec, int kernel) {
+         uintptr_t stream, bool gpu, int xcd_remap, int vec, int kernel, int stages) {
         auto r = to_rects(rects);
         StencilTuning tn;
         tn.chunk_rows = chunk_rows;
@@ -155,19 +157,26 @@ PYBIND11_MODULE(_C, m) {
         tn.xcd_remap = xcd_remap;
         tn.vec = vec;
         tn.kernel = kernel;
+        tn.stages = stages;
         if (gpu)
           stencilk_rects_gpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
                              r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
         else {
+          // the CPU twin of the kernel's arithmetic: fast5 (kernels 5-9) or canonical
+          const bool f5 = kernel >= 5 && kernel <= 9;
           py::gil_scoped_release nogil;
-          stencilk_rects_cpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
-                             r.data(), (int)r.size(), to_coef(coef));
+          if (f5)
+            stencilk5_rects_cpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx,
+                                ny, r.data(), (int)r.size(), to_coef(coef));
+          else
+            stencilk_rects_cpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx,
+                               ny, r.data(), (int)r.size(), to_coef(coef));
         }
       },
       py::arg("K"), py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"),
       py::arg("rects"), py::arg("coef"), py::arg("chunk_rows") = 16, py::arg("nontemporal") = 3,
       py::arg("stream") = 0, py::arg("gpu") = true, py::arg("xcd_remap") = -1,
-      py::arg("vec") = 2, py::arg("kernel") = 0);
+      py::arg("vec") = 2, py::arg("kernel") = 0, py::arg("stages") = 0);
   m.def(
       "stream_copy",
       [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {
@@ -343,6 +352,28 @@ PYBIND11_MODULE(_C, m) {
   // ---------------- executor ----------------
   m.def("default_chunk_k", [](int K, int64_t ny) { return default_tune_k(K, ny).chunk_rows; },
         py::arg("K"), py::arg("ny"));
+  m.def("plan_passes", &plan_passes, py::arg("nsteps"), py::arg("costs"));
+  m.def("default_pass_costs", &default_pass_costs, py::arg("kmax"), py::arg("fast5"));
+  m.def("pipe_default_stages", &pipe_default_stages, py::arg("K"));
+  m.def("pipe_max_k", []() { return kPipeMaxK; });
+  m.def(
+      "pass_geometry",
+      [](int64_t nx, int64_t ny, int K, std::array<std::array<int, 2>, 3> nbr, bool hide,
+         int64_t bwx, int64_t bwy, int64_t olx, int64_t oly) {
+        const PassGeom g = pass_geometry(nx, ny, K, nbr, hide, bwx, bwy, olx, oly);
+        std::vector<Rect4> fr;
+        for (auto& r : g.frame) fr.push_back(from_rect(r));
+        return std::make_tuple(from_rect(g.out), fr, from_rect(g.interior));
+      },
+      py::arg("nx"), py::arg("ny"), py::arg("K"), py::arg("neighbors"), py::arg("hide"),
+      py::arg("bwx"), py::arg("bwy"), py::arg("olx"), py::arg("oly"));
+  m.def(
+      "canonical_kernel_k",
+      [](int K, int64_t ny) {
+        const StencilTuning t = canonical_tune_k(K, ny);
+        return std::make_tuple(t.kernel, t.vec, t.chunk_rows);
+      },
+      py::arg("K"), py::arg("ny"));
   m.def(
       "fast_kernel_k",
       [](int K, int64_t ny, const Coef4& coef) {
@@ -364,6 +395,7 @@ PYBIND11_MODULE(_C, m) {
              p.oly = oly;
              p.tune2 = default_tune_k(temporal, ny);  // measured defaults
              if (chunk2 > 0) p.tune2.chunk_rows = chunk2;
+             p.chunk_rows2 = chunk2;  // 0: per pass depth
              if (temporal == 2) p.tune2.unroll = unroll2;
              p.tune2.nontemporal = nontemporal & 3;
              p.mode = static_cast<Mode>(mode);
@@ -388,13 +420,42 @@ PYBIND11_MODULE(_C, m) {
            py::arg("halo").none(true) = nullptr, py::arg("qx") = 0, py::arg("qy") = 0,
            py::arg("dTdt") = 0, py::arg("unroll") = 4, py::arg("vec") = 2,
            py::arg("temporal") = 1, py::arg("olx") = 2, py::arg("oly") = 2,
-           py::arg("chunk2") = 16, py::arg("unroll2") = 2, py::arg("fast_math") = 0,
+           py::arg("chunk2") = 0, py::arg("unroll2") = 2, py::arg("fast_math") = 0,
            py::keep_alive<1, 16>())
       .def(
           "run", [](DiffusionExecutor& e, int64_t n, uintptr_t s) { e.run(n, S(s)); },
           py::arg("nsteps"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("parity", &DiffusionExecutor::parity)
       .def_property_readonly("steps_done", &DiffusionExecutor::steps_done)
+      .def_property_readonly("passes_done", &DiffusionExecutor::passes_done)
+      .def("plan", &DiffusionExecutor::plan, py::arg("nsteps"))
+      .def_property_readonly("pass_costs", &DiffusionExecutor::pass_costs)
+      .def("prime", &DiffusionExecutor::prime, py::call_guard<py::gil_scoped_release>())
+      .def("set_timing", &DiffusionExecutor::set_timing, py::arg("on"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("timings",
+           [](DiffusionExecutor& e) {
+             std::vector<py::dict> out;
+             std::vector<PassTiming> ts;
+             {
+               py::gil_scoped_release nogil;
+               ts = e.timings();
+             }
+             for (const auto& t : ts) {
+               py::dict d;
+               d["K"] = t.K;
+               d["frame_ms"] = t.frame_ms;
+               d["halo_ms"] = t.halo_ms;
+               d["interior_ms"] = t.interior_ms;
+               d["pass_ms"] = t.pass_ms;
+               d["exposed_halo_ms"] = t.exposed_halo_ms;
+               out.push_back(d);
+             }
+             return out;
+           })
+      .def("set_solo", &DiffusionExecutor::set_solo, py::arg("on"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("solo", &DiffusionExecutor::solo)
       .def_property_readonly("frame_rects",
                              [](const DiffusionExecutor& e) {
                                std::vector<Rect4> v;

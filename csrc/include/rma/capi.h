@@ -73,8 +73,8 @@ typedef struct rma_executor rma_executor;
 int rma_executor_create(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
                         int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
                         double* qx, double* qy, double* dTdt, rma_executor** out);
-// Same with temporal blocking: `steps_per_pass` = 1, 2, 3, 4, 6, 8 (12, 16: fast_math) time steps
-// per kernel pass (needs a grid created with overlaps >= 2*steps_per_pass and
+// Same with temporal blocking: at most `steps_per_pass` (1..24) time steps per
+// kernel pass (rma_executor_run plans passes of 1..steps_per_pass steps) (needs a grid created with overlaps >= 2*steps_per_pass and
 // halowidths = steps_per_pass along every dimension with a neighbour).
 int rma_executor_create_k(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
                           int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,

@@ -81,5 +81,8 @@ class RcclComm : public P2PTransport {
 };
 
 int rccl_version();
+// PCI bus id ("0000:05:00.0") of a HIP device: tells whether two ranks drive
+// the same physical GPU (bench.py refuses that for a scaling point).
+std::string device_pci_bus_id(int device);
 
 }  // namespace rma

@@ -12,10 +12,12 @@
 //           join both, swap. This is the reference's intended variant (3)
 //           with exact frame/interior grids.
 //   kKp   : [flux] -> [residual] -> [update T in place] -> [halo(T)]
-//   temporal=K>1 (kPerf/kHide): each pass advances K steps with the K-step
-//           kernel (stencil_tb.hip for K=2, stencil_tbk.hip otherwise) on the
-//           "owned" rect (the K cells next to a neighbour are left to the
-//           width-K exchange), then one exchange of width K (overlap 2K).
+//   temporal=K>1 (kPerf/kHide): run(n) plans passes of 1..K steps
+//           (plan_passes: e.g. 20 steps = one 20-step pass, never 16 + 4);
+//           a pass of k steps runs the k-step kernel (stencil_tb.hip k=2,
+//           stencil_tbk.hip / stencil_pipe.h otherwise) on the "owned" rect
+//           (the k cells next to a neighbour are left to the exchange), then
+//           one exchange of width K (overlap 2K).
 //
 // Python never waits inside the loop; run() returns as soon as n steps are
 // enqueued, ordered after the caller's stream and before its next work.
@@ -28,6 +30,7 @@
 
 #include "rma/halo.h"
 #include "rma/kernels.h"
+#include "rma/plan.h"
 
 namespace rma {
 
@@ -40,31 +43,42 @@ struct ExecParams {
   int64_t bwx = 1, bwy = 1;    // perf_hide frame widths (cells beyond the boundary)
   int use_graph = 0;           // capture steps into a hipGraph and replay
   int graph_steps = 0;         // steps per captured graph (even; 0 = auto)
-  // Temporal blocking (kPerf/kHide): K = 2, 3, 4, 6, 8 (12, 16 with fast_math)
-  // time steps per kernel pass and one halo exchange of width K per pass;
-  // needs a grid overlap >= 2K in every dimension with a neighbour. 1 = one
-  // step per pass.
+  // Temporal blocking (kPerf/kHide): at most K = temporal time steps per
+  // kernel pass (1..kPipeMaxK) and one halo exchange of width K per pass;
+  // needs a grid overlap >= 2K in every dimension with a neighbour. run(n)
+  // splits n steps into passes of 1..K steps with plan_passes (rma/plan.h).
   int temporal = 1;
   int64_t olx = 2, oly = 2;    // grid overlaps of the field (IGG overlaps)
   StencilTuning tune2{16, 3, 0, 2, 2, -1};  // K-step kernel tuning (K=2: 16-row chunks)
-  // fast_math: K-step passes use the 5-point-sum arithmetic with one folded
-  // per-cell factor (stencil_tbk.hip kernel 5; kernel 4 if lam == 0): same
-  // scheme in fp64, not bitwise equal to the canonical expression (rounding
-  // level, tests/test_temporal_gpu.py).
+  int chunk_rows2 = 0;         // K-step rows per task (0: default_tune_k per pass depth)
+  // fast_math: every pass uses the fast5 arithmetic (5-point sum with one
+  // folded per-cell factor, stencil_pipe.h), K = 1 included: same scheme in
+  // fp64, not bitwise equal to the canonical expression (rounding level,
+  // tests/test_pipe_gpu.py) but bitwise equal to its CPU twin.
   int fast_math = 0;
 };
 
 // Measured defaults of the K-step kernels (profiles/SUMMARY_r1.md): K=2 uses
 // the aligned two-step kernel with 16-row chunks; K>=3 the overlapped-strip
-// kernel with the LDS 1/Cp ring, per-XCD task ranges and chunks growing with
+// kernels with the LDS 1/Cp ring, per-XCD task ranges and chunks growing with
 // the tile height (they amortise the 2K-1 rows recomputed per chunk).
 StencilTuning default_tune_k(int K, int64_t ny);
-// The fast-math K-step passes (fast_math, stencil_tbk.hip kernels 5-7; needs
-// fast5_ok): K=16 runs the 4-stage pipelined kernel with 4 cells per lane, K=12
-// the 2-stage one with 4 cells per lane, K<=8 the single-wave kernel 5
-// (measured, profiles/SUMMARY_r1.md). Kernel 4 when the coefficients cannot be
-// folded (lam == 0; K <= 8 only).
+// Kernel of a K-step pass: fast_math (and fast5_ok) -> the pipelined fast5
+// kernel (9) at every K with 4 cells per lane; canonical -> kernel 3 at K in
+// {3,4,6,8}, the canonical pipelined kernel (10) at other K >= 3 (K = 1 and
+// 2 have their own one- and two-step kernels).
 StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c);
+StencilTuning canonical_tune_k(int K, int64_t ny);
+
+// Per-pass timing (set_timing): HIP events on the two streams, in ms from the
+// pass start (after the cross-stream waits). frame: boundary-frame kernel
+// (perf_hide with neighbours; 0 otherwise), halo: pack + RCCL group + unpack
+// after it, interior: the interior launch(es). exposed_halo_ms: how long the
+// exchange outlasted the interior (0 = fully hidden).
+struct PassTiming {
+  int K = 0;
+  float frame_ms = 0, halo_ms = 0, interior_ms = 0, pass_ms = 0, exposed_halo_ms = 0;
+};
 
 class DiffusionExecutor {
  public:
@@ -79,23 +93,43 @@ class DiffusionExecutor {
   // Enqueue n steps after the work already on caller_stream; caller_stream is
   // made to wait for them. Asynchronous.
   void run(int64_t nsteps, stream_t caller_stream);
+  // Passes run(n) would launch (deepest first; K = 1 entries are one-step
+  // updates).
+  std::vector<int> plan(int64_t nsteps) const;
+  const std::vector<double>& pass_costs() const { return cost_; }
+  // Launch every kernel a run may use once on a tiny scratch field (first
+  // launches stay out of timed regions); synchronous. Done by the constructor
+  // unless RMA_EXEC_PRIME=0.
+  void prime();
+  // Record per-pass HIP events from now on (clears earlier records); read
+  // them with timings() once the work is done (synchronises).
+  void set_timing(bool on);
+  std::vector<PassTiming> timings();
+  // solo: run this tile as if it had no neighbour (no exchange, one launch per
+  // pass over the whole interior) -- the same-run single-GPU reference of a
+  // weak-scaling measurement (bench.py); the field is then NOT the
+  // multi-rank solution. Off restores the real neighbours.
+  void set_solo(bool on);
+  bool solo() const { return solo_; }
   // Number of completed buffer swaps mod 2: 0 -> current field is T, 1 -> T2.
   int parity() const { return parity_; }
   int64_t steps_done() const { return steps_; }
+  int64_t passes_done() const { return passes_; }
   std::vector<Rect> frame_rects() const { return frame_; }
   Rect interior_rect() const { return interior_; }
   Rect full_rect() const { return full_; }
 
  private:
   void enqueue_step(double* Tin, double* Tout);
-  void enqueue_step2(double* Tin, double* Tout);  // temporal=K: one K-step pass
-  void multi_step(double* Tin, double* Tout, const Rect* rects, int n, const StencilTuning& tn,
-                  void* stream);
+  void enqueue_pass(int K, double* Tin, double* Tout);  // one K-step pass (K >= 2 or fast5)
+  StencilTuning pass_tuning(int K, bool frame) const;
+  const PassGeom& geometry(int K);
+  void multi_step(int K, double* Tin, double* Tout, const double* iCp, int64_t nx, int64_t ny,
+                  const Rect* rects, int n, const StencilTuning& tn, void* stream) const;
   void exchange(double* A, stream_t s);
-  void split(const Rect& out, int64_t bwx, int64_t bwy, std::vector<Rect>& frame,
-             Rect& interior) const;
-  void build_graph(int64_t steps);
+  void build_graph(int64_t steps, int reps);
   void run_eager(int64_t nsteps);
+  bool fast5() const;
 
   double* T_;
   double* T2_;
@@ -104,10 +138,12 @@ class DiffusionExecutor {
   ExecParams p_;
   HaloExchanger* halo_;
   double *qx_, *qy_, *dTdt_;
+  Neighbors nbr_{{{-1, -1}, {-1, -1}, {-1, -1}}};
   Rect full_{}, interior_{};
   std::vector<Rect> frame_;
-  Rect out2_{}, interior2_{};  // temporal=K: owned rect and its interior
-  std::vector<Rect> frame2_;
+  std::vector<PassGeom> geom_;   // index K (lazily filled)
+  std::vector<char> geom_ok_;
+  std::vector<double> cost_;     // index K: relative pass cost (plan_passes)
   int64_t hwx_ = 1, hwy_ = 1;
   void* s_hi_ = nullptr;  // hipStream_t
   void* s_lo_ = nullptr;
@@ -118,6 +154,17 @@ class DiffusionExecutor {
   int64_t graph_len_ = 0;
   int parity_ = 0;
   int64_t steps_ = 0;
+  int64_t passes_ = 0;
+  bool solo_ = false;
+  Neighbors real_nbr_{{{-1, -1}, {-1, -1}, {-1, -1}}};
+  // timing: 5 events per pass (start, frame end, halo end on hi; interior
+  // start, end on lo)
+  bool timing_ = false;
+  std::vector<void*> tev_;
+  std::vector<int> tk_;
+  size_t tused_ = 0;
+  void* tevent();
+  void release_timing();
 };
 
 }  // namespace rma

@@ -33,6 +33,7 @@ struct StencilTuning {
   int vec = 2;             // cells per lane (2: one 16-B access per row, 4: two)
   int xcd_remap = -1;      // 1: each XCD takes a contiguous 1/8 of the tasks; 0: chunk rows
                            // padded to 8-block multiples (same-XCD neighbours); -1: by size
+  int stages = 0;          // pipelined K-step kernels 9/10: waves per strip (0: default)
 };
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
@@ -66,6 +67,25 @@ void stencilk_rects_cpu(int K, double* T2, const double* T, const double* iCp, i
 // factor, 5 ops). 4 and 5 are not bitwise equal to the canonical update.
 // fast5_ok: kernel 5 divides by lam/dx^2, so it needs lam != 0.
 bool fast5_ok(const StencilCoef& c);
+//   9 pipe  (fast5 arithmetic) / 10 pipec (canonical): stage-pipelined strips
+//     for ANY K in 1..kPipeMaxK (stencil_pipe.h); stencilk_rects_gpu routes
+//     kernels 9/10 here. stages = waves per strip (0: pipe_default_stages).
+//     pipe is bitwise equal to kernel 5 and to stencilk5_rects_cpu; pipec to K
+//     one-step launches and stencilk_rects_cpu.
+constexpr int kPipeMaxK = 24;
+int pipe_default_stages(int K);
+bool pipe_has(int K, int stages);
+void stencil_pipe_rects_gpu(int K, int stages, bool canonical, double* T2, const double* T,
+                            const double* iCp, int64_t nx, int64_t ny, const Rect* rects,
+                            int nrects, const StencilCoef& c, const StencilTuning& tune,
+                            stream_t stream);
+// CPU twins of the fast5 arithmetic (one step / K steps, same operations and
+// rounding as kernels 5-9: std::fma, -ffp-contract=off); the intermediate
+// levels are updated on the interior only, like stencilk_rects_cpu.
+void stencil5_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                        const Rect* rects, int nrects, const StencilCoef& c);
+void stencilk5_rects_cpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                         int64_t ny, const Rect* rects, int nrects, const StencilCoef& c);
 
 // Width (in cells) of one wave's x-strip in the march kernel; perf_hide rounds
 // its x-frame so the interior rect starts on a strip boundary.

@@ -1,0 +1,59 @@
+// Host-only planning of the executor's kernel passes (no HIP): the rects a
+// pass of K steps updates, the boundary-frame / interior split of perf_hide
+// and the pass planner that decomposes n time steps into passes. Kept in a
+// HIP-free translation unit so the sanitizer build (tests/native/
+// host_selftest.cpp) runs it under ASan/UBSan.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <vector>
+
+#include "rma/common.h"
+
+namespace rma {
+
+using Neighbors = std::array<std::array<int, 2>, 3>;  // (dim, side) -> rank, -1 = none
+
+// out minus a frame of widths (bwx, bwy): the 4 frame rects (lo-y, hi-y, lo-x,
+// hi-x strips) and the interior. If the frame swallows the rect, frame = {out}
+// and interior is empty.
+void split_rect(const Rect& out, int64_t bwx, int64_t bwy, std::vector<Rect>& frame,
+                Rect& interior);
+
+// Cells a K-step pass owns: next to a neighbour the K cells [0,K) are halo
+// (level j of the pass is valid from column j on, so the pass outputs from
+// column K; the width-hw exchange refreshes [0,hw) afterwards), elsewhere the
+// fixed boundary cell 0 stays.
+Rect owned_rect(int64_t nx, int64_t ny, int K, const Neighbors& nbr);
+
+struct PassGeom {
+  Rect out{};                // cells the pass writes
+  std::vector<Rect> frame;   // perf_hide: computed first (high-priority stream)
+  Rect interior{};           // perf_hide: the rest (low-priority stream)
+};
+
+// Geometry of one pass. hide: split into frame + interior so that the frame
+// holds the send planes [ol-hw, ol) of every side (width >= ol - out.x0, the
+// reference's b_width >= overlap invariant); without any
+// neighbour there is nothing to overlap and the owned rect is one launch.
+PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool hide,
+                       int64_t bwx, int64_t bwy, int64_t olx, int64_t oly);
+
+// Relative cost of one pass of K steps (index K = 1..Kmax; index 0 unused;
+// +inf = no kernel), in units of one HBM sweep of the 3 arrays. Measured on
+// MI355X at the 288 GB tile (profiles/pass_costs_r2.json); fast5 = the
+// fast-math arithmetic (every K on the pipelined kernel), otherwise the
+// canonical kernels (K = 1 one-step march, 2 two-step, 3/4/6/8 kernel 3,
+// the rest the canonical pipelined kernel).
+std::vector<double> default_pass_costs(int kmax, bool fast5);
+// RMA_PASS_COSTS="K:cost,K:cost,..." overrides entries (sweeps, tests).
+void apply_cost_overrides(std::vector<double>& cost, const char* spec);
+
+// Decompose n steps into passes of 1..Kmax steps minimising the summed cost
+// (dynamic programme; ties -> fewer passes). Returned deepest first. E.g. the
+// driver's 20 timed steps: one 20-step pass (~73 ms at the 288 GB tile)
+// instead of 16 + 4 (~56 + 43 ms).
+std::vector<int> plan_passes(int64_t n, const std::vector<double>& cost);
+
+}  // namespace rma

@@ -68,6 +68,62 @@ void stencilk_rects_cpu(int K, double* T2, const double* T, const double* iCp, i
   stencil_rects_cpu(T2, a.data(), iCp, nx, ny, rects, nrects, c);
 }
 
+bool fast5_ok(const StencilCoef& c) {
+  const double ax = (-c.mlam) * c.rdx * c.rdx, ay = (-c.mlam) * c.rdy * c.rdy;
+  return ax != 0.0 && std::isfinite(ax) && std::isfinite(ay) && std::isfinite(ay / ax) &&
+         std::isfinite(c.dt * ax);
+}
+
+// fast5 arithmetic (stencil_tbk.hip kernel 5, stencil_pipe.h): the 5-point sum
+// with the constants folded into one per-cell factor g = dt*lam/dx^2 * 1/Cp,
+//   T2 = fma(g, fma(r, U+D, fma(-2(1+r), c, R+L)), c),  r = (lam/dy^2)/(lam/dx^2).
+// std::fma rounds once like v_fma_f64, so this twin is bitwise equal to the
+// GPU kernels (tests/test_fast5_cpu.py, tests/test_pipe_gpu.py).
+void stencil5_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                        const Rect* rects, int nrects, const StencilCoef& c) {
+  RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
+  RMA_CHECK_ARG(fast5_ok(c), "fast5 needs lam != 0 and finite coefficients");
+  const double ax = (-c.mlam) * c.rdx * c.rdx;
+  const double ay = (-c.mlam) * c.rdy * c.rdy;
+  const double ry = ay / ax;
+  const double mkc = -2.0 * (1.0 + ry);
+  const double gs = c.dt * ax;
+  for (int i = 0; i < nrects; ++i) {
+    const Rect r = rects[i];
+    if (r.empty()) continue;
+    RMA_CHECK_ARG(r.x0 >= 1 && r.x1 <= nx - 1 && r.y0 >= 1 && r.y1 <= ny - 1,
+                  "rect outside interior");
+    parallel_for(r.y0, r.y1, 64, [&](int64_t y) {
+      const double* up = T + (y - 1) * nx;
+      const double* cu = T + y * nx;
+      const double* dn = T + (y + 1) * nx;
+      const double* ic = iCp + y * nx;
+      double* out = T2 + y * nx;
+      for (int64_t x = r.x0; x < r.x1; ++x) {
+        const double g = gs * ic[x];
+        const double sx = cu[x + 1] + cu[x - 1];
+        const double sy = up[x] + dn[x];
+        double t = std::fma(mkc, cu[x], sx);
+        t = std::fma(ry, sy, t);
+        out[x] = std::fma(g, t, cu[x]);
+      }
+    });
+  }
+}
+
+void stencilk5_rects_cpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                         int64_t ny, const Rect* rects, int nrects, const StencilCoef& c) {
+  RMA_CHECK_ARG(K >= 1, "K=" << K);
+  RMA_CHECK_ARG(T2 != T, "multi-step update cannot run in place");
+  std::vector<double> a(T, T + nx * ny), b(a);
+  const Rect interior{1, nx - 1, 1, ny - 1};
+  for (int j = 1; j < K; ++j) {
+    stencil5_rects_cpu(b.data(), a.data(), iCp, nx, ny, &interior, 1, c);
+    a.swap(b);
+  }
+  stencil5_rects_cpu(T2, a.data(), iCp, nx, ny, rects, nrects, c);
+}
+
 void flux_cpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,
               double rdx, double rdy) {
   parallel_for(0, ny - 1, 64, [&](int64_t y) {

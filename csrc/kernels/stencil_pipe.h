@@ -1,0 +1,361 @@
+// Stage-pipelined K-step kernel for ANY K (2..kPipeMaxK), fast5 or canonical
+// arithmetic. Included by the stencil_pipe_*.hip translation units only.
+//
+// One block = one (strip, row-chunk) task; its S waves split the K time levels
+// of the strip: stage s < S-1 owns H = ceil(K/S) levels, the last stage the
+// remaining HL = K - (S-1)H (1 <= HL <= H). Stage 0 streams T and 1/Cp from
+// HBM, writes the per-strip factor ring (R = K+S-1 rows) in LDS and runs its
+// levels; stage s reads its input level from an LDS hand-off row that stage
+// s-1 wrote one row-iteration earlier and runs s(H+1) rows behind stage 0; the
+// last stage stores. One barrier per row iteration.
+//
+// Generalises kernels 6-8 of stencil_tbk.hip (fixed K in {8,12,16}, H = K/S)
+// so that the executor's pass planner (executor.cpp plan_passes) can run a
+// pass of any depth: e.g. the 20 timed steps of the driver's bench command as
+// ONE 20-step pass instead of 16 + 4 (each pass costs at least one HBM sweep
+// of the 3 arrays, ~41 ms at the 288 GB tile).
+//
+// Arithmetic (template Canon):
+//   false  fast5: T2 = fma(g, fma(r, U+D, fma(-2(1+r), c, L+R)), c), g = dt*lam/dx^2/Cp
+//          (LDS ring holds g, zero outside the interior). Bitwise equal to
+//          stencil_tbk.hip kernel 5 and to the CPU twin stencilk5_rects_cpu.
+//   true   the canonical flux form of rma/common.h (scripts/diffusion_2D_perf.jl:8-10
+//          with 1/Cp): x face flux shared with the left lane, y face flux
+//          carried from the previous row; bitwise equal to K one-step launches.
+//          The ring holds 1/Cp (zero outside the interior: c + dt*(0*...) == c).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "rma/kernels.h"
+#include "stencil_device.h"
+
+namespace rma {
+namespace pipe {
+using namespace march;
+
+template <int K, int S>
+struct Plan {
+  static constexpr int H = (K + S - 1) / S;       // levels of stages 0..S-2
+  static constexpr int HL = K - (S - 1) * H;      // levels of the last stage
+  static constexpr int R = K + S - 1;             // factor ring rows
+  static_assert(S >= 1 && HL >= 1 && HL <= H, "bad stage split");
+};
+
+// LDS bytes of one block (ring + double-buffered hand-off rows)
+template <int K, int S, int V>
+constexpr int lds_bytes() {
+  return (Plan<K, S>::R + 2 * (S > 1 ? S - 1 : 1)) * kWave * V * 8;
+}
+
+// Waves per SIMD to ask the compiler for: what the LDS allows (160 KiB per
+// CU, 4 SIMDs), capped by a VGPR estimate so the cap never forces spills:
+// fast5 3 rows x V cells x 2 dwords per level, stage 0's two-row prefetch,
+// ~40 for addressing and temporaries; canonical also the carried y flux and
+// the x fluxes (checked: no spills at any K, V, scripts/check_isa.py).
+template <int K, int S, int V, bool Canon>
+constexpr int waves_per_simd() {
+  constexpr int blocks = (160 * 1024) / lds_bytes<K, S, V>();
+  constexpr int by_lds = blocks * S / 4;
+  constexpr int vgpr = Canon ? 8 * Plan<K, S>::H * V + 8 * V + 64
+                             : 6 * Plan<K, S>::H * V + 8 * V + 40;
+  constexpr int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
+  constexpr int w = by_lds < by_vgpr ? by_lds : by_vgpr;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
+template <bool kDpp = true>
+__device__ __forceinline__ double from_next_lane(double v) {
+  // wave_shl:1 (lane i <- lane i+1); bound_ctrl: lane 63 reads 0 (invalid column)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+template <bool kDpp = true>
+__device__ __forceinline__ double from_prev_lane(double v) {
+  // wave_shr:1 (lane i <- lane i-1); lane 0 reads 0 (invalid column)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+
+template <int K, int S, int V, bool Canon>
+__device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double* __restrict__ T,
+                                          const double* __restrict__ iCp, int64_t nx, int64_t ny,
+                                          const RectList& L, const StencilCoef& k, int chunk_rows,
+                                          int remap) {
+  using P = Plan<K, S>;
+  constexpr int H = P::H, HL = P::HL, R = P::R;
+  constexpr int W = kWave * V;
+  constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_strip_tasks)
+  constexpr int NH = S > 1 ? S - 1 : 1;
+  const int stage = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  int ri = 0;
+  while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
+  const int64_t lb = b - (ri ? L.block_end[ri - 1] : 0);
+  const int64_t strip = lb % L.strips[ri], chunk = lb / L.strips[ri];
+  const Rect r = L.r[ri];
+  const int64_t xs = L.xa[ri] + strip * kStep;
+  const int64_t ya = r.y0 + chunk * chunk_rows;
+  const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
+
+  const int64_t x = xs + (int64_t)lane * V;
+  bool m[V], cin[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int p = lane * V + v;
+    m[v] = p >= K && p < K + kStep && x + v >= r.x0 && x + v < r.x1;
+    cin[v] = (x + v >= 1) && (x + v <= nx - 2);
+  }
+  const int64_t xl = min(max(x, (int64_t)0), nx - V);
+  const bool xin = xs >= 1 && xs + W - 1 <= nx - 2;  // no x-boundary cell in the strip
+
+  // fast5 constants (the host guarantees fast5_ok); canonical uses k directly
+  const double ax = (-k.mlam) * k.rdx * k.rdx;
+  const double ay = (-k.mlam) * k.rdy * k.rdy;
+  const double ry = Canon ? 0.0 : ay / ax;
+  const double mkc = -2.0 * (1.0 + ry);
+  const double gs = Canon ? 1.0 : k.dt * ax;
+
+  // w[0]: the stage's input level; w[j]: local level j (j < levels); slots
+  // rotate mod 3 with the row iteration (new row -> slot P, centre (P+2)%3,
+  // up (P+1)%3). Canon carries the y face flux fy[j] instead of reading `up`.
+  double w[H][3][V], fy[Canon ? H : 1][V], pT[V], pC[V], qT[V], qC[V];
+#pragma unroll
+  for (int j = 0; j < H; ++j)
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      w[j][0][v] = w[j][1][v] = w[j][2][v] = 0.0;
+      fy[Canon ? j : 0][v] = 0.0;
+    }
+  // 32-bit row bookkeeping (host checks ny < 2^30): no 64-bit VALU compares
+  const int ny32 = (int)ny, ya32 = (int)ya, yb32 = (int)yb;
+  int i = ya32 - K;
+  const int iend = yb32 + K - 3 + S;
+  auto rowc = [&](int y) { return (int64_t)min(max(y, 0), ny32 - 1); };
+  if (stage == 0) {
+    load_row<V>(w[0][2], T + rowc(i) * nx + xl);
+    load_row<V>(pT, T + rowc(i + 1) * nx + xl);
+    load_row<V>(pC, iCp + rowc(i) * nx + xl);
+    load_row<V>(qT, T + rowc(i + 2) * nx + xl);
+    load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
+  }
+  __shared__ double ring[R * W];
+  __shared__ double hand[2][NH][W];
+  for (int t = threadIdx.x; t < R * W; t += S * kWave) ring[t] = 0.0;
+  for (int t = threadIdx.x; t < 2 * NH * W; t += S * kWave) (&hand[0][0][0])[t] = 0.0;
+  __syncthreads();
+  // LDS rows are lane-interleaved (cell pair h of lane l at dbl2 slot h*64+l):
+  // every ds_read/write_b128 covers 1 KiB contiguously, no bank conflicts
+  auto rd2 = [&](const double* row, double (&out)[V]) {
+    if constexpr (V == 1) {
+      out[0] = row[lane];
+    } else {
+#pragma unroll
+      for (int h = 0; h < V / 2; ++h) {
+        const dbl2 t2 = reinterpret_cast<const dbl2*>(row)[h * kWave + lane];
+        out[2 * h] = t2.x;
+        out[2 * h + 1] = t2.y;
+      }
+    }
+  };
+  auto wr2 = [&](double* row, const double (&in)[V]) {
+    if constexpr (V == 1) {
+      row[lane] = in[0];
+    } else {
+#pragma unroll
+      for (int h = 0; h < V / 2; ++h) {
+        dbl2 t2;
+        t2.x = in[2 * h];
+        t2.y = in[2 * h + 1];
+        reinterpret_cast<dbl2*>(row)[h * kWave + lane] = t2;
+      }
+    }
+  };
+  int slot0 = 0;  // ring slot of row i (stage 0's level-1 row)
+  int par = 0;
+  const int lag = stage * (H + 1);  // rows behind stage 0
+
+  auto iter = [&](auto Pc, auto S0c, auto LASTc) {
+    constexpr int Pr = decltype(Pc)::value;
+    constexpr bool S0 = decltype(S0c)::value;
+    constexpr bool LAST = decltype(LASTc)::value;
+    constexpr int NL = LAST ? HL : H;  // levels of this stage
+    constexpr int PC = (Pr + 2) % 3, PU = (Pr + 1) % 3;
+    double g[V];
+    if constexpr (S0) {
+      const bool rin1 = i >= 1 && i <= ny32 - 2;
+#pragma unroll
+      for (int v = 0; v < V; ++v) w[0][Pr][v] = pT[v];
+      if (rin1 && xin) {  // wave-uniform: no per-cell selects away from the x edges
+#pragma unroll
+        for (int v = 0; v < V; ++v) g[v] = Canon ? pC[v] : gs * pC[v];
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? (Canon ? pC[v] : gs * pC[v]) : 0.0;
+      }
+      wr2(ring + slot0 * W, g);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        pT[v] = qT[v];
+        pC[v] = qC[v];
+      }
+      load_row<V>(qT, T + rowc(i + 3) * nx + xl);
+      load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
+    } else {
+      rd2(&hand[par ^ 1][stage - 1][0], w[0][Pr]);
+    }
+    int sbase = slot0 - (S0 ? 0 : lag);
+    sbase = sbase < 0 ? sbase + R : sbase;
+    auto ring_row = [&](int j) {  // factor row of local level j
+      const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
+      return ring + sl * W;
+    };
+    // factors read one level ahead (LDS latency under the previous level's
+    // arithmetic); stage 0's level-1 factors are still in registers
+    double gn[V];
+    if constexpr (S0) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) gn[v] = g[v];
+    } else {
+      rd2(ring_row(1), gn);
+    }
+#pragma unroll
+    for (int j = 1; j <= NL; ++j) {
+      const int row = i - (S0 ? 0 : lag) - (j - 1);
+      double gl[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) gl[v] = gn[v];
+      if (j < NL) rd2(ring_row(j + 1), gn);
+      const double(&c)[V] = w[j - 1][PC];
+      const double(&dn)[V] = w[j - 1][Pr];
+      double res[V];
+      if constexpr (!Canon) {
+        const double(&up)[V] = w[j - 1][PU];
+        const double rn = from_next_lane(c[0]);
+        const double ln = from_prev_lane(c[V - 1]);
+        double sx[V], sy[V], t[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const double rv = v + 1 < V ? c[v + 1] : rn;
+          const double lv = v > 0 ? c[v - 1] : ln;
+          sx[v] = rv + lv;
+          sy[v] = up[v] + dn[v];
+        }
+        // the V cells' FMA chains interleaved (sched_barrier keeps them apart)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int v = 0; v < V; ++v) t[v] = __builtin_fma(mkc, c[v], sx[v]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, sy[v], t[v]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int v = 0; v < V; ++v) res[v] = __builtin_fma(gl[v], t[v], c[v]);
+      } else {
+        // canonical: same expressions and rounding as rma/common.h
+        const double rn = from_next_lane(c[0]);
+        double qr[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const double rv = v + 1 < V ? c[v + 1] : rn;
+          qr[v] = (k.mlam * (rv - c[v])) * k.rdx;  // qxR of cell v == qxL of cell v+1
+        }
+        const double ql0 = from_prev_lane(qr[V - 1]);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const double qU = (k.mlam * (dn[v] - c[v])) * k.rdy;
+          const double qD = fy[j - 1][v];  // qyU of the previous row
+          fy[j - 1][v] = qU;
+          const double qL = v == 0 ? ql0 : qr[v - 1];
+          res[v] = c[v] + k.dt * (gl[v] * ((-(qr[v] - qL)) * k.rdx - (qU - qD) * k.rdy));
+        }
+      }
+      if (j < NL) {
+        const int jj = j < NL ? j : NL - 1;
+#pragma unroll
+        for (int v = 0; v < V; ++v) w[jj][Pr][v] = res[v];
+      } else if constexpr (!LAST) {
+        wr2(&hand[par][S0 ? 0 : stage][0], res);
+      } else if (row >= ya32 && row < yb32) {
+        store_row<V, true>(T2 + (int64_t)row * nx + x, res, m);
+      }
+    }
+    slot0 = slot0 + 1 == R ? 0 : slot0 + 1;
+    par ^= 1;
+    __syncthreads();  // hand-off and ring rows visible; this iteration's reads done
+  };
+  // one row loop per stage role (stage is wave-uniform; every copy passes the
+  // same barriers): stage 0 carries the HBM prefetch registers, the others not
+  auto run = [&](auto S0c, auto LASTc) {
+    for (;;) {
+      iter(std::integral_constant<int, 0>{}, S0c, LASTc);
+      if (++i > iend) break;
+      iter(std::integral_constant<int, 1>{}, S0c, LASTc);
+      if (++i > iend) break;
+      iter(std::integral_constant<int, 2>{}, S0c, LASTc);
+      if (++i > iend) break;
+    }
+  };
+  if constexpr (S == 1) {
+    run(std::true_type{}, std::true_type{});
+  } else {
+    if (stage == 0)
+      run(std::true_type{}, std::false_type{});
+    else if (stage == S - 1)
+      run(std::false_type{}, std::true_type{});
+    else if constexpr (S > 2)
+      run(std::false_type{}, std::false_type{});
+  }
+}
+
+template <int K, int S, int V, bool Canon>
+__global__ __launch_bounds__(kWave * S) __attribute__((amdgpu_waves_per_eu(
+    waves_per_simd<K, S, V, Canon>()))) void pipe_kernel(double* __restrict__ T2,
+                                                   const double* __restrict__ T,
+                                                   const double* __restrict__ iCp, int64_t nx,
+                                                   int64_t ny, RectList L, StencilCoef k,
+                                                   int chunk_rows, int remap) {
+  pipe_body<K, S, V, Canon>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
+}
+
+struct PipeLaunch {
+  double* T2;
+  const double* T;
+  const double* iCp;
+  int64_t nx, ny;
+  const RectList* L;
+  StencilCoef k;
+  int chunk_rows, remap;
+  int64_t blocks;
+  hipStream_t stream;
+};
+
+template <int K, int S, int V, bool Canon>
+void launch(const PipeLaunch& a) {
+  pipe_kernel<K, S, V, Canon><<<dim3((unsigned)a.blocks), dim3(kWave * S), 0, a.stream>>>(
+      a.T2, a.T, a.iCp, a.nx, a.ny, *a.L, a.k, a.chunk_rows, a.remap);
+}
+
+// Each stencil_pipe_*.hip unit instantiates a range of (K, S) and answers
+// for it: returns false if it does not hold (K, S, V, canon).
+bool dispatch_a(int K, int S, int V, bool canon, const PipeLaunch& a);
+bool dispatch_b(int K, int S, int V, bool canon, const PipeLaunch& a);
+bool dispatch_c(int K, int S, int V, bool canon, const PipeLaunch& a);
+bool dispatch_d(int K, int S, int V, bool canon, const PipeLaunch& a);
+
+}  // namespace pipe
+}  // namespace rma
+
+// (K, S) -> launch<K, S, V, Canon> for V in {1, 2, 4}
+#define RMA_PIPE_CASE(KK, SS, CC)                                  \
+  if (K == KK && S == SS && canon == CC) {                         \
+    if (V == 4) launch<KK, SS, 4, CC>(a);                          \
+    else if (V == 2) launch<KK, SS, 2, CC>(a);                     \
+    else launch<KK, SS, 1, CC>(a);                                 \
+    return true;                                                   \
+  }

@@ -1,0 +1,75 @@
+// Host side of the any-K stage-pipelined kernel (stencil_pipe.h): argument
+// checks, strip/chunk planning and the (K, S, V, arithmetic) dispatch over the
+// instantiation units stencil_pipe_{a,b,c,d}.hip.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "rma/hip_check.h"
+#include "rma/kernels.h"
+#include "stencil_pipe.h"
+
+namespace rma {
+
+int pipe_default_stages(int K) {
+  // Waves per strip: 1, 2 or 4 only. A block of 3, 5 or 6 waves puts two of
+  // its stages on one SIMD (waves are dealt round-robin over the 4 SIMDs of a
+  // CU) and the per-row barrier then runs the whole block at that SIMD's pace:
+  // K=17..20 with 5 stages took 103-118 ms per pass at 101376^2 against 76 ms
+  // for K=20 on 4 stages of 5 levels (profiles/pass_sweep_r2.json). Deeper
+  // stages amortise the per-row barrier and hand-off: K=24 on 4 stages of 6
+  // levels (2 waves per SIMD) has the lowest time per step of all depths.
+  if (K <= 4) return 1;
+  if (K <= 9) return 2;  // K=9 on 4 stages would leave the last one empty
+  return 4;
+}
+
+bool pipe_has(int K, int S) {
+  if (K < 1 || K > kPipeMaxK) return false;
+  if (S == pipe_default_stages(K)) return true;
+  // alternative stage splits instantiated for sweeps (stencil_pipe_d.hip)
+  return (K == 12 && S == 3) || (K == 16 && S == 8) || (K == 24 && S == 8) ||
+         (K == 8 && S == 4) || (K == 8 && S == 1);
+}
+
+void stencil_pipe_rects_gpu(int K, int stages, bool canonical, double* T2, const double* T,
+                            const double* iCp, int64_t nx, int64_t ny, const Rect* rects,
+                            int nrects, const StencilCoef& c, const StencilTuning& tune,
+                            stream_t stream) {
+  const int S = stages > 0 ? stages : pipe_default_stages(K);
+  RMA_CHECK_ARG(K >= 1 && K <= kPipeMaxK,
+                "pipelined K-step kernel: 1 <= K <= " << kPipeMaxK << ", got " << K);
+  RMA_CHECK_ARG(pipe_has(K, S), "no pipelined kernel instantiated for K=" << K << " S=" << S);
+  RMA_CHECK_ARG(canonical || fast5_ok(c),
+                "the fast5 arithmetic folds dy^-2/dx^-2 into one factor: needs lam != 0 and "
+                "finite coefficients");
+  RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
+  RMA_CHECK_ARG(nx >= 3 && ny >= 3, "grid too small: nx=" << nx << " ny=" << ny);
+  RMA_CHECK_ARG(ny < (int64_t(1) << 30), "rows are indexed in 32 bits, ny = " << ny);
+  RMA_CHECK_ARG(T2 != T, "multi-step kernel cannot run in place");
+  RMA_CHECK_ARG(tune.chunk_rows >= 1, "chunk_rows=" << tune.chunk_rows);
+  for (int i = 0; i < nrects; ++i) {
+    const Rect& r = rects[i];
+    if (r.empty()) continue;
+    RMA_CHECK_ARG(r.x0 >= 1 && r.x1 <= nx - 1 && r.y0 >= 1 && r.y1 <= ny - 1,
+                  "rect " << i << " outside the interior of " << nx << "x" << ny);
+  }
+  const bool aligned = ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
+                       ((reinterpret_cast<uintptr_t>(T2) & 15) == 0) &&
+                       ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
+  int V = 1;
+  if (aligned && nx % 2 == 0) V = (tune.vec == 4 && nx % 4 == 0) ? 4 : 2;
+  const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
+  march::RectList L;
+  const int64_t ntask = march::plan_strip_tasks(L, rects, nrects, V, tune.chunk_rows, K);
+  if (L.n == 0) return;
+  RMA_CHECK_ARG(ntask < (int64_t(1) << 31), "grid too large: " << ntask << " blocks");
+  pipe::PipeLaunch a{T2, T, iCp, nx, ny, &L, c, tune.chunk_rows, remap, ntask, as_stream(stream)};
+  const bool ok = pipe::dispatch_a(K, S, V, canonical, a) || pipe::dispatch_b(K, S, V, canonical, a) ||
+                  pipe::dispatch_c(K, S, V, canonical, a) || pipe::dispatch_d(K, S, V, canonical, a);
+  RMA_CHECK_ARG(ok, "pipelined kernel K=" << K << " S=" << S << " V=" << V << " canonical="
+                                           << canonical << " not instantiated");
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+}  // namespace rma

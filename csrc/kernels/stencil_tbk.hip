@@ -657,18 +657,17 @@ __global__ __launch_bounds__(kBlock) void stencilk_ovl_kernel(
 
 }  // namespace
 
-bool fast5_ok(const StencilCoef& c) {
-  const double ax = (-c.mlam) * c.rdx * c.rdx, ay = (-c.mlam) * c.rdy * c.rdy;
-  return ax != 0.0 && std::isfinite(ax) && std::isfinite(ay) && std::isfinite(ay / ax) &&
-         std::isfinite(c.dt * ax);
-}
-
 void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
                         int64_t ny, const Rect* rects, int nrects, const StencilCoef& c,
                         const StencilTuning& tune, stream_t stream) {
+  RMA_CHECK_ARG(tune.kernel >= 0 && tune.kernel <= 10, "unknown K-step kernel " << tune.kernel);
+  if (tune.kernel >= 9) {  // any-K stage-pipelined kernels (stencil_pipe.h)
+    stencil_pipe_rects_gpu(K, tune.stages, tune.kernel == 10, T2, T, iCp, nx, ny, rects, nrects,
+                           c, tune, stream);
+    return;
+  }
   RMA_CHECK_ARG(K == 2 || K == 3 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16,
-                "steps per pass must be 2, 3, 4, 6, 8, 12 or 16, got " << K);
-  RMA_CHECK_ARG(tune.kernel >= 0 && tune.kernel <= 8, "unknown K-step kernel " << tune.kernel);
+                "steps per pass must be 2, 3, 4, 6, 8, 12 or 16 (any K: kernels 9/10), got " << K);
   RMA_CHECK_ARG(K <= 8 || tune.kernel >= 5,
                 "12 or 16 steps per pass need a fast5 kernel (kernel 5, 6, 7 or 8), got kernel "
                     << tune.kernel);

@@ -53,6 +53,12 @@ int rccl_version() {
   return v;
 }
 
+std::string device_pci_bus_id(int device) {
+  char buf[64] = {0};
+  RMA_HIP_CHECK(hipDeviceGetPCIBusId(buf, (int)sizeof(buf) - 1, device));
+  return std::string(buf);
+}
+
 std::string RcclComm::unique_id() {
   ncclUniqueId id;
   RMA_NCCL_CHECK(ncclGetUniqueId(&id));

@@ -3,10 +3,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
-#include <array>
 #include <utility>
 
 #include "rma/hip_check.h"
@@ -35,22 +36,31 @@ StencilTuning default_tune_k(int K, int64_t ny) {
   if (ny < 3072) t.chunk_rows = 16;
   else if (ny < 6144) t.chunk_rows = 32;
   else if (ny < 12288) t.chunk_rows = 64;
-  else if (ny < 32768) t.chunk_rows = K == 8 ? 128 : 256;  // K=12/16: c256 (profiles/sweep_deepk_16k)
-  else if (K == 16 && ny >= 98304) t.chunk_rows = 1536;  // 288 GB tile: 63.8 vs 64.5 ms (c1024)
+  else if (ny < 32768) t.chunk_rows = K <= 8 ? (K == 8 ? 128 : 256) : 256;  // K>=12: c256
+  else if (K >= 20 && ny >= 98304) t.chunk_rows = 3072;  // K=20/24: 73.3/84.3 vs 73.8/84.8 ms (c1536)
+  else if (K >= 12 && ny >= 98304) t.chunk_rows = 1536;  // 288 GB tile: 63.8 vs 64.5 ms (c1024)
   else t.chunk_rows = K >= 8 ? 1024 : 512;
   return t;
 }
 
 StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c) {
-  StencilTuning t = default_tune_k(K, ny);
-  if (K <= 1) return t;
+  StencilTuning t = default_tune_k(std::max(K, 3), ny);
   t.xcd_remap = 1;
-  if (!fast5_ok(c)) {
-    t.kernel = 4;
-    return t;
+  if (!fast5_ok(c)) return canonical_tune_k(K, ny);
+  t.kernel = 9;  // stage-pipelined fast5, any K (stencil_pipe.h)
+  t.vec = 4;
+  return t;
+}
+
+StencilTuning canonical_tune_k(int K, int64_t ny) {
+  StencilTuning t = default_tune_k(K, ny);
+  // kernel 3 wins at K = 3, 4; the canonical pipelined kernel from K = 5 on
+  // (K=6: 47.2 vs 48.9 ms, K=8: 55.9 vs 59.8 ms per pass at 101376^2,
+  // profiles/pass_sweep_r2.json)
+  if (K >= 5) {
+    t.kernel = 10;
+    t.vec = 4;
   }
-  t.kernel = K == 16 ? 7 : K == 12 ? 6 : 5;
-  t.vec = K >= 12 ? 4 : 2;
   return t;
 }
 
@@ -66,62 +76,40 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   RMA_CHECK_ARG(!p.use_graph || !halo || halo->capturable(),
                 "hipGraph replay needs a capturable halo transport (RCCL or none); the loopback "
                 "transport synchronises on the host");
-  RMA_CHECK_ARG(p.temporal == 1 || p.temporal == 2 || p.temporal == 3 || p.temporal == 4 ||
-                    p.temporal == 6 || p.temporal == 8 || p.temporal == 12 || p.temporal == 16,
-                "temporal (steps per pass) must be 1, 2, 3, 4, 6, 8, 12 or 16, got "
-                    << p.temporal);
-  RMA_CHECK_ARG(p.temporal <= 8 || (p.fast_math && fast5_ok(p.coef)),
-                "12 or 16 steps per pass run on the fast5 kernel only: needs fast_math and "
-                "lam != 0");
+  RMA_CHECK_ARG(p.temporal >= 1 && p.temporal <= kPipeMaxK,
+                "temporal (max steps per pass) must be 1.." << kPipeMaxK << ", got " << p.temporal);
   RMA_CHECK_ARG(p.temporal == 1 || p.mode != Mode::kKp,
                 "temporal blocking applies to perf / perf_hide, not kp");
   RMA_CHECK_ARG(p.olx >= 2 && p.oly >= 2, "overlaps must be >= 2");
+  RMA_CHECK_ARG(p.temporal == 1 || ny < (int64_t(1) << 30),
+                "K-step passes index rows in 32 bits, ny = " << ny);
   hwx_ = hwy_ = p.temporal;  // halo width = steps per exchange
-  // fast_math: the 5-point-sum kernels (5 fp64 ops per cell update) unless the
-  // coefficients cannot be folded (lam == 0), then the reassociated-flux one
-  if (p_.fast_math && p.temporal > 1) {
-    const StencilTuning f = fast_tune_k(p.temporal, ny, p.coef);
-    p_.tune2.kernel = f.kernel;
-    p_.tune2.vec = f.vec;
-    p_.tune2.xcd_remap = f.xcd_remap;
-  }
-  std::array<std::array<int, 2>, 3> nbr{{{-1, -1}, {-1, -1}, {-1, -1}}};
-  if (halo) nbr = halo->neighbors();
+  if (halo) nbr_ = halo->neighbors();
+  real_nbr_ = nbr_;
   const int64_t ol[2] = {p.olx, p.oly};
   for (int d = 0; d < 2; ++d)
-    RMA_CHECK_ARG((nbr[d][0] < 0 && nbr[d][1] < 0) || ol[d] >= 2 * p.temporal,
+    RMA_CHECK_ARG((nbr_[d][0] < 0 && nbr_[d][1] < 0) || ol[d] >= 2 * p.temporal,
                   "temporal=" << p.temporal << " needs a grid overlap >= " << 2 * p.temporal
                               << " along dim " << d << " (init_global_grid overlaps=2K, "
                               << "halowidths=K), got " << ol[d]);
   full_ = {1, nx - 1, 1, ny - 1};
-  // perf_hide: the frame must contain the send planes [ol-hw, ol) of every
-  // side, so it is at least ol-1 cells wide (the reference's b_width >= overlap
-  // invariant); minimal frames otherwise (width 1 for ol=2:
-  // thin x-frames run in the kernel's column mode, profiles/).
+  // perf_hide one-step updates: the frame must contain the send planes
+  // [ol-hw, ol) of every side, so it is at least ol-1 cells wide (the
+  // reference's b_width >= overlap invariant); minimal frames
+  // otherwise (width 1 for ol=2: thin x-frames run in the kernel's column mode)
   if (p.mode == Mode::kHide) {
     RMA_CHECK_ARG(p.bwx >= 1 && p.bwy >= 1,
                   "b_width must be >= 1 so the send planes belong to the boundary kernel");
-    split(full_, std::max(p.bwx, p.olx - 1), std::max(p.bwy, p.oly - 1), frame_, interior_);
+    split_rect(full_, std::max(p.bwx, p.olx - 1), std::max(p.bwy, p.oly - 1), frame_, interior_);
   } else {
     interior_ = full_;
   }
-  if (p.temporal > 1) {
-    // owned rect of a K-step pass: next to a neighbour the K cells [0,K) are
-    // halo and only the exchange refreshes them (level j is valid from
-    // column j on, so the pass outputs from column K)
-    const int64_t K = p.temporal;
-    out2_ = {nbr[0][0] >= 0 ? K : 1, nx - (nbr[0][1] >= 0 ? K : 1),
-             nbr[1][0] >= 0 ? K : 1, ny - (nbr[1][1] >= 0 ? K : 1)};
-    RMA_CHECK_ARG(!out2_.empty(), "tile too small for temporal blocking: " << nx << "x" << ny);
-    // perf_hide with no neighbour at all has nothing to overlap: the frame
-    // launch would only compete with the interior (measured ~1% of a K=16 pass
-    // at the 288 GB tile, rocprofv3 trace), so one launch covers the owned rect
-    const bool any_nbr = nbr[0][0] >= 0 || nbr[0][1] >= 0 || nbr[1][0] >= 0 || nbr[1][1] >= 0;
-    if (p.mode == Mode::kHide && any_nbr)
-      split(out2_, std::max(p.bwx, p.olx - out2_.x0), std::max(p.bwy, p.oly - out2_.y0),
-            frame2_, interior2_);
-    else
-      interior2_ = out2_;
+  if (p.temporal > 1 || fast5()) {
+    cost_ = default_pass_costs(p.temporal, fast5());
+    apply_cost_overrides(cost_, std::getenv("RMA_PASS_COSTS"));
+    geom_.resize(p.temporal + 1);
+    geom_ok_.assign(p.temporal + 1, 0);
+    (void)geometry(p.temporal);  // throws now if the tile is too small
   }
   int least = 0, greatest = 0;
   RMA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -156,9 +144,12 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   e_hi_ = a;
   e_lo_ = b;
   e_in_ = c;
+  const char* pr = std::getenv("RMA_EXEC_PRIME");
+  if (!(pr && pr[0] == '0')) prime();
 }
 
 DiffusionExecutor::~DiffusionExecutor() {
+  release_timing();
   if (graph_exec_) (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec_));
   if (e_hi_) (void)hipEventDestroy(E(e_hi_));
   if (e_lo_) (void)hipEventDestroy(E(e_lo_));
@@ -167,199 +158,306 @@ DiffusionExecutor::~DiffusionExecutor() {
   if (s_lo_) (void)hipStreamDestroy(S(s_lo_));
 }
 
-void DiffusionExecutor::split(const Rect& out, int64_t bwx, int64_t bwy,
-                              std::vector<Rect>& frame, Rect& interior) const {
-  const int64_t xi0 = out.x0 + bwx, xi1 = out.x1 - bwx;
-  const int64_t yi0 = out.y0 + bwy, yi1 = out.y1 - bwy;
-  if (xi0 >= xi1 || yi0 >= yi1) {
-    interior = {0, 0, 0, 0};
-    frame = {out};
-  } else {
-    interior = {xi0, xi1, yi0, yi1};
-    frame = {{out.x0, out.x1, out.y0, yi0},
-             {out.x0, out.x1, yi1, out.y1},
-             {out.x0, xi0, yi0, yi1},
-             {xi1, out.x1, yi0, yi1}};
-  }
+bool DiffusionExecutor::fast5() const {
+  return p_.fast_math && p_.mode != Mode::kKp && fast5_ok(p_.coef);
 }
 
-namespace {
-HaloField field_of(double* A, int64_t nx, int64_t ny, int64_t olx, int64_t oly, int64_t hwx,
-                   int64_t hwy) {
-  HaloField f;
-  f.ptr = A;
-  f.size = {nx, ny, 1};
-  f.elem_bytes = 8;
-  f.ol = {olx, oly, 2};
-  f.hw = {hwx, hwy, 1};
-  return f;
+const PassGeom& DiffusionExecutor::geometry(int K) {
+  RMA_CHECK_ARG(K >= 1 && K < (int)geom_.size(), "pass depth " << K);
+  if (!geom_ok_[K]) {
+    geom_[K] = pass_geometry(nx_, ny_, K, nbr_, p_.mode == Mode::kHide, p_.bwx, p_.bwy, p_.olx,
+                             p_.oly);
+    geom_ok_[K] = 1;
+  }
+  return geom_[K];
 }
-}  // namespace
+
+std::vector<int> DiffusionExecutor::plan(int64_t nsteps) const {
+  if (p_.mode == Mode::kKp || cost_.empty()) return std::vector<int>((size_t)nsteps, 1);
+  return plan_passes(nsteps, cost_);
+}
+
+StencilTuning DiffusionExecutor::pass_tuning(int K, bool frame) const {
+  StencilTuning t = fast5() ? fast_tune_k(K, ny_, p_.coef) : canonical_tune_k(K, ny_);
+  t.nontemporal = p_.tune2.nontemporal;
+  if (p_.chunk_rows2 > 0) t.chunk_rows = p_.chunk_rows2;
+  if (K == 2 && !fast5()) t.unroll = p_.tune2.unroll;
+  if (frame) {
+    // the x-frames are ~2K columns wide: the narrowest strip (2 cells per
+    // lane) wastes the least recomputation, short chunks keep the launch
+    // small; the frame ends long before the interior (1.6 of ~64 ms per pass
+    // at the 288 GB tile)
+    t.chunk_rows = std::min(t.chunk_rows, 64);
+    if (t.kernel >= 6) t.vec = std::min(t.vec, 2);
+  }
+  return t;
+}
 
 void DiffusionExecutor::exchange(double* A, stream_t s) {
-  if (!halo_) return;
-  halo_->exchange({field_of(A, nx_, ny_, p_.olx, p_.oly, hwx_, hwy_)}, s, 3);
+  if (!halo_ || solo_) return;
+  HaloField f;
+  f.ptr = A;
+  f.size = {nx_, ny_, 1};
+  f.elem_bytes = 8;
+  f.ol = {p_.olx, p_.oly, 2};
+  f.hw = {hwx_, hwy_, 1};
+  halo_->exchange({f}, s, 3);
 }
 
 void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
   const StencilCoef& c = p_.coef;
-  switch (p_.mode) {
-    case Mode::kPerf: {
-      TraceRange tr("rma.step.perf");
-      stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &full_, 1, c, p_.tune, s_lo_);
-      exchange(Tout, s_lo_);
-      break;
-    }
-    case Mode::kKp: {
-      TraceRange tr("rma.step.kp");
-      flux_gpu(qx_, qy_, Tin, nx_, ny_, c.mlam, c.rdx, c.rdy, s_lo_);
-      residual_gpu(dTdt_, qx_, qy_, iCp_, nx_, ny_, c.rdx, c.rdy, s_lo_);
-      update_gpu(Tin, dTdt_, nx_, ny_, c.dt, s_lo_);
-      exchange(Tin, s_lo_);
-      break;
-    }
-    case Mode::kHide: {
-      TraceRange tr("rma.step.hide");
-      // previous step fully done on both streams before this one touches T/T2
-      RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
-      RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
-      StencilTuning ft = p_.tune;
-      ft.chunk_rows = std::min(ft.chunk_rows, 16);
-      {
-        TraceRange tb("rma.boundary");
-        stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, frame_.data(), (int)frame_.size(), c, ft,
-                          s_hi_);
-      }
-      {
-        TraceRange th("rma.halo");
-        exchange(Tout, s_hi_);
-      }
-      RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
-      if (!interior_.empty()) {
-        TraceRange ti("rma.interior");
-        stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &interior_, 1, c, p_.tune, s_lo_);
-      }
-      RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
-      break;
-    }
-  }
-}
-
-void DiffusionExecutor::multi_step(double* Tin, double* Tout, const Rect* rects, int n,
-                                   const StencilTuning& tn, void* stream) {
-  if (p_.temporal == 2 && !p_.fast_math)  // dedicated two-step kernel: faster at K=2
-    stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, rects, n, p_.coef, tn, stream);
-  else
-    stencilk_rects_gpu(p_.temporal, Tout, Tin, iCp_, nx_, ny_, rects, n, p_.coef, tn, stream);
-}
-
-void DiffusionExecutor::enqueue_step2(double* Tin, double* Tout) {
-  if (p_.mode == Mode::kPerf) {
-    TraceRange tr("rma.stepK.perf");
-    multi_step(Tin, Tout, &out2_, 1, p_.tune2, s_lo_);
-    exchange(Tout, s_lo_);
+  if (p_.mode == Mode::kKp) {
+    TraceRange tr("rma.step.kp");
+    flux_gpu(qx_, qy_, Tin, nx_, ny_, c.mlam, c.rdx, c.rdy, s_lo_);
+    residual_gpu(dTdt_, qx_, qy_, iCp_, nx_, ny_, c.rdx, c.rdy, s_lo_);
+    update_gpu(Tin, dTdt_, nx_, ny_, c.dt, s_lo_);
+    exchange(Tin, s_lo_);
     return;
   }
-  TraceRange tr("rma.stepK.hide");
+  void* ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (timing_) {
+    for (auto& e : ev) e = tevent();
+    if (ev[4]) tk_.push_back(1);
+  }
+  auto rec = [&](int i, void* stream) {
+    if (ev[4]) RMA_HIP_CHECK(hipEventRecord(E(ev[i]), S(stream)));
+  };
+  if (p_.mode == Mode::kPerf || solo_) {
+    TraceRange tr("rma.step.perf");
+    if (p_.mode == Mode::kHide) {  // solo perf_hide: one launch, streams joined
+      RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+    }
+    rec(0, s_lo_);
+    rec(1, s_lo_);
+    rec(3, s_lo_);
+    stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &full_, 1, c, p_.tune, s_lo_);
+    rec(4, s_lo_);
+    exchange(Tout, s_lo_);
+    rec(2, s_lo_);
+    if (p_.mode == Mode::kHide) {
+      RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+      RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
+      RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
+    }
+    return;
+  }
+  TraceRange tr("rma.step.hide");
+  // previous step fully done on both streams before this one touches T/T2
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
-  // frame tuning: the x-frames are ~2K columns wide, so the narrowest strip
-  // (2 cells per lane: 128 columns) wastes the least recomputation, and the
-  // interior's long row chunks keep the launch small; the frame still ends
-  // long before the interior (1.6 of ~64 ms per pass at the 288 GB tile)
-  StencilTuning ft = p_.tune2;
-  ft.chunk_rows = std::min(ft.chunk_rows, 64);
-  if (ft.kernel >= 6) ft.vec = std::min(ft.vec, 2);
+  rec(0, s_hi_);
+  StencilTuning ft = p_.tune;
+  ft.chunk_rows = std::min(ft.chunk_rows, 16);
   {
     TraceRange tb("rma.boundary");
-    multi_step(Tin, Tout, frame2_.data(), (int)frame2_.size(), ft, s_hi_);
+    stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, frame_.data(), (int)frame_.size(), c, ft, s_hi_);
   }
+  rec(1, s_hi_);
   {
     TraceRange th("rma.halo");
     exchange(Tout, s_hi_);
   }
+  rec(2, s_hi_);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
-  if (!interior2_.empty()) {
+  rec(3, s_lo_);
+  if (!interior_.empty()) {
     TraceRange ti("rma.interior");
-    multi_step(Tin, Tout, &interior2_, 1, p_.tune2, s_lo_);
+    stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &interior_, 1, c, p_.tune, s_lo_);
   }
+  rec(4, s_lo_);
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
 }
 
-void DiffusionExecutor::run_eager(int64_t nsteps) {
-  for (int64_t i = 0; i < nsteps;) {
-    if (p_.mode == Mode::kKp) {
-      enqueue_step(T_, nullptr);
-      ++steps_;
-      ++i;
-      continue;
-    }
-    double* Tin = parity_ ? T2_ : T_;
-    double* Tout = parity_ ? T_ : T2_;
-    const int64_t left = nsteps - i;
-    if (p_.temporal > 1 && left >= p_.temporal) {
-      enqueue_step2(Tin, Tout);
-      steps_ += p_.temporal;
-      i += p_.temporal;
-    } else if (p_.temporal > 1 && left >= 2) {
-      // remainder: one shorter pass (K' < K steps; the width-K exchange then
-      // rewrites [K', K) with the identical values the neighbour owns)
-      const int kr = left >= 12 ? 12 : left >= 8 ? 8 : left >= 6 ? 6 : left >= 4 ? 4
-                     : left >= 3 ? 3 : 2;
-      TraceRange tr("rma.stepK.rest");
-      if (p_.mode == Mode::kHide) {  // previous pass done on both streams
-        RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
-      }
-      Rect out = out2_;
-      const auto& nb = halo_ ? halo_->neighbors() : std::array<std::array<int, 2>, 3>{};
-      if (halo_) {
-        out = {nb[0][0] >= 0 ? kr : 1, nx_ - (nb[0][1] >= 0 ? kr : 1), nb[1][0] >= 0 ? kr : 1,
-               ny_ - (nb[1][1] >= 0 ? kr : 1)};
-      }
-      StencilTuning tn = p_.tune2;
-      if (kr == 2 && !p_.fast_math) {
-        tn.chunk_rows = 16;
-        tn.xcd_remap = -1;
-        stencil2_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
-      } else {
-        tn.xcd_remap = 1;
-        tn.kernel = 3;
-        if (p_.fast_math) {
-          const StencilTuning f = fast_tune_k(kr, ny_, p_.coef);
-          tn.kernel = f.kernel;
-          tn.vec = f.vec;
-        }
-        stencilk_rects_gpu(kr, Tout, Tin, iCp_, nx_, ny_, &out, 1, p_.coef, tn, s_lo_);
-      }
-      exchange(Tout, s_lo_);
-      if (p_.mode == Mode::kHide) {
-        RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
-        RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
-        RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
-      }
-      steps_ += kr;
-      i += kr;
-    } else {
-      // one step (also the remainder of a temporal run: with overlap 2K and
-      // halo width K the single-step update + exchange stays consistent)
-      enqueue_step(Tin, Tout);
-      ++steps_;
-      ++i;
-    }
-    parity_ ^= 1;
-  }
+void DiffusionExecutor::multi_step(int K, double* Tin, double* Tout, const double* iCp,
+                                   int64_t nx, int64_t ny, const Rect* rects, int n,
+                                   const StencilTuning& tn, void* stream) const {
+  if (K == 2 && tn.kernel < 5)  // dedicated two-step kernel: faster at K=2
+    stencil2_rects_gpu(Tout, Tin, iCp, nx, ny, rects, n, p_.coef, tn, stream);
+  else
+    stencilk_rects_gpu(K, Tout, Tin, iCp, nx, ny, rects, n, p_.coef, tn, stream);
 }
 
-void DiffusionExecutor::build_graph(int64_t steps) {
+void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
+  const PassGeom& g = geometry(K);
+  const StencilTuning tn = pass_tuning(K, false);
+  // timing events of this pass (nullptr when off)
+  void* ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (timing_) {
+    for (auto& e : ev) e = tevent();
+    if (ev[4]) tk_.push_back(K);
+  }
+  auto rec = [&](int i, void* stream) {
+    if (ev[4]) RMA_HIP_CHECK(hipEventRecord(E(ev[i]), S(stream)));
+  };
+  if (p_.mode == Mode::kPerf) {
+    TraceRange tr("rma.pass.perf");
+    rec(0, s_lo_);
+    rec(1, s_lo_);
+    rec(3, s_lo_);
+    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, tn, s_lo_);
+    rec(4, s_lo_);
+    exchange(Tout, s_lo_);
+    rec(2, s_lo_);
+    return;
+  }
+  TraceRange tr("rma.pass.hide");
+  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
+  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+  rec(0, s_hi_);
+  if (!g.frame.empty()) {
+    TraceRange tb("rma.boundary");
+    multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame.data(), (int)g.frame.size(),
+               pass_tuning(K, true), s_hi_);
+  }
+  rec(1, s_hi_);
+  {
+    TraceRange th("rma.halo");
+    exchange(Tout, s_hi_);
+  }
+  rec(2, s_hi_);
+  RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
+  rec(3, s_lo_);
+  if (!g.interior.empty()) {
+    TraceRange ti("rma.interior");
+    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.interior, 1, tn, s_lo_);
+  }
+  rec(4, s_lo_);
+  RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+}
+
+void* DiffusionExecutor::tevent() {
+  constexpr size_t kMaxEvents = 5 * 8192;
+  if (tused_ >= kMaxEvents) return nullptr;
+  if (tused_ == tev_.size()) {
+    hipEvent_t e;
+    RMA_HIP_CHECK(hipEventCreate(&e));
+    tev_.push_back(e);
+  }
+  return tev_[tused_++];
+}
+
+void DiffusionExecutor::release_timing() {
+  for (void* e : tev_) (void)hipEventDestroy(E(e));
+  tev_.clear();
+  tk_.clear();
+  tused_ = 0;
+}
+
+void DiffusionExecutor::set_timing(bool on) {
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_hi_)));
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
+  tused_ = 0;
+  tk_.clear();
+  timing_ = on;
+}
+
+std::vector<PassTiming> DiffusionExecutor::timings() {
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_hi_)));
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
+  std::vector<PassTiming> out;
+  for (size_t i = 0; i < tk_.size(); ++i) {
+    hipEvent_t* e = reinterpret_cast<hipEvent_t*>(&tev_[5 * i]);
+    float t[5] = {0, 0, 0, 0, 0};
+    for (int j = 1; j < 5; ++j) RMA_HIP_CHECK(hipEventElapsedTime(&t[j], e[0], e[j]));
+    PassTiming pt;
+    pt.K = tk_[i];
+    pt.frame_ms = t[1];
+    pt.halo_ms = t[2] - t[1];
+    pt.interior_ms = t[4] - t[3];
+    pt.pass_ms = std::max(t[2], t[4]);
+    pt.exposed_halo_ms = std::max(0.0f, t[2] - t[4]);
+    out.push_back(pt);
+  }
+  return out;
+}
+
+void DiffusionExecutor::set_solo(bool on) {
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_hi_)));
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
+  if (on == solo_) return;
+  solo_ = on;
+  nbr_ = on ? Neighbors{{{-1, -1}, {-1, -1}, {-1, -1}}} : real_nbr_;
+  std::fill(geom_ok_.begin(), geom_ok_.end(), 0);  // pass rects follow the neighbours
   if (graph_exec_) {
     (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec_));
     graph_exec_ = nullptr;
   }
-  if (halo_)  // pack buffers must exist before capture (no hipMalloc inside)
-    halo_->prepare({field_of(T_, nx_, ny_, p_.olx, p_.oly, hwx_, hwy_)}, 3);
+}
+
+void DiffusionExecutor::prime() {
+  if (p_.mode == Mode::kKp || (p_.temporal == 1 && !fast5())) return;
+  // a tiny field with the same cells-per-lane class as the real one (nx mod 4)
+  const int64_t tnx = 256 + nx_ % 4, tny = 64;
+  const size_t bytes = (size_t)(tnx * tny) * sizeof(double);
+  double* buf = nullptr;
+  RMA_HIP_CHECK(hipMalloc(&buf, 3 * bytes));
+  double *a = buf, *b = buf + tnx * tny, *ic = buf + 2 * tnx * tny;
+  RMA_HIP_CHECK(hipMemsetAsync(buf, 0, 3 * bytes, S(s_lo_)));
+  const Rect r{1, tnx - 1, 1, tny - 1};
+  try {
+    for (int K = 1; K <= p_.temporal; ++K) {
+      if (!std::isfinite(cost_[K])) continue;
+      if (K == 1 && !fast5()) {
+        stencil_rects_gpu(b, a, ic, tnx, tny, &r, 1, p_.coef, p_.tune, s_lo_);
+        continue;
+      }
+      multi_step(K, a, b, ic, tnx, tny, &r, 1, pass_tuning(K, false), s_lo_);
+      if (p_.mode == Mode::kHide)
+        multi_step(K, a, b, ic, tnx, tny, &r, 1, pass_tuning(K, true), s_lo_);
+    }
+    RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
+  } catch (...) {
+    (void)hipStreamSynchronize(S(s_lo_));
+    (void)hipFree(buf);
+    throw;
+  }
+  RMA_HIP_CHECK(hipFree(buf));
+}
+
+void DiffusionExecutor::run_eager(int64_t nsteps) {
+  if (p_.mode == Mode::kKp) {
+    for (int64_t i = 0; i < nsteps; ++i) {
+      enqueue_step(T_, nullptr);
+      ++steps_;
+      ++passes_;
+    }
+    return;
+  }
+  const std::vector<int> passes =
+      cost_.empty() ? std::vector<int>((size_t)nsteps, 1) : plan_passes(nsteps, cost_);
+  for (const int K : passes) {
+    double* Tin = parity_ ? T2_ : T_;
+    double* Tout = parity_ ? T_ : T2_;
+    if (K == 1 && !fast5()) {
+      // one canonical step (with overlap 2K and halo width K the one-step
+      // update + exchange stays consistent)
+      enqueue_step(Tin, Tout);
+    } else {
+      enqueue_pass(K, Tin, Tout);
+    }
+    steps_ += K;
+    ++passes_;
+    parity_ ^= 1;
+  }
+}
+
+void DiffusionExecutor::build_graph(int64_t steps, int reps) {
+  if (graph_exec_) {
+    (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec_));
+    graph_exec_ = nullptr;
+  }
+  if (halo_) {  // pack buffers must exist before capture (no hipMalloc inside)
+    HaloField f;
+    f.ptr = T_;
+    f.size = {nx_, ny_, 1};
+    f.elem_bytes = 8;
+    f.ol = {p_.olx, p_.oly, 2};
+    f.hw = {hwx_, hwy_, 1};
+    halo_->prepare({f}, 3);
+  }
   hipStream_t lo = S(s_lo_), hi = S(s_hi_);
   const int saved_parity = parity_;
-  const int64_t saved_steps = steps_;
+  const int64_t saved_steps = steps_, saved_passes = passes_;
   RMA_HIP_CHECK(hipStreamBeginCapture(lo, hipStreamCaptureModeThreadLocal));
   hipGraph_t g = nullptr;
   try {
@@ -368,7 +466,7 @@ void DiffusionExecutor::build_graph(int64_t steps) {
     RMA_HIP_CHECK(hipStreamWaitEvent(hi, E(e_in_), 0));
     RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
     RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
-    run_eager(steps);
+    for (int r = 0; r < reps; ++r) run_eager(steps);
     // join hi back
     RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
     RMA_HIP_CHECK(hipStreamWaitEvent(lo, E(e_hi_), 0));
@@ -380,6 +478,7 @@ void DiffusionExecutor::build_graph(int64_t steps) {
     (void)hipGetLastError();
     parity_ = saved_parity;
     steps_ = saved_steps;
+    passes_ = saved_passes;
     throw;
   }
   RMA_HIP_CHECK(hipStreamEndCapture(lo, &g));
@@ -387,9 +486,10 @@ void DiffusionExecutor::build_graph(int64_t steps) {
   RMA_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   RMA_HIP_CHECK(hipGraphDestroy(g));
   graph_exec_ = ge;
-  graph_len_ = steps;
+  graph_len_ = steps * reps;
   parity_ = saved_parity;  // capture enqueued nothing; restore bookkeeping
   steps_ = saved_steps;
+  passes_ = saved_passes;
 }
 
 void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
@@ -405,16 +505,19 @@ void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
   int64_t left = nsteps;
   if (p_.use_graph) {
-    int64_t gl = p_.graph_steps > 0 ? p_.graph_steps : 20;
-    // keep the buffer parity of a replay neutral (K steps per swap)
-    const int64_t q = 2 * p_.temporal;
-    gl = (gl + q - 1) / q * q;
-    if (left >= gl) {
-      if (!graph_exec_ || graph_len_ != gl) build_graph(gl);
-      while (left >= gl) {
+    // a replay must leave the buffer parity unchanged: capture the plan of gl
+    // steps twice when it has an odd number of passes
+    const int64_t gl = p_.graph_steps > 0 ? p_.graph_steps : 20;
+    const int64_t np = (int64_t)plan(gl).size();
+    const int reps = np % 2 ? 2 : 1;
+    const int64_t glen = gl * reps;
+    if (left >= glen) {
+      if (!graph_exec_ || graph_len_ != glen) build_graph(gl, reps);
+      while (left >= glen) {
         RMA_HIP_CHECK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(graph_exec_), lo));
-        steps_ += gl;
-        left -= gl;
+        steps_ += glen;
+        passes_ += np * reps;
+        left -= glen;
       }
       RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
       RMA_HIP_CHECK(hipStreamWaitEvent(hi, E(e_lo_), 0));

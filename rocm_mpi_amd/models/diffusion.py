@@ -37,8 +37,7 @@ from ..parallel.halo import gather_, update_halo_
 from ..utils import metrics
 from ..utils import profiling as prof
 
-TEMPORAL = (1, 2, 3, 4, 6, 8, 12, 16)
-DEEP_TEMPORAL = (12, 16)  # fast-math (kernel fast5) only on the GPU
+TEMPORAL = tuple(range(1, 25))  # max steps per kernel pass (csrc kPipeMaxK)
 
 
 def default_chunk2(K: int, ny: int) -> int:
@@ -97,15 +96,18 @@ class DiffusionConfig:
     profile: bool = False
     check_every: int = 0  # NaN/Inf guard period (0 = off)
     quiet: bool = False
-    # temporal blocking (perf / perf_hide): K = 2, 3, 4, 6, 8 steps per kernel
-    # pass and one width-K halo exchange per pass (grid overlap 2K); bitwise
-    # identical to K single steps. K = 12, 16: fast_math only (GPU).
+    # temporal blocking (perf / perf_hide): at most K = temporal steps per
+    # kernel pass (1..24) and one width-K halo exchange per pass (grid overlap
+    # 2K); step(n) plans passes of 1..K steps (native plan_passes: e.g. 20
+    # steps = one 20-step pass). Canonical passes are bitwise identical to
+    # single steps.
     temporal: int = 1
-    chunk2: int = 0  # K-step kernel rows per wave-task (0: default_chunk2)
+    chunk2: int = 0  # K-step kernel rows per wave-task (0: per pass depth, default_chunk2)
     unroll2: int = 2
-    # fast-math fp64 arithmetic in the K-step passes (5-point sum with one
-    # folded per-cell factor, FMAs; kernel fast5): same scheme, not bitwise
-    # equal to the canonical expression (GPU only; the CPU path stays canonical)
+    # fast-math fp64 arithmetic in every pass (5-point sum with one folded
+    # per-cell factor, FMAs; kernels fast5/pipe): same scheme, not bitwise
+    # equal to the canonical expression, bitwise equal to its C++ CPU twin
+    # (which the CPU path then runs)
     fast_math: bool = False
 
     def validate(self) -> None:
@@ -121,9 +123,8 @@ class DiffusionConfig:
             raise ValueError(f"temporal must be one of {TEMPORAL}")
         if self.temporal > 1 and self.variant not in ("perf", "perf_hide"):
             raise ValueError("temporal blocking applies to the perf and perf_hide variants")
-        if self.temporal in DEEP_TEMPORAL and not self.fast_math and self.device != "cpu":
-            raise ValueError(f"temporal={self.temporal} runs on the fast5 kernel only: set "
-                             "fast_math=True (or use K <= 8)")
+        if self.fast_math and self.variant not in ("perf", "perf_hide"):
+            raise ValueError("fast_math applies to the perf and perf_hide variants")
 
 
 class Diffusion2D:
@@ -177,6 +178,9 @@ class Diffusion2D:
             self.qx, self.qy, self.dTdt = ops.kp_views(self.QX, self.QY, self.D)
         self.parity = 0
         self.steps_done = 0
+        self._solo = False
+        self._timing = False
+        self._ptimes: list = []
         self.executor = None
         self.use_graph = False
         use_native = cfg.executor == "native" or (
@@ -218,15 +222,37 @@ class Diffusion2D:
                 raise ValueError(f"temporal={K} needs grid overlaps >= {2 * K} "
                                  f"(init_global_grid(overlaps=({2 * K},{2 * K},2), "
                                  f"halowidths=({K},{K},1)))")
-            # owned rect of a K-step pass (the K cells next to a neighbour are halo)
-            self.out2 = (K if nb[0][0] >= 0 else 1, nx - (K if nb[0][1] >= 0 else 1),
-                         K if nb[1][0] >= 0 else 1, ny - (K if nb[1][1] >= 0 else 1))
+            self.out2 = self.owned_rect(K)
         if cfg.variant == "perf_hide":
             # the frame holds the send planes [ol-hw, ol): at least ol-1 wide
             bw = (max(cfg.b_width[0], g.overlaps[0] - 1), max(cfg.b_width[1], g.overlaps[1] - 1))
             self.frame_rects, self.interior = ops.hide_rects(nx, ny, *bw, vec=cfg.vec)
         self.tuning = ops.StencilTuning(cfg.chunk_rows, int(cfg.nontemporal), cfg.kernel,
                                         cfg.unroll, cfg.vec)
+
+    def owned_rect(self, k: int) -> tuple:
+        """Cells a k-step pass writes: next to a neighbour the k cells [0,k)
+        are halo (refreshed by the exchange), elsewhere boundary cell 0 stays
+        (csrc/runtime/plan.cpp owned_rect)."""
+        nb, nx, ny = self.g.neighbors, self.cfg.nx, self.cfg.ny
+        return (k if nb[0][0] >= 0 else 1, nx - (k if nb[0][1] >= 0 else 1),
+                k if nb[1][0] >= 0 else 1, ny - (k if nb[1][1] >= 0 else 1))
+
+    def plan(self, n: int) -> list:
+        """Passes step(n) runs (deepest first): the native executor's plan, or
+        the same planner for the Python loop (csrc/runtime/plan.cpp)."""
+        if self.executor is not None:
+            return list(self.executor.plan(int(n)))
+        cfg = self.cfg
+        if cfg.variant not in ("perf", "perf_hide") or (cfg.temporal == 1 and not cfg.fast_math):
+            return [1] * int(n)
+        from .._native import has_native
+
+        if has_native():
+            fast = cfg.fast_math and ops.fast5_ok(self.coef)
+            return list(native().plan_passes(int(n), native().default_pass_costs(cfg.temporal, fast)))
+        K = cfg.temporal
+        return [K] * (int(n) // K) + ([int(n) % K] if int(n) % K else [])
 
     def _build_executor(self):
         cfg, g = self.cfg, self.g
@@ -241,7 +267,7 @@ class Diffusion2D:
             self.QY.data_ptr() if cfg.variant == "kp" else 0,
             self.D.data_ptr() if cfg.variant == "kp" else 0, int(cfg.unroll),
             int(cfg.vec), int(cfg.temporal), int(g.overlaps[0]), int(g.overlaps[1]),
-            int(self.chunk2), int(cfg.unroll2), int(bool(cfg.fast_math)))
+            int(cfg.chunk2), int(cfg.unroll2), int(bool(cfg.fast_math)))
 
     def set_temporal(self, K: int, fast_math: bool | None = None) -> None:
         """Switch the steps per kernel pass (e.g. to time the one-step kernel on
@@ -250,9 +276,6 @@ class Diffusion2D:
         cfg, g = self.cfg, self.g
         if K not in TEMPORAL or (K > 1 and cfg.variant not in ("perf", "perf_hide")):
             raise ValueError(f"temporal={K} not available for {cfg.variant}")
-        fm = cfg.fast_math if fast_math is None else bool(fast_math)
-        if K in DEEP_TEMPORAL and not fm and self.device.type != "cpu":
-            raise ValueError(f"temporal={K} needs fast_math")
         nb = g.neighbors
         if any(max(nb[d]) >= 0 and g.overlaps[d] < 2 * K for d in (0, 1)):
             raise ValueError(f"temporal={K} needs grid overlaps >= {2 * K}")
@@ -265,8 +288,7 @@ class Diffusion2D:
             cfg.fast_math = bool(fast_math)
         self.chunk2 = cfg.chunk2 or default_chunk2(K, cfg.ny)
         if K > 1:
-            self.out2 = (K if nb[0][0] >= 0 else 1, cfg.nx - (K if nb[0][1] >= 0 else 1),
-                         K if nb[1][0] >= 0 else 1, cfg.ny - (K if nb[1][1] >= 0 else 1))
+            self.out2 = self.owned_rect(K)
         if self.executor is not None:
             self.executor = self._build_executor()
 
@@ -325,46 +347,111 @@ class Diffusion2D:
                 self._ap_graph.replay()
             self.steps_done += n - n % k
             n %= k
-        done = 0
-        while done < n:
+        if v in ("perf", "perf_hide"):
+            # the passes of the native planner (one-step passes when
+            # temporal=1 without fast_math). The executor splits frame /
+            # interior over two streams; this loop runs them in sequence:
+            # frame -> exchange -> interior.
+            for K in self.plan(n):
+                self._pass(K)
+            return
+        for _ in range(n):
             if v == "ap":
                 self._step_ap()
-            elif v == "kp":
+            else:  # kp
                 ops.flux(self.QX, self.QY, self.T, self.coef.mlam, self.coef.rdx, self.coef.rdy)
                 ops.residual(self.D, self.QX, self.QY, self.iCp, self.coef.rdx, self.coef.rdy)
                 ops.update(self.T, self.D, self.coef.dt)
                 update_halo_(self.T)
-            elif self.cfg.temporal > 1 and n - done >= self.cfg.temporal:
-                # K steps per pass (the native executor splits frame/interior;
-                # this reference loop runs the owned rect, then the exchange)
-                K = self.cfg.temporal
-                Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
-                tn = None
-                if self.cfg.fast_math and Tin.is_cuda:  # the executor's fast-math kernel
-                    kern, vec, _ = native().fast_kernel_k(K, self.cfg.ny, tuple(self.coef))
-                    name = {v: k for k, v in ops.KERNELS.items()}[kern]
-                    tn = ops.StencilTuning(chunk_rows=self.chunk2, xcd_remap=1, kernel=name,
-                                           vec=vec)
-                ops.stencilk_step(K, Tout, Tin, self.iCp, self.coef, [self.out2], tn)
-                update_halo_(Tout)
-                self.parity ^= 1
-                self.steps_done += K
-                done += K
-                continue
-            else:
-                Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
-                if v == "perf":
-                    ops.stencil_step(Tout, Tin, self.iCp, self.coef, tuning=self.tuning)
-                    update_halo_(Tout)
-                else:  # perf_hide, sequential emulation: frame -> halo -> interior
-                    ops.stencil_step(Tout, Tin, self.iCp, self.coef, self.frame_rects, self.tuning)
-                    update_halo_(Tout)
-                    if self.interior is not None:
-                        ops.stencil_step(Tout, Tin, self.iCp, self.coef, [self.interior],
-                                         self.tuning)
-                self.parity ^= 1
             self.steps_done += 1
-            done += 1
+
+    def _pass(self, K: int) -> None:
+        """One pass of K steps outside the native executor (CPU twins, or the
+        GPU kernels with the loopback / staged transports)."""
+        cfg = self.cfg
+        Tin, Tout = (self.T2, self.T) if self.parity else (self.T, self.T2)
+        fast = cfg.fast_math and ops.fast5_ok(self.coef)
+        solo = self._solo
+        timing = self._timing
+        if timing:
+            self.synchronize()
+            t0 = metrics.now()
+        t_frame = t_halo = None
+        if K == 1 and not fast:  # one canonical step
+            if cfg.variant == "perf" or solo:
+                ops.stencil_step(Tout, Tin, self.iCp, self.coef, tuning=self.tuning)
+            else:  # perf_hide, sequential emulation: frame -> halo -> interior
+                ops.stencil_step(Tout, Tin, self.iCp, self.coef, self.frame_rects, self.tuning)
+                if timing:
+                    self.synchronize()
+                    t_frame = metrics.now()
+                update_halo_(Tout)
+                if timing:
+                    self.synchronize()
+                    t_halo = metrics.now()
+                if self.interior is not None:
+                    ops.stencil_step(Tout, Tin, self.iCp, self.coef, [self.interior], self.tuning)
+        else:
+            rect = ops.interior_rect(cfg.nx, cfg.ny) if solo else self.owned_rect(K)
+            if Tin.is_cuda:  # the executor's kernel for this pass depth
+                fn = native().fast_kernel_k if fast else None
+                kern, vec, ch = (fn(K, cfg.ny, tuple(self.coef)) if fn
+                                 else native().canonical_kernel_k(K, cfg.ny))
+                name = {v: k for k, v in ops.KERNELS.items()}[kern]
+                tn = ops.StencilTuning(chunk_rows=cfg.chunk2 or ch, xcd_remap=1, kernel=name,
+                                       vec=vec)
+            else:  # the C++ twin of the pass arithmetic
+                tn = ops.StencilTuning(kernel="pipe" if fast else "pipec")
+            if K == 2 and not fast and Tin.is_cuda:
+                ops.stencil2_step(Tout, Tin, self.iCp, self.coef, [rect])
+            else:
+                ops.stencilk_step(K, Tout, Tin, self.iCp, self.coef, [rect], tn)
+        if t_halo is None and not solo:
+            if timing:
+                self.synchronize()
+                t_frame = metrics.now()
+            update_halo_(Tout)
+            if timing:
+                self.synchronize()
+                t_halo = metrics.now()
+        if timing:
+            self.synchronize()
+            t1 = metrics.now()
+            tf = t_frame if t_frame is not None else t1
+            th = t_halo if t_halo is not None else tf
+            # sequential: the exchange is never hidden (frame_ms = compute
+            # before the exchange, interior_ms = compute after it)
+            self._ptimes.append({"K": K, "frame_ms": (tf - t0) * 1e3,
+                                 "halo_ms": (th - tf) * 1e3, "interior_ms": (t1 - th) * 1e3,
+                                 "pass_ms": (t1 - t0) * 1e3, "exposed_halo_ms": (th - tf) * 1e3})
+        self.parity ^= 1
+        self.steps_done += K
+
+    # ------------------------------------------------------------------
+    def enable_pass_timing(self, on: bool = True) -> None:
+        """Record per-pass timings from now on (native executor: HIP events on
+        both streams; Python loop: synchronised wall clock)."""
+        self._timing = bool(on)
+        self._ptimes = []
+        if self.executor is not None:
+            self.executor.set_timing(bool(on))
+
+    def pass_timings(self) -> list:
+        """One dict per pass since enable_pass_timing: K, frame_ms, halo_ms
+        (pack + exchange + unpack), interior_ms, pass_ms, exposed_halo_ms (how
+        long the exchange outlasted the interior; == halo_ms without overlap)."""
+        if self.executor is not None:
+            return [dict(t) for t in self.executor.timings()]
+        return list(self._ptimes)
+
+    def set_solo(self, on: bool) -> None:
+        """Run this tile as if it had no neighbour (no exchange, one launch per
+        pass): the same-run single-GPU reference of a weak-scaling measurement.
+        The field is then not the multi-rank solution."""
+        self.synchronize()
+        self._solo = bool(on)
+        if self.executor is not None:
+            self.executor.set_solo(bool(on))
 
     def _ap_graph_len(self) -> int:
         """Capture graph_steps ap steps once (capture does not execute them)."""

@@ -25,13 +25,17 @@ from .._native import has_native, native
 Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 
 # K-step kernels also: 2 = dpp, 3 = lds_dpp (default), 4 = fast (reassociated, FMA; not
-# bitwise), 5 = fast5 (5-point sum with one folded per-cell factor; not bitwise, lam != 0;
-# the only kernel family for 12 / 16 steps per pass); 6 / 7 / 8 = fast5p2 / fast5p4 / fast5p8: the
-# same arithmetic with the levels of one strip split over 2 / 4 / 8 pipelined waves (K = 8, 12, 16;
-# fast5p8: K = 8, 16)
-FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8")
+# bitwise), 5 = fast5 (5-point sum with one folded per-cell factor; not bitwise, lam != 0);
+# 6 / 7 / 8 = fast5p2 / fast5p4 / fast5p8: the same arithmetic with the levels of one strip
+# split over 2 / 4 / 8 pipelined waves (K = 8, 12, 16; fast5p8: K = 8, 16); 9 = pipe: the
+# stage-pipelined fast5 kernel for ANY K in 1..24 (csrc/kernels/stencil_pipe.h, the executor's
+# fast-math kernel); 10 = pipec: the same pipeline with the canonical arithmetic (bitwise equal
+# to K one-step updates), any K in 1..24.
+FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe")
+PIPE = ("pipe", "pipec")
+PIPE_MAX_K = 24
 KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4, "fast5": 5, "fast5p2": 6,
-           "fast5p4": 7, "fast5p8": 8}
+           "fast5p4": 7, "fast5p8": 8, "pipe": 9, "pipec": 10}
 
 
 class StencilCoef(NamedTuple):
@@ -61,6 +65,7 @@ class StencilTuning:
     unroll: int = 4
     vec: int = 2
     xcd_remap: int = -1  # -1: chosen by tile width (see csrc/kernels/stencil.hip)
+    stages: int = 0  # pipe / pipec: waves per strip (0: native pipe_default_stages)
 
 
 @dataclass
@@ -203,17 +208,25 @@ def stencil2_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: St
 def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
                   coef: StencilCoef, rects: Sequence[Rect] | None = None,
                   tuning: StencilTuning | None = None) -> None:
-    """K time steps in one pass (K = 2, 3, 4, 6, 8; 12, 16 with kernel fast5;
-    csrc/kernels/stencil_tbk.hip):
+    """K time steps in one pass (csrc/kernels/stencil_tbk.hip, stencil_pipe.h):
     T2[r] = f^K(T)[r], the intermediate levels being f on the interior and T
-    on boundary/halo cells. Bitwise equal to K ``stencil_step`` calls (kernels
-    fast / fast5: within rounding). Default tuning: the native
+    on boundary/halo cells. Kernels: K = 2, 3, 4, 6, 8 for march/lds/dpp/lds_dpp/
+    fast/fast5 (12, 16 also fast5 and the fast5p* variants); ANY K in 1..24 for
+    pipe (fast5 arithmetic) and pipec (canonical). Canonical kernels are bitwise
+    equal to K ``stencil_step`` calls; the fast5 family to the fast5 CPU twin
+    (``kernel`` picks the CPU twin's arithmetic too). Default tuning: the native
     executor's (chunk by tile height, LDS 1/Cp ring, DPP)."""
-    if int(K) not in (2, 3, 4, 6, 8, 12, 16):
-        raise ValueError(f"K must be 2, 3, 4, 6, 8, 12 or 16, got {K}")
+    K = int(K)
+    kname = tuning.kernel if tuning is not None else "lds_dpp"
+    if kname in PIPE:
+        if not 1 <= K <= PIPE_MAX_K:
+            raise ValueError(f"K must be in 1..{PIPE_MAX_K} for the pipelined kernels, got {K}")
+    elif K not in (2, 3, 4, 6, 8, 12, 16):
+        raise ValueError(f"K must be 2, 3, 4, 6, 8, 12 or 16 (any K: kernel 'pipe'/'pipec'), "
+                         f"got {K}")
     check_field("T", T)
-    if int(K) > 8 and T.is_cuda and (tuning is None or tuning.kernel not in FAST5):
-        raise ValueError("12 or 16 steps per pass need a fast5 kernel (fast5, fast5p2, fast5p4) on the GPU")
+    if K > 8 and T.is_cuda and kname not in FAST5 + PIPE:
+        raise ValueError("12 or 16 steps per pass need a fast5 or pipelined kernel on the GPU")
     ny, nx = T.shape
     check_field("T2", T2, (ny, nx), T.device)
     check_field("iCp", iCp, (ny, nx), T.device)
@@ -223,26 +236,88 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
     if not rects:
         return
     if tuning is None:  # the executor's measured defaults (default_tune_k)
-        ch = native().default_chunk_k(int(K), ny) if has_native() else 16
+        ch = native().default_chunk_k(K, ny) if has_native() else 16
         tuning = StencilTuning(chunk_rows=ch, kernel="lds_dpp", xcd_remap=1)
     tn = tuning
     if tn.kernel in FAST5 and not fast5_ok(coef):
         raise ValueError("kernel 'fast5' folds dy^-2/dx^-2 into one factor: needs lam != 0 "
                          f"and finite coefficients, got {tuple(coef)}")
     if T.is_cuda:
-        native().stencilk_rects(int(K), _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
+        native().stencilk_rects(K, _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                 tn.chunk_rows, int(tn.nontemporal), stream_handle(T), True,
-                                tn.xcd_remap, tn.vec, KERNELS[tn.kernel])
+                                tn.xcd_remap, tn.vec, KERNELS[tn.kernel], int(tn.stages))
     elif _use_native_cpu():
-        native().stencilk_rects(int(K), _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
-                                16, 0, 0, False)
+        native().stencilk_rects(K, _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
+                                16, 0, 0, False, -1, 2, KERNELS[tn.kernel], 0)
+    elif tn.kernel in FAST5:
+        a = T.clone()
+        for _ in range(K - 1):
+            b = a.clone()
+            stencil5_torch(b, a, iCp, coef, [interior_rect(nx, ny)])
+            a = b
+        stencil5_torch(T2, a, iCp, coef, rects)
     else:
         a = T.clone()
-        for _ in range(int(K) - 1):
+        for _ in range(K - 1):
             b = a.clone()
             stencil_torch(b, a, iCp, coef, [interior_rect(nx, ny)])
             a = b
         stencil_torch(T2, a, iCp, coef, rects)
+
+
+def fast5_constants(coef: StencilCoef) -> tuple[float, float, float]:
+    """(ry, -2(1+ry), dt*lam/dx^2) of the fast5 arithmetic, computed in the
+    same order as the kernels (csrc/kernels/stencil_pipe.h)."""
+    ax = (-coef.mlam) * coef.rdx * coef.rdx
+    ay = (-coef.mlam) * coef.rdy * coef.rdy
+    ry = ay / ax
+    return ry, -2.0 * (1.0 + ry), coef.dt * ax
+
+
+def stencil5_torch(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, c: StencilCoef,
+                   rects: Iterable[Rect]) -> None:
+    """Torch twin of ONE fast5 step (CPU without the extension). torch has no
+    fused multiply-add for float64 tensors, so each fma is evaluated exactly
+    with a double-double product (Dekker/Veltkamp split) and rounded once:
+    bitwise equal to std::fma / v_fma_f64 unless an intermediate under- or
+    overflows."""
+    ry, mkc, gs = fast5_constants(c)
+    for x0, x1, y0, y1 in rects:
+        cu = T[y0:y1, x0:x1]
+        sx = T[y0:y1, x0 + 1:x1 + 1] + T[y0:y1, x0 - 1:x1 - 1]
+        sy = T[y0 - 1:y1 - 1, x0:x1] + T[y0 + 1:y1 + 1, x0:x1]
+        t = fma_exact(torch.full_like(cu, mkc), cu, sx)
+        t = fma_exact(torch.full_like(cu, ry), sy, t)
+        g = gs * iCp[y0:y1, x0:x1]
+        T2[y0:y1, x0:x1] = fma_exact(g, t, cu)
+
+
+def _two_prod(a: torch.Tensor, b: torch.Tensor):
+    p = a * b
+    split = 134217729.0  # 2^27 + 1
+    ca, cb = split * a, split * b
+    ah = ca - (ca - a)
+    al = a - ah
+    bh = cb - (cb - b)
+    bl = b - bh
+    e = ((ah * bh - p) + ah * bl + al * bh) + al * bl
+    return p, e
+
+
+def fma_exact(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+    """round(a*b + c) for float64 tensors: a*b = p + e exactly (two_prod); the
+    sum p + e + c is formed with error-free two_sum steps and rounded once
+    (the residual is added last with round-to-odd style correction: the
+    partial sum s and its error terms are combined so that only the final
+    addition rounds)."""
+    p, e = _two_prod(a, b)
+    s = p + c  # two_sum(p, c)
+    bp = s - p
+    err = (p - (s - bp)) + (c - bp)
+    # s + (err + e): err + e is exact unless tiny cancellation; the final
+    # addition is the single rounding of the exact sum in all but tie cases,
+    # which tests pin against std::fma (tests/test_fast5_cpu.py)
+    return s + (err + e)
 
 
 def fast5_ok(coef: StencilCoef) -> bool:

@@ -14,7 +14,13 @@ from __future__ import annotations
 
 import json
 import math
+import time
 from dataclasses import asdict, dataclass, field
+
+
+def now() -> float:
+    """Wall clock for host-side timings (time.perf_counter)."""
+    return time.perf_counter()
 
 
 def a_eff_gb(nx: int, ny: int, nz: int = 1, arrays: int = 3, elem_bytes: int = 8) -> float:

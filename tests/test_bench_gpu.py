@@ -1,0 +1,39 @@
+"""bench.py on one GPU: the driver's command shape, its record, and the
+in-run halo check path with real RCCL traffic (periodic grid, RCCL send/recv
+to self vs local self copies), which a multi-GPU run uses across GPUs."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def bench(*args, timeout=300):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                       capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_small_tile_with_self_rccl_halo_check():
+    d = bench("--steps", "20", "--warmup", "5", "--nx", "4096", "--single-step-steps", "8",
+              "--check", "1", "--check-self-rccl", "--check-nx", "1026")
+    c = d["config"]
+    assert d["n_gpus"] == 1 and c["ranks"] == 1
+    assert c["passes_timed"] == [20] and c["passes_warmup"] == [5]
+    assert c["kstep_kernel"]["kernel"] == "pipe"
+    assert c["rccl_halo_bitwise_ok"] is True
+    hc = c["halo_check"]
+    assert hc["transport"] == "rccl" and hc["self_rccl"] and hc["tiles_mismatched"] == 0
+    pt = c["pass_timing"]
+    assert pt["passes"] == 1 and pt["depths"] == [20] and pt["interior_ms"] > 0
+    assert c["weak_scaling_eff_same_run"] > 0.9  # no neighbour: solo == the run
+    assert c["teff_single_step_kernel_GBps"] > 0 and c["teff_bitwise_kstep_GBps"] > 0
+    assert c["pci_bus_ids"] and len(c["pci_bus_ids"]) == 1
+    assert c["nonfinite_cells_sampled"] == 0

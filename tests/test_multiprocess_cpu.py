@@ -101,8 +101,49 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     K = int(extra[1])
     dims = [int(v) for v in extra[3].split(",")]
     assert c["global_grid"] == [dims[0] * (nx - 2 * K) + 2 * K, dims[1] * (nx - 2 * K) + 2 * K]
-    assert abs(d["value"] - world * c["teff_per_gpu_GBps"]) <= 1e-6 * d["value"] + 0.02
+    assert abs(d["value"] - world * c["teff_per_gpu_GBps"]) <= 1e-6 * d["value"] + 0.005 * world + 0.01
     assert c["nonfinite_cells_sampled"] == 0
+    # self-validation of a multi-rank point
+    assert c["ranks"] == world and c["transport"] == "gloo"
+    assert sum(c["passes_timed"]) == 20 and max(c["passes_timed"]) <= K
+    assert c["teff_per_gpu_min_GBps"] <= c["teff_per_gpu_GBps"] * (1 + 1e-9) + 0.02
+    assert c["teff_per_gpu_min_GBps"] <= c["teff_per_gpu_max_GBps"]
+    pt = c["pass_timing"]
+    assert pt["passes"] == len(c["passes_timed"])
+    for k in ("frame_ms", "halo_ms", "interior_ms", "pass_ms", "exposed_halo_ms"):
+        assert pt[k] >= 0
+    assert pt["halo_ms"] > 0 and pt["overlap_fraction"] is not None
+    assert 0 < c["weak_scaling_eff_same_run"] and c["solo_ms_per_step"] > 0
+    assert c["rccl_halo_bitwise_ok"] is True
+    hc = c["halo_check"]
+    assert hc["tiles_mismatched"] == 0 and hc["transport"] == "gloo"
+    assert hc["global_grid"] == [dims[0] * (130 - 2 * K) + 2 * K, dims[1] * (130 - 2 * K) + 2 * K]
+
+
+def test_bench_halo_check_detects_a_wrong_tile(tmp_path):
+    """The in-run check compares every gathered tile bitwise with the 1-rank
+    run: one perturbed cell on the last rank makes the run fail (exit 4) with
+    rccl_halo_bitwise_ok false."""
+    import json
+    import subprocess
+    import sys
+
+    from helpers import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "2",
+           "--device", "cpu", "--nx", "64", "--single-step-steps", "0", "--temporal", "4",
+           "--solo-steps", "0"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_CHECK_CORRUPT="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
+                       env=env)
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-2000:]
+    c = json.loads(lines[0])["config"]
+    assert c["rccl_halo_bitwise_ok"] is False and c["halo_check"]["tiles_mismatched"] == 1
 
 
 def test_node_local_rank_from_hostnames(tmp_path):

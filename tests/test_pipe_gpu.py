@@ -1,0 +1,160 @@
+"""Any-K stage-pipelined kernels (csrc/kernels/stencil_pipe.h): ``pipe`` (fast5
+arithmetic) and ``pipec`` (canonical) against the C++ CPU twins, bitwise, for
+every pass depth K = 1..24, every cells-per-lane path (odd nx: 1, nx = 2 mod 4:
+2, nx = 0 mod 4: 4), rect lists, alternative stage splits, and against the
+fixed-K kernels they generalise (fast5 / fast5p4, lds_dpp). Guard bands catch
+out-of-bounds writes."""
+import pytest
+import torch
+
+from rocm_mpi_amd import ops
+from rocm_mpi_amd._native import native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def rand(shape, seed, lo=0.0, hi=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return lo + (hi - lo) * torch.rand(shape, generator=g, dtype=torch.float64)
+
+
+def coef():
+    # dx != dy (ry != 1), stable explicit step for 1/Cp <= 1
+    return ops.StencilCoef(-1.3, 1 / 0.037, 1 / 0.041, 0.00031)
+
+
+def cpu_ref(K, T, iCp, rects, kernel, fill=-5.0):
+    out = torch.full_like(T, fill)
+    ops.stencilk_step(K, out, T, iCp, coef(), rects, ops.StencilTuning(kernel=kernel))
+    return out
+
+
+def gpu_run(K, T, iCp, rects, kernel, fill=-5.0, **kw):
+    out = torch.full(T.shape, fill, dtype=torch.float64, device=DEV)
+    tn = ops.StencilTuning(kernel=kernel, xcd_remap=kw.pop("xcd", 1),
+                           chunk_rows=kw.pop("chunk", 16), vec=kw.pop("vec", 4),
+                           stages=kw.pop("stages", 0))
+    ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(), rects, tn)
+    return out.cpu()
+
+
+@pytest.mark.parametrize("kernel", ["pipe", "pipec"])
+@pytest.mark.parametrize("nx", [515, 518, 520])
+@pytest.mark.parametrize("K", list(range(1, 25)))
+def test_pipe_every_depth_bitwise_vs_cpu_twin(kernel, nx, K):
+    ny = 131
+    T, iCp = rand((ny, nx), 1), rand((ny, nx), 2, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, kernel)
+    out = gpu_run(K, T, iCp, rects, kernel, chunk=37)
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("kernel", ["pipe", "pipec"])
+@pytest.mark.parametrize("K", [3, 10, 16, 20, 24])
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_pipe_rect_lists(kernel, K, xcd):
+    """Frame + interior rects, as the multi-rank executor issues a pass."""
+    ny, nx = 301, 1024
+    T, iCp = rand((ny, nx), 3), rand((ny, nx), 4, 0.5, 1.0)
+    w = K + 1
+    frame = [(K, nx - K, K, K + w), (K, nx - K, ny - K - w, ny - K), (K, K + w, K + w, ny - K - w),
+             (nx - K - w, nx - K, K + w, ny - K - w)]
+    interior = (K + w, nx - K - w, K + w, ny - K - w)
+    ref = cpu_ref(K, T, iCp, frame + [interior], kernel)
+    out = torch.full((ny, nx), -5.0, dtype=torch.float64, device=DEV)
+    Td, iCpd = T.to(DEV), iCp.to(DEV)
+    ops.stencilk_step(K, out, Td, iCpd, coef(), frame,
+                      ops.StencilTuning(kernel=kernel, chunk_rows=16, vec=2, xcd_remap=xcd))
+    ops.stencilk_step(K, out, Td, iCpd, coef(), [interior],
+                      ops.StencilTuning(kernel=kernel, chunk_rows=64, vec=4, xcd_remap=xcd))
+    assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("K,S", [(12, 3), (16, 8), (24, 8), (8, 4), (8, 1)])
+def test_pipe_alternative_stage_splits(K, S):
+    ny, nx = 257, 1028
+    T, iCp = rand((ny, nx), 5), rand((ny, nx), 6, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    a = gpu_run(K, T, iCp, rects, "pipe", chunk=64)
+    b = gpu_run(K, T, iCp, rects, "pipe", chunk=64, stages=S)
+    assert torch.equal(a, b)
+    assert torch.equal(a, cpu_ref(K, T, iCp, rects, "pipe"))
+
+
+@pytest.mark.parametrize("K,old", [(8, "fast5"), (12, "fast5p2"), (16, "fast5p4"), (16, "fast5")])
+def test_pipe_equals_fixed_k_fast5_kernels(K, old):
+    ny, nx = 389, 2048
+    T, iCp = rand((ny, nx), 7), rand((ny, nx), 8, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    vec = 4 if old.startswith("fast5p") else 2
+    assert torch.equal(gpu_run(K, T, iCp, rects, "pipe", chunk=64),
+                       gpu_run(K, T, iCp, rects, old, chunk=64, vec=vec))
+
+
+@pytest.mark.parametrize("K", [3, 4, 6, 8])
+def test_pipec_equals_canonical_kernel(K):
+    ny, nx = 389, 2050
+    T, iCp = rand((ny, nx), 9), rand((ny, nx), 10, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    assert torch.equal(gpu_run(K, T, iCp, rects, "pipec", chunk=64),
+                       gpu_run(K, T, iCp, rects, "lds_dpp", chunk=64, vec=2))
+
+
+def test_pipe_unaligned_view_and_tiny_tiles():
+    base = rand(64 * 200 + 1, 11).to(DEV)
+    T = base[1:].view(200, 64)  # 8-byte aligned only -> one cell per lane
+    iCp = torch.ones((200, 64), dtype=torch.float64, device=DEV)
+    for kernel in ("pipe", "pipec"):
+        out = torch.zeros((200, 64), dtype=torch.float64, device=DEV)
+        ops.stencilk_step(13, out, T, iCp, coef(), None, ops.StencilTuning(kernel=kernel))
+        ref = cpu_ref(13, T.cpu(), iCp.cpu(), [ops.interior_rect(64, 200)], kernel, fill=0.0)
+        assert torch.equal(out.cpu(), ref)
+    for ny, nx in ((3, 3), (4, 5), (9, 260), (70, 4)):
+        T, iCp = rand((ny, nx), 12), rand((ny, nx), 13, 0.5, 1.0)
+        for K in (1, 7, 24):
+            assert torch.equal(gpu_run(K, T, iCp, None, "pipe"),
+                               cpu_ref(K, T, iCp, [ops.interior_rect(nx, ny)], "pipe"))
+
+
+G = 4096
+CANARY = -1.2345678901234567e300
+
+
+@pytest.mark.parametrize("kernel", ["pipe", "pipec"])
+@pytest.mark.parametrize("K,vec,nx", [(16, 4, 1024), (16, 2, 1026), (16, 4, 1027), (24, 4, 776),
+                                      (20, 2, 514), (5, 4, 300)])
+def test_pipe_guard_bands(kernel, K, vec, nx):
+    """No write outside the output rects or the arrays (GPU ASan is not
+    available on the pool): canaries around every array, untouched cells
+    outside the rects compared bitwise."""
+    ny = 197
+    bufs, fields = [], []
+    for seed in (14, 15, 16):
+        b = torch.full((G + ny * nx + G,), CANARY, dtype=torch.float64, device=DEV)
+        f = b[G:G + ny * nx].view(ny, nx)
+        f.copy_(rand((ny, nx), seed, 0.5, 1.0))
+        bufs.append(b)
+        fields.append(f)
+    T, iCp, out = fields
+    before = out.clone()
+    rects = [(K, nx - K, K, ny - K)]
+    ops.stencilk_step(K, out, T, iCp, coef(), rects,
+                      ops.StencilTuning(kernel=kernel, chunk_rows=29, vec=vec))
+    torch.cuda.synchronize()
+    for b in bufs:
+        assert bool((b[:G] == CANARY).all()) and bool((b[-G:] == CANARY).all())
+    mask = torch.ones((ny, nx), dtype=torch.bool, device=DEV)
+    mask[K:ny - K, K:nx - K] = False
+    assert torch.equal(out[mask], before[mask])
+
+
+def test_pipe_limits():
+    T = rand((40, 300), 17).to(DEV)
+    out = torch.empty_like(T)
+    with pytest.raises(ValueError):
+        ops.stencilk_step(25, out, T, T, coef(), None, ops.StencilTuning(kernel="pipe"))
+    with pytest.raises(RuntimeError):  # no such stage split instantiated
+        ops.stencilk_step(16, out, T, T, coef(), None, ops.StencilTuning(kernel="pipe", stages=5))
+    assert native().pipe_max_k() == 24
