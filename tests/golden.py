@@ -41,3 +41,47 @@ def run(nxg, nyg, nt, lx=10.0, ly=10.0, lam=1.0, Cp0=1.0, T0=None):
     for _ in range(nt):
         T = step(T, iCp, -lam, 1.0 / dx, 1.0 / dy, dt)
     return T
+
+
+# ---------------------------------------------------------------------------
+# fast5 arithmetic (csrc/kernels/stencil_pipe.h, stencil_tbk.hip kernel 5): the
+# 5-point sum with one folded per-cell factor,
+#   T2 = fma(g, fma(ry, U+D, fma(-2(1+ry), c, R+L)), c),  g = dt*lam/dx^2 * iCp,
+# evaluated with EXACT rational fused multiply-adds (fractions.Fraction; int /
+# int true division in CPython is correctly rounded, so float(Fraction) is the
+# round-to-nearest-even of the exact value, i.e. what v_fma_f64 / std::fma
+# return). Independent of the package: slow, for small grids only.
+# ---------------------------------------------------------------------------
+def fma(a: float, b: float, c: float) -> float:
+    from fractions import Fraction
+
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def fast5_constants(mlam, rdx, rdy, dt):
+    ax = (-mlam) * rdx * rdx
+    ay = (-mlam) * rdy * rdy
+    ry = ay / ax
+    return ry, -2.0 * (1.0 + ry), dt * ax
+
+
+def step5(T, iCp, mlam, rdx, rdy, dt):
+    ry, mkc, gs = fast5_constants(mlam, rdx, rdy, dt)
+    ny, nx = T.shape
+    out = T.copy()
+    for y in range(1, ny - 1):
+        for x in range(1, nx - 1):
+            c = float(T[y, x])
+            sx = float(T[y, x + 1]) + float(T[y, x - 1])
+            sy = float(T[y - 1, x]) + float(T[y + 1, x])
+            t = fma(mkc, c, sx)
+            t = fma(ry, sy, t)
+            out[y, x] = fma(gs * float(iCp[y, x]), t, c)
+    return out
+
+
+def run5(T0, iCp, nt, mlam, rdx, rdy, dt):
+    T = np.array(T0, dtype=np.float64)
+    for _ in range(nt):
+        T = step5(T, iCp, mlam, rdx, rdy, dt)
+    return T
