@@ -12,6 +12,12 @@ The ratio of the two step times bounds what the distributed path costs per
 rank (xGMI wire time aside: self messages stay on the GPU).
 
     python bench/rccl_self_overhead.py [--n 0 (auto: 288 GB tile)] [--steps 320]
+    python bench/rccl_self_overhead.py --n 16384 --K 1 --variants perf,perf_hide --steps 400
+
+Also reported per configuration: the host time to ENQUEUE the steps (the
+executor's per-step launch + RCCL group overhead, measured as the time until
+step() returns) and the per-pass HIP-event split (frame / halo / interior /
+exposed halo) of the executor.
 """
 from __future__ import annotations
 
@@ -25,7 +31,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(n: int, K: int, steps: int, periodic: bool) -> float:
+def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide") -> dict:
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
@@ -33,21 +39,31 @@ def run(n: int, K: int, steps: int, periodic: bool) -> float:
 
     p = 1 if periodic else 0
     gg.init_global_grid(n, n, 1, periodx=p, periody=p, quiet=True, transport="rccl",
-                        overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
+                        overlaps=(max(2, 2 * K), max(2, 2 * K), 2), halowidths=(K, K, 1),
                         self_via_transport=periodic)
-    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=n, ny=n, nt=steps, quiet=True,
+    m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=n, nt=steps, quiet=True,
                                     init="random", periods=(p, p, 0), temporal=K,
-                                    fast_math=K > 8))
+                                    fast_math=K > 1))
     m.step(2 * K)
     m.synchronize()
     t0 = time.perf_counter()
     m.step(steps)
+    t_enq = time.perf_counter() - t0
     m.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    # pass split on a second, shorter run
+    m.enable_pass_timing(True)
+    m.step(min(steps, 8 * K))
+    ts = m.pass_timings()
+    m.enable_pass_timing(False)
     m.close()
     gg.finalize_global_grid()
     torch.cuda.empty_cache()
-    return dt
+    nps = len(ts)
+    split = {k: sum(t[k] for t in ts) / nps for k in ("frame_ms", "halo_ms", "interior_ms",
+                                                     "exposed_halo_ms", "pass_ms")} if nps else {}
+    return {"ms_per_step": dt * 1e3, "enqueue_ms_per_step": t_enq / steps * 1e3,
+            "pass_split_ms": split}
 
 
 def main(argv=None) -> int:
@@ -55,6 +71,7 @@ def main(argv=None) -> int:
     ap.add_argument("--n", type=int, default=0, help="tile edge (0: 80%% of free HBM)")
     ap.add_argument("--K", type=int, default=16)
     ap.add_argument("--steps", type=int, default=320)
+    ap.add_argument("--variants", default="perf_hide")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -63,16 +80,18 @@ def main(argv=None) -> int:
     if not n:
         free, _ = torch.cuda.mem_get_info()
         n = int(math.isqrt(int(0.8 * free / 24))) // 256 * 256
-    rows = []
-    for periodic in (False, True, False, True):
-        dt = run(n, a.K, a.steps, periodic)
-        rows.append({"periodic_rccl_self": periodic, "ms_per_step": dt * 1e3,
-                     "teff_GBps": 3 * n * n * 8 / 1e9 / dt})
-        print(json.dumps(rows[-1]), flush=True)
-    op = [r["ms_per_step"] for r in rows if not r["periodic_rccl_self"]]
-    pe = [r["ms_per_step"] for r in rows if r["periodic_rccl_self"]]
-    out = {"tile": n, "K": a.K, "steps": a.steps, "runs": rows,
-           "overhead": min(pe) / min(op) - 1.0}
+    out = {"tile": n, "K": a.K, "steps": a.steps, "variants": {}}
+    for variant in a.variants.split(","):
+        rows = []
+        for periodic in (False, True, False, True):
+            r = run(n, a.K, a.steps, periodic, variant)
+            r.update({"periodic_rccl_self": periodic,
+                      "teff_GBps": 3 * n * n * 8 / 1e9 / (r["ms_per_step"] / 1e3)})
+            rows.append(r)
+            print(json.dumps({"variant": variant, **r}), flush=True)
+        op = [r["ms_per_step"] for r in rows if not r["periodic_rccl_self"]]
+        pe = [r["ms_per_step"] for r in rows if r["periodic_rccl_self"]]
+        out["variants"][variant] = {"runs": rows, "overhead": min(pe) / min(op) - 1.0}
     print(json.dumps(out), flush=True)
     if a.out:
         with open(a.out, "w") as f:

@@ -303,6 +303,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("nranks"), py::arg("rank"), py::arg("uid"), py::arg("device"),
            py::arg("init_timeout_s") = 0.0)
       .def_property_readonly("nonblocking", &RcclComm::nonblocking)
+      .def_property_readonly("data_blocking", &RcclComm::data_blocking)
       .def_property_readonly("device", &RcclComm::device)
       .def("allreduce",
            [](RcclComm& c, uintptr_t sb, uintptr_t rb, size_t count, DType dt, RedOp op,

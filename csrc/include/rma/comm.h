@@ -66,13 +66,22 @@ class RcclComm : public P2PTransport {
   void check_async();
   void abort();
   bool aborted() const { return aborted_; }
+  // nonblocking(): the communicator was created non-blocking (init with a
+  // timeout; group ends are then polled until RCCL has enqueued them);
+  // data_blocking(): the data path runs on a blocking communicator
+  // (RMA_RCCL_BLOCKING=1 init, or RMA_RCCL_DATA_BLOCKING=1: split from the
+  // non-blocking one after init; no host-time gain measured, see comm.cpp).
   bool nonblocking() const { return nonblocking_; }
+  bool data_blocking() const { return parent_ != nullptr || !nonblocking_; }
 
  private:
-  // Non-blocking communicators: wait until the last call left ncclInProgress.
+  // Non-blocking data communicator: wait until the last call left ncclInProgress.
   void settle(const char* what);
+  void poll_ready(void* comm, const char* what);
+  void split_blocking(int rank);
   int nranks_, rank_, device_;
-  void* comm_ = nullptr;  // ncclComm_t
+  void* comm_ = nullptr;  // ncclComm_t of the data path
+  void* parent_ = nullptr;  // the non-blocking communicator comm_ was split from
   double* scratch_ = nullptr;  // 2 doubles of device memory for barrier()
   bool aborted_ = false;
   bool nonblocking_ = false;

@@ -156,12 +156,14 @@ class DiffusionExecutor {
   int64_t steps_ = 0;
   int64_t passes_ = 0;
   bool solo_ = false;
+  bool pooled_ = false;  // streams borrowed from the process-wide pool
   Neighbors real_nbr_{{{-1, -1}, {-1, -1}, {-1, -1}}};
   // timing: 5 events per pass (start, frame end, halo end on hi; interior
   // start, end on lo)
   bool timing_ = false;
   std::vector<void*> tev_;
   std::vector<int> tk_;
+  std::vector<char> tseq_;  // 1: sequential pass (exchange after the kernel)
   size_t tused_ = 0;
   void* tevent();
   void release_timing();

@@ -22,27 +22,10 @@
 #include <vector>
 
 #include "rma/comm.h"
+#include "rma/halo_plan.h"
 #include "rma/kernels.h"
 
 namespace rma {
-
-struct HaloField {
-  void* ptr = nullptr;
-  std::array<int64_t, 3> size{1, 1, 1};  // extent along x, y, z (x fastest)
-  int elem_bytes = 8;
-  std::array<int64_t, 3> ol{2, 2, 2};    // overlap of this array per dim
-  std::array<int64_t, 3> hw{1, 1, 1};    // halo width per dim
-};
-
-// A strided view of one plane block of a field: n_o rows of n_k contiguous
-// elements, rows `ld` elements apart, starting at element `offset`.
-struct PlaneView {
-  int64_t offset, n_o, n_k, ld;
-  bool contiguous() const { return n_o == 1 || ld == n_k; }
-  int64_t elems() const { return n_o * n_k; }
-};
-PlaneView plane_view(const HaloField& f, int dim, int64_t index0);
-bool has_halo(const HaloField& f, int dim);
 
 class HaloExchanger {
  public:

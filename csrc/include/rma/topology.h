@@ -42,4 +42,22 @@ class CartTopology {
   std::array<int, 3> periods_;
 };
 
+// The implicit global grid of one rank (ImplicitGlobalGrid init_global_grid,
+// SURVEY.md C16/C17), host-only: what the C ABI (capi.cpp) and the Python
+// layer compute before any GPU or communicator exists.
+struct GridDesc {
+  int nprocs = 1, me = 0;
+  std::array<int, 3> nxyz{1, 1, 1}, dims{1, 1, 1}, periods{0, 0, 0}, overlaps{2, 2, 2},
+      hw{1, 1, 1}, coords{0, 0, 0};
+  std::array<int64_t, 3> nxyz_g{1, 1, 1};
+  std::array<std::array<int, 2>, 3> neighbors{{{-1, -1}, {-1, -1}, {-1, -1}}};
+};
+// Null dims / periods / overlaps / halowidths mean IGG's defaults (auto, open,
+// 2, overlap/2). Validates every argument (throws rma::Error).
+GridDesc make_grid_desc(int nx, int ny, int nz, const int dims[3], const int periods[3],
+                        const int overlaps[3], const int halowidths[3], int nprocs, int rank);
+// IGG x_g / y_g / z_g: global coordinate of local index ix (0-based) of an
+// array of size size_A along d (staggered arrays are offset by half a cell).
+double grid_coord(const GridDesc& g, int d, int64_t ix, double dd, int64_t size_A);
+
 }  // namespace rma

@@ -415,8 +415,10 @@ __global__ __launch_bounds__(kBlock) void stencilk5_kernel(
   stencilk5_body<K, V, NT>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
 }
 
-// kernel=6/7 ("fast5p2" / "fast5p4"): kernel 5's arithmetic with the K levels
-// of ONE strip split over the S waves of a block (S = 2 / 4 stages of H = K/S
+// kernel=6/7/8 ("fast5p2" / "fast5p4" / "fast5p8"): kernel 5's arithmetic with
+// the K levels of ONE strip split over the S waves of a block (S = 2 / 4 / 8
+// stages of H = K/S; fixed K in {8, 12, 16}, fast5p8 K in {8, 16}; the any-K
+// generalisation is stencil_pipe.h, kernels 9/10)
 // levels each). Stage s keeps only its own H three-row windows (K=16, S=4:
 // 48 instead of 192 VGPRs of windows, so 5 waves per SIMD instead of 2 hide
 // the fp64 and LDS latencies). Stage 0 streams T / 1/Cp from HBM and fills
@@ -639,6 +641,8 @@ __device__ __forceinline__ void stencilk5p_body(
     run(std::false_type{});
 }
 
+// Waves per SIMD: S=4 -> 3 (below), S=8 -> 4 (512-thread blocks, 75.8 KB LDS
+// at V=4: 2 blocks per CU, VGPR budget 128), S=2 -> no cap.
 // 3 waves per SIMD: the 51.2 KB LDS of a K=16, S=4 block allows 3 blocks per
 // CU, so the VGPR budget is 168 (512 / 3, 8-register granules)
 template <int K, int S, int V, bool NT>

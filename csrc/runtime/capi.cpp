@@ -19,11 +19,8 @@
 #include "rma/kernels.h"
 #include "rma/topology.h"
 
-struct rma_grid {
-  int nprocs = 1, me = 0, device = 0;
-  std::array<int, 3> nxyz{1, 1, 1}, dims{1, 1, 1}, periods{0, 0, 0}, overlaps{2, 2, 2},
-      hw{1, 1, 1}, coords{0, 0, 0};
-  std::array<int64_t, 3> nxyz_g{1, 1, 1};
+struct rma_grid : rma::GridDesc {  // host part: topology.cpp make_grid_desc
+  int device = 0;
   std::unique_ptr<rma::CartTopology> topo;
   std::unique_ptr<rma::RcclComm> comm;
   std::unique_ptr<rma::HaloExchanger> halo;
@@ -45,15 +42,7 @@ int guard(F&& f) {
 }
 
 double coord(const rma_grid* g, int d, int64_t ix, double dd, int64_t size_A) {
-  const double x0 = 0.5 * (double)(g->nxyz[d] - size_A) * dd;
-  double x = (double)((int64_t)g->coords[d] * (g->nxyz[d] - g->overlaps[d]) + ix) * dd + x0;
-  if (g->periods[d]) {
-    const int64_t n = g->nxyz_g[d];
-    x = x - dd;
-    if (x > (double)(n - 1) * dd) x = x - (double)n * dd;
-    if (x < 0) x = x + (double)n * dd;
-  }
-  return x;
+  return rma::grid_coord(*g, d, ix, dd, size_A);
 }
 }  // namespace
 
@@ -77,25 +66,10 @@ int rma_init_global_grid(int nx, int ny, int nz, const int dims[3], const int pe
   return guard([&] {
     RMA_CHECK_ARG(out_grid != nullptr, "out_grid is NULL");
     auto g = std::make_unique<rma_grid>();
-    g->nxyz = {nx, ny, nz};
-    g->nprocs = nprocs;
-    g->me = rank;
+    static_cast<rma::GridDesc&>(*g) =
+        rma::make_grid_desc(nx, ny, nz, dims, periods, overlaps, halowidths, nprocs, rank);
     g->device = device;
-    std::array<int, 3> din{0, 0, 0};
-    for (int d = 0; d < 3; ++d) {
-      din[d] = dims ? dims[d] : 0;
-      g->periods[d] = periods ? periods[d] : 0;
-      g->overlaps[d] = overlaps ? overlaps[d] : 2;
-      g->hw[d] = halowidths ? halowidths[d] : std::max(1, g->overlaps[d] / 2);
-      if (g->nxyz[d] == 1) din[d] = 1;
-    }
-    g->dims = rma::dims_create(nprocs, din);
     g->topo = std::make_unique<rma::CartTopology>(nprocs, g->dims, g->periods);
-    g->coords = g->topo->coords(rank);
-    for (int d = 0; d < 3; ++d)
-      g->nxyz_g[d] = g->nxyz[d] == 1 ? 1
-                                     : (int64_t)g->dims[d] * (g->nxyz[d] - g->overlaps[d]) +
-                                           (g->periods[d] ? 0 : g->overlaps[d]);
     RMA_HIP_CHECK(hipSetDevice(device));
     if (nprocs > 1) {
       RMA_CHECK_ARG(unique_id != nullptr, "unique_id required when nprocs > 1");

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <utility>
 
@@ -18,6 +19,14 @@ namespace rma {
 namespace {
 hipStream_t S(void* p) { return reinterpret_cast<hipStream_t>(p); }
 hipEvent_t E(void* p) { return reinterpret_cast<hipEvent_t>(p); }
+
+// Process-wide pool of (low, high)-priority stream pairs: an executor takes a
+// free pair (or creates one, low priority first) and returns it when it is
+// destroyed, so rebuilding executors (set_temporal, loopback ranks, tests)
+// reuses the same HIP streams instead of creating new ones
+// (RMA_EXEC_STREAMS=pool; profiles/stream_order_r2.json).
+std::mutex g_pool_mu;
+std::vector<std::pair<hipStream_t, hipStream_t>> g_pool;
 }  // namespace
 
 StencilTuning default_tune_k(int K, int64_t ny) {
@@ -114,15 +123,32 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   int least = 0, greatest = 0;
   RMA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   hipStream_t hi, lo;
-  // Create the low-priority (interior) stream FIRST. Measured on MI355X /
-  // ROCm 7 (bench/probe_set_temporal.py, profiles/SUMMARY_r1.md): creating the
-  // high-priority stream first left every second executor of a process with
-  // a low-priority stream running the stencil ~25% slower (4.6 vs 6.2 TB/s);
-  // low-first (or unprioritised streams) is fast for every instance.
-  // RMA_EXEC_STREAMS=plain|hifirst selects the alternatives for diagnostics.
+  // Streams come from a process-wide pool, created low priority first.
+  // Mechanism (bench/probe_stream_order.py, rocprofv3 kernel trace with queue
+  // ids, profiles/stream_order_r2.md): every new HIP stream of a process is
+  // bound to the next hardware queue, and on MI355X / ROCm 7 the one-step
+  // kernel (many short workgroups, dispatch-rate sensitive) dispatched from
+  // the process's 5th queue ran 28 % slower (1.32 vs 1.03 ms at 16384^2).
+  // With two executors alive, creating high-priority streams first put the
+  // SECOND executor's interior stream on that queue (r1's "every second
+  // executor 25 % slower"); low-priority first puts only its tiny frame
+  // kernels there. The pool additionally reuses the streams of destroyed
+  // executors (rebuilds, set_temporal), so no new queues accumulate.
+  // RMA_EXEC_STREAMS=lofirst|hifirst|plain create per executor (diagnostics).
   const char* sm = std::getenv("RMA_EXEC_STREAMS");
-  const std::string mode = sm ? sm : "lofirst";
-  if (mode == "plain") {
+  const std::string mode = sm ? sm : "pool";
+  if (mode == "pool") {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!g_pool.empty()) {
+      lo = g_pool.back().first;
+      hi = g_pool.back().second;
+      g_pool.pop_back();
+    } else {
+      RMA_HIP_CHECK(hipStreamCreateWithPriority(&lo, hipStreamNonBlocking, least));
+      RMA_HIP_CHECK(hipStreamCreateWithPriority(&hi, hipStreamNonBlocking, greatest));
+    }
+    pooled_ = true;
+  } else if (mode == "plain") {
     RMA_HIP_CHECK(hipStreamCreateWithFlags(&lo, hipStreamNonBlocking));
     RMA_HIP_CHECK(hipStreamCreateWithFlags(&hi, hipStreamNonBlocking));
   } else if (mode == "hifirst") {
@@ -154,6 +180,13 @@ DiffusionExecutor::~DiffusionExecutor() {
   if (e_hi_) (void)hipEventDestroy(E(e_hi_));
   if (e_lo_) (void)hipEventDestroy(E(e_lo_));
   if (e_in_) (void)hipEventDestroy(E(e_in_));
+  if (pooled_) {  // back to the pool, drained
+    (void)hipStreamSynchronize(S(s_hi_));
+    (void)hipStreamSynchronize(S(s_lo_));
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.emplace_back(S(s_lo_), S(s_hi_));
+    return;
+  }
   if (s_hi_) (void)hipStreamDestroy(S(s_hi_));
   if (s_lo_) (void)hipStreamDestroy(S(s_lo_));
 }
@@ -228,12 +261,13 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
       RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
     }
     rec(0, s_lo_);
-    rec(1, s_lo_);
     rec(3, s_lo_);
     stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &full_, 1, c, p_.tune, s_lo_);
     rec(4, s_lo_);
+    rec(1, s_lo_);
     exchange(Tout, s_lo_);
     rec(2, s_lo_);
+    if (ev[4]) tseq_.push_back(1);
     if (p_.mode == Mode::kHide) {
       RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
       RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
@@ -266,6 +300,7 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
   }
   rec(4, s_lo_);
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+  if (ev[4]) tseq_.push_back(0);
 }
 
 void DiffusionExecutor::multi_step(int K, double* Tin, double* Tout, const double* iCp,
@@ -289,15 +324,16 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   auto rec = [&](int i, void* stream) {
     if (ev[4]) RMA_HIP_CHECK(hipEventRecord(E(ev[i]), S(stream)));
   };
-  if (p_.mode == Mode::kPerf) {
+  if (p_.mode == Mode::kPerf) {  // no frame; the exchange follows the pass
     TraceRange tr("rma.pass.perf");
     rec(0, s_lo_);
-    rec(1, s_lo_);
     rec(3, s_lo_);
     multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, tn, s_lo_);
     rec(4, s_lo_);
+    rec(1, s_lo_);
     exchange(Tout, s_lo_);
     rec(2, s_lo_);
+    if (ev[4]) tseq_.push_back(1);
     return;
   }
   TraceRange tr("rma.pass.hide");
@@ -323,6 +359,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   }
   rec(4, s_lo_);
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+  if (ev[4]) tseq_.push_back(0);
 }
 
 void* DiffusionExecutor::tevent() {
@@ -340,6 +377,7 @@ void DiffusionExecutor::release_timing() {
   for (void* e : tev_) (void)hipEventDestroy(E(e));
   tev_.clear();
   tk_.clear();
+  tseq_.clear();
   tused_ = 0;
 }
 
@@ -348,6 +386,7 @@ void DiffusionExecutor::set_timing(bool on) {
   RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
   tused_ = 0;
   tk_.clear();
+  tseq_.clear();
   timing_ = on;
 }
 
@@ -361,7 +400,8 @@ std::vector<PassTiming> DiffusionExecutor::timings() {
     for (int j = 1; j < 5; ++j) RMA_HIP_CHECK(hipEventElapsedTime(&t[j], e[0], e[j]));
     PassTiming pt;
     pt.K = tk_[i];
-    pt.frame_ms = t[1];
+    // sequential passes (perf, solo): the exchange starts after the kernel
+    pt.frame_ms = tseq_[i] ? 0.0f : t[1];
     pt.halo_ms = t[2] - t[1];
     pt.interior_ms = t[4] - t[3];
     pt.pass_ms = std::max(t[2], t[4]);

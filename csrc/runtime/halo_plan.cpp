@@ -1,0 +1,78 @@
+#include "rma/halo_plan.h"
+
+namespace rma {
+
+PlaneView plane_view(const HaloField& f, int dim, int64_t i0) {
+  const int64_t nx = f.size[0], ny = f.size[1], nz = f.size[2];
+  const int64_t hw = f.hw[dim];
+  switch (dim) {
+    case 0: return {i0, nz * ny, hw, nx};
+    case 1: return {i0 * nx, nz, hw * nx, ny * nx};
+    default: return {i0 * nx * ny, 1, hw * nx * ny, nx * ny * nz};
+  }
+}
+
+bool has_halo(const HaloField& f, int d) {
+  return f.size[d] > 1 && f.ol[d] >= 2 * f.hw[d] && f.size[d] >= f.ol[d] + f.hw[d];
+}
+
+void validate_field(const HaloField& f) {
+  RMA_CHECK_ARG(f.ptr != nullptr, "null field");
+  RMA_CHECK_ARG(f.elem_bytes == 2 || f.elem_bytes == 4 || f.elem_bytes == 8 || f.elem_bytes == 16,
+                "elem_bytes=" << f.elem_bytes);
+  for (int d = 0; d < 3; ++d) RMA_CHECK_ARG(f.hw[d] >= 1 && f.size[d] >= 1, "bad field dims");
+}
+
+HaloPlan plan_exchange(const std::vector<HaloField>& fields,
+                       const std::array<std::array<int, 2>, 3>& nbr, int self,
+                       bool self_via_comm, int dims_mask) {
+  HaloPlan plan;
+  for (const auto& f : fields) validate_field(f);
+  for (int d = 0; d < 3; ++d) {
+    if (!(dims_mask >> d & 1) || (nbr[d][0] < 0 && nbr[d][1] < 0)) continue;
+    HaloDimPlan dp;
+    dp.dim = d;
+    for (int fi = 0; fi < (int)fields.size(); ++fi) {
+      const HaloField& f = fields[fi];
+      if (!has_halo(f, d)) continue;
+      const int64_t n = f.size[d], ol = f.ol[d], hw = f.hw[d];
+      // send planes: lo [ol-hw, ol), hi [n-ol, n-ol+hw); recv planes: lo [0,hw), hi [n-hw, n)
+      const PlaneView send_v[2] = {plane_view(f, d, ol - hw), plane_view(f, d, n - ol)};
+      const PlaneView recv_v[2] = {plane_view(f, d, 0), plane_view(f, d, n - hw)};
+      const size_t bytes = (size_t)send_v[0].elems() * f.elem_bytes;
+      HaloMsg s_ops[2], r_ops[2];
+      bool on[2] = {false, false};
+      for (int s = 0; s < 2; ++s) {
+        const int p = nbr[d][s];
+        if (p < 0) continue;
+        if (p == self && !self_via_comm) {
+          // periodic, single process along d: my side-s halo <- my opposite send plane
+          dp.copies.push_back({fi, recv_v[s], send_v[1 - s]});
+          continue;
+        }
+        on[s] = true;
+        if (send_v[s].contiguous()) {  // zero-copy: straight from / into the field
+          s_ops[s] = {p, fi, send_v[s], -1, bytes};
+          r_ops[s] = {p, fi, recv_v[s], -1, bytes};
+        } else {
+          const int sb = (int)plan.slot_bytes.size();
+          plan.slot_bytes.push_back(bytes);
+          plan.slot_bytes.push_back(bytes);
+          dp.packs.push_back({fi, send_v[s], sb});
+          s_ops[s] = {p, fi, send_v[s], sb, bytes};
+          r_ops[s] = {p, fi, recv_v[s], sb + 1, bytes};
+          dp.unpacks.push_back({fi, recv_v[s], sb + 1});
+        }
+        plan.bytes_sent += (int64_t)bytes;
+      }
+      for (int s = 0; s < 2; ++s)
+        if (on[s]) dp.sends.push_back(s_ops[s]);
+      for (int s = 1; s >= 0; --s)
+        if (on[s]) dp.recvs.push_back(r_ops[s]);
+    }
+    plan.dims.push_back(std::move(dp));
+  }
+  return plan;
+}
+
+}  // namespace rma

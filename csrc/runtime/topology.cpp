@@ -81,4 +81,55 @@ std::array<std::array<int, 2>, 3> CartTopology::neighbors(int rank) const {
   return {shift(rank, 0), shift(rank, 1), shift(rank, 2)};
 }
 
+GridDesc make_grid_desc(int nx, int ny, int nz, const int dims[3], const int periods[3],
+                        const int overlaps[3], const int halowidths[3], int nprocs, int rank) {
+  RMA_CHECK_ARG(nprocs >= 1 && rank >= 0 && rank < nprocs, "rank " << rank << " of " << nprocs);
+  RMA_CHECK_ARG(nx >= 1 && ny >= 1 && nz >= 1, "local sizes " << nx << "x" << ny << "x" << nz);
+  GridDesc g;
+  g.nxyz = {nx, ny, nz};
+  g.nprocs = nprocs;
+  g.me = rank;
+  std::array<int, 3> din{0, 0, 0};
+  for (int d = 0; d < 3; ++d) {
+    din[d] = dims ? dims[d] : 0;
+    g.periods[d] = periods ? (periods[d] ? 1 : 0) : 0;
+    g.overlaps[d] = overlaps ? overlaps[d] : 2;
+    g.hw[d] = halowidths ? halowidths[d] : std::max(1, g.overlaps[d] / 2);
+    RMA_CHECK_ARG(din[d] >= 0, "dims[" << d << "] = " << din[d]);
+    if (g.nxyz[d] == 1) {
+      RMA_CHECK_ARG(din[d] <= 1 && !g.periods[d],
+                    "dimension " << d << " has local size 1: it cannot be split or periodic");
+      din[d] = 1;
+    } else {
+      RMA_CHECK_ARG(g.hw[d] >= 1 && g.overlaps[d] >= 2 * g.hw[d],
+                    "dim " << d << ": overlap " << g.overlaps[d] << " must be >= 2*halowidth "
+                           << g.hw[d]);
+      RMA_CHECK_ARG(g.nxyz[d] >= g.overlaps[d] + g.hw[d],
+                    "dim " << d << ": local size " << g.nxyz[d] << " < overlap + halowidth");
+    }
+  }
+  g.dims = dims_create(nprocs, din);
+  const CartTopology topo(nprocs, g.dims, g.periods);
+  g.coords = topo.coords(rank);
+  g.neighbors = topo.neighbors(rank);
+  for (int d = 0; d < 3; ++d)
+    g.nxyz_g[d] = g.nxyz[d] == 1 ? 1
+                                 : (int64_t)g.dims[d] * (g.nxyz[d] - g.overlaps[d]) +
+                                       (g.periods[d] ? 0 : g.overlaps[d]);
+  return g;
+}
+
+double grid_coord(const GridDesc& g, int d, int64_t ix, double dd, int64_t size_A) {
+  RMA_CHECK_ARG(d >= 0 && d < 3, "dim " << d);
+  const double x0 = 0.5 * (double)(g.nxyz[d] - size_A) * dd;
+  double x = (double)((int64_t)g.coords[d] * (g.nxyz[d] - g.overlaps[d]) + ix) * dd + x0;
+  if (g.periods[d]) {
+    const int64_t n = g.nxyz_g[d];
+    x = x - dd;
+    if (x > (double)(n - 1) * dd) x = x - (double)n * dd;
+    if (x < 0) x = x + (double)n * dd;
+  }
+  return x;
+}
+
 }  // namespace rma

@@ -547,10 +547,24 @@ class Diffusion2D:
             self.check_finite()
 
     # ------------------------------------------------------------------
-    def gather_interior(self, root: int = 0):
+    def gather_interior(self, root: int = 0, max_bytes: int | None = None):
         """T_v: the halo-stripped fields of all ranks assembled on root
-        (ap.jl:45-46: T_nh .= Array(T[2:end-1,2:end-1]); gather!(T_nh, T_v))."""
-        T_nh = self.field[1:-1, 1:-1].contiguous()
+        (ap.jl:45-46: T_nh .= Array(T[2:end-1,2:end-1]); gather!(T_nh, T_v)).
+
+        The gather lands on the root's device (RCCL) or host: refused above
+        ``max_bytes`` (default ``RMA_GATHER_MAX_BYTES`` or 8 GiB) -- a 288 GB
+        tile per rank would need N x 80 GB there; ``visualise`` subsamples."""
+        import os
+
+        limit = int(max_bytes if max_bytes is not None
+                    else os.environ.get("RMA_GATHER_MAX_BYTES", 8 << 30))
+        inner = self.field[1:-1, 1:-1]
+        total = inner.numel() * inner.element_size() * self.g.nprocs
+        if total > limit:
+            raise ValueError(f"gather_interior would assemble {total / 2**30:.1f} GiB on rank "
+                             f"{root} (limit {limit / 2**30:.1f} GiB): subsample first "
+                             "(visualise(max_pixels=...)) or raise max_bytes")
+        T_nh = inner.contiguous()
         return gather_(T_nh, None, root)
 
     def visualise(self, max_pixels: int = 2048) -> dict | None:

@@ -175,21 +175,38 @@ def _gloo_group():
     return _gloo_pg
 
 
-def shutdown_distributed() -> None:
+def shutdown_distributed(barrier: bool = True, timeout_s: float | None = None) -> None:
     """Destroy the default process group once every rank has reached teardown.
 
     Without the barrier a rank that finishes first closes its gloo pairs while
     a peer's last collective is still draining them; the peer's gloo thread
     then aborts the process ("terminate called without an active exception",
     seen at 4 and 8 ranks), turning a finished run into a failed one.
+
+    The barrier is bounded (``RMA_TEARDOWN_TIMEOUT``, default 30 s): if a peer
+    died or is stuck in another collective, the others give up waiting and
+    destroy their group instead of blocking for the full communication
+    timeout. Error paths pass ``barrier=False`` (or run inside an exception
+    handler, detected here) and destroy directly.
     """
     global _gloo_pg
     if not dist.is_initialized():
         return
+    import datetime
+    import sys
+
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("RMA_TEARDOWN_TIMEOUT", "30"))
+    if sys.exc_info()[0] is not None:  # called from an error path (finally / except)
+        barrier = False
     try:
-        # a CPU all-reduce is a barrier on the gloo side of a "cpu:gloo,cuda:nccl"
-        # group (dist.barrier there would create a torch RCCL communicator)
-        dist.all_reduce(torch.zeros(1), group=_gloo_group())
+        if barrier:
+            # a CPU all-reduce is a barrier on the gloo side of a "cpu:gloo,cuda:nccl"
+            # group (dist.barrier there would create a torch RCCL communicator)
+            work = dist.all_reduce(torch.zeros(1), group=_gloo_group(), async_op=True)
+            work.wait(timeout=datetime.timedelta(seconds=timeout_s))
+    except Exception:  # noqa: BLE001 - a dead peer must not block teardown
+        pass
     finally:
         dist.destroy_process_group()
         _gloo_pg = None

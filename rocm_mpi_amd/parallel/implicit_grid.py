@@ -198,14 +198,18 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
         try:
             comm = C.RcclComm(dev, timeout_s=timeout_s)
         except RuntimeError as e:
-            if os.environ.get("RMA_RCCL_STRICT", "0") == "1":
+            # RCCL is the perf path: a failed init is fatal unless the caller
+            # opted into the host-staged validation transport
+            # (RMA_RCCL_FALLBACK=1; bench.py never does: a scaling point must
+            # not silently run staged)
+            if (os.environ.get("RMA_RCCL_FALLBACK", "0") != "1"
+                    or os.environ.get("RMA_RCCL_STRICT", "0") == "1"
+                    or not torch.distributed.is_initialized()):
                 raise
-            # keep the job alive on the validation transport rather than dying
-            # (loud: the perf path is RCCL; RMA_RCCL_STRICT=1 makes this fatal)
             import warnings
 
             warnings.warn(f"RCCL communicator init failed ({e}); falling back to the host-staged "
-                          "transport", RuntimeWarning, stacklevel=2)
+                          "transport (RMA_RCCL_FALLBACK=1)", RuntimeWarning, stacklevel=2)
             tname = "staged"
             comm = C.TorchDistComm(staged=True)
     else:

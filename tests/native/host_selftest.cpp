@@ -1,13 +1,26 @@
 // Host-side self test of the native core, built with AddressSanitizer and
 // UndefinedBehaviorSanitizer (tests/test_native_host_asan.py). Covers the pure
-// host code: topology, CPU stencil / kp twins, pack/unpack, reductions,
-// argument validation (exceptions instead of out-of-bounds access).
+// host code: topology and the C ABI's grid description, CPU stencil / kp /
+// fast5 twins, pack/unpack, reductions, the executor's pass geometry and pass
+// planner (plan.cpp), the halo exchange plan (halo_plan.cpp) executed on host
+// memory for several fake ranks of one process (periodic self neighbours,
+// minimal tiles, staggered n+1 fields, 2K overlaps, 3D), parallel_for
+// exception propagation, and argument validation (exceptions instead of
+// out-of-bounds access).
 #include <cmath>
 #include <cstdio>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
 #include <random>
+#include <stdexcept>
 #include <vector>
 
+#include "rma/halo_plan.h"
 #include "rma/kernels.h"
+#include "rma/parallel_for.h"
+#include "rma/plan.h"
 #include "rma/topology.h"
 
 #define EXPECT(c)                                                   \
@@ -17,6 +30,148 @@
       return 1;                                                     \
     }                                                               \
   } while (0)
+
+namespace {
+using namespace rma;
+
+template <typename F>
+bool throws(F&& f) {
+  try {
+    f();
+  } catch (const Error&) {
+    return true;
+  }
+  return false;
+}
+
+// N fake ranks of a Cartesian grid, each owning a local tile of a global
+// field; one halo exchange executed from the plan on host memory (copy2d_cpu
+// for copies / packs / unpacks, per-pair FIFO queues matching sends and
+// receives in order, like RCCL). Afterwards every tile must equal its window
+// of the global field.
+int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<int, 3> n,
+              std::array<int, 3> ol, std::array<int, 3> hw, int stagger_x, bool via_comm) {
+  const int P = dims[0] * dims[1] * dims[2];
+  CartTopology topo(P, dims, periods);
+  std::array<int64_t, 3> ng;
+  for (int d = 0; d < 3; ++d)
+    ng[d] = n[d] == 1 ? 1 : (int64_t)dims[d] * (n[d] - ol[d]) + (periods[d] ? 0 : ol[d]);
+  // field 0: n; field 1: staggered along x (size n+stagger_x, overlap ol+stagger_x)
+  auto gval = [&](int f, int64_t gx, int64_t gy, int64_t gz) {
+    return 1000.0 * f + gx + 1e3 * (gy + 1) + 1e6 * (gz + 1);
+  };
+  struct Tile {
+    std::array<std::vector<double>, 2> a;
+    std::array<std::array<int64_t, 3>, 2> size;
+  };
+  std::vector<Tile> tiles(P);
+  std::vector<std::vector<HaloField>> fields(P);
+  auto gidx = [&](int r, int f, int d, int64_t i) {
+    const int64_t c = topo.coords(r)[d];
+    const int64_t nd = n[d] + (f == 1 && d == 0 ? stagger_x : 0);
+    const int64_t ngd = ng[d] + (f == 1 && d == 0 && !periods[d] ? stagger_x : 0);
+    int64_t g = c * (n[d] - ol[d]) + i;
+    if (periods[d]) g = ((g % ngd) + ngd) % ngd;
+    (void)nd;
+    return g;
+  };
+  for (int r = 0; r < P; ++r) {
+    for (int f = 0; f < 2; ++f) {
+      auto& sz = tiles[r].size[f];
+      sz = {n[0] + (f == 1 ? stagger_x : 0), n[1], n[2]};
+      tiles[r].a[f].assign(sz[0] * sz[1] * sz[2], -7.0);
+      const auto nb = topo.neighbors(r);
+      for (int64_t z = 0; z < sz[2]; ++z)
+        for (int64_t y = 0; y < sz[1]; ++y)
+          for (int64_t x = 0; x < sz[0]; ++x) {
+            // halo planes start as garbage, every other cell holds the global value
+            const int64_t ix[3] = {x, y, z};
+            bool halo = false;
+            for (int d = 0; d < 3; ++d) {
+              const int64_t s = sz[d], h = hw[d];
+              const int64_t old = ol[d] + (s - n[d]);
+              const bool hh = s > 1 && old >= 2 * h && s >= old + h;
+              if (!hh) continue;
+              if (nb[d][0] >= 0 && ix[d] < h) halo = true;
+              if (nb[d][1] >= 0 && ix[d] >= s - h) halo = true;
+            }
+            if (!halo)
+              tiles[r].a[f][(z * sz[1] + y) * sz[0] + x] =
+                  gval(f, gidx(r, f, 0, x), gidx(r, f, 1, y), gidx(r, f, 2, z));
+          }
+      HaloField hf;
+      hf.ptr = tiles[r].a[f].data();
+      hf.size = sz;
+      hf.elem_bytes = 8;
+      for (int d = 0; d < 3; ++d) {
+        hf.ol[d] = ol[d] + (sz[d] - n[d]);
+        hf.hw[d] = hw[d];
+      }
+      fields[r].push_back(hf);
+    }
+  }
+  std::vector<HaloPlan> plans(P);
+  std::vector<std::vector<std::vector<double>>> bufs(P);
+  for (int r = 0; r < P; ++r) {
+    plans[r] = plan_exchange(fields[r], topo.neighbors(r), r, via_comm, 7);
+    for (size_t b : plans[r].slot_bytes) bufs[r].push_back(std::vector<double>(b / 8, -9.0));
+  }
+  auto at = [&](int r, int f, const PlaneView& v) {
+    return reinterpret_cast<char*>(fields[r][f].ptr) + v.offset * 8;
+  };
+  // dimension by dimension on every rank (the plans list the same dims)
+  std::map<std::pair<int, int>, std::deque<std::vector<char>>> wire;
+  for (size_t k = 0; k < plans[0].dims.size(); ++k) {
+    for (int r = 0; r < P; ++r) {
+      if (plans[r].dims.size() != plans[0].dims.size()) return 101;
+      const HaloDimPlan& dp = plans[r].dims[k];
+      for (const auto& c : dp.copies)
+        copy2d_cpu(at(r, c.field, c.dst), c.dst.ld, at(r, c.field, c.src), c.src.ld, c.src.n_o,
+                   c.src.n_k, 8);
+      for (const auto& p : dp.packs)
+        copy2d_cpu(bufs[r][p.slot].data(), p.view.n_k, at(r, p.field, p.view), p.view.ld,
+                   p.view.n_o, p.view.n_k, 8);
+      for (const auto& m : dp.sends) {
+        const char* src = m.slot >= 0 ? reinterpret_cast<const char*>(bufs[r][m.slot].data())
+                                      : at(r, m.field, m.view);
+        wire[{r, m.peer}].emplace_back(src, src + m.bytes);
+      }
+    }
+    for (int r = 0; r < P; ++r) {
+      const HaloDimPlan& dp = plans[r].dims[k];
+      for (const auto& m : dp.recvs) {
+        auto& q = wire[{m.peer, r}];
+        if (q.empty()) return 102;
+        if (q.front().size() != m.bytes) return 103;
+        char* dst = m.slot >= 0 ? reinterpret_cast<char*>(bufs[r][m.slot].data())
+                                : at(r, m.field, m.view);
+        std::memcpy(dst, q.front().data(), m.bytes);
+        q.pop_front();
+      }
+      for (const auto& u : dp.unpacks)
+        copy2d_cpu(at(r, u.field, u.view), u.view.ld, bufs[r][u.slot].data(), u.view.n_k,
+                   u.view.n_o, u.view.n_k, 8);
+    }
+  }
+  for (auto& kv : wire)
+    if (!kv.second.empty()) return 104;
+  for (int r = 0; r < P; ++r)
+    for (int f = 0; f < 2; ++f) {
+      const auto& sz = tiles[r].size[f];
+      for (int64_t z = 0; z < sz[2]; ++z)
+        for (int64_t y = 0; y < sz[1]; ++y)
+          for (int64_t x = 0; x < sz[0]; ++x) {
+            const double want = gval(f, gidx(r, f, 0, x), gidx(r, f, 1, y), gidx(r, f, 2, z));
+            if (tiles[r].a[f][(z * sz[1] + y) * sz[0] + x] != want) {
+              std::fprintf(stderr, "halo mismatch rank %d field %d at (%ld,%ld,%ld)\n", r, f,
+                           (long)x, (long)y, (long)z);
+              return 105;
+            }
+          }
+    }
+  return 0;
+}
+}  // namespace
 
 int main() {
   using namespace rma;
@@ -71,6 +226,144 @@ int main() {
   EXPECT(reduce_cpu(T.data(), nx * ny, kMaxAbs) <= 1.0);
   T[11] = NAN;
   EXPECT(reduce_cpu(T.data(), nx * ny, kNonFinite) == 1.0);
+  // fast5 CPU twin: K passes == K one-step passes, finite, differs from canonical
+  {
+    std::vector<double> a(nx * ny), b(nx * ny), k3(nx * ny);
+    for (auto& v : T) v = u(g);
+    stencil5_rects_cpu(a.data(), T.data(), iCp.data(), nx, ny, &r, 1, c);
+    for (int64_t i = 0; i < nx * ny; ++i)
+      if (!(i % nx == 0 || i % nx == nx - 1 || i / nx == 0 || i / nx == ny - 1)) continue;
+      else a[i] = T[i];
+    stencil5_rects_cpu(b.data(), a.data(), iCp.data(), nx, ny, &r, 1, c);
+    stencilk5_rects_cpu(2, k3.data(), T.data(), iCp.data(), nx, ny, &r, 1, c);
+    for (int64_t y = 1; y < ny - 1; ++y)
+      for (int64_t x = 1; x < nx - 1; ++x) EXPECT(k3[y * nx + x] == b[y * nx + x]);
+    EXPECT(throws([&] { stencil5_rects_cpu(b.data(), T.data(), iCp.data(), nx, ny, &r, 1,
+                                           StencilCoef{0.0, 27.0, 24.0, 3e-4}); }));
+  }
+  // executor pass geometry (plan.cpp)
+  {
+    std::vector<Rect> fr;
+    Rect in;
+    split_rect({1, 99, 1, 49}, 4, 3, fr, in);
+    EXPECT(fr.size() == 4 && in.x0 == 5 && in.x1 == 95 && in.y0 == 4 && in.y1 == 46);
+    int64_t cells = in.cells();
+    for (auto& q : fr) cells += q.cells();
+    EXPECT(cells == 98 * 48);
+    split_rect({1, 9, 1, 9}, 5, 1, fr, in);  // frame swallows the rect
+    EXPECT(fr.size() == 1 && in.empty());
+    split_rect({1, 1, 1, 9}, 1, 1, fr, in);  // empty rect
+    EXPECT(fr.empty() && in.empty());
+    EXPECT(throws([&] { split_rect({1, 9, 1, 9}, -1, 1, fr, in); }));
+    const Neighbors none{{{-1, -1}, {-1, -1}, {-1, -1}}}, all{{{1, 1}, {2, 2}, {-1, -1}}},
+        self{{{0, 0}, {0, 0}, {-1, -1}}};
+    Rect o = owned_rect(100, 60, 16, all);
+    EXPECT(o.x0 == 16 && o.x1 == 84 && o.y0 == 16 && o.y1 == 44);
+    o = owned_rect(100, 60, 16, none);
+    EXPECT(o.x0 == 1 && o.x1 == 99 && o.y0 == 1 && o.y1 == 59);
+    EXPECT(throws([&] { owned_rect(20, 60, 10, all); }));  // minimal tile: nothing owned
+    for (int K = 1; K <= 24; ++K) {
+      for (const Neighbors* nb : {&none, &all, &self}) {
+        const int64_t n0 = 2 * (2 * 24) + 8;  // overlap 2*24 on a small tile
+        PassGeom pg = pass_geometry(n0, n0 + 3, K, *nb, true, 1, 1, 48, 48);
+        int64_t c2 = pg.interior.cells();
+        for (auto& q : pg.frame) {
+          c2 += q.cells();
+          EXPECT(q.x0 >= pg.out.x0 && q.x1 <= pg.out.x1 && q.y0 >= pg.out.y0 && q.y1 <= pg.out.y1);
+        }
+        EXPECT(c2 == pg.out.cells());
+        if (nb != &none && !pg.frame.empty()) {  // the frame holds the send planes [ol-hw, ol)
+          EXPECT(pg.interior.empty() || (pg.interior.x0 >= 48 && pg.interior.y0 >= 48));
+        }
+      }
+    }
+  }
+  // pass planner
+  {
+    const auto cf = default_pass_costs(24, true), cc = default_pass_costs(24, false);
+    EXPECT(cf.size() == 25 && cc.size() == 25);
+    for (int64_t nsteps : {0, 1, 2, 5, 19, 20, 21, 47, 1000, 5000, 100003}) {
+      for (const auto* cost : {&cf, &cc}) {
+        const auto p = plan_passes(nsteps, *cost);
+        int64_t sum = 0;
+        for (int k : p) {
+          EXPECT(k >= 1 && k <= 24);
+          sum += k;
+        }
+        EXPECT(sum == nsteps);
+        for (size_t i = 1; i < p.size(); ++i) EXPECT(p[i] <= p[i - 1]);
+      }
+    }
+    EXPECT(plan_passes(20, cf) == std::vector<int>{20});
+    // DP optimality against brute force on small n
+    std::function<double(int)> best = [&](int m) -> double {
+      if (m == 0) return 0.0;
+      double b = 1e300;
+      for (int k = 1; k <= std::min(m, 24); ++k) b = std::min(b, best(m - k) + cf[k]);
+      return b;
+    };
+    for (int m = 1; m <= 30; ++m) {
+      double sum = 0;
+      for (int k : plan_passes(m, cf)) sum += cf[k];
+      EXPECT(std::fabs(sum - best(m)) < 1e-9);
+    }
+    auto c2 = cf;
+    apply_cost_overrides(c2, "20:9.5,3:0.5");
+    EXPECT(c2[20] == 9.5 && c2[3] == 0.5);
+    EXPECT(plan_passes(20, c2)[0] != 20);
+    EXPECT(throws([&] { apply_cost_overrides(c2, "30:1.0"); }));
+    EXPECT(throws([&] { apply_cost_overrides(c2, "5"); }));
+    EXPECT(throws([&] { apply_cost_overrides(c2, "5:-1"); }));
+    EXPECT(throws([&] { plan_passes(-1, cf); }));
+  }
+  // halo exchange plans executed on host memory
+  EXPECT(halo_case({2, 2, 1}, {0, 0, 0}, {12, 10, 1}, {2, 2, 2}, {1, 1, 1}, 1, false) == 0);
+  EXPECT(halo_case({4, 2, 1}, {0, 0, 0}, {40, 36, 1}, {32, 32, 2}, {16, 16, 1}, 1, false) == 0);
+  EXPECT(halo_case({2, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, false) == 0);
+  EXPECT(halo_case({1, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, false) == 0);
+  EXPECT(halo_case({1, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, true) == 0);
+  EXPECT(halo_case({2, 2, 1}, {1, 0, 0}, {6, 6, 1}, {2, 2, 2}, {1, 1, 1}, 1, true) == 0);  // minimal
+  EXPECT(halo_case({2, 1, 2}, {0, 0, 1}, {8, 7, 6}, {2, 2, 2}, {1, 1, 1}, 0, false) == 0);  // 3D
+  {
+    HaloField f;
+    EXPECT(throws([&] { plan_exchange({f}, {{{1, 1}, {-1, -1}, {-1, -1}}}, 0, false, 7); }));
+    double x = 0;
+    f.ptr = &x;
+    f.elem_bytes = 3;
+    EXPECT(throws([&] { plan_exchange({f}, {{{1, 1}, {-1, -1}, {-1, -1}}}, 0, false, 7); }));
+  }
+  // grid description of the C ABI (make_grid_desc / grid_coord)
+  {
+    const int ol[3] = {4, 4, 2}, hw[3] = {2, 2, 1}, per[3] = {1, 0, 0};
+    GridDesc gd = make_grid_desc(20, 12, 1, nullptr, per, ol, hw, 8, 5);
+    EXPECT((gd.dims == std::array<int, 3>{4, 2, 1}));
+    EXPECT(gd.nxyz_g[0] == 4 * 16 && gd.nxyz_g[1] == 2 * 8 + 4 && gd.nxyz_g[2] == 1);
+    EXPECT(gd.neighbors[0][0] >= 0 && gd.neighbors[0][1] >= 0);
+    EXPECT(grid_coord(gd, 1, 0, 0.5, 12) >= 0.0);
+    EXPECT(throws([&] { make_grid_desc(20, 12, 1, nullptr, per, ol, hw, 8, 8); }));  // rank
+    EXPECT(throws([&] { make_grid_desc(5, 12, 1, nullptr, per, ol, hw, 2, 0); }));   // n < ol+hw
+    const int bad_hw[3] = {3, 2, 1};
+    EXPECT(throws([&] { make_grid_desc(20, 12, 1, nullptr, per, ol, bad_hw, 2, 0); }));
+    const int per_z[3] = {0, 0, 1};
+    EXPECT(throws([&] { make_grid_desc(20, 12, 1, nullptr, per_z, ol, hw, 2, 0); }));
+    const int dims_bad[3] = {3, 0, 1};
+    EXPECT(throws([&] { make_grid_desc(20, 12, 1, dims_bad, per, ol, hw, 8, 0); }));
+  }
+  // parallel_for: an exception on a worker (or the caller) reaches the caller
+  {
+    bool caught = false;
+    try {
+      parallel_for(0, 1 << 16, 1, [](int64_t i) {
+        if (i == 40000) throw std::runtime_error("boom");
+      });
+    } catch (const std::runtime_error&) {
+      caught = true;
+    }
+    EXPECT(caught);
+    std::vector<int> hit(1 << 12, 0);
+    parallel_for(0, 1 << 12, 1, [&](int64_t i) { hit[i] += 1; });
+    for (int h : hit) EXPECT(h == 1);
+  }
   std::puts("host selftest OK");
   return 0;
 }

@@ -1,7 +1,9 @@
 """Host code of the native core under AddressSanitizer + UBSan.
 
 GPU-side sanitizers are not available on the MI355X pool; the host parts
-(topology, CPU twins, pack/unpack, reductions, validation) are compiled with
+(topology and the C ABI grid description, CPU twins, pack/unpack, reductions,
+the executor's pass geometry and planner, the halo exchange plan run for fake
+ranks on host memory, parallel_for, validation) are compiled with
 g++ -fsanitize=address,undefined and run here."""
 import os
 import shutil
@@ -18,6 +20,8 @@ def test_host_selftest_asan_ubsan(tmp_path):
     srcs = [os.path.join(ROOT, "tests", "native", "host_selftest.cpp"),
             os.path.join(ROOT, "csrc", "runtime", "topology.cpp"),
             os.path.join(ROOT, "csrc", "runtime", "errors.cpp"),
+            os.path.join(ROOT, "csrc", "runtime", "plan.cpp"),
+            os.path.join(ROOT, "csrc", "runtime", "halo_plan.cpp"),
             os.path.join(ROOT, "csrc", "kernels", "cpu_kernels.cpp")]
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-ffp-contract=off", "-fno-omit-frame-pointer",
            "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
