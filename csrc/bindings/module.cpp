@@ -162,8 +162,8 @@ PYBIND11_MODULE(_C, m) {
           stencilk_rects_gpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
                              r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
         else {
-          // the CPU twin of the kernel's arithmetic: fast5 (kernels 5-9) or canonical
-          const bool f5 = kernel >= 5 && kernel <= 9;
+          // the CPU twin of the kernel's arithmetic: fast5 (kernels 5-9, 11) or canonical
+          const bool f5 = (kernel >= 5 && kernel <= 9) || kernel == 11;
           py::gil_scoped_release nogil;
           if (f5)
             stencilk5_rects_cpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx,

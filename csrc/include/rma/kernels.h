@@ -67,15 +67,17 @@ void stencilk_rects_cpu(int K, double* T2, const double* T, const double* iCp, i
 // factor, 5 ops). 4 and 5 are not bitwise equal to the canonical update.
 // fast5_ok: kernel 5 divides by lam/dx^2, so it needs lam != 0.
 bool fast5_ok(const StencilCoef& c);
-//   9 pipe  (fast5 arithmetic) / 10 pipec (canonical): stage-pipelined strips
+//   9 pipe  (fast5 arithmetic) / 10 pipec (canonical) / 11 pipeb (fast5, lane
+//     moves by ds_bpermute; K = 16, 20, 24 only): stage-pipelined strips
 //     for ANY K in 1..kPipeMaxK (stencil_pipe.h); stencilk_rects_gpu routes
 //     kernels 9/10 here. stages = waves per strip (0: pipe_default_stages).
 //     pipe is bitwise equal to kernel 5 and to stencilk5_rects_cpu; pipec to K
 //     one-step launches and stencilk_rects_cpu.
 constexpr int kPipeMaxK = 24;
 int pipe_default_stages(int K);
-bool pipe_has(int K, int stages);
-void stencil_pipe_rects_gpu(int K, int stages, bool canonical, double* T2, const double* T,
+bool pipe_has(int K, int stages, int arith = 0);
+// arith: 0 fast5, 1 canonical, 2 fast5 with ds_bpermute lane moves (kernel 11)
+void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const double* T,
                             const double* iCp, int64_t nx, int64_t ny, const Rect* rects,
                             int nrects, const StencilCoef& c, const StencilTuning& tune,
                             stream_t stream);

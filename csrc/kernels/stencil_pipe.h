@@ -15,7 +15,9 @@
 // ONE 20-step pass instead of 16 + 4 (each pass costs at least one HBM sweep
 // of the 3 arrays, ~41 ms at the 288 GB tile).
 //
-// Arithmetic (template Canon):
+// Arithmetic (template Ar: kArFast5 = 0, kArCanon = 1; kArFast5Perm = 2 is
+// fast5 with the lane moves done by ds_bpermute on the LDS pipe instead of
+// DPP on the VALU, an energy / issue experiment, profiles/SUMMARY_r2.md):
 //   false  fast5: T2 = fma(g, fma(r, U+D, fma(-2(1+r), c, L+R)), c), g = dt*lam/dx^2/Cp
 //          (LDS ring holds g, zero outside the interior). Bitwise equal to
 //          stencil_tbk.hip kernel 5 and to the CPU twin stencilk5_rects_cpu.
@@ -55,6 +57,8 @@ constexpr int lds_bytes() {
 // fast5 3 rows x V cells x 2 dwords per level, stage 0's two-row prefetch,
 // ~40 for addressing and temporaries; canonical also the carried y flux and
 // the x fluxes (checked: no spills at any K, V, scripts/check_isa.py).
+constexpr int kArFast5 = 0, kArCanon = 1, kArFast5Perm = 2;
+
 template <int K, int S, int V, bool Canon>
 constexpr int waves_per_simd() {
   constexpr int blocks = (160 * 1024) / lds_bytes<K, S, V>();
@@ -68,25 +72,34 @@ constexpr int waves_per_simd() {
 
 template <bool kDpp = true>
 __device__ __forceinline__ double from_next_lane(double v) {
-  // wave_shl:1 (lane i <- lane i+1); bound_ctrl: lane 63 reads 0 (invalid column)
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
-  return __hiloint2double(hi, lo);
+  if constexpr (kDpp) {
+    // wave_shl:1 (lane i <- lane i+1); bound_ctrl: lane 63 reads 0 (invalid column)
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+  } else {
+    return __shfl_down(v, 1);  // ds_bpermute x2 (LDS pipe); lane 63: its own value
+  }
 }
 template <bool kDpp = true>
 __device__ __forceinline__ double from_prev_lane(double v) {
-  // wave_shr:1 (lane i <- lane i-1); lane 0 reads 0 (invalid column)
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
-  return __hiloint2double(hi, lo);
+  if constexpr (kDpp) {
+    // wave_shr:1 (lane i <- lane i-1); lane 0 reads 0 (invalid column)
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+  } else {
+    return __shfl_up(v, 1);  // lane 0: its own value (an invalid column either way)
+  }
 }
 
-template <int K, int S, int V, bool Canon>
+template <int K, int S, int V, int Ar>
 __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double* __restrict__ T,
                                           const double* __restrict__ iCp, int64_t nx, int64_t ny,
                                           const RectList& L, const StencilCoef& k, int chunk_rows,
                                           int remap) {
   using P = Plan<K, S>;
+  constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm;
   constexpr int H = P::H, HL = P::HL, R = P::R;
   constexpr int W = kWave * V;
   constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_strip_tasks)
@@ -236,8 +249,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       double res[V];
       if constexpr (!Canon) {
         const double(&up)[V] = w[j - 1][PU];
-        const double rn = from_next_lane(c[0]);
-        const double ln = from_prev_lane(c[V - 1]);
+        const double rn = from_next_lane<kDpp>(c[0]);
+        const double ln = from_prev_lane<kDpp>(c[V - 1]);
         double sx[V], sy[V], t[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -313,14 +326,14 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   }
 }
 
-template <int K, int S, int V, bool Canon>
+template <int K, int S, int V, int Ar>
 __global__ __launch_bounds__(kWave * S) __attribute__((amdgpu_waves_per_eu(
-    waves_per_simd<K, S, V, Canon>()))) void pipe_kernel(double* __restrict__ T2,
+    waves_per_simd<K, S, V, Ar == kArCanon>()))) void pipe_kernel(double* __restrict__ T2,
                                                    const double* __restrict__ T,
                                                    const double* __restrict__ iCp, int64_t nx,
                                                    int64_t ny, RectList L, StencilCoef k,
                                                    int chunk_rows, int remap) {
-  pipe_body<K, S, V, Canon>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
+  pipe_body<K, S, V, Ar>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
 }
 
 struct PipeLaunch {
@@ -335,25 +348,25 @@ struct PipeLaunch {
   hipStream_t stream;
 };
 
-template <int K, int S, int V, bool Canon>
+template <int K, int S, int V, int Ar>
 void launch(const PipeLaunch& a) {
-  pipe_kernel<K, S, V, Canon><<<dim3((unsigned)a.blocks), dim3(kWave * S), 0, a.stream>>>(
+  pipe_kernel<K, S, V, Ar><<<dim3((unsigned)a.blocks), dim3(kWave * S), 0, a.stream>>>(
       a.T2, a.T, a.iCp, a.nx, a.ny, *a.L, a.k, a.chunk_rows, a.remap);
 }
 
 // Each stencil_pipe_*.hip unit instantiates a range of (K, S) and answers
-// for it: returns false if it does not hold (K, S, V, canon).
-bool dispatch_a(int K, int S, int V, bool canon, const PipeLaunch& a);
-bool dispatch_b(int K, int S, int V, bool canon, const PipeLaunch& a);
-bool dispatch_c(int K, int S, int V, bool canon, const PipeLaunch& a);
-bool dispatch_d(int K, int S, int V, bool canon, const PipeLaunch& a);
+// for it: returns false if it does not hold (K, S, V, arithmetic).
+bool dispatch_a(int K, int S, int V, int ar, const PipeLaunch& a);
+bool dispatch_b(int K, int S, int V, int ar, const PipeLaunch& a);
+bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
+bool dispatch_d(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe
 }  // namespace rma
 
-// (K, S) -> launch<K, S, V, Canon> for V in {1, 2, 4}
+// (K, S, arithmetic) -> launch<K, S, V, Ar> for V in {1, 2, 4}
 #define RMA_PIPE_CASE(KK, SS, CC)                                  \
-  if (K == KK && S == SS && canon == CC) {                         \
+  if (K == KK && S == SS && ar == CC) {                            \
     if (V == 4) launch<KK, SS, 4, CC>(a);                          \
     else if (V == 2) launch<KK, SS, 2, CC>(a);                     \
     else launch<KK, SS, 1, CC>(a);                                 \

@@ -24,22 +24,26 @@ int pipe_default_stages(int K) {
   return 4;
 }
 
-bool pipe_has(int K, int S) {
+bool pipe_has(int K, int S, int arith) {
   if (K < 1 || K > kPipeMaxK) return false;
+  if (arith == pipe::kArFast5Perm) return S == 4 && (K == 16 || K == 20 || K == 24);
   if (S == pipe_default_stages(K)) return true;
   // alternative stage splits instantiated for sweeps (stencil_pipe_d.hip)
   return (K == 12 && S == 3) || (K == 16 && S == 8) || (K == 24 && S == 8) ||
          (K == 8 && S == 4) || (K == 8 && S == 1);
 }
 
-void stencil_pipe_rects_gpu(int K, int stages, bool canonical, double* T2, const double* T,
+void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const double* T,
                             const double* iCp, int64_t nx, int64_t ny, const Rect* rects,
                             int nrects, const StencilCoef& c, const StencilTuning& tune,
                             stream_t stream) {
   const int S = stages > 0 ? stages : pipe_default_stages(K);
   RMA_CHECK_ARG(K >= 1 && K <= kPipeMaxK,
                 "pipelined K-step kernel: 1 <= K <= " << kPipeMaxK << ", got " << K);
-  RMA_CHECK_ARG(pipe_has(K, S), "no pipelined kernel instantiated for K=" << K << " S=" << S);
+  RMA_CHECK_ARG(pipe_has(K, S, arith), "no pipelined kernel instantiated for K=" << K << " S=" << S
+                                                                             << " arithmetic " << arith);
+  RMA_CHECK_ARG(arith >= 0 && arith <= 2, "pipelined kernel arithmetic " << arith);
+  const bool canonical = arith == pipe::kArCanon;
   RMA_CHECK_ARG(canonical || fast5_ok(c),
                 "the fast5 arithmetic folds dy^-2/dx^-2 into one factor: needs lam != 0 and "
                 "finite coefficients");
@@ -65,10 +69,10 @@ void stencil_pipe_rects_gpu(int K, int stages, bool canonical, double* T2, const
   if (L.n == 0) return;
   RMA_CHECK_ARG(ntask < (int64_t(1) << 31), "grid too large: " << ntask << " blocks");
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, &L, c, tune.chunk_rows, remap, ntask, as_stream(stream)};
-  const bool ok = pipe::dispatch_a(K, S, V, canonical, a) || pipe::dispatch_b(K, S, V, canonical, a) ||
-                  pipe::dispatch_c(K, S, V, canonical, a) || pipe::dispatch_d(K, S, V, canonical, a);
-  RMA_CHECK_ARG(ok, "pipelined kernel K=" << K << " S=" << S << " V=" << V << " canonical="
-                                           << canonical << " not instantiated");
+  const bool ok = pipe::dispatch_a(K, S, V, arith, a) || pipe::dispatch_b(K, S, V, arith, a) ||
+                  pipe::dispatch_c(K, S, V, arith, a) || pipe::dispatch_d(K, S, V, arith, a);
+  RMA_CHECK_ARG(ok, "pipelined kernel K=" << K << " S=" << S << " V=" << V << " arithmetic="
+                                           << arith << " not instantiated");
   RMA_HIP_LAUNCH_CHECK();
 }
 

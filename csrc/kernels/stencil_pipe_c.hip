@@ -5,19 +5,19 @@
 namespace rma {
 namespace pipe {
 
-bool dispatch_c(int K, int S, int V, bool canon, const PipeLaunch& a) {
-  RMA_PIPE_CASE(13, 4, false)
-  RMA_PIPE_CASE(14, 4, false)
-  RMA_PIPE_CASE(15, 4, false)
-  RMA_PIPE_CASE(16, 4, false)
-  RMA_PIPE_CASE(17, 4, false)
-  RMA_PIPE_CASE(18, 4, false)
-  RMA_PIPE_CASE(19, 4, false)
-  RMA_PIPE_CASE(20, 4, false)
-  RMA_PIPE_CASE(21, 4, false)
-  RMA_PIPE_CASE(22, 4, false)
-  RMA_PIPE_CASE(23, 4, false)
-  RMA_PIPE_CASE(24, 4, false)
+bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a) {
+  RMA_PIPE_CASE(13, 4, kArFast5)
+  RMA_PIPE_CASE(14, 4, kArFast5)
+  RMA_PIPE_CASE(15, 4, kArFast5)
+  RMA_PIPE_CASE(16, 4, kArFast5)
+  RMA_PIPE_CASE(17, 4, kArFast5)
+  RMA_PIPE_CASE(18, 4, kArFast5)
+  RMA_PIPE_CASE(19, 4, kArFast5)
+  RMA_PIPE_CASE(20, 4, kArFast5)
+  RMA_PIPE_CASE(21, 4, kArFast5)
+  RMA_PIPE_CASE(22, 4, kArFast5)
+  RMA_PIPE_CASE(23, 4, kArFast5)
+  RMA_PIPE_CASE(24, 4, kArFast5)
   return false;
 }
 

@@ -78,15 +78,17 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
-    ap.add_argument("--temporal", type=int, default=1, choices=[1, 2, 3, 4, 6, 8, 12, 16],
-                    help="perf/perf_hide: K steps per kernel pass + width-K halos "
-                         "(grid overlap 2K); bitwise identical to 1 (12, 16: --fast-math)")
+    ap.add_argument("--temporal", type=int, default=1, choices=list(range(1, 25)),
+                    metavar="K",
+                    help="perf/perf_hide: at most K (1..24) steps per kernel pass + width-K "
+                         "halos (grid overlap 2K); the executor plans the passes; bitwise "
+                         "identical to one-step updates without --fast-math")
     ap.add_argument("--chunk2", type=int, default=0)
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
     ap.add_argument("--fast-math", action="store_true",
-                    help="K-step passes with fast-math fp64 arithmetic (5-point sum, one "
-                         "folded per-cell factor, FMAs): same scheme, not bitwise equal to the "
-                         "canonical update")
+                    help="passes with fast-math fp64 arithmetic (5-point sum, one folded "
+                         "per-cell factor, FMAs): same scheme, not bitwise equal to the "
+                         "canonical update, bitwise equal to its CPU twin")
     ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf guard period")
     ap.add_argument("--checkpoint", default="", help="save the final state to this directory")
     ap.add_argument("--resume", default="", help="start from a checkpoint directory")

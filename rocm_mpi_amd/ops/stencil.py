@@ -30,12 +30,13 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 # split over 2 / 4 / 8 pipelined waves (K = 8, 12, 16; fast5p8: K = 8, 16); 9 = pipe: the
 # stage-pipelined fast5 kernel for ANY K in 1..24 (csrc/kernels/stencil_pipe.h, the executor's
 # fast-math kernel); 10 = pipec: the same pipeline with the canonical arithmetic (bitwise equal
-# to K one-step updates), any K in 1..24.
-FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe")
-PIPE = ("pipe", "pipec")
+# to K one-step updates), any K in 1..24; 11 = pipeb: pipe with the lane moves on the LDS
+# pipe (ds_bpermute) instead of DPP (K = 16, 20, 24; an experiment).
+FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe", "pipeb")
+PIPE = ("pipe", "pipec", "pipeb")
 PIPE_MAX_K = 24
 KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4, "fast5": 5, "fast5p2": 6,
-           "fast5p4": 7, "fast5p8": 8, "pipe": 9, "pipec": 10}
+           "fast5p4": 7, "fast5p8": 8, "pipe": 9, "pipec": 10, "pipeb": 11}
 
 
 class StencilCoef(NamedTuple):

@@ -83,6 +83,15 @@ def test_pipe_alternative_stage_splits(K, S):
     assert torch.equal(a, cpu_ref(K, T, iCp, rects, "pipe"))
 
 
+@pytest.mark.parametrize("K", [16, 20, 24])
+def test_pipeb_lane_moves_by_bpermute_bitwise(K):
+    ny, nx = 257, 1028
+    T, iCp = rand((ny, nx), 18), rand((ny, nx), 19, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    assert torch.equal(gpu_run(K, T, iCp, rects, "pipeb", chunk=64),
+                       cpu_ref(K, T, iCp, rects, "pipe"))
+
+
 @pytest.mark.parametrize("K,old", [(8, "fast5"), (12, "fast5p2"), (16, "fast5p4"), (16, "fast5")])
 def test_pipe_equals_fixed_k_fast5_kernels(K, old):
     ny, nx = 389, 2048
