@@ -82,7 +82,8 @@ int main(int argc, char** argv) {
   rma_grid* g = nullptr;
   int me = 0, dims[3], coords[3];
   const int dims_in[3] = {0, 0, 1};
-  // temporal blocking: K steps per kernel pass need overlap 2K and halo width K
+  // temporal blocking: at most K steps per kernel pass (the executor plans the
+  // passes) need overlap 2K and halo width K
   const int ol[3] = {2 * std::max(1, K), 2 * std::max(1, K), 2};
   const int hw[3] = {std::max(1, K), std::max(1, K), 1};
   CK(rma_init_global_grid((int)n, (int)n, 1, dims_in, nullptr, ol, hw, size, rank,

@@ -111,8 +111,10 @@ mutable struct DiffusionExecutor
     T2::Any
 end
 
-# fast_math=true: the K-step passes use the 5-point-sum arithmetic (required
-# for steps_per_pass = 12 or 16; rounding-level difference from the canonical update).
+# steps_per_pass = K (1..24): at most K steps per kernel pass; run! plans the
+# passes (csrc/runtime/plan.cpp). fast_math=true: every pass uses the
+# 5-point-sum arithmetic (rounding-level difference from the canonical update,
+# bitwise equal to its C++ CPU twin).
 function DiffusionExecutor(T, T2, iCp, coef::NTuple{4,Float64}; mode::Integer=1,
                            steps_per_pass::Integer=1, b_width=(1, 1), fast_math::Bool=false)
     out = Ref{Ptr{Cvoid}}(C_NULL)

@@ -92,9 +92,18 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
     """Compile (incrementally) and link ``rocm_mpi_amd/_C*.so``; returns its path."""
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
-    BUILD.mkdir(parents=True, exist_ok=True)
     headers = list(INC.rglob("*.h")) + list((CSRC / "kernels").glob("*.h"))
     newest_header = max((p.stat().st_mtime for p in headers), default=0.0)
+    out, core = ext_path(), core_path()
+    if not clean and out.exists() and core.exists():
+        # the shipped libraries are newer than every source: nothing to do (a
+        # repository snapshot on a GPU box carries the .so files but not the
+        # object files, which would otherwise force a full rebuild there)
+        newest_src = max([newest_header] + [p.stat().st_mtime for p in
+                                            HIP_SOURCES + HOST_SOURCES + EXAMPLES])
+        if min(out.stat().st_mtime, core.stat().st_mtime) >= newest_src:
+            return out
+    BUILD.mkdir(parents=True, exist_ok=True)
     jobs = jobs or min(16, os.cpu_count() or 4)
     todo = []
     objs = []

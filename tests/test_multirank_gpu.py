@@ -233,3 +233,80 @@ def test_fast_math_decomposition_invariant_and_close(K, nt):
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx])
     np.testing.assert_allclose(one, can, rtol=1e-13, atol=1e-13)
     assert not np.array_equal(one, can)  # it really is the other arithmetic
+
+
+def spmd_planned(rank, hub, nx, ny, steps, dims, K, fast, timing=False):
+    """A run split into several step() calls so the planner mixes pass depths
+    (e.g. 5 + 20 + 13 steps with at most K per pass); returns (coords, field,
+    global sizes, plans, per-pass timings)."""
+    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], overlaps=(2 * K, 2 * K, 2),
+                        halowidths=(K, K, 1), quiet=True, loopback=(hub, rank))
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=sum(steps),
+                                    init="random", quiet=True, dims=dims, temporal=K,
+                                    fast_math=fast))
+    assert m.executor is not None
+    plans, ts = [], []
+    if timing:
+        m.enable_pass_timing(True)
+    for s in steps:
+        plans.append(m.plan(s))
+        m.step(s)
+    if timing:
+        ts = m.pass_timings()
+        m.enable_pass_timing(False)
+    out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g, plans, ts)
+    m.close()
+    gg.finalize_global_grid()
+    return out
+
+
+@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("K,steps", [(24, (5, 20, 13)), (16, (1, 17, 3)), (7, (9, 2, 11))])
+def test_planned_mixed_depth_passes_decomposition_invariant(fast, K, steps):
+    """The executor's planner runs passes of several depths (<= K) between
+    width-K exchanges (the bench's warmup [5] + timed [20] shape): 4 loopback
+    ranks (2x2, frames on the high-priority stream) == 1 rank of the global
+    grid, bitwise, for both arithmetics."""
+    nx = ny = 6 * K + 40
+    res = run_loopback(4, spmd_planned, nx, ny, steps, (2, 2), K, fast, timeout=180)
+    nxg, nyg, _ = res[0][2]
+    assert [sum(p) for p in res[0][3]] == list(steps)
+    assert any(len(set(p)) > 1 or p[0] != K for p in res[0][3])  # really mixed depths
+    one = run_loopback(1, spmd_planned, nxg, nyg, steps, (1, 1), K, fast, timeout=180)[0][1]
+    for coords, T, _, _, _ in res:
+        gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
+        assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx])
+
+
+def test_pass_timing_and_solo_on_loopback_ranks():
+    """bench.py's instrumentation on the native multi-rank path: per-pass
+    HIP-event timings show a frame and an exchange for ranks with neighbours;
+    solo mode (exchange off, one launch per pass) keeps the run going and
+    restores the neighbours afterwards (a later run == a fresh one)."""
+    K, nx, ny = 16, 300, 260
+
+    def body(rank, hub):
+        gg.init_global_grid(nx, ny, 1, dimx=2, dimy=1, overlaps=(2 * K, 2 * K, 2),
+                            halowidths=(K, K, 1), quiet=True, loopback=(hub, rank))
+        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=60, init="random",
+                                        quiet=True, dims=(2, 1, 0), temporal=K, fast_math=True))
+        m.enable_pass_timing(True)
+        m.step(20)
+        ts = m.pass_timings()
+        m.enable_pass_timing(False)
+        m.set_solo(True)
+        m.step(20)
+        assert m.executor.solo
+        m.set_solo(False)
+        assert not m.executor.solo
+        out = (ts, m.executor.plan(20))
+        m.close()
+        gg.finalize_global_grid()
+        return out
+
+    res = run_loopback(2, body, timeout=120)
+    for ts, plan in res:
+        assert [t["K"] for t in ts] == plan and sum(plan) == 20  # K <= 16: [12, 8]
+        t = ts[0]
+        assert t["frame_ms"] > 0 and t["halo_ms"] > 0 and t["interior_ms"] > 0
+        assert t["pass_ms"] >= t["interior_ms"] and t["exposed_halo_ms"] >= 0
