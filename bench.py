@@ -411,8 +411,13 @@ def main(argv=None) -> int:
     check_on = a.check == 1 or (a.check < 0 and world > 1)
     check_ok, check_info = None, None
     if check_on and a.variant != "kp":
-        check_ok, check_info = halo_check(a, dims[:2], K, dev, world,
-                                          self_rccl=a.check_self_rccl and world == 1 and gpu)
+        try:
+            check_ok, check_info = halo_check(a, dims[:2], K, dev, world,
+                                              self_rccl=a.check_self_rccl and world == 1 and gpu)
+        except Exception as e:  # noqa: BLE001 - keep the timed record; say the check broke
+            check_ok, check_info = None, {"error": f"{type(e).__name__}: {e}"[:500]}
+            print(f"bench.py rank {rank}: halo check did not complete: {e}", file=sys.stderr,
+                  flush=True)
 
     t_it = wall / a.steps
     teff_gpu = a_eff / t_it

@@ -354,7 +354,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("default_chunk_k", [](int K, int64_t ny) { return default_tune_k(K, ny).chunk_rows; },
         py::arg("K"), py::arg("ny"));
   m.def("plan_passes", &plan_passes, py::arg("nsteps"), py::arg("costs"));
-  m.def("default_pass_costs", &default_pass_costs, py::arg("kmax"), py::arg("fast5"));
+  m.def("default_pass_costs", &default_pass_costs, py::arg("kmax"), py::arg("fast5"),
+        py::arg("cells") = 0.0);
   m.def("pipe_default_stages", &pipe_default_stages, py::arg("K"));
   m.def("pipe_max_k", []() { return kPipeMaxK; });
   m.def(

@@ -42,11 +42,13 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
 
 // Relative cost of one pass of K steps (index K = 1..Kmax; index 0 unused;
 // +inf = no kernel), in units of one HBM sweep of the 3 arrays. Measured on
-// MI355X at the 288 GB tile (profiles/pass_costs_r2.json); fast5 = the
+// MI355X (profiles/pass_sweep*_r2.json); fast5 = the
 // fast-math arithmetic (every K on the pipelined kernel), otherwise the
-// canonical kernels (K = 1 one-step march, 2 two-step, 3/4/6/8 kernel 3,
+// canonical kernels (K = 1 one-step march, 2 two-step, 3/4 kernel 3,
 // the rest the canonical pipelined kernel).
-std::vector<double> default_pass_costs(int kmax, bool fast5);
+// cells = nx*ny of the tile (0: the 288 GB tile): the nearest measured tile
+// class (4096^2, 8192^2, 16384^2, 101376^2) in log scale.
+std::vector<double> default_pass_costs(int kmax, bool fast5, double cells = 0);
 // RMA_PASS_COSTS="K:cost,K:cost,..." overrides entries (sweeps, tests).
 void apply_cost_overrides(std::vector<double>& cost, const char* spec);
 

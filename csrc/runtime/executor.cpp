@@ -114,7 +114,7 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
     interior_ = full_;
   }
   if (p.temporal > 1 || fast5()) {
-    cost_ = default_pass_costs(p.temporal, fast5());
+    cost_ = default_pass_costs(p.temporal, fast5(), (double)nx * (double)ny);
     apply_cost_overrides(cost_, std::getenv("RMA_PASS_COSTS"));
     geom_.resize(p.temporal + 1);
     geom_ok_.assign(p.temporal + 1, 0);

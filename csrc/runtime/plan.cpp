@@ -52,35 +52,56 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
 namespace {
 constexpr double kInf = std::numeric_limits<double>::infinity();
 
-// Pass time relative to one HBM sweep (the one-step march kernel: 39.5 ms at
-// 101376^2), measured on MI355X: profiles/pass_sweep_r2.json (bench/pass_sweep.py,
-// median of 3 interleaved rounds, the executor's kernel and chunk rows per
-// depth). A pass costs at least the sweep plus the strip-overlap reads
-// (~1.12-1.24 up to K=12); from K~13 the fp64 VALU work dominates, and
-// K=17..24 run 5-6 levels per wave at 2 waves per SIMD.
-constexpr double kFast5[] = {0,     1.230, 1.225, 1.209, 1.158, 1.242, 1.205, 1.192, 1.122,
-                             1.140, 1.187, 1.222, 1.222, 1.319, 1.357, 1.400, 1.424, 1.730,
-                             1.762, 1.836, 1.853, 2.023, 2.055, 2.124, 2.133};
-// canonical: K=1 one-step march, 2 two-step kernel, 3/4 kernel 3 (lds_dpp),
-// the rest the canonical pipelined kernel (K=13-15, 17-19, 21-23 interpolated;
-// K=24 at 1 wave per SIMD)
-constexpr double kCanon[] = {0,     1.000, 1.074, 1.141, 1.065, 1.208, 1.193, 1.374, 1.413,
-                             1.637, 1.793, 1.872, 1.927, 2.096, 2.264, 2.433, 2.601, 2.758,
-                             2.916, 3.073, 3.230, 3.641, 4.051, 4.462, 4.872};
+// Pass time per depth K = 1..24 relative to the one-step march kernel on the
+// same tile (one HBM sweep of the three arrays), measured on MI355X with the
+// kernel the executor runs at each depth (bench/pass_sweep.py; emitted by
+// scripts/fit_pass_costs.py from profiles/pass_sweep{,_16384,_8192,_4096}_r2.json;
+// canonical depths that were not swept are interpolated). fast5: the
+// pipelined fast-math kernel at every K; canonical: K=1 one-step march, 2
+// two-step kernel, 3/4 kernel 3, K >= 5 the canonical pipelined kernel.
+// On the 288 GB tile a pass costs at least the sweep plus the strip-overlap
+// reads up to K~12 and the fp64 arithmetic beyond; on smaller tiles the
+// deeper passes fill the chip worse (4096^2: the best depth per step is 12,
+// 16384^2: 16, 101376^2: 24).
+constexpr int kTables = 4;
+constexpr double kTileCells[kTables] = {4096.0 * 4096, 8192.0 * 8192, 16384.0 * 16384,
+                                        101376.0 * 101376};
+constexpr double kFast5[kTables][25] = {
+    {0, 1.054, 1.111, 1.119, 1.128, 1.232, 1.223, 1.318, 1.366, 1.550, 1.512, 1.581, 1.645,
+     1.898, 1.991, 2.264, 2.369, 3.249, 3.353, 3.464, 3.608, 4.101, 4.214, 4.338, 4.462},
+    {0, 1.343, 1.406, 1.460, 1.365, 1.398, 1.337, 1.342, 1.274, 1.302, 1.347, 1.402, 1.423,
+     1.586, 1.652, 1.796, 1.885, 2.696, 2.697, 2.680, 2.731, 3.221, 3.254, 3.312, 3.341},
+    {0, 1.422, 1.503, 1.468, 1.361, 1.417, 1.377, 1.376, 1.268, 1.329, 1.273, 1.298, 1.284,
+     1.408, 1.440, 1.499, 1.535, 2.014, 1.957, 1.964, 1.989, 2.225, 2.215, 2.279, 2.337},
+    {0, 1.230, 1.225, 1.209, 1.158, 1.242, 1.205, 1.192, 1.122, 1.140, 1.187, 1.222, 1.222,
+     1.319, 1.357, 1.400, 1.424, 1.730, 1.762, 1.836, 1.853, 2.023, 2.055, 2.124, 2.133}};
+constexpr double kCanon[kTables][25] = {
+    {0, 1.000, 1.071, 1.093, 1.188, 1.371, 1.421, 1.732, 1.884, 2.270, 2.514, 2.600, 2.758,
+     3.244, 3.731, 4.217, 4.704, 5.102, 5.500, 5.899, 6.297, 6.695, 7.094, 7.492, 7.890},
+    {0, 1.000, 1.070, 1.278, 1.261, 1.317, 1.332, 1.416, 1.588, 1.908, 2.195, 2.322, 2.395,
+     2.754, 3.114, 3.473, 3.833, 4.111, 4.390, 4.669, 4.947, 5.226, 5.504, 5.783, 6.061},
+    {0, 1.000, 1.088, 1.325, 1.248, 1.394, 1.380, 1.392, 1.425, 1.758, 1.862, 1.862, 1.951,
+     2.200, 2.449, 2.697, 2.946, 3.105, 3.264, 3.423, 3.582, 3.740, 3.899, 4.058, 4.217},
+    {0, 1.000, 1.074, 1.141, 1.065, 1.208, 1.193, 1.374, 1.413, 1.637, 1.793, 1.872, 1.927,
+     2.096, 2.264, 2.433, 2.601, 2.758, 2.915, 3.073, 3.230, 3.640, 4.051, 4.461, 4.872}};
 }  // namespace
 
-std::vector<double> default_pass_costs(int kmax, bool fast5) {
-  RMA_CHECK_ARG(kmax >= 1, "kmax=" << kmax);
-  std::vector<double> c(kmax + 1, kInf);
-  const int nf = sizeof(kFast5) / sizeof(double) - 1, nc = sizeof(kCanon) / sizeof(double) - 1;
-  for (int K = 1; K <= kmax; ++K) {
-    if (fast5) {
-      c[K] = K <= nf ? kFast5[K] : kFast5[nf] * (K * (256.0 / (256 - 2 * K))) /
-                                       (nf * (256.0 / (256 - 2 * nf)));
-    } else {
-      c[K] = K <= nc ? kCanon[K] : kCanon[nc] * K / nc;  // (nc == kPipeMaxK today)
+std::vector<double> default_pass_costs(int kmax, bool fast5, double cells) {
+  RMA_CHECK_ARG(kmax >= 1 && kmax <= 24, "kmax=" << kmax << " (tables cover 1..24)");
+  // the measured tile class nearest in log(cells); 0 = the 288 GB tile
+  int t = kTables - 1;
+  if (cells > 0) {
+    double best = 1e300;
+    for (int i = 0; i < kTables; ++i) {
+      const double d = std::fabs(std::log(cells / kTileCells[i]));
+      if (d < best) {
+        best = d;
+        t = i;
+      }
     }
   }
+  std::vector<double> c(kmax + 1, kInf);
+  for (int K = 1; K <= kmax; ++K) c[K] = fast5 ? kFast5[t][K] : kCanon[t][K];
   return c;
 }
 

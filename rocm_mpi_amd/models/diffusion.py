@@ -250,7 +250,8 @@ class Diffusion2D:
 
         if has_native():
             fast = cfg.fast_math and ops.fast5_ok(self.coef)
-            return list(native().plan_passes(int(n), native().default_pass_costs(cfg.temporal, fast)))
+            costs = native().default_pass_costs(cfg.temporal, fast, float(cfg.nx) * cfg.ny)
+            return list(native().plan_passes(int(n), costs))
         K = cfg.temporal
         return [K] * (int(n) // K) + ([int(n) % K] if int(n) % K else [])
 

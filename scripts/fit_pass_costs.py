@@ -1,0 +1,71 @@
+#!/usr/bin/env python
+"""Emit the planner's per-depth pass-cost tables (csrc/runtime/plan.cpp) from
+bench/pass_sweep.py results: rel = pass time / one-step march kernel time on
+the same tile, for the kernel the executor runs at each depth (fast5: the
+pipelined kernel; canonical: march K=1, two-step K=2, lds_dpp K=3/4, the
+canonical pipelined kernel from K=5), missing depths interpolated linearly.
+
+    python scripts/fit_pass_costs.py profiles/pass_sweep_r2.json profiles/pass_sweep_{16384,8192,4096}_r2.json
+"""
+import json
+import sys
+
+KMAX = 24
+
+
+def fill(vals: dict) -> list:
+    ks = sorted(vals)
+    out = []
+    for K in range(1, KMAX + 1):
+        if K in vals:
+            out.append(vals[K])
+            continue
+        lo = max([k for k in ks if k < K], default=None)
+        hi = min([k for k in ks if k > K], default=None)
+        if lo is not None and hi is not None:
+            out.append(vals[lo] + (vals[hi] - vals[lo]) * (K - lo) / (hi - lo))
+        else:  # extrapolate from the last two points
+            a, b = ks[-2], ks[-1]
+            out.append(vals[b] + (vals[b] - vals[a]) / (b - a) * (K - b))
+    return out
+
+
+def tables(path: str):
+    d = json.load(open(path))
+    rows = d["rows"]
+
+    def rel(kind, K, stages=None):
+        for r in rows:
+            if r["kernel"] == kind and r["K"] == K and (r.get("chunk_rows") is None or True):
+                if stages is None or r["stages"] == stages:
+                    return r["rel"]
+        return None
+
+    from_default = {}
+    for r in rows:  # first (default-chunk, default-stage) row per depth
+        if r["kernel"] == "pipe" and r["K"] not in from_default:
+            from_default[r["K"]] = r["rel"]
+    fast = fill(from_default)
+    can = {1: 1.0}
+    if rel("two_step", 2):
+        can[2] = rel("two_step", 2)
+    for K in (3, 4):
+        if rel("lds_dpp", K):
+            can[K] = rel("lds_dpp", K)
+    for r in rows:
+        if r["kernel"] == "pipec" and r["K"] >= 5 and r["K"] not in can:
+            can[r["K"]] = r["rel"]
+    return d["tile"], fast, fill(can)
+
+
+def fmt(name, vals):
+    body = ", ".join(f"{v:.3f}" for v in vals)
+    return f"    {{{body}}},  // {name}"
+
+
+if __name__ == "__main__":
+    for p in sys.argv[1:]:
+        tile, fast, can = tables(p)
+        print(f"// tile {tile}: {p}")
+        print(fmt(f"fast5 {tile}", fast))
+        print(fmt(f"canonical {tile}", can))

@@ -82,6 +82,24 @@ def test_multi_step_kernels_stay_in_bounds(ny, nx, K):
         check_stencil(lambda o, t, c, r: ops.stencil2_step(o, t, c, coef(), r), ny, nx, rects)
 
 
+@pytest.mark.parametrize("ny,nx", SHAPES + [(97, 1027), (131, 1026)])
+@pytest.mark.parametrize("K", [12, 16, 20, 24])
+def test_deep_pipelined_kernels_stay_in_bounds(ny, nx, K):
+    """The deep passes (fast5p4 / fast5p8 at K=16 with 512-thread
+    blocks and 75.8 KB LDS were never guard-checked): every pipelined kernel
+    with 2 and 4 cells per lane, odd nx (1 cell per lane) included."""
+    rects = [ops.interior_rect(nx, ny)]
+    cases = [("pipe", 2), ("pipe", 4), ("pipec", 2), ("pipec", 4)]
+    if K in (12, 16):
+        cases += [("fast5p2", 2), ("fast5p2", 4), ("fast5p4", 2), ("fast5p4", 4)]
+    if K == 16:
+        cases += [("fast5p8", 2), ("fast5p8", 4)]
+    for kern, vec in cases:
+        tn = ops.StencilTuning(chunk_rows=7, kernel=kern, vec=vec)
+        check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny, nx,
+                      rects)
+
+
 @pytest.mark.parametrize("ny,nx", SHAPES)
 def test_kp_kernels_stay_in_bounds(ny, nx):
     c = coef()
