@@ -324,6 +324,7 @@ def main(argv=None) -> int:
     comm.barrier()
     setup_s = time.perf_counter() - t_setup
 
+    fast_used = bool(model.cfg.fast_math)  # the side measurements below switch it off
     plan_warm = model.plan(a.warmup)
     plan_timed = model.plan(a.steps)
     model.step(a.warmup)
@@ -383,7 +384,7 @@ def main(argv=None) -> int:
         from rocm_mpi_amd._native import has_native, native
 
         if has_native():
-            cc = native().default_pass_costs(K, False)
+            cc = native().default_pass_costs(K, False, float(nx) * float(ny))
             kc = min(range(1, K + 1), key=lambda k: cc[k] / k)
         else:
             kc = min(K, 8)
@@ -462,7 +463,7 @@ def main(argv=None) -> int:
             "passes_warmup": plan_warm,
             "passes_timed": plan_timed,
             "kstep_kernel": kinfo,
-            "fast_math": bool(cfg.fast_math),
+            "fast_math": fast_used,
             "pass_timing": timings,
             "solo_ms_per_step": round(solo * 1e3, 6) if solo else None,
             "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,

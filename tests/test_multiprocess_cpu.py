@@ -106,6 +106,7 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     # self-validation of a multi-rank point
     assert c["ranks"] == world and c["transport"] == "gloo"
     assert sum(c["passes_timed"]) == 20 and max(c["passes_timed"]) <= K
+    assert c["fast_math"] is True  # the timed passes, not the canonical side run after them
     assert c["teff_per_gpu_min_GBps"] <= c["teff_per_gpu_GBps"] * (1 + 1e-9) + 0.02
     assert c["teff_per_gpu_min_GBps"] <= c["teff_per_gpu_max_GBps"]
     pt = c["pass_timing"]
