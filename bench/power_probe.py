@@ -41,6 +41,17 @@ def smi_sample() -> dict:
     return d
 
 
+def smi_power_cap() -> float | None:
+    """The board's power cap (rocm-smi --showmaxpower), recorded next to the readings."""
+    try:
+        out = subprocess.run(["rocm-smi", "--showmaxpower"], capture_output=True, text=True,
+                             timeout=10).stdout
+    except Exception:  # noqa: BLE001
+        return None
+    m = re.search(r"Max Graphics Package Power \(W\):\s*([0-9.]+)", out)
+    return float(m.group(1)) if m else None
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=0)
@@ -80,6 +91,7 @@ def main(argv=None) -> int:
     th = threading.Thread(target=sampler, daemon=True)
     th.start()
     idle = smi_sample()
+    cap = smi_power_cap()
     rows = []
     for item in a.configs.split(","):
         kind, K = item.split(":")
@@ -115,7 +127,7 @@ def main(argv=None) -> int:
         print(json.dumps(rows[-1]), flush=True)
     stop.set()
     th.join(5)
-    doc = {"tile": n, "idle": idle, "rows": rows}
+    doc = {"tile": n, "idle": idle, "power_cap_W": cap, "rows": rows}
     print(json.dumps(doc), flush=True)
     if a.out:
         with open(a.out, "w") as fh:

@@ -46,28 +46,47 @@ struct Plan {
   static_assert(S >= 1 && HL >= 1 && HL <= H, "bad stage split");
 };
 
-// LDS bytes of one block (ring + double-buffered hand-off rows)
-template <int K, int S, int V>
-constexpr int lds_bytes() {
-  return (Plan<K, S>::R + 2 * (S > 1 ? S - 1 : 1)) * kWave * V * 8;
-}
-
-// Waves per SIMD to ask the compiler for: what the LDS allows (160 KiB per
-// CU, 4 SIMDs), capped by a VGPR estimate so the cap never forces spills:
-// fast5 3 rows x V cells x 2 dwords per level, stage 0's two-row prefetch,
-// ~40 for addressing and temporaries; canonical also the carried y flux and
-// the x fluxes (checked: no spills at any K, V, scripts/check_isa.py).
+// Waves per SIMD a block shape allows: the LDS (160 KiB per CU, 4 SIMDs)
+// and a VGPR estimate, so a waves_per_eu cap never forces spills: fast5
+// 3 rows x V cells x 2 dwords per level, stage 0's two-row prefetch, ~40 for
+// addressing and temporaries; canonical also the carried y flux and the x
+// fluxes (checked: no spills at any K, V, scripts/check_isa.py).
 constexpr int kArFast5 = 0, kArCanon = 1, kArFast5Perm = 2;
 
 template <int K, int S, int V, bool Canon>
-constexpr int waves_per_simd() {
-  constexpr int blocks = (160 * 1024) / lds_bytes<K, S, V>();
-  constexpr int by_lds = blocks * S / 4;
-  constexpr int vgpr = Canon ? 8 * Plan<K, S>::H * V + 8 * V + 64
-                             : 6 * Plan<K, S>::H * V + 8 * V + 40;
-  constexpr int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
-  constexpr int w = by_lds < by_vgpr ? by_lds : by_vgpr;
+constexpr int occupancy(int lds) {
+  const int by_lds = (160 * 1024) / lds * S / 4;
+  const int vgpr = Canon ? 8 * Plan<K, S>::H * V + 8 * V + 64 : 6 * Plan<K, S>::H * V + 8 * V + 40;
+  const int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
+  const int w = by_lds < by_vgpr ? by_lds : by_vgpr;
   return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
+// Mirror rows of the factor ring: the H levels of a stage read the ring rows
+// of H consecutive slots (descending); with the last H-1 slots mirrored in
+// front of slot 0 the reads never wrap, so one base address and immediate
+// ds_read offsets serve all levels (no per-level modulo and address VALU op:
+// -3 % VALU, -50 % SALU instructions in the K=24 row loop). Only where the
+// extra rows cost no occupancy.
+template <int K, int S, int V, bool Canon>
+constexpr int mirror_rows() {
+  constexpr int H = Plan<K, S>::H, row = kWave * V * 8;
+  constexpr int base = (Plan<K, S>::R + 2 * (S > 1 ? S - 1 : 1)) * row;
+  return occupancy<K, S, V, Canon>(base + (H - 1) * row) == occupancy<K, S, V, Canon>(base)
+             ? H - 1
+             : 0;
+}
+
+// LDS bytes of one block (ring + mirrors + double-buffered hand-off rows)
+template <int K, int S, int V, bool Canon>
+constexpr int lds_bytes() {
+  return (Plan<K, S>::R + mirror_rows<K, S, V, Canon>() + 2 * (S > 1 ? S - 1 : 1)) * kWave * V *
+         8;
+}
+
+template <int K, int S, int V, bool Canon>
+constexpr int waves_per_simd() {
+  return occupancy<K, S, V, Canon>(lds_bytes<K, S, V, Canon>());
 }
 
 template <bool kDpp = true>
@@ -100,7 +119,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
                                           int remap) {
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm;
-  constexpr int H = P::H, HL = P::HL, R = P::R;
+  constexpr int H = P::H, HL = P::HL, R = P::R, M = mirror_rows<K, S, V, Canon>();
   constexpr int W = kWave * V;
   constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_strip_tasks)
   constexpr int NH = S > 1 ? S - 1 : 1;
@@ -157,9 +176,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     load_row<V>(qT, T + rowc(i + 2) * nx + xl);
     load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
   }
-  __shared__ double ring[R * W];
+  // physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R)
+  __shared__ double ring[(R + M) * W];
   __shared__ double hand[2][NH][W];
-  for (int t = threadIdx.x; t < R * W; t += S * kWave) ring[t] = 0.0;
+  for (int t = threadIdx.x; t < (R + M) * W; t += S * kWave) ring[t] = 0.0;
   for (int t = threadIdx.x; t < 2 * NH * W; t += S * kWave) (&hand[0][0][0])[t] = 0.0;
   __syncthreads();
   // LDS rows are lane-interleaved (cell pair h of lane l at dbl2 slot h*64+l):
@@ -211,7 +231,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 #pragma unroll
         for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? (Canon ? pC[v] : gs * pC[v]) : 0.0;
       }
-      wr2(ring + slot0 * W, g);
+      wr2(ring + (slot0 + M) * W, g);
+      if constexpr (M > 0) {
+        if (slot0 >= R - M) wr2(ring + (slot0 - (R - M)) * W, g);
+      }
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         pT[v] = qT[v];
@@ -224,9 +247,14 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     }
     int sbase = slot0 - (S0 ? 0 : lag);
     sbase = sbase < 0 ? sbase + R : sbase;
-    auto ring_row = [&](int j) {  // factor row of local level j
-      const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
-      return ring + sl * W;
+    const double* rbase = ring + (sbase + M) * W;
+    auto ring_row = [&](int j) {  // factor row of local level j (slot sbase - (j-1))
+      if constexpr (M > 0) {
+        return rbase - (j - 1) * W;  // j - 1 <= H - 1 = M: inside the mirrors
+      } else {
+        const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
+        return (const double*)(ring + sl * W);
+      }
     };
     // factors read one level ahead (LDS latency under the previous level's
     // arithmetic); stage 0's level-1 factors are still in registers

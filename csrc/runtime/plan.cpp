@@ -55,35 +55,35 @@ constexpr double kInf = std::numeric_limits<double>::infinity();
 // Pass time per depth K = 1..24 relative to the one-step march kernel on the
 // same tile (one HBM sweep of the three arrays), measured on MI355X with the
 // kernel the executor runs at each depth (bench/pass_sweep.py; emitted by
-// scripts/fit_pass_costs.py from profiles/pass_sweep{,_16384,_8192,_4096}_r2.json;
+// scripts/fit_pass_costs.py from profiles/pass_sweep_{101376,16384,8192,4096}_r2_final.json;
 // canonical depths that were not swept are interpolated). fast5: the
 // pipelined fast-math kernel at every K; canonical: K=1 one-step march, 2
 // two-step kernel, 3/4 kernel 3, K >= 5 the canonical pipelined kernel.
 // On the 288 GB tile a pass costs at least the sweep plus the strip-overlap
 // reads up to K~12 and the fp64 arithmetic beyond; on smaller tiles the
-// deeper passes fill the chip worse (4096^2: the best depth per step is 12,
-// 16384^2: 16, 101376^2: 24).
+// deeper passes fill the chip worse (best depth per step: 4096^2 and 8192^2
+// 12, 16384^2 24 (16 within 2 %), 101376^2 24).
 constexpr int kTables = 4;
 constexpr double kTileCells[kTables] = {4096.0 * 4096, 8192.0 * 8192, 16384.0 * 16384,
                                         101376.0 * 101376};
 constexpr double kFast5[kTables][25] = {
-    {0, 1.054, 1.111, 1.119, 1.128, 1.232, 1.223, 1.318, 1.366, 1.550, 1.512, 1.581, 1.645,
-     1.898, 1.991, 2.264, 2.369, 3.249, 3.353, 3.464, 3.608, 4.101, 4.214, 4.338, 4.462},
-    {0, 1.343, 1.406, 1.460, 1.365, 1.398, 1.337, 1.342, 1.274, 1.302, 1.347, 1.402, 1.423,
-     1.586, 1.652, 1.796, 1.885, 2.696, 2.697, 2.680, 2.731, 3.221, 3.254, 3.312, 3.341},
-    {0, 1.422, 1.503, 1.468, 1.361, 1.417, 1.377, 1.376, 1.268, 1.329, 1.273, 1.298, 1.284,
-     1.408, 1.440, 1.499, 1.535, 2.014, 1.957, 1.964, 1.989, 2.225, 2.215, 2.279, 2.337},
-    {0, 1.230, 1.225, 1.209, 1.158, 1.242, 1.205, 1.192, 1.122, 1.140, 1.187, 1.222, 1.222,
-     1.319, 1.357, 1.400, 1.424, 1.730, 1.762, 1.836, 1.853, 2.023, 2.055, 2.124, 2.133}};
+    {0, 1.104, 1.089, 1.099, 1.143, 1.174, 1.185, 1.272, 1.311, 1.502, 1.551, 1.625, 1.684,
+     1.949, 2.042, 2.405, 2.529, 3.357, 3.447, 3.593, 3.591, 4.124, 4.266, 4.393, 4.477},
+    {0, 1.462, 1.551, 1.591, 1.497, 1.493, 1.499, 1.494, 1.383, 1.443, 1.480, 1.540, 1.507,
+     1.654, 1.760, 1.900, 2.036, 2.769, 2.823, 2.793, 2.746, 3.115, 3.161, 3.235, 3.281},
+    {0, 1.379, 1.440, 1.417, 1.310, 1.356, 1.341, 1.336, 1.223, 1.282, 1.237, 1.254, 1.272,
+     1.418, 1.406, 1.502, 1.522, 1.974, 1.877, 1.897, 1.923, 2.230, 2.221, 2.283, 2.236},
+    {0, 1.234, 1.230, 1.214, 1.161, 1.232, 1.210, 1.198, 1.126, 1.152, 1.200, 1.227, 1.239,
+     1.335, 1.367, 1.445, 1.473, 1.753, 1.764, 1.827, 1.824, 1.989, 2.028, 2.085, 2.099}};
 constexpr double kCanon[kTables][25] = {
-    {0, 1.000, 1.071, 1.093, 1.188, 1.371, 1.421, 1.732, 1.884, 2.270, 2.514, 2.600, 2.758,
-     3.244, 3.731, 4.217, 4.704, 5.102, 5.500, 5.899, 6.297, 6.695, 7.094, 7.492, 7.890},
-    {0, 1.000, 1.070, 1.278, 1.261, 1.317, 1.332, 1.416, 1.588, 1.908, 2.195, 2.322, 2.395,
-     2.754, 3.114, 3.473, 3.833, 4.111, 4.390, 4.669, 4.947, 5.226, 5.504, 5.783, 6.061},
-    {0, 1.000, 1.088, 1.325, 1.248, 1.394, 1.380, 1.392, 1.425, 1.758, 1.862, 1.862, 1.951,
-     2.200, 2.449, 2.697, 2.946, 3.105, 3.264, 3.423, 3.582, 3.740, 3.899, 4.058, 4.217},
-    {0, 1.000, 1.074, 1.141, 1.065, 1.208, 1.193, 1.374, 1.413, 1.637, 1.793, 1.872, 1.927,
-     2.096, 2.264, 2.433, 2.601, 2.758, 2.915, 3.073, 3.230, 3.640, 4.051, 4.461, 4.872}};
+    {0, 1.000, 1.060, 1.090, 1.258, 1.359, 1.402, 1.841, 1.946, 2.296, 2.582, 2.696, 2.837,
+     3.355, 3.873, 4.391, 4.909, 5.344, 5.779, 6.213, 6.648, 7.083, 7.518, 7.952, 8.387},
+    {0, 1.000, 1.105, 1.412, 1.374, 1.464, 1.480, 1.552, 1.663, 1.958, 2.287, 2.362, 2.462,
+     2.827, 3.192, 3.557, 3.922, 4.201, 4.480, 4.759, 5.038, 5.317, 5.596, 5.875, 6.154},
+    {0, 1.000, 1.080, 1.284, 1.218, 1.338, 1.337, 1.361, 1.477, 1.753, 1.874, 1.885, 2.016,
+     2.230, 2.444, 2.658, 2.872, 3.011, 3.150, 3.289, 3.428, 3.566, 3.705, 3.844, 3.983},
+    {0, 1.000, 1.080, 1.143, 1.068, 1.208, 1.200, 1.401, 1.431, 1.650, 1.808, 1.882, 1.927,
+     2.110, 2.293, 2.476, 2.659, 2.820, 2.981, 3.142, 3.303, 3.465, 3.626, 3.787, 3.948}};
 }  // namespace
 
 std::vector<double> default_pass_costs(int kmax, bool fast5, double cells) {
