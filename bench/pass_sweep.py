@@ -44,6 +44,8 @@ def main(argv=None):
     ap.add_argument("--alt", default="12:3,16:8,24:8,8:4,8:1", help="pipe K:stages splits")
     ap.add_argument("--chunk", type=int, default=0, help="rows per task (0: executor default)")
     ap.add_argument("--chunks", default="", help="pipe K:c1/c2/..., extra chunk-row variants")
+    ap.add_argument("--pipe2", default="", help="depths of the 2-column-wave pipe kernel")
+    ap.add_argument("--chunks2", default="", help="pipe2 K:c1/c2/..., chunk-row variants")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -86,6 +88,11 @@ def main(argv=None):
         K, cs = item.split(":")
         for c in cs.split("/"):
             cfgs.append(("pipe", int(K), 0, int(c)))
+    cfgs += [("pipe2", K, 0) for K in krange(a.pipe2)]
+    for item in filter(None, a.chunks2.split(",")):
+        K, cs = item.split(":")
+        for c in cs.split("/"):
+            cfgs.append(("pipe2", int(K), 0, int(c)))
 
     rect = [ops.interior_rect(n, n)]
 
@@ -96,8 +103,8 @@ def main(argv=None):
             ops.stencil2_step(T2, T, iCp, coef, rect, ops.StencilTuning(chunk_rows=16, unroll=2))
         else:
             vec = 2 if kind in ("lds_dpp", "fast5") else 4
-            tn = ops.StencilTuning(chunk_rows=chunk(K, c), kernel=kind, vec=vec, xcd_remap=1,
-                                   stages=S)
+            tn = ops.StencilTuning(chunk_rows=chunk(K, c), kernel="pipe" if kind == "pipe2" else kind,
+                                   vec=vec, xcd_remap=1, stages=S, cols=2 if kind == "pipe2" else 0)
             ops.stencilk_step(K, T2, T, iCp, coef, rect, tn)
 
     times: dict = {c: [] for c in cfgs}
@@ -122,7 +129,8 @@ def main(argv=None):
         kind, K, S = c[:3]
         med = statistics.median(times[c])
         rows.append({"kernel": kind, "K": K, "stages": S or (native().pipe_default_stages(K)
-                                                             if kind in ops.PIPE else 0),
+                                                             if kind in ops.PIPE + ("pipe2",)
+                                                             else 0),
                      "chunk_rows": (chunk(K, c[3] if len(c) > 3 else 0)
                                     if kind not in ("march", "two_step") else None),
                      "ms_per_pass": round(med, 3), "ms_min": round(min(times[c]), 3),

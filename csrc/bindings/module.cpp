@@ -149,9 +149,10 @@ PYBIND11_MODULE(_C, m) {
       "stencilk_rects",
       [](int K, uintptr_t T2, uintptr_t T, uintptr_t iCp, int64_t nx, int64_t ny,
          const std::vector<Rect4>& rects, const Coef4& coef, int chunk_rows, int nontemporal,
-         uintptr_t stream, bool gpu, int xcd_remap, int vec, int kernel, int stages) {
+         uintptr_t stream, bool gpu, int xcd_remap, int vec, int kernel, int stages, int cols) {
         auto r = to_rects(rects);
         StencilTuning tn;
+        tn.cols = cols;
         tn.chunk_rows = chunk_rows;
         tn.nontemporal = nontemporal;
         tn.xcd_remap = xcd_remap;
@@ -176,7 +177,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("K"), py::arg("T2"), py::arg("T"), py::arg("iCp"), py::arg("nx"), py::arg("ny"),
       py::arg("rects"), py::arg("coef"), py::arg("chunk_rows") = 16, py::arg("nontemporal") = 3,
       py::arg("stream") = 0, py::arg("gpu") = true, py::arg("xcd_remap") = -1,
-      py::arg("vec") = 2, py::arg("kernel") = 0, py::arg("stages") = 0);
+      py::arg("vec") = 2, py::arg("kernel") = 0, py::arg("stages") = 0, py::arg("cols") = 0);
   m.def(
       "stream_copy",
       [](uintptr_t b, uintptr_t a, int64_t n, uintptr_t s, int nt, int blocks) {
@@ -357,6 +358,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("default_pass_costs", &default_pass_costs, py::arg("kmax"), py::arg("fast5"),
         py::arg("cells") = 0.0);
   m.def("pipe_default_stages", &pipe_default_stages, py::arg("K"));
+  m.def("pipe_default_cols", &pipe_default_cols, py::arg("K"), py::arg("stages"),
+        py::arg("arith") = 0);
+  m.def("pipe_has_cols", &pipe_has_cols, py::arg("K"), py::arg("stages"), py::arg("arith"),
+        py::arg("cols"));
   m.def("pipe_max_k", []() { return kPipeMaxK; });
   m.def(
       "pass_geometry",

@@ -34,6 +34,7 @@ struct StencilTuning {
   int xcd_remap = -1;      // 1: each XCD takes a contiguous 1/8 of the tasks; 0: chunk rows
                            // padded to 8-block multiples (same-XCD neighbours); -1: by size
   int stages = 0;          // pipelined K-step kernels 9/10: waves per strip (0: default)
+  int cols = 0;            // pipelined kernels: column waves per stage (0: default, 1, 2)
 };
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
@@ -76,6 +77,12 @@ bool fast5_ok(const StencilCoef& c);
 constexpr int kPipeMaxK = 24;
 int pipe_default_stages(int K);
 bool pipe_has(int K, int stages, int arith = 0);
+// Column waves per stage: 2 = blocks of 2 x stages waves over ~500 columns
+// (V = 4 only, fast5 K = 16/20/24, stencil_pipe_e.hip, an experiment: slower
+// than 1); pipe_has_cols says whether (K, S, arith, cols) is instantiated,
+// pipe_default_cols is what a tuning of cols = 0 runs.
+bool pipe_has_cols(int K, int stages, int arith, int cols);
+int pipe_default_cols(int K, int stages, int arith);
 // arith: 0 fast5, 1 canonical, 2 fast5 with ds_bpermute lane moves (kernel 11)
 void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const double* T,
                             const double* iCp, int64_t nx, int64_t ny, const Rect* rects,

@@ -178,11 +178,12 @@ inline int64_t plan_rects(RectList& L, const Rect* rects, int nrects, int V, int
 // stencil_pipe.h kernels 9/10):
 // one block per (strip, chunk) task, strips as in plan_rects with halo > 0;
 // block b of a rect is (chunk = lb / strips, strip = lb % strips).
+// sw_block: input columns of one strip task (0: one wave window, 64 V).
 inline int64_t plan_strip_tasks(RectList& L, const Rect* rects, int nrects, int V,
-                                int chunk_rows, int halo) {
+                                int chunk_rows, int halo, int64_t sw_block = 0) {
   L = RectList{};
   int64_t total = 0;
-  const int64_t sw = (int64_t)kWave * V;
+  const int64_t sw = sw_block > 0 ? sw_block : (int64_t)kWave * V;
   const int64_t step = (sw - 2 * halo) / V * V;
   for (int i = 0; i < nrects; ++i) {
     const Rect& r = rects[i];

@@ -46,6 +46,23 @@ struct Plan {
   static_assert(S >= 1 && HL >= 1 && HL <= H, "bad stage split");
 };
 
+// Block geometry with C column waves per stage (C = 1: one 64V-column window
+// per strip). With C > 1 the C waves of a stage sit D = 64V - 2*Hp columns
+// apart (Hp = H rounded up to even) and all exchange through the block-wide
+// LDS rows once per row iteration, so a stage boundary inside the block
+// recomputes only ~2H columns instead of the strip's 2K: the block of
+// WB = (C-1) D + 64V input columns outputs WB - 2K (K=24, C=2: 452 of 500
+// columns, 1.13x recompute against 1.23x for C = 1).
+template <int K, int S, int V, int C>
+struct Geo {
+  static constexpr int W = kWave * V;                // one wave's window
+  static constexpr int Hp = (Plan<K, S>::H + 1) / 2 * 2;
+  static constexpr int D = C > 1 ? W - 2 * Hp : W;   // wave stride inside the block
+  static constexpr int WB = (C - 1) * D + W;         // block row columns
+  static constexpr int kStep = (WB - 2 * K) / V * V; // output columns per strip
+  static_assert(C == 1 || (V == 4 && D % 4 == 0 && D > 2 * K / S), "bad column split");
+};
+
 // Waves per SIMD a block shape allows: the LDS (160 KiB per CU, 4 SIMDs)
 // and a VGPR estimate, so a waves_per_eu cap never forces spills: fast5
 // 3 rows x V cells x 2 dwords per level, stage 0's two-row prefetch, ~40 for
@@ -53,9 +70,9 @@ struct Plan {
 // fluxes (checked: no spills at any K, V, scripts/check_isa.py).
 constexpr int kArFast5 = 0, kArCanon = 1, kArFast5Perm = 2;
 
-template <int K, int S, int V, bool Canon>
+template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int occupancy(int lds) {
-  const int by_lds = (160 * 1024) / lds * S / 4;
+  const int by_lds = (160 * 1024) / lds * S * C / 4;
   const int vgpr = Canon ? 8 * Plan<K, S>::H * V + 8 * V + 64 : 6 * Plan<K, S>::H * V + 8 * V + 40;
   const int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
   const int w = by_lds < by_vgpr ? by_lds : by_vgpr;
@@ -68,25 +85,26 @@ constexpr int occupancy(int lds) {
 // ds_read offsets serve all levels (no per-level modulo and address VALU op:
 // -3 % VALU, -50 % SALU instructions in the K=24 row loop). Only where the
 // extra rows cost no occupancy.
-template <int K, int S, int V, bool Canon>
+template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int mirror_rows() {
-  constexpr int H = Plan<K, S>::H, row = kWave * V * 8;
+  constexpr int H = Plan<K, S>::H, row = Geo<K, S, V, C>::WB * 8;
   constexpr int base = (Plan<K, S>::R + 2 * (S > 1 ? S - 1 : 1)) * row;
-  return occupancy<K, S, V, Canon>(base + (H - 1) * row) == occupancy<K, S, V, Canon>(base)
+  return occupancy<K, S, V, Canon, C>(base + (H - 1) * row) ==
+                 occupancy<K, S, V, Canon, C>(base)
              ? H - 1
              : 0;
 }
 
 // LDS bytes of one block (ring + mirrors + double-buffered hand-off rows)
-template <int K, int S, int V, bool Canon>
+template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int lds_bytes() {
-  return (Plan<K, S>::R + mirror_rows<K, S, V, Canon>() + 2 * (S > 1 ? S - 1 : 1)) * kWave * V *
-         8;
+  return (Plan<K, S>::R + mirror_rows<K, S, V, Canon, C>() + 2 * (S > 1 ? S - 1 : 1)) *
+         Geo<K, S, V, C>::WB * 8;
 }
 
-template <int K, int S, int V, bool Canon>
+template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int waves_per_simd() {
-  return occupancy<K, S, V, Canon>(lds_bytes<K, S, V, Canon>());
+  return occupancy<K, S, V, Canon, C>(lds_bytes<K, S, V, Canon, C>());
 }
 
 template <bool kDpp = true>
@@ -112,18 +130,21 @@ __device__ __forceinline__ double from_prev_lane(double v) {
   }
 }
 
-template <int K, int S, int V, int Ar>
+template <int K, int S, int V, int Ar, int C>
 __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double* __restrict__ T,
                                           const double* __restrict__ iCp, int64_t nx, int64_t ny,
                                           const RectList& L, const StencilCoef& k, int chunk_rows,
                                           int remap) {
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm;
-  constexpr int H = P::H, HL = P::HL, R = P::R, M = mirror_rows<K, S, V, Canon>();
-  constexpr int W = kWave * V;
-  constexpr int kStep = (W - 2 * K) / V * V;  // output columns per strip (plan_strip_tasks)
+  using G = Geo<K, S, V, C>;
+  constexpr int H = P::H, HL = P::HL, R = P::R, M = mirror_rows<K, S, V, Canon, C>();
+  constexpr int W = G::W, WB = G::WB, D = G::D;
+  constexpr int kStep = G::kStep;  // output columns per strip (plan_strip_tasks, sw = WB)
   constexpr int NH = S > 1 ? S - 1 : 1;
-  const int stage = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int stage = C > 1 ? wv % S : wv;  // waves c*S .. c*S+S-1: column c, one per SIMD
+  const int col = C > 1 ? wv / S : 0;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   int ri = 0;
@@ -135,16 +156,21 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   const int64_t ya = r.y0 + chunk * chunk_rows;
   const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
 
-  const int64_t x = xs + (int64_t)lane * V;
+  // the columns [lo, hi) of this wave's window it writes to the block rows
+  // (the stage boundary with the neighbouring column wave at the window
+  // offsets Hp and D + Hp, inside both waves' valid ranges)
+  const int lo = col > 0 ? G::Hp : 0, hi = col < C - 1 ? D + G::Hp : W;
+  const int64_t xw = xs + (int64_t)col * D;  // window origin
+  const int64_t x = xw + (int64_t)lane * V;
   bool m[V], cin[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
-    const int p = lane * V + v;
-    m[v] = p >= K && p < K + kStep && x + v >= r.x0 && x + v < r.x1;
+    const int p = lane * V + v, pb = col * D + p;
+    m[v] = pb >= K && pb < K + kStep && p >= lo && p < hi && x + v >= r.x0 && x + v < r.x1;
     cin[v] = (x + v >= 1) && (x + v <= nx - 2);
   }
   const int64_t xl = min(max(x, (int64_t)0), nx - V);
-  const bool xin = xs >= 1 && xs + W - 1 <= nx - 2;  // no x-boundary cell in the strip
+  const bool xin = xw >= 1 && xw + W - 1 <= nx - 2;  // no x-boundary cell in the window
 
   // fast5 constants (the host guarantees fast5_ok); canonical uses k directly
   const double ax = (-k.mlam) * k.rdx * k.rdx;
@@ -177,20 +203,24 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
   }
   // physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R)
-  __shared__ double ring[(R + M) * W];
-  __shared__ double hand[2][NH][W];
-  for (int t = threadIdx.x; t < (R + M) * W; t += S * kWave) ring[t] = 0.0;
-  for (int t = threadIdx.x; t < 2 * NH * W; t += S * kWave) (&hand[0][0][0])[t] = 0.0;
+  __shared__ double ring[(R + M) * WB];
+  __shared__ double hand[2][NH][WB];
+  for (int t = threadIdx.x; t < (R + M) * WB; t += S * C * kWave) ring[t] = 0.0;
+  for (int t = threadIdx.x; t < 2 * NH * WB; t += S * C * kWave) (&hand[0][0][0])[t] = 0.0;
   __syncthreads();
-  // LDS rows are lane-interleaved (cell pair h of lane l at dbl2 slot h*64+l):
-  // every ds_read/write_b128 covers 1 KiB contiguously, no bank conflicts
+  // LDS rows hold cell pairs interleaved by parity (pair p at dbl2 slot
+  // (p & 1) * WB/4 + p/2): a wave window starting at an even pair (D % 4 == 0)
+  // reads/writes each of its two pairs per lane as one contiguous 1 KiB
+  // ds_read/write_b128, no bank conflicts (C = 1: slot h*64 + lane).
+  constexpr int NPH = V == 4 ? WB / 4 : kWave;
+  const int cq = col * (D / 4);
   auto rd2 = [&](const double* row, double (&out)[V]) {
     if constexpr (V == 1) {
       out[0] = row[lane];
     } else {
 #pragma unroll
       for (int h = 0; h < V / 2; ++h) {
-        const dbl2 t2 = reinterpret_cast<const dbl2*>(row)[h * kWave + lane];
+        const dbl2 t2 = reinterpret_cast<const dbl2*>(row)[h * NPH + cq + lane];
         out[2 * h] = t2.x;
         out[2 * h + 1] = t2.y;
       }
@@ -205,7 +235,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         dbl2 t2;
         t2.x = in[2 * h];
         t2.y = in[2 * h + 1];
-        reinterpret_cast<dbl2*>(row)[h * kWave + lane] = t2;
+        if (C == 1 || (lane * V + 2 * h >= lo && lane * V + 2 * h < hi))
+          reinterpret_cast<dbl2*>(row)[h * NPH + cq + lane] = t2;
       }
     }
   };
@@ -231,9 +262,9 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 #pragma unroll
         for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? (Canon ? pC[v] : gs * pC[v]) : 0.0;
       }
-      wr2(ring + (slot0 + M) * W, g);
+      wr2(ring + (slot0 + M) * WB, g);
       if constexpr (M > 0) {
-        if (slot0 >= R - M) wr2(ring + (slot0 - (R - M)) * W, g);
+        if (slot0 >= R - M) wr2(ring + (slot0 - (R - M)) * WB, g);
       }
 #pragma unroll
       for (int v = 0; v < V; ++v) {
@@ -247,13 +278,13 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     }
     int sbase = slot0 - (S0 ? 0 : lag);
     sbase = sbase < 0 ? sbase + R : sbase;
-    const double* rbase = ring + (sbase + M) * W;
+    const double* rbase = ring + (sbase + M) * WB;
     auto ring_row = [&](int j) {  // factor row of local level j (slot sbase - (j-1))
       if constexpr (M > 0) {
-        return rbase - (j - 1) * W;  // j - 1 <= H - 1 = M: inside the mirrors
+        return rbase - (j - 1) * WB;  // j - 1 <= H - 1 = M: inside the mirrors
       } else {
         const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
-        return (const double*)(ring + sl * W);
+        return (const double*)(ring + sl * WB);
       }
     };
     // factors read one level ahead (LDS latency under the previous level's
@@ -354,14 +385,15 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   }
 }
 
-template <int K, int S, int V, int Ar>
-__global__ __launch_bounds__(kWave * S) __attribute__((amdgpu_waves_per_eu(
-    waves_per_simd<K, S, V, Ar == kArCanon>()))) void pipe_kernel(double* __restrict__ T2,
-                                                   const double* __restrict__ T,
-                                                   const double* __restrict__ iCp, int64_t nx,
-                                                   int64_t ny, RectList L, StencilCoef k,
-                                                   int chunk_rows, int remap) {
-  pipe_body<K, S, V, Ar>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
+template <int K, int S, int V, int Ar, int C>
+__global__ __launch_bounds__(kWave * S * C) __attribute__((amdgpu_waves_per_eu(
+    waves_per_simd<K, S, V, Ar == kArCanon, C>()))) void pipe_kernel(double* __restrict__ T2,
+                                                      const double* __restrict__ T,
+                                                      const double* __restrict__ iCp,
+                                                      int64_t nx, int64_t ny, RectList L,
+                                                      StencilCoef k, int chunk_rows,
+                                                      int remap) {
+  pipe_body<K, S, V, Ar, C>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
 }
 
 struct PipeLaunch {
@@ -376,9 +408,9 @@ struct PipeLaunch {
   hipStream_t stream;
 };
 
-template <int K, int S, int V, int Ar>
+template <int K, int S, int V, int Ar, int C = 1>
 void launch(const PipeLaunch& a) {
-  pipe_kernel<K, S, V, Ar><<<dim3((unsigned)a.blocks), dim3(kWave * S), 0, a.stream>>>(
+  pipe_kernel<K, S, V, Ar, C><<<dim3((unsigned)a.blocks), dim3(kWave * S * C), 0, a.stream>>>(
       a.T2, a.T, a.iCp, a.nx, a.ny, *a.L, a.k, a.chunk_rows, a.remap);
 }
 
@@ -388,6 +420,8 @@ bool dispatch_a(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_b(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_d(int K, int S, int V, int ar, const PipeLaunch& a);
+// two column waves per stage (V = 4 only), stencil_pipe_e.hip
+bool dispatch_e(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe
 }  // namespace rma

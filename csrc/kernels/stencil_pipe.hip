@@ -33,6 +33,21 @@ bool pipe_has(int K, int S, int arith) {
          (K == 8 && S == 4) || (K == 8 && S == 1);
 }
 
+bool pipe_has_cols(int K, int S, int arith, int cols) {
+  if (cols <= 1) return pipe_has(K, S, arith);
+  return cols == 2 && arith == pipe::kArFast5 && S == 4 && (K == 16 || K == 20 || K == 24);
+}
+
+int pipe_default_cols(int K, int S, int arith) {
+  // one column wave: the 2-column blocks (stencil_pipe_e.hip) do 8 % less
+  // arithmetic at K=24 but run one block per CU and lose 5-20 % to the
+  // unhidden per-row barrier (profiles/pass_sweep_cols2_r2.json)
+  (void)K;
+  (void)S;
+  (void)arith;
+  return 1;
+}
+
 void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const double* T,
                             const double* iCp, int64_t nx, int64_t ny, const Rect* rects,
                             int nrects, const StencilCoef& c, const StencilTuning& tune,
@@ -63,16 +78,26 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
                        ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
   int V = 1;
   if (aligned && nx % 2 == 0) V = (tune.vec == 4 && nx % 4 == 0) ? 4 : 2;
+  int C = tune.cols > 0 ? tune.cols : pipe_default_cols(K, S, arith);
+  RMA_CHECK_ARG(pipe_has_cols(K, S, arith, C), "no pipelined kernel with " << C
+                                                   << " column waves for K=" << K << " S=" << S
+                                                   << " arithmetic " << arith);
+  if (V != 4) C = 1;  // the 2-column blocks need 16-B pairs at 4 cells per lane
+  // block input columns (stencil_pipe.h Geo): (C-1) * (64V - 2 Hp) + 64V
+  const int Hp = ((K + S - 1) / S + 1) / 2 * 2;
+  const int64_t WB = (int64_t)(C - 1) * (64 * V - 2 * Hp) + 64 * V;
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   march::RectList L;
-  const int64_t ntask = march::plan_strip_tasks(L, rects, nrects, V, tune.chunk_rows, K);
+  const int64_t ntask = march::plan_strip_tasks(L, rects, nrects, V, tune.chunk_rows, K, WB);
   if (L.n == 0) return;
   RMA_CHECK_ARG(ntask < (int64_t(1) << 31), "grid too large: " << ntask << " blocks");
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, &L, c, tune.chunk_rows, remap, ntask, as_stream(stream)};
-  const bool ok = pipe::dispatch_a(K, S, V, arith, a) || pipe::dispatch_b(K, S, V, arith, a) ||
-                  pipe::dispatch_c(K, S, V, arith, a) || pipe::dispatch_d(K, S, V, arith, a);
-  RMA_CHECK_ARG(ok, "pipelined kernel K=" << K << " S=" << S << " V=" << V << " arithmetic="
-                                           << arith << " not instantiated");
+  const bool ok =
+      C == 2 ? pipe::dispatch_e(K, S, V, arith, a)
+             : (pipe::dispatch_a(K, S, V, arith, a) || pipe::dispatch_b(K, S, V, arith, a) ||
+                pipe::dispatch_c(K, S, V, arith, a) || pipe::dispatch_d(K, S, V, arith, a));
+  RMA_CHECK_ARG(ok, "pipelined kernel K=" << K << " S=" << S << " V=" << V << " C=" << C
+                                           << " arithmetic=" << arith << " not instantiated");
   RMA_HIP_LAUNCH_CHECK();
 }
 

@@ -67,6 +67,7 @@ class StencilTuning:
     vec: int = 2
     xcd_remap: int = -1  # -1: chosen by tile width (see csrc/kernels/stencil.hip)
     stages: int = 0  # pipe / pipec: waves per strip (0: native pipe_default_stages)
+    cols: int = 0  # pipe: column waves per stage (0: native pipe_default_cols; 2 needs vec=4)
 
 
 @dataclass
@@ -246,7 +247,8 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
     if T.is_cuda:
         native().stencilk_rects(K, _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                 tn.chunk_rows, int(tn.nontemporal), stream_handle(T), True,
-                                tn.xcd_remap, tn.vec, KERNELS[tn.kernel], int(tn.stages))
+                                tn.xcd_remap, tn.vec, KERNELS[tn.kernel], int(tn.stages),
+                                int(tn.cols))
     elif _use_native_cpu():
         native().stencilk_rects(K, _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                 16, 0, 0, False, -1, 2, KERNELS[tn.kernel], 0)

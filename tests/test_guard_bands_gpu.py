@@ -94,8 +94,11 @@ def test_deep_pipelined_kernels_stay_in_bounds(ny, nx, K):
         cases += [("fast5p2", 2), ("fast5p2", 4), ("fast5p4", 2), ("fast5p4", 4)]
     if K == 16:
         cases += [("fast5p8", 2), ("fast5p8", 4)]
-    for kern, vec in cases:
-        tn = ops.StencilTuning(chunk_rows=7, kernel=kern, vec=vec)
+    cases = [(k, v, 0) for k, v in cases]
+    if K in (16, 20, 24):  # 8-wave blocks of 2 column waves per stage (152 KB LDS at K=24)
+        cases += [("pipe", 4, 2)]
+    for kern, vec, cols in cases:
+        tn = ops.StencilTuning(chunk_rows=7, kernel=kern, vec=vec, cols=cols)
         check_stencil(lambda o, t, c, r: ops.stencilk_step(K, o, t, c, coef(), r, tn), ny, nx,
                       rects)
 

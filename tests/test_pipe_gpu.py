@@ -34,7 +34,7 @@ def gpu_run(K, T, iCp, rects, kernel, fill=-5.0, **kw):
     out = torch.full(T.shape, fill, dtype=torch.float64, device=DEV)
     tn = ops.StencilTuning(kernel=kernel, xcd_remap=kw.pop("xcd", 1),
                            chunk_rows=kw.pop("chunk", 16), vec=kw.pop("vec", 4),
-                           stages=kw.pop("stages", 0))
+                           stages=kw.pop("stages", 0), cols=kw.pop("cols", 0))
     ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(), rects, tn)
     return out.cpu()
 
@@ -70,6 +70,32 @@ def test_pipe_rect_lists(kernel, K, xcd):
     ops.stencilk_step(K, out, Td, iCpd, coef(), [interior],
                       ops.StencilTuning(kernel=kernel, chunk_rows=64, vec=4, xcd_remap=xcd))
     assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("nx", [516, 1028, 1500, 2052])
+@pytest.mark.parametrize("K", [16, 20, 24])
+def test_pipe_two_column_waves_bitwise(nx, K):
+    """Blocks of 2 column waves per stage (8 waves over 500 columns, stage
+    boundaries inside the block exchanged through LDS each row): bitwise equal
+    to the CPU twin, also on rect lists whose strips end mid-block."""
+    ny = 149
+    T, iCp = rand((ny, nx), 11 + K), rand((ny, nx), 12, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, "pipe")
+    assert torch.equal(gpu_run(K, T, iCp, rects, "pipe", chunk=41, cols=2), ref)
+    sub = [(K + 3, nx - K - 7, K + 2, ny - K - 5), (1, K + 3, 1, ny - 1)]
+    ref = cpu_ref(K, T, iCp, sub, "pipe")
+    assert torch.equal(gpu_run(K, T, iCp, sub, "pipe", chunk=23, cols=2, xcd=0), ref)
+
+
+def test_pipe_two_column_waves_need_vec4():
+    """cols=2 on a tile that only allows 2 cells per lane runs the 1-column kernel."""
+    ny, nx, K = 67, 518, 20
+    T, iCp = rand((ny, nx), 13), rand((ny, nx), 14, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    assert torch.equal(gpu_run(K, T, iCp, rects, "pipe", cols=2), cpu_ref(K, T, iCp, rects, "pipe"))
+    with pytest.raises(Exception):
+        gpu_run(8, T, iCp, rects, "pipe", cols=2)  # instantiated for K = 16, 20, 24 only
 
 
 @pytest.mark.parametrize("K,S", [(12, 3), (16, 8), (24, 8), (8, 4), (8, 1)])
