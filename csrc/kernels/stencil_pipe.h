@@ -31,6 +31,7 @@
 
 #include <type_traits>
 
+#include "rma/common.h"
 #include "rma/kernels.h"
 #include "stencil_device.h"
 
@@ -401,17 +402,25 @@ struct PipeLaunch {
   const double* T;
   const double* iCp;
   int64_t nx, ny;
-  const RectList* L;
+  const Rect* rects;
+  int nrects;
   StencilCoef k;
   int chunk_rows, remap;
-  int64_t blocks;
   hipStream_t stream;
 };
 
+// Plans the (strip, chunk) tasks with this instantiation's block width
+// (Geo::WB, kStep), so host planning and kernel geometry cannot disagree.
 template <int K, int S, int V, int Ar, int C = 1>
 void launch(const PipeLaunch& a) {
-  pipe_kernel<K, S, V, Ar, C><<<dim3((unsigned)a.blocks), dim3(kWave * S * C), 0, a.stream>>>(
-      a.T2, a.T, a.iCp, a.nx, a.ny, *a.L, a.k, a.chunk_rows, a.remap);
+  RectList L;
+  const int64_t blocks =
+      plan_strip_tasks(L, a.rects, a.nrects, V, a.chunk_rows, K, Geo<K, S, V, C>::WB);
+  static_assert(Geo<K, S, V, C>::kStep == (Geo<K, S, V, C>::WB - 2 * K) / V * V, "strip step");
+  if (L.n == 0) return;
+  RMA_CHECK_ARG(blocks < (int64_t(1) << 31), "grid too large: " << blocks << " blocks");
+  pipe_kernel<K, S, V, Ar, C><<<dim3((unsigned)blocks), dim3(kWave * S * C), 0, a.stream>>>(
+      a.T2, a.T, a.iCp, a.nx, a.ny, L, a.k, a.chunk_rows, a.remap);
 }
 
 // Each stencil_pipe_*.hip unit instantiates a range of (K, S) and answers

@@ -83,15 +83,9 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
                                                    << " column waves for K=" << K << " S=" << S
                                                    << " arithmetic " << arith);
   if (V != 4) C = 1;  // the 2-column blocks need 16-B pairs at 4 cells per lane
-  // block input columns (stencil_pipe.h Geo): (C-1) * (64V - 2 Hp) + 64V
-  const int Hp = ((K + S - 1) / S + 1) / 2 * 2;
-  const int64_t WB = (int64_t)(C - 1) * (64 * V - 2 * Hp) + 64 * V;
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
-  march::RectList L;
-  const int64_t ntask = march::plan_strip_tasks(L, rects, nrects, V, tune.chunk_rows, K, WB);
-  if (L.n == 0) return;
-  RMA_CHECK_ARG(ntask < (int64_t(1) << 31), "grid too large: " << ntask << " blocks");
-  pipe::PipeLaunch a{T2, T, iCp, nx, ny, &L, c, tune.chunk_rows, remap, ntask, as_stream(stream)};
+  pipe::PipeLaunch a{T2, T, iCp, nx, ny, rects, nrects, c, tune.chunk_rows, remap,
+                     as_stream(stream)};
   const bool ok =
       C == 2 ? pipe::dispatch_e(K, S, V, arith, a)
              : (pipe::dispatch_a(K, S, V, arith, a) || pipe::dispatch_b(K, S, V, arith, a) ||
