@@ -295,6 +295,19 @@ int main() {
       }
     }
     EXPECT(plan_passes(20, cf) == std::vector<int>{20});
+    // tile classes: nearest measured table in log(cells); 0 = the 288 GB tile
+    EXPECT(default_pass_costs(24, true, 101376.0 * 101376.0) == cf);
+    EXPECT(default_pass_costs(24, true, 4096.0 * 4096.0) != cf);
+    EXPECT(default_pass_costs(24, true, 4000.0 * 4000.0) ==
+           default_pass_costs(24, true, 4096.0 * 4096.0));
+    EXPECT(default_pass_costs(24, true, 64.0 * 64.0) ==
+           default_pass_costs(24, true, 4096.0 * 4096.0));  // below the smallest class
+    EXPECT(default_pass_costs(24, true, 2e11) == cf);       // above the largest
+    EXPECT(plan_passes(20, default_pass_costs(24, true, 4096.0 * 4096.0)) ==
+           (std::vector<int>{12, 8}));
+    EXPECT(default_pass_costs(12, false, 16384.0 * 16384.0).size() == 13);
+    EXPECT(throws([&] { default_pass_costs(25, true); }));
+    EXPECT(throws([&] { default_pass_costs(0, true); }));
     // DP optimality against brute force on small n
     std::function<double(int)> best = [&](int m) -> double {
       if (m == 0) return 0.0;
