@@ -61,33 +61,51 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("trace_dir")
     ap.add_argument("--md", default="")
-    ap.add_argument("--interior-min-ms", type=float, default=0.5,
-                    help="a stream is 'interior' if it runs pipelined kernels longer than this")
+    ap.add_argument("--from-pass", type=int, default=0,
+                    help="start the window at the n-th long interior kernel (skip warm-up passes)")
+    ap.add_argument("--interior-frac", type=float, default=0.5,
+                    help="a stream is 'interior' if its longest pipelined kernel lasts at least "
+                         "this fraction of the longest one in the trace")
+    ap.add_argument("--window", default="",
+                    help="restrict to [first start, last end] of operations whose name contains "
+                         "this (e.g. rccl: the run with RCCL traffic)")
     a = ap.parse_args(argv)
     ops = load(a.trace_dir)
     # skip setup work (init / fill kernels) before the first pipelined pass
+    t1 = max(o[4] for o in ops)
+    if a.window:
+        sel = [o for o in ops if a.window in o[1]]
+        ops = [o for o in ops if o[3] >= min(x[3] for x in sel) and o[4] <= max(x[4] for x in sel)]
+    longest = max((o[4] - o[3] for o in ops if "pipe_kernel" in o[1]), default=0)
+    thr = a.interior_frac * longest
     t0 = min((o[3] for o in ops if "pipe_kernel" in o[1]), default=0)
-    ops = [o for o in ops if o[3] >= t0]
+    long_starts = sorted(o[3] for o in ops if "pipe_kernel" in o[1] and o[4] - o[3] >= thr)
+    if a.from_pass and len(long_starts) > a.from_pass:
+        t0 = long_starts[a.from_pass]
+    ops = [o for o in ops if o[3] >= t0 and o[4] <= t1]
     streams = collections.defaultdict(list)
     for o in ops:
         streams[o[2]].append(o)
     interior_streams = {s for s, L in streams.items()
-                        if any("pipe_kernel" in o[1] and (o[4] - o[3]) / 1e6 > a.interior_min_ms
-                               for o in L)}
+                        if any("pipe_kernel" in o[1] and o[4] - o[3] >= thr for o in L)}
     iu = union([(o[3], o[4]) for s in interior_streams for o in streams[s]])
     bnd = [o for s, L in streams.items() if s not in interior_streams for o in L]
     b_total = sum(o[4] - o[3] for o in bnd)
     b_hidden = sum(covered(o[3], o[4], iu) for o in bnd)
     wall = max(o[4] for o in ops) - min(o[3] for o in ops)
     busy = sum(b - a_ for a_, b in iu)
-    lines = ["| stream | role | ops | busy ms | kernels (top 3 by time) |", "|---|---|---|---|---|"]
+    lines = ["| stream | role | ops | busy ms | under an interior kernel | kernels (top 3 by time) |",
+             "|---|---|---|---|---|---|"]
     for s, L in sorted(streams.items(), key=lambda kv: str(kv[0])):
         by = collections.Counter()
         for o in L:
             by[o[1][:60]] += o[4] - o[3]
         top = ", ".join(f"{k} {v / 1e6:.2f}" for k, v in by.most_common(3))
         role = "interior" if s in interior_streams else "boundary"
-        lines.append(f"| {s} | {role} | {len(L)} | {sum(o[4] - o[3] for o in L) / 1e6:.2f} | {top} |")
+        tot = sum(o[4] - o[3] for o in L)
+        hid = "" if role == "interior" else \
+            f"{sum(covered(o[3], o[4], iu) for o in L) / max(tot, 1):.1%}"
+        lines.append(f"| {s} | {role} | {len(L)} | {tot / 1e6:.2f} | {hid} | {top} |")
     summary = (f"window {wall / 1e6:.2f} ms; interior streams busy {busy / 1e6:.2f} ms "
                f"({busy / max(wall, 1):.1%} of the window); boundary work {b_total / 1e6:.3f} ms, "
                f"of which {b_hidden / 1e6:.3f} ms ({b_hidden / max(b_total, 1):.1%}) ran while an "
