@@ -11,6 +11,7 @@ running (1.0 = the exchange and frame are fully hidden), plus a per-stream
 table. Usage:
 
     python scripts/overlap_timeline.py gpurun_out/r2t/trace [--md out.md]
+    python scripts/overlap_timeline.py profiles/traces_r2/loopback2_k24_kernel_trace.csv --from-pass 4
 """
 from __future__ import annotations
 
@@ -22,7 +23,8 @@ import os
 
 def load(d: str) -> list:
     ops = []
-    kt = os.path.join(d, "run_kernel_trace.csv")
+    kt = d if os.path.isfile(d) else os.path.join(d, "run_kernel_trace.csv")
+    d = os.path.dirname(kt)
     for r in csv.DictReader(open(kt)):
         ops.append(("kernel", r["Kernel_Name"].replace("(anonymous namespace)::", "")
                     .split("(")[0].replace("void ", ""),
