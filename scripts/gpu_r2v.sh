@@ -1,4 +1,5 @@
 #!/bin/bash
+# (experiment record: the pipem kernel variant was removed after this run, profiles/SUMMARY_r2.md)
 # r2 experiment: EXEC-masking lanes with no valid cell per level (pipem) vs pipe
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
