@@ -1,0 +1,46 @@
+"""The measurement tools behind profiles/: the planner's cost tables in
+csrc/runtime/plan.cpp are exactly what scripts/fit_pass_costs.py derives from
+the committed pass sweeps, and the overlap analysis of the committed kernel
+traces (scripts/overlap_timeline.py) reproduces profiles/overlap_r2.md."""
+import importlib.util
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = os.path.join(ROOT, "profiles")
+
+
+def load(name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "scripts", name + ".py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.parametrize("tile", [101376, 16384, 8192, 4096])
+def test_planner_tables_come_from_the_committed_sweeps(tile):
+    native = pytest.importorskip("rocm_mpi_amd._native").native
+    try:
+        N = native()
+    except Exception as e:  # noqa: BLE001
+        pytest.skip(f"native core not built: {e}")
+    n, fast, can = load("fit_pass_costs").tables(os.path.join(P, f"pass_sweep_{tile}_r2_final.json"))
+    assert n == tile
+    cells = float(tile) * tile
+    got_f = list(N.default_pass_costs(24, True, cells))[1:]
+    got_c = list(N.default_pass_costs(24, False, cells))[1:]
+    assert got_f == pytest.approx(fast, abs=6e-4)
+    assert got_c == pytest.approx(can, abs=6e-4)
+
+
+def test_overlap_analysis_of_committed_traces(capsys):
+    ot = load("overlap_timeline")
+    tr = os.path.join(P, "traces_r2", "loopback2_k24_kernel_trace.csv")
+    assert ot.main([tr, "--from-pass", "4"]) == 0
+    out = capsys.readouterr().out
+    first = out.splitlines()[0]
+    frac = float(first.split("(")[-1].split("%")[0]) / 100
+    assert frac > 0.9, first
+    md = open(os.path.join(P, "overlap_r2.md")).read()
+    assert first in md
