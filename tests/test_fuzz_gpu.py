@@ -15,3 +15,32 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(128))
 def test_random_decompositions_match_one_cpu_rank(seed):
     check(seed, "cuda")
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_rccl_self_send_matches_cpu(seed):
+    """One rank, periodic in both dims, every halo plane through RCCL
+    send/recv to itself (the multi-GPU message pattern on one GPU), random
+    tile / K / steps / arithmetic == the CPU run of the same periodic grid."""
+    import random
+
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    r = random.Random(1000 + seed)
+    K = r.randint(1, 24)
+    nx, ny, nt = 4 * K + r.randint(6, 150), 4 * K + r.randint(6, 90), r.randint(1, 2 * K + 5)
+    variant, fast = r.choice(["perf", "perf_hide"]), r.random() < 0.6
+    outs = []
+    for dev in ("cuda", "cpu"):
+        kw = dict(transport="rccl", self_via_transport=True) if dev == "cuda" else dict(device="cpu")
+        gg.init_global_grid(nx, ny, 1, periodx=1, periody=1, quiet=True,
+                            overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1), **kw)
+        m = Diffusion2D(DiffusionConfig(variant=variant, nx=nx, ny=ny, nt=nt, quiet=True,
+                                        init="random", periods=(1, 1, 0), temporal=K,
+                                        fast_math=fast, device=dev))
+        m.step(nt)
+        outs.append(m.field.cpu().clone())
+        m.close()
+        gg.finalize_global_grid()
+    assert outs[0].equal(outs[1]), (K, nx, ny, nt, variant, fast)
