@@ -42,6 +42,7 @@ CORE_HOST_SOURCES = sorted((CSRC / "kernels").glob("*.cpp"))
 BIND_SOURCES = [CSRC / "bindings" / "module.cpp"]
 HOST_SOURCES = CORE_HOST_SOURCES + BIND_SOURCES
 EXAMPLES = sorted((ROOT / "examples").glob("*.cpp"))
+TOOLS = sorted((ROOT / "bench" / "native").glob("*.hip"))  # standalone probes -> build/bench/
 
 
 def ext_path() -> Path:
@@ -100,7 +101,7 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
         # repository snapshot on a GPU box carries the .so files but not the
         # object files, which would otherwise force a full rebuild there)
         newest_src = max([newest_header] + [p.stat().st_mtime for p in
-                                            HIP_SOURCES + HOST_SOURCES + EXAMPLES])
+                                            HIP_SOURCES + HOST_SOURCES + EXAMPLES + TOOLS])
         if min(out.stat().st_mtime, core.stat().st_mtime) >= newest_src:
             return out
     BUILD.mkdir(parents=True, exist_ok=True)
@@ -164,6 +165,17 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"example build failed: {src}\n{r.stdout}\n{r.stderr}")
+            print(f"[rocm_mpi_amd build] built {exe.relative_to(ROOT)}", flush=True)
+    tooldir = ROOT / "build" / "bench"
+    for src in TOOLS:
+        exe = tooldir / src.stem
+        if newer(exe, [src]):
+            tooldir.mkdir(parents=True, exist_ok=True)
+            cmd = [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", str(src),
+                   "-o", str(exe)]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"tool build failed: {src}\n{r.stdout}\n{r.stderr}")
             print(f"[rocm_mpi_amd build] built {exe.relative_to(ROOT)}", flush=True)
     return out
 
