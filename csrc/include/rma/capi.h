@@ -80,8 +80,9 @@ int rma_executor_create_k(rma_grid* g, int mode, double* T, double* T2, const do
                           int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
                           int steps_per_pass, double* qx, double* qy, double* dTdt,
                           rma_executor** out);
-// Same with `fast_math` != 0: the K-step passes use the 5-point-sum arithmetic
-// (not bitwise equal to the canonical update; required for 12 and 16 steps per pass).
+// Same with `fast_math` != 0: every pass uses the 5-point-sum arithmetic (5 fp64
+// operations per cell update instead of 14; rounding-level, not bitwise, equal to
+// the canonical update; the bench default). Both arithmetics run any depth 1..24.
 int rma_executor_create_kf(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
                            int64_t nx, int64_t ny, const double coef[4], int64_t bwx,
                            int64_t bwy, int steps_per_pass, int fast_math, double* qx,
