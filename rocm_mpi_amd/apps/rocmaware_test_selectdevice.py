@@ -21,7 +21,11 @@ import sys
 import torch
 
 
-def run(n: int = 4, transport: str = "auto", verbose: bool = True) -> list[float]:
+def run(n: int = 4, transport: str = "auto", verbose: bool = True,
+        self_ring: bool = False) -> list[float]:
+    """The ring exchange; returns what this rank received. ``self_ring``: with
+    one rank, still send/recv through the transport (RCCL send/recv to itself
+    on one GPU: the device-buffer P2P path without a second GPU)."""
     from ..parallel import comm as C
     from ..parallel.implicit_grid import _choose_transport
 
@@ -47,7 +51,7 @@ def run(n: int = 4, transport: str = "auto", verbose: bool = True) -> list[float
     comm.barrier()
     if rank == 0 and verbose:
         print("start sending...", flush=True)
-    if size == 1:
+    if size == 1 and not self_ring:
         recv.copy_(send)
     else:
         comm.sendrecv(send, dst, recv, src)
@@ -66,11 +70,13 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("-n", type=int, default=4)
     ap.add_argument("--transport", default="auto")
+    ap.add_argument("--self-ring", action="store_true",
+                    help="one rank: send/recv to itself through the transport")
     a = ap.parse_args(argv)
     from ..parallel import comm as C
 
     rank, size, _ = C.env_world()
-    vals = run(a.n, a.transport)
+    vals = run(a.n, a.transport, self_ring=a.self_ring)
     ok = all(v == float((rank - 1) % size) for v in vals)
     return 0 if ok else 1
 

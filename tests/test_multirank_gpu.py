@@ -310,3 +310,14 @@ def test_pass_timing_and_solo_on_loopback_ranks():
         t = ts[0]
         assert t["frame_ms"] > 0 and t["halo_ms"] > 0 and t["interior_ms"] > 0
         assert t["pass_ms"] >= t["interior_ms"] and t["exposed_halo_ms"] >= 0
+
+
+def test_p2p_smoke_test_through_rccl_on_one_gpu(capsys):
+    """rocmaware_test_selectdevice.jl's ring on device buffers, one rank: the
+    4-element buffer goes out and back through RCCL send/recv (to itself)."""
+    from rocm_mpi_amd.apps import rocmaware_test_selectdevice as app
+
+    vals = app.run(4, transport="rccl", verbose=True, self_ring=True)
+    assert vals == [0.0] * 4
+    out = capsys.readouterr().out
+    assert "transport=rccl" in out and "recv_mesg on proc 0: [0.0, 0.0, 0.0, 0.0]" in out
