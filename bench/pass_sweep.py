@@ -44,6 +44,7 @@ def main(argv=None):
     ap.add_argument("--alt", default="12:3,16:8,24:8,8:4,8:1", help="pipe K:stages splits")
     ap.add_argument("--chunk", type=int, default=0, help="rows per task (0: executor default)")
     ap.add_argument("--chunks", default="", help="pipe K:c1/c2/..., extra chunk-row variants")
+    ap.add_argument("--chunksc", default="", help="pipec K:c1/c2/..., chunk-row variants")
     ap.add_argument("--pipe2", default="", help="depths of the 2-column-wave pipe kernel")
     ap.add_argument("--chunks2", default="", help="pipe2 K:c1/c2/..., chunk-row variants")
     ap.add_argument("--out", default="")
@@ -70,8 +71,15 @@ def main(argv=None):
     coef = ops.StencilCoef.from_physics(1.0, dx, dx, dx * dx / 4.1)
     N = native()
 
-    def chunk(K, c=0):
-        return c or a.chunk or N.default_chunk_k(max(K, 3), n)
+    def chunk(K, c=0, kind="pipe"):
+        # the executor's rows per task for this kernel and depth
+        if c or a.chunk:
+            return c or a.chunk
+        if kind in ("pipe", "pipe2", "pipeb"):
+            return N.pipe_chunk_rows(K, n, False) or N.default_chunk_k(max(K, 3), n)
+        if kind == "pipec":
+            return N.pipe_chunk_rows(K, n, True) or N.default_chunk_k(max(K, 3), n)
+        return N.default_chunk_k(max(K, 3), n)
 
     cfgs = [("march", 1, 0)]
     cfgs += [("pipe", K, 0) for K in krange(a.pipe)]
@@ -88,6 +96,10 @@ def main(argv=None):
         K, cs = item.split(":")
         for c in cs.split("/"):
             cfgs.append(("pipe", int(K), 0, int(c)))
+    for item in filter(None, a.chunksc.split(",")):
+        K, cs = item.split(":")
+        for c in cs.split("/"):
+            cfgs.append(("pipec", int(K), 0, int(c)))
     cfgs += [("pipe2", K, 0) for K in krange(a.pipe2)]
     for item in filter(None, a.chunks2.split(",")):
         K, cs = item.split(":")
@@ -103,7 +115,8 @@ def main(argv=None):
             ops.stencil2_step(T2, T, iCp, coef, rect, ops.StencilTuning(chunk_rows=16, unroll=2))
         else:
             vec = 2 if kind in ("lds_dpp", "fast5") else 4
-            tn = ops.StencilTuning(chunk_rows=chunk(K, c), kernel="pipe" if kind == "pipe2" else kind,
+            tn = ops.StencilTuning(chunk_rows=chunk(K, c, kind),
+                                   kernel="pipe" if kind == "pipe2" else kind,
                                    vec=vec, xcd_remap=1, stages=S, cols=2 if kind == "pipe2" else 0)
             ops.stencilk_step(K, T2, T, iCp, coef, rect, tn)
 
@@ -131,7 +144,7 @@ def main(argv=None):
         rows.append({"kernel": kind, "K": K, "stages": S or (native().pipe_default_stages(K)
                                                              if kind in ops.PIPE + ("pipe2",)
                                                              else 0),
-                     "chunk_rows": (chunk(K, c[3] if len(c) > 3 else 0)
+                     "chunk_rows": (chunk(K, c[3] if len(c) > 3 else 0, kind)
                                     if kind not in ("march", "two_step") else None),
                      "ms_per_pass": round(med, 3), "ms_min": round(min(times[c]), 3),
                      "ms_per_step": round(med / K, 4), "rel": round(med / base, 4),

@@ -352,6 +352,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("bytes_sent_last", &HaloExchanger::bytes_sent_last);
 
   // ---------------- executor ----------------
+  m.def("pipe_chunk_rows", &pipe_chunk_rows, py::arg("K"), py::arg("ny"),
+        py::arg("canonical") = false);
   m.def("default_chunk_k", [](int K, int64_t ny) { return default_tune_k(K, ny).chunk_rows; },
         py::arg("K"), py::arg("ny"));
   m.def("plan_passes", &plan_passes, py::arg("nsteps"), py::arg("costs"));

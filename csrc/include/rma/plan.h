@@ -52,6 +52,15 @@ std::vector<double> default_pass_costs(int kmax, bool fast5, double cells = 0);
 // RMA_PASS_COSTS="K:cost,K:cost,..." overrides entries (sweeps, tests).
 void apply_cost_overrides(std::vector<double>& cost, const char* spec);
 
+// Rows per (strip, chunk) task of the pipelined K-step kernels (stencil_pipe.h)
+// on a tile of ny rows, fast5 or canonical arithmetic: a chunk recomputes
+// ~2K+S rows of overlap, so short chunks waste work on the deep passes while
+// long ones leave small tiles with too few blocks. Measured best per tile
+// class and depth (profiles/chunk_sweep_r2.json, bench/pass_sweep.py
+// --chunks): 4096^2 K=24 192 rows (-38 % vs r1's 32), 8192^2 256 (-23 %),
+// 16384^2 512 (-7 %); 0 = no table entry (the one-step kernels' rule).
+int pipe_chunk_rows(int K, int64_t ny, bool canonical);
+
 // Decompose n steps into passes of 1..Kmax steps minimising the summed cost
 // (dynamic programme; ties -> fewer passes). Returned deepest first. E.g. the
 // driver's 20 timed steps: one 20-step pass (~73 ms at the 288 GB tile)

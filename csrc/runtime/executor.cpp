@@ -58,6 +58,7 @@ StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c) {
   if (!fast5_ok(c)) return canonical_tune_k(K, ny);
   t.kernel = 9;  // stage-pipelined fast5, any K (stencil_pipe.h)
   t.vec = 4;
+  if (const int ch = pipe_chunk_rows(K, ny, false)) t.chunk_rows = ch;
   return t;
 }
 
@@ -69,6 +70,7 @@ StencilTuning canonical_tune_k(int K, int64_t ny) {
   if (K >= 5) {
     t.kernel = 10;
     t.vec = 4;
+    if (const int ch = pipe_chunk_rows(K, ny, true)) t.chunk_rows = ch;
   }
   return t;
 }

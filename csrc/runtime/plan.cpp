@@ -61,30 +61,49 @@ constexpr double kInf = std::numeric_limits<double>::infinity();
 // two-step kernel, 3/4 kernel 3, K >= 5 the canonical pipelined kernel.
 // On the 288 GB tile a pass costs at least the sweep plus the strip-overlap
 // reads up to K~12 and the fp64 arithmetic beyond; on smaller tiles the
-// deeper passes fill the chip worse (best depth per step: 4096^2 and 8192^2
-// 12, 16384^2 24 (16 within 2 %), 101376^2 24).
+// deeper passes fill the chip worse. With the per-tile chunk table
+// (pipe_chunk_rows) K=24 has the lowest time per step at every class
+// (0.084-0.109 one-step units); canonical: K=12 (K=20 at 101376^2), and
+// K >= 21 canonical passes drop to one wave per SIMD (188 ms at 101376^2).
 constexpr int kTables = 4;
 constexpr double kTileCells[kTables] = {4096.0 * 4096, 8192.0 * 8192, 16384.0 * 16384,
                                         101376.0 * 101376};
 constexpr double kFast5[kTables][25] = {
-    {0, 1.104, 1.089, 1.099, 1.143, 1.174, 1.185, 1.272, 1.311, 1.502, 1.551, 1.625, 1.684,
-     1.949, 2.042, 2.405, 2.529, 3.357, 3.447, 3.593, 3.591, 4.124, 4.266, 4.393, 4.477},
-    {0, 1.462, 1.551, 1.591, 1.497, 1.493, 1.499, 1.494, 1.383, 1.443, 1.480, 1.540, 1.507,
-     1.654, 1.760, 1.900, 2.036, 2.769, 2.823, 2.793, 2.746, 3.115, 3.161, 3.235, 3.281},
-    {0, 1.379, 1.440, 1.417, 1.310, 1.356, 1.341, 1.336, 1.223, 1.282, 1.237, 1.254, 1.272,
-     1.418, 1.406, 1.502, 1.522, 1.974, 1.877, 1.897, 1.923, 2.230, 2.221, 2.283, 2.236},
-    {0, 1.234, 1.230, 1.214, 1.161, 1.232, 1.210, 1.198, 1.126, 1.152, 1.200, 1.227, 1.239,
-     1.335, 1.367, 1.445, 1.473, 1.753, 1.764, 1.827, 1.824, 1.989, 2.028, 2.085, 2.099}};
+    {0, 1.087, 1.056, 1.102, 1.123, 1.173, 1.169, 1.207, 1.228, 1.579, 1.404, 1.355, 1.379,
+     1.598, 1.638, 1.745, 1.811, 2.143, 2.208, 2.275, 2.288, 2.553, 2.575, 2.617, 2.607},
+    {0, 1.530, 1.519, 1.452, 1.377, 1.487, 1.432, 1.473, 1.334, 1.823, 1.414, 1.422, 1.391,
+     1.488, 1.529, 1.745, 1.782, 2.286, 2.295, 2.308, 2.255, 2.390, 2.419, 2.434, 2.450},
+    {0, 1.373, 1.375, 1.412, 1.298, 1.282, 1.275, 1.273, 1.217, 1.414, 1.326, 1.328, 1.294,
+     1.410, 1.440, 1.605, 1.575, 1.966, 1.952, 1.974, 1.969, 2.101, 2.119, 2.168, 2.203},
+    {0, 1.235, 1.230, 1.215, 1.163, 1.232, 1.210, 1.199, 1.126, 1.149, 1.185, 1.210, 1.203,
+     1.298, 1.323, 1.385, 1.409, 1.680, 1.703, 1.769, 1.768, 1.908, 1.944, 2.003, 2.013}};
 constexpr double kCanon[kTables][25] = {
-    {0, 1.000, 1.060, 1.090, 1.258, 1.359, 1.402, 1.841, 1.946, 2.296, 2.582, 2.696, 2.837,
-     3.355, 3.873, 4.391, 4.909, 5.344, 5.779, 6.213, 6.648, 7.083, 7.518, 7.952, 8.387},
-    {0, 1.000, 1.105, 1.412, 1.374, 1.464, 1.480, 1.552, 1.663, 1.958, 2.287, 2.362, 2.462,
-     2.827, 3.192, 3.557, 3.922, 4.201, 4.480, 4.759, 5.038, 5.317, 5.596, 5.875, 6.154},
-    {0, 1.000, 1.080, 1.284, 1.218, 1.338, 1.337, 1.361, 1.477, 1.753, 1.874, 1.885, 2.016,
-     2.230, 2.444, 2.658, 2.872, 3.011, 3.150, 3.289, 3.428, 3.566, 3.705, 3.844, 3.983},
-    {0, 1.000, 1.080, 1.143, 1.068, 1.208, 1.200, 1.401, 1.431, 1.650, 1.808, 1.882, 1.927,
-     2.110, 2.293, 2.476, 2.659, 2.820, 2.981, 3.142, 3.303, 3.465, 3.626, 3.787, 3.948}};
+    {0, 1.000, 1.058, 1.095, 1.246, 1.335, 1.326, 1.757, 1.897, 2.226, 2.214, 2.295, 2.384,
+     3.189, 3.233, 3.308, 3.355, 4.007, 4.073, 4.101, 4.158, 6.194, 6.136, 6.273, 6.421},
+    {0, 1.000, 1.107, 1.406, 1.375, 1.462, 1.476, 1.646, 1.596, 1.830, 1.959, 2.005, 2.095,
+     2.944, 3.023, 3.038, 3.010, 3.566, 3.589, 3.593, 3.659, 5.558, 5.537, 5.664, 5.745},
+    {0, 1.000, 1.124, 1.382, 1.302, 1.444, 1.436, 1.451, 1.455, 1.733, 1.867, 1.889, 1.970,
+     2.784, 2.772, 2.798, 2.857, 3.333, 3.319, 3.364, 3.467, 5.660, 5.443, 5.489, 5.591},
+    {0, 1.000, 1.079, 1.146, 1.067, 1.212, 1.178, 1.362, 1.398, 1.597, 1.755, 1.833, 1.885,
+     2.306, 2.383, 2.491, 2.533, 2.863, 2.947, 3.079, 3.131, 4.643, 4.586, 4.713, 4.770}};
 }  // namespace
+
+int pipe_chunk_rows(int K, int64_t ny, bool canonical) {
+  if (ny < 3072) return 0;
+  if (ny < 6144) {  // 4096^2 class
+    if (canonical) return K <= 12 ? 64 : 192;
+    return K <= 4 ? 32 : K <= 9 ? 64 : K <= 16 ? 128 : 192;
+  }
+  if (ny < 12288) {  // 8192^2
+    if (canonical) return K <= 12 ? 128 : 256;
+    return K <= 9 ? 256 : K <= 16 ? 128 : 256;
+  }
+  if (ny < 24576) {  // 16384^2
+    if (canonical) return K <= 9 ? 256 : K <= 12 ? 512 : 384;
+    return K <= 4 ? 768 : K <= 9 ? 1536 : 512;
+  }
+  return 0;  // 32768^2 .. 101376^2: the r1 table is within 1-2 % of the best
+}
 
 std::vector<double> default_pass_costs(int kmax, bool fast5, double cells) {
   RMA_CHECK_ARG(kmax >= 1 && kmax <= 24, "kmax=" << kmax << " (tables cover 1..24)");

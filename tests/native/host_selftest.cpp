@@ -303,8 +303,12 @@ int main() {
     EXPECT(default_pass_costs(24, true, 64.0 * 64.0) ==
            default_pass_costs(24, true, 4096.0 * 4096.0));  // below the smallest class
     EXPECT(default_pass_costs(24, true, 2e11) == cf);       // above the largest
-    EXPECT(plan_passes(20, default_pass_costs(24, true, 4096.0 * 4096.0)) ==
-           (std::vector<int>{12, 8}));
+    {  // a cheaper table entry changes the plan of that class only
+      auto c4 = default_pass_costs(24, true, 4096.0 * 4096.0);
+      c4[10] = 0.01;
+      EXPECT(plan_passes(20, c4) == (std::vector<int>{10, 10}));
+      EXPECT(plan_passes(20, cf) == std::vector<int>{20});
+    }
     EXPECT(default_pass_costs(12, false, 16384.0 * 16384.0).size() == 13);
     EXPECT(throws([&] { default_pass_costs(25, true); }));
     EXPECT(throws([&] { default_pass_costs(0, true); }));

@@ -26,7 +26,7 @@ def test_bench_small_tile_with_self_rccl_halo_check():
               "--check", "1", "--check-self-rccl", "--check-nx", "1026")
     c = d["config"]
     assert d["n_gpus"] == 1 and c["ranks"] == 1
-    # the planner's choice for this tile class (4096^2: 12 + 8 beats one 20-step pass)
+    # the planner's choice for this tile class (its own cost table)
     from rocm_mpi_amd._native import native
     costs = native().default_pass_costs(24, True, 4096.0 * 4096.0)
     plan = list(native().plan_passes(20, costs))

@@ -306,7 +306,7 @@ def test_pass_timing_and_solo_on_loopback_ranks():
 
     res = run_loopback(2, body, timeout=120)
     for ts, plan in res:
-        assert [t["K"] for t in ts] == plan and sum(plan) == 20  # K <= 16: [12, 8]
+        assert [t["K"] for t in ts] == plan and sum(plan) == 20  # the plan of this tile class
         t = ts[0]
         assert t["frame_ms"] > 0 and t["halo_ms"] > 0 and t["interior_ms"] > 0
         assert t["pass_ms"] >= t["interior_ms"] and t["exposed_halo_ms"] >= 0
