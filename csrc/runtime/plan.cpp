@@ -98,9 +98,13 @@ int pipe_chunk_rows(int K, int64_t ny, bool canonical) {
     if (canonical) return K <= 12 ? 128 : 256;
     return K <= 9 ? 256 : K <= 16 ? 128 : 256;
   }
-  if (ny < 24576) {  // 16384^2
+  if (ny < 24576) {  // 16384^2 (12288^2: K=24 c512 within 2 % of the best)
     if (canonical) return K <= 9 ? 256 : K <= 12 ? 512 : 384;
     return K <= 4 ? 768 : K <= 9 ? 1536 : 512;
+  }
+  if (ny < 32768) {  // 24576^2: K=24 c768 5.07 vs 5.47 ms (the old c256)
+    if (K <= 9) return 0;
+    return canonical ? 512 : 768;
   }
   return 0;  // 32768^2 .. 101376^2: the r1 table is within 1-2 % of the best
 }
