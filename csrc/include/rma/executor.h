@@ -122,7 +122,9 @@ class DiffusionExecutor {
  private:
   void enqueue_step(double* Tin, double* Tout);
   void enqueue_pass(int K, double* Tin, double* Tout);  // one K-step pass (K >= 2 or fast5)
-  StencilTuning pass_tuning(int K, bool frame) const;
+  // kernel tuning of a K-step launch: part 0 = the interior / whole tile,
+  // 1 = wide (y) frame strips, 2 = tall (x) frame strips
+  StencilTuning pass_tuning(int K, int part = 0) const;
   const PassGeom& geometry(int K);
   void multi_step(int K, double* Tin, double* Tout, const double* iCp, int64_t nx, int64_t ny,
                   const Rect* rects, int n, const StencilTuning& tn, void* stream) const;

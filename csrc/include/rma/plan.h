@@ -31,6 +31,9 @@ struct PassGeom {
   Rect out{};                // cells the pass writes
   std::vector<Rect> frame;   // perf_hide: computed first (high-priority stream)
   Rect interior{};           // perf_hide: the rest (low-priority stream)
+  // the frame split by shape: wide (y-frames: full width, ~ol rows) and tall
+  // (x-frames: ~ol columns, full height) strips run with different tunings
+  std::vector<Rect> frame_wide, frame_tall;
 };
 
 // Geometry of one pass. hide: split into frame + interior so that the frame

@@ -212,19 +212,26 @@ std::vector<int> DiffusionExecutor::plan(int64_t nsteps) const {
   return plan_passes(nsteps, cost_);
 }
 
-StencilTuning DiffusionExecutor::pass_tuning(int K, bool frame) const {
+StencilTuning DiffusionExecutor::pass_tuning(int K, int part) const {
   StencilTuning t = fast5() ? fast_tune_k(K, ny_, p_.coef) : canonical_tune_k(K, ny_);
   t.nontemporal = p_.tune2.nontemporal;
   if (p_.chunk_rows2 > 0) t.chunk_rows = p_.chunk_rows2;
   if (K == 2 && !fast5()) t.unroll = p_.tune2.unroll;
-  if (frame) {
-    // the x-frames are ~2K columns wide: the narrowest strip (2 cells per
-    // lane) wastes the least recomputation, short chunks keep the launch
-    // small; the frame ends long before the interior (1.6 of ~64 ms per pass
-    // at the 288 GB tile)
-    t.chunk_rows = std::min(t.chunk_rows, 64);
-    if (t.kernel >= 6) t.vec = std::min(t.vec, 2);
+  if (part == 0) return t;
+  if (t.kernel >= 9 && part == 1) {
+    // pipelined passes, wide y-frames (~2K rows, full width): the interior's
+    // 4 cells per lane (1.23x column recompute instead of 1.6x at 2 cells).
+    // RCCL-self halo overhead at 16384^2, K=24: 8.7 -> 6.6 % per step; the
+    // tall x-frames keep 2 cells per lane and 64-row chunks (longer chunks:
+    // no gain at 16384^2, +0.2-0.3 % at the 288 GB tile, where each long
+    // frame block holds CU slots for the interior's whole block time;
+    // profiles/frame_tuning_r2.json)
+    return t;
   }
+  // tall x-frames, and every frame of the fixed-depth kernels (K <= 4
+  // canonical): the narrowest strip and short chunks
+  t.chunk_rows = std::min(t.chunk_rows, 64);
+  if (t.kernel >= 6) t.vec = std::min(t.vec, 2);
   return t;
 }
 
@@ -316,7 +323,7 @@ void DiffusionExecutor::multi_step(int K, double* Tin, double* Tout, const doubl
 
 void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   const PassGeom& g = geometry(K);
-  const StencilTuning tn = pass_tuning(K, false);
+  const StencilTuning tn = pass_tuning(K, 0);
   // timing events of this pass (nullptr when off)
   void* ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   if (timing_) {
@@ -344,8 +351,12 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   rec(0, s_hi_);
   if (!g.frame.empty()) {
     TraceRange tb("rma.boundary");
-    multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame.data(), (int)g.frame.size(),
-               pass_tuning(K, true), s_hi_);
+    if (!g.frame_wide.empty())
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_wide.data(), (int)g.frame_wide.size(),
+                 pass_tuning(K, 1), s_hi_);
+    if (!g.frame_tall.empty())
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_tall.data(), (int)g.frame_tall.size(),
+                 pass_tuning(K, 2), s_hi_);
   }
   rec(1, s_hi_);
   {
@@ -443,9 +454,10 @@ void DiffusionExecutor::prime() {
         stencil_rects_gpu(b, a, ic, tnx, tny, &r, 1, p_.coef, p_.tune, s_lo_);
         continue;
       }
-      multi_step(K, a, b, ic, tnx, tny, &r, 1, pass_tuning(K, false), s_lo_);
+      multi_step(K, a, b, ic, tnx, tny, &r, 1, pass_tuning(K, 0), s_lo_);
       if (p_.mode == Mode::kHide)
-        multi_step(K, a, b, ic, tnx, tny, &r, 1, pass_tuning(K, true), s_lo_);
+        for (int part = 1; part <= 2; ++part)
+          multi_step(K, a, b, ic, tnx, tny, &r, 1, pass_tuning(K, part), s_lo_);
     }
     RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
   } catch (...) {

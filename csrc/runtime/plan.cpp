@@ -43,6 +43,8 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
   if (hide && any_nbr) {
     split_rect(g.out, std::max(bwx, olx - g.out.x0), std::max(bwy, oly - g.out.y0), g.frame,
                g.interior);
+    for (const Rect& r : g.frame)
+      (r.x1 - r.x0 >= r.y1 - r.y0 ? g.frame_wide : g.frame_tall).push_back(r);
   } else {
     g.interior = g.out;
   }

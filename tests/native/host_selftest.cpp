@@ -272,6 +272,18 @@ int main() {
           EXPECT(q.x0 >= pg.out.x0 && q.x1 <= pg.out.x1 && q.y0 >= pg.out.y0 && q.y1 <= pg.out.y1);
         }
         EXPECT(c2 == pg.out.cells());
+        // the shape split partitions the frame: wide strips are not taller than wide
+        EXPECT(pg.frame_wide.size() + pg.frame_tall.size() == pg.frame.size());
+        int64_t c3 = 0;
+        for (auto& q : pg.frame_wide) {
+          c3 += q.cells();
+          EXPECT(q.x1 - q.x0 >= q.y1 - q.y0);
+        }
+        for (auto& q : pg.frame_tall) {
+          c3 += q.cells();
+          EXPECT(q.x1 - q.x0 < q.y1 - q.y0);
+        }
+        EXPECT(c3 + pg.interior.cells() == pg.out.cells());
         if (nb != &none && !pg.frame.empty()) {  // the frame holds the send planes [ol-hw, ol)
           EXPECT(pg.interior.empty() || (pg.interior.x0 >= 48 && pg.interior.y0 >= 48));
         }
