@@ -14,7 +14,6 @@ from __future__ import annotations
 import argparse
 import collections
 import json
-import math
 import sys
 
 # one-step march kernel time per cell on MI355X (24 B/cell at ~6.2 TB/s):
@@ -23,6 +22,7 @@ _MS_PER_CELL = 39.6 / (101376.0 * 101376.0)
 
 
 def describe(nx: int, ny: int, steps: int, temporal: int = 24, fast_math: bool = True) -> dict:
+    from .. import ops
     from .._native import native
 
     N = native()
@@ -31,7 +31,7 @@ def describe(nx: int, ny: int, steps: int, temporal: int = 24, fast_math: bool =
     plan = list(N.plan_passes(int(steps), costs))
     unit_ms = _MS_PER_CELL * cells
     kernels = {}
-    names = {v: k for k, v in __import__("rocm_mpi_amd.ops", fromlist=["KERNELS"]).KERNELS.items()}
+    names = {v: k for k, v in ops.KERNELS.items()}
     for K in sorted(set(plan)):
         if fast_math:
             kern, vec, ch = N.fast_kernel_k(K, ny, (-1.0, 1.0, 1.0, 0.1))
