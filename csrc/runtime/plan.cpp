@@ -41,8 +41,15 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
   g.out = K == 1 ? Rect{1, nx - 1, 1, ny - 1} : owned_rect(nx, ny, K, nbr);
   const bool any_nbr = nbr[0][0] >= 0 || nbr[0][1] >= 0 || nbr[1][0] >= 0 || nbr[1][1] >= 0;
   if (hide && any_nbr) {
-    split_rect(g.out, std::max(bwx, olx - g.out.x0), std::max(bwy, oly - g.out.y0), g.frame,
-               g.interior);
+    int64_t fx = std::max(bwx, olx - g.out.x0);
+    // the tall x-frames of a pipelined pass (K >= 5) run in 128-column strips
+    // (2 cells per lane) that output 128 - 2K columns whatever the frame
+    // width: widen the frame to that capacity, so those columns leave the
+    // interior instead of being computed twice (RMA_FRAME_FILL=0: off)
+    static const char* ff = std::getenv("RMA_FRAME_FILL");
+    if (K >= 5 && !(ff && ff[0] == '0'))
+      fx = std::max<int64_t>(fx, std::min<int64_t>(128 - 2 * K, (g.out.x1 - g.out.x0) / 4));
+    split_rect(g.out, fx, std::max(bwy, oly - g.out.y0), g.frame, g.interior);
     for (const Rect& r : g.frame)
       (r.x1 - r.x0 >= r.y1 - r.y0 ? g.frame_wide : g.frame_tall).push_back(r);
   } else {
