@@ -97,6 +97,10 @@ def parse(argv=None):
                     help="local tile of the halo check (0: 2050 on GPU, 130 on CPU)")
     ap.add_argument("--check-self-rccl", action="store_true",
                     help="one rank: run the halo check periodic with RCCL send/recv to self")
+    ap.add_argument("--shared-gpu-test", action="store_true",
+                    help="functional test of the multi-process path on ONE GPU: ranks share "
+                         "the card over the host-staged transport; the record says so and is "
+                         "never a scaling point")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the same driver on the C++ CPU twins over gloo (tests of the "
@@ -257,7 +261,10 @@ def main(argv=None) -> int:
         return fail(f"--temporal must be 1..24, got {a.temporal}", rank)
 
     gpu = a.device == "cuda"
-    if gpu and world > 1:
+    shared = a.shared_gpu_test and gpu and world > 1
+    if shared:
+        os.environ["RMA_TRANSPORT"] = "staged"
+    elif gpu and world > 1:
         # a scaling point must never silently run on the host-staged transport
         os.environ["RMA_RCCL_STRICT"] = "1"
         os.environ["RMA_TRANSPORT"] = "rccl"
@@ -272,7 +279,7 @@ def main(argv=None) -> int:
     if not gpu and not a.nx:
         return fail("--device cpu needs --nx", rank)
     if world > 1:
-        C.init_distributed(None if gpu else "gloo")
+        C.init_distributed(None if gpu and not shared else "gloo")
     local, _ = C.node_local_rank(rank, world)
     dev = str(C.select_device(local)) if gpu else "cpu"
 
@@ -286,7 +293,7 @@ def main(argv=None) -> int:
         bus = f"cpu-rank-{rank}"
     buses = gather_obj(bus, world)
     n_gpus = len(set(buses)) if gpu else world
-    if gpu and n_gpus != world:
+    if gpu and n_gpus != world and not shared:
         return fail(f"{world} ranks share {n_gpus} physical GPU(s) (PCI bus ids {buses}); "
                     "a scaling point needs one GPU per rank", rank)
 
@@ -318,7 +325,7 @@ def main(argv=None) -> int:
     model = Diffusion2D(cfg, grid_kwargs=gkw)
     g = model.g
     comm = g.comm
-    if gpu and world > 1 and g.transport != "rccl":
+    if gpu and world > 1 and g.transport != "rccl" and not shared:
         return fail(f"halo transport is {g.transport!r}, a multi-GPU point needs RCCL", rank)
     model.synchronize()
     comm.barrier()
@@ -434,8 +441,10 @@ def main(argv=None) -> int:
                                   "overlapped with the interior" if a.variant == "perf_hide"
                                   else ", exchange after each pass")
     eff_same = (solo / t_it) if solo else None
+    if shared:
+        par = f"SHARED-GPU FUNCTIONAL TEST, {world} ranks on {n_gpus} GPU, not a scaling point; {par}"
     out = {
-        "metric": METRIC,
+        "metric": METRIC + (" [shared-GPU functional test]" if shared else ""),
         "value": round(total, 2),
         "unit": "GB/s",
         "n_gpus": n_gpus,
@@ -490,6 +499,7 @@ def main(argv=None) -> int:
             "hipgraph": bool(a.graph),
             "setup_s": round(setup_s, 3),
             "nonfinite_cells_sampled": int(bad),
+            "shared_gpu_test": bool(shared),
         },
     }
     if rank == 0:

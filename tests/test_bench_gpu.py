@@ -43,3 +43,17 @@ def test_bench_small_tile_with_self_rccl_halo_check():
     assert c["teff_single_step_kernel_GBps"] > 0 and c["teff_bitwise_kstep_GBps"] > 0
     assert c["pci_bus_ids"] and len(c["pci_bus_ids"]) == 1
     assert c["nonfinite_cells_sampled"] == 0
+
+
+def test_bench_two_processes_sharing_the_gpu(tmp_path):
+    """The multi-process bench flow on one GPU (torchrun-style ranks, staged
+    halo transport, per-rank timings, solo re-time, in-run halo check): a
+    functional test, labelled so it can never pass for a scaling point."""
+    d = bench("--gpus", "2", "--shared-gpu-test", "--nx", "4096", "--steps", "24", "--warmup", "5",
+              "--single-step-steps", "4", "--check-nx", "530", timeout=600)
+    c = d["config"]
+    assert c["shared_gpu_test"] is True and "shared-GPU" in d["metric"]
+    assert c["ranks"] == 2 and d["n_gpus"] == 1 and c["transport"] == "staged"
+    assert c["rccl_halo_bitwise_ok"] is True and c["halo_check"]["tiles_mismatched"] == 0
+    assert c["pass_timing"]["passes"] == len(c["passes_timed"]) and sum(c["passes_timed"]) == 24
+    assert len(c["pci_bus_ids"]) == 2 and c["nonfinite_cells_sampled"] == 0
