@@ -34,14 +34,25 @@ struct PassGeom {
   // the frame split by shape: wide (y-frames: full width, ~ol rows) and tall
   // (x-frames: ~ol columns, full height) strips run with different tunings
   std::vector<Rect> frame_wide, frame_tall;
+  // aligned: the frame is whole (strip, chunk) tasks of the interior's own
+  // task grid (task_w x task_h given), so frame + interior do the work of ONE
+  // launch; frame launches then use the interior tuning
+  bool aligned = false;
 };
 
 // Geometry of one pass. hide: split into frame + interior so that the frame
 // holds the send planes [ol-hw, ol) of every side (width >= ol - out.x0, the
 // reference's b_width >= overlap invariant); without any
 // neighbour there is nothing to overlap and the owned rect is one launch.
+// task_w / task_h > 0 (pipelined passes): output columns per strip and rows
+// per chunk of the interior launch (strips start at x0 - K rounded down to
+// `vec` cells, stencil_device.h plan_strip_tasks); the frame is then its
+// first / last strip column and chunk row (a few % of the tile) instead of
+// ol-wide strips, which a trapezoid kernel computes at several times the
+// interior's cost per cell.
 PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool hide,
-                       int64_t bwx, int64_t bwy, int64_t olx, int64_t oly);
+                       int64_t bwx, int64_t bwy, int64_t olx, int64_t oly, int64_t task_w = 0,
+                       int64_t task_h = 0, int vec = 1);
 
 // Relative cost of one pass of K steps (index K = 1..Kmax; index 0 unused;
 // +inf = no kernel), in units of one HBM sweep of the 3 arrays. Measured on

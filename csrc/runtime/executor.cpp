@@ -200,8 +200,15 @@ bool DiffusionExecutor::fast5() const {
 const PassGeom& DiffusionExecutor::geometry(int K) {
   RMA_CHECK_ARG(K >= 1 && K < (int)geom_.size(), "pass depth " << K);
   if (!geom_ok_[K]) {
+    // pipelined passes: the frame is whole tasks of the interior's grid
+    const StencilTuning t = pass_tuning(K, 0);
+    int64_t tw = 0, th = 0;
+    if (t.kernel >= 9) {
+      tw = (64 * t.vec - 2 * K) / t.vec * t.vec;
+      th = t.chunk_rows;
+    }
     geom_[K] = pass_geometry(nx_, ny_, K, nbr_, p_.mode == Mode::kHide, p_.bwx, p_.bwy, p_.olx,
-                             p_.oly);
+                             p_.oly, tw, th, t.vec);
     geom_ok_[K] = 1;
   }
   return geom_[K];
@@ -351,12 +358,16 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   rec(0, s_hi_);
   if (!g.frame.empty()) {
     TraceRange tb("rma.boundary");
-    if (!g.frame_wide.empty())
-      multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_wide.data(), (int)g.frame_wide.size(),
-                 pass_tuning(K, 1), s_hi_);
-    if (!g.frame_tall.empty())
-      multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_tall.data(), (int)g.frame_tall.size(),
-                 pass_tuning(K, 2), s_hi_);
+    if (g.aligned) {  // whole tasks of the interior grid: one launch, its tuning
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame.data(), (int)g.frame.size(), tn, s_hi_);
+    } else {
+      if (!g.frame_wide.empty())
+        multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_wide.data(), (int)g.frame_wide.size(),
+                   pass_tuning(K, 1), s_hi_);
+      if (!g.frame_tall.empty())
+        multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_tall.data(), (int)g.frame_tall.size(),
+                   pass_tuning(K, 2), s_hi_);
+    }
   }
   rec(1, s_hi_);
   {

@@ -36,10 +36,44 @@ Rect owned_rect(int64_t nx, int64_t ny, int K, const Neighbors& nbr) {
 }
 
 PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool hide,
-                       int64_t bwx, int64_t bwy, int64_t olx, int64_t oly) {
+                       int64_t bwx, int64_t bwy, int64_t olx, int64_t oly, int64_t task_w,
+                       int64_t task_h, int vec) {
   PassGeom g;
   g.out = K == 1 ? Rect{1, nx - 1, 1, ny - 1} : owned_rect(nx, ny, K, nbr);
   const bool any_nbr = nbr[0][0] >= 0 || nbr[0][1] >= 0 || nbr[1][0] >= 0 || nbr[1][1] >= 0;
+  const Rect& o = g.out;
+  const int64_t need_x = std::max(bwx, olx - o.x0), need_y = std::max(bwy, oly - o.y0);
+  // RMA_FRAME_ALIGNED=0 / 1 forces the choice; by default aligned frames are
+  // used up to 1024-row chunks. Measured RCCL-self halo overhead per step at
+  // K=24 (profiles/frame_aligned_r2.json): 16384^2 5.7 -> 0.1 %, 32768^2
+  // 2.3-3.1 -> ~0 %, 65536^2 1.9-2.2 -> 0.1-0.4 %; at the 288 GB tile (3072-row
+  // chunks: ~6 % of the pass in the bands, ahead of the exchange) 1.3-1.5 %
+  // with ol-wide strips vs 1.6-1.9 % aligned, and bands shorter than a chunk
+  // were worse still (3.2-3.8 %).
+  static const char* fa = std::getenv("RMA_FRAME_ALIGNED");
+  const bool want = fa && fa[0] ? fa[0] != '0' : task_h <= 1024;
+  if (want && hide && any_nbr && task_w >= need_x && task_h >= need_y &&
+      o.x1 - o.x0 >= 3 * task_w && o.y1 - o.y0 >= 3 * task_h) {
+    // frame = the interior launch's first / last chunk row (wide bands) and
+    // first / last strip column (tall strips): every frame cell is computed
+    // once, with the same recompute as in one launch of the owned rect
+    g.aligned = true;
+    const int64_t V = std::max(1, vec);
+    auto floor_v = [&](int64_t a) { return a - (((a % V) + V) % V); };
+    // left strip: exactly the first strip of the owned rect's grid
+    const int64_t xl = floor_v(o.x0 - K) + K + task_w;
+    // right strip: starts where a strip's origin (start - K) is V-aligned and
+    // its output still reaches x1
+    int64_t xr = o.x1 - task_w;
+    xr += ((V - ((xr - K) % V + V) % V) % V);
+    g.frame_wide = {{o.x0, o.x1, o.y0, o.y0 + task_h}, {o.x0, o.x1, o.y1 - task_h, o.y1}};
+    g.frame_tall = {{o.x0, xl, o.y0 + task_h, o.y1 - task_h},
+                    {xr, o.x1, o.y0 + task_h, o.y1 - task_h}};
+    g.frame = g.frame_wide;
+    g.frame.insert(g.frame.end(), g.frame_tall.begin(), g.frame_tall.end());
+    g.interior = {xl, xr, o.y0 + task_h, o.y1 - task_h};
+    return g;
+  }
   if (hide && any_nbr) {
     int64_t fx = std::max(bwx, olx - g.out.x0);
     // the tall x-frames of a pipelined pass (K >= 5) run in 128-column strips

@@ -263,9 +263,25 @@ int main() {
     EXPECT(o.x0 == 1 && o.x1 == 99 && o.y0 == 1 && o.y1 == 59);
     EXPECT(throws([&] { owned_rect(20, 60, 10, all); }));  // minimal tile: nothing owned
     for (int K = 1; K <= 24; ++K) {
-      for (const Neighbors* nb : {&none, &all, &self}) {
-        const int64_t n0 = 2 * (2 * 24) + 8;  // overlap 2*24 on a small tile
-        PassGeom pg = pass_geometry(n0, n0 + 3, K, *nb, true, 1, 1, 48, 48);
+      for (const Neighbors* nb : {&none, &all, &self})
+        for (int variant = 0; variant < 3; ++variant) {
+        // variant 0: ol-wide frame strips on a small tile; 1, 2: frames of
+        // whole pipelined tasks (aligned) on tiles large enough for them
+        const int64_t n0 = variant == 0 ? 2 * (2 * 24) + 8 : 2000 + 17 * variant;
+        const int vec = variant == 2 ? 2 : 4;
+        const int64_t tw = (64 * vec - 2 * K) / vec * vec, th = 64 * variant;
+        PassGeom pg = pass_geometry(n0, n0 + 3, K, *nb, true, 1, 1, 48, 48,
+                                    variant ? tw : 0, variant ? th : 0, vec);
+        if (variant && nb != &none && K >= 1) {
+          EXPECT(pg.aligned == (tw >= 48 - pg.out.x0 && th >= 48 - pg.out.y0));
+        }
+        if (pg.aligned) {  // every frame strip is one strip column of the grid
+          for (auto& q : pg.frame_tall) {
+            const int64_t xa = (q.x0 - K) - ((((q.x0 - K) % vec) + vec) % vec);
+            EXPECT(q.x1 <= xa + K + tw && q.x1 > q.x0);
+          }
+          EXPECT(((pg.interior.x0 - K) % vec + vec) % vec == 0);
+        }
         int64_t c2 = pg.interior.cells();
         for (auto& q : pg.frame) {
           c2 += q.cells();
@@ -287,7 +303,7 @@ int main() {
         if (nb != &none && !pg.frame.empty()) {  // the frame holds the send planes [ol-hw, ol)
           EXPECT(pg.interior.empty() || (pg.interior.x0 >= 48 && pg.interior.y0 >= 48));
         }
-      }
+        }
     }
   }
   // pass planner
