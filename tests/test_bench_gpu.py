@@ -13,8 +13,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def bench(*args, timeout=300):
+    from helpers import free_port
+
+    env = dict(os.environ, MASTER_PORT=str(free_port()))  # multi-rank runs self-launch
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
-                       capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+                       capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
