@@ -62,3 +62,21 @@ def test_plan_app_predicts_the_measured_headline(capsys):
     assert sum(K * n for K, n in c["passes"].items()) == 45
     assert app.main(["--nx", "8192", "--steps", "100"]) == 0
     assert '"pred_teff_GBps"' in capsys.readouterr().out
+
+
+def test_pipe_chunk_rows_by_tile_class():
+    """Rows per task of the pipelined passes (csrc/runtime/plan.cpp), the
+    measured best per tile class (profiles/chunk_sweep_r2.json)."""
+    nat = pytest.importorskip("rocm_mpi_amd._native")
+    try:
+        N = nat.native()
+    except Exception as e:  # noqa: BLE001
+        pytest.skip(f"native core not built: {e}")
+    assert [N.pipe_chunk_rows(24, n) for n in (2048, 4096, 8192, 16384, 24576)] == \
+        [48, 192, 256, 512, 768]
+    assert N.pipe_chunk_rows(24, 101376) == 0 and N.pipe_chunk_rows(4, 512) == 0  # r1 rule
+    assert N.pipe_chunk_rows(12, 4096, True) == 64 and N.pipe_chunk_rows(16, 8192, True) == 256
+    # the executor's tuning uses them (fast and canonical pipelined kernels)
+    coef = (-1.0, 10.0, 10.0, 1e-3)
+    assert N.fast_kernel_k(24, 4096, coef)[2] == 192
+    assert N.canonical_kernel_k(16, 8192)[2] == 256
