@@ -1,19 +1,21 @@
-// Stage-pipelined K-step kernel for ANY K (2..kPipeMaxK), fast5 or canonical
+// Stage-pipelined K-step kernel for ANY K (1..kPipeMaxK), fast5 or canonical
 // arithmetic. Included by the stencil_pipe_*.hip translation units only.
 //
 // One block = one (strip, row-chunk) task; its S waves split the K time levels
 // of the strip: stage s < S-1 owns H = ceil(K/S) levels, the last stage the
 // remaining HL = K - (S-1)H (1 <= HL <= H). Stage 0 streams T and 1/Cp from
-// HBM, writes the per-strip factor ring (R = K+S-1 rows) in LDS and runs its
-// levels; stage s reads its input level from an LDS hand-off row that stage
-// s-1 wrote one row-iteration earlier and runs s(H+1) rows behind stage 0; the
-// last stage stores. One barrier per row iteration.
+// HBM, writes the per-strip factor ring (R = K+S-1 rows, plus H-1 mirrored
+// rows where they cost no occupancy) in LDS and runs its levels; stage s
+// reads its input level from an LDS hand-off row that stage s-1 wrote one
+// row-iteration earlier and runs s(H+1) rows behind stage 0; the last stage
+// stores. One barrier per row iteration. Measured: profiles/SUMMARY_r2.md,
+// profiles/pmc_pipe_r2.md (what was tried and not kept is listed there).
 //
 // Generalises kernels 6-8 of stencil_tbk.hip (fixed K in {8,12,16}, H = K/S)
 // so that the executor's pass planner (executor.cpp plan_passes) can run a
 // pass of any depth: e.g. the 20 timed steps of the driver's bench command as
-// ONE 20-step pass instead of 16 + 4 (each pass costs at least one HBM sweep
-// of the 3 arrays, ~41 ms at the 288 GB tile).
+// ONE 20-step pass (~70 ms) instead of 16 + 4 (each pass costs at least one
+// HBM sweep of the 3 arrays, ~40 ms at the 288 GB tile).
 //
 // Arithmetic (template Ar: kArFast5 = 0, kArCanon = 1; kArFast5Perm = 2 is
 // fast5 with the lane moves done by ds_bpermute on the LDS pipe instead of
