@@ -31,7 +31,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide") -> dict:
+def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
+        chunk2: int = 0) -> dict:
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
@@ -43,7 +44,7 @@ def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide") 
                         self_via_transport=periodic)
     m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=n, nt=steps, quiet=True,
                                     init="random", periods=(p, p, 0), temporal=K,
-                                    fast_math=K > 1))
+                                    fast_math=K > 1, chunk2=chunk2))
     m.step(2 * K)
     m.synchronize()
     t0 = time.perf_counter()
@@ -72,6 +73,7 @@ def main(argv=None) -> int:
     ap.add_argument("--K", type=int, default=16)
     ap.add_argument("--steps", type=int, default=320)
     ap.add_argument("--variants", default="perf_hide")
+    ap.add_argument("--chunk2", type=int, default=0, help="rows per task of the K-step passes (0: table)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -84,7 +86,7 @@ def main(argv=None) -> int:
     for variant in a.variants.split(","):
         rows = []
         for periodic in (False, True, False, True):
-            r = run(n, a.K, a.steps, periodic, variant)
+            r = run(n, a.K, a.steps, periodic, variant, a.chunk2)
             r.update({"periodic_rccl_self": periodic,
                       "teff_GBps": 3 * n * n * 8 / 1e9 / (r["ms_per_step"] / 1e3)})
             rows.append(r)
