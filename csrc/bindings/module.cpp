@@ -244,6 +244,20 @@ PYBIND11_MODULE(_C, m) {
     else
       copy2d_cpu(P<void>(dst), dst_ld, P<const void>(src), src_ld, n_o, n_k, elem_bytes);
   });
+  // copies: [(dst, dst_ld, src, src_ld, n_o, n_k)], one element size, one launch
+  m.def("copy2d_batch", [](const std::vector<std::tuple<uintptr_t, int64_t, uintptr_t, int64_t,
+                                                        int64_t, int64_t>>& copies,
+                           int elem_bytes, uintptr_t stream, bool gpu) {
+    std::vector<Copy2d> c;
+    for (const auto& t : copies)
+      c.push_back({P<void>(std::get<0>(t)), std::get<1>(t), P<const void>(std::get<2>(t)),
+                   std::get<3>(t), std::get<4>(t), std::get<5>(t)});
+    if (gpu)
+      copy2d_batch_gpu(c.data(), (int)c.size(), elem_bytes, S(stream));
+    else
+      copy2d_batch_cpu(c.data(), (int)c.size(), elem_bytes);
+  });
+  m.def("copy2d_batch_max", [] { return kCopy2dBatch; });
   m.def("reduce_workspace_doubles", &reduce_workspace_doubles);
   m.def("reduce_gpu", [](uintptr_t A, int64_t n, int op, uintptr_t out, uintptr_t ws,
                          uintptr_t stream) {

@@ -8,9 +8,11 @@
 #include <array>
 #include <cstddef>
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "rma/common.h"
+#include "rma/kernels.h"  // Copy2d (HIP-free)
 
 namespace rma {
 
@@ -74,5 +76,20 @@ struct HaloPlan {
 HaloPlan plan_exchange(const std::vector<HaloField>& fields,
                        const std::array<std::array<int, 2>, 3>& nbr, int self,
                        bool self_via_comm, int dims_mask);
+
+// The plane copies of one phase of a dimension, as (element bytes, copy) in
+// plan order: phase 0 = self copies + packs (before the group; independent:
+// halo planes [0,hw), [n-hw,n) vs send planes [ol-hw,ol), [n-ol,n-ol+hw) with
+// ol >= 2hw), phase 1 = unpacks (after it). slots[i] is buffer slot i.
+std::vector<std::pair<int, Copy2d>> dim_copies(const HaloDimPlan& dp,
+                                               const std::vector<HaloField>& fields,
+                                               const std::vector<void*>& slots, int phase);
+// Batches of <= kCopy2dBatch copies of one element size (one launch each):
+// a single batch for the usual all-fp64 phase.
+struct CopyBatch {
+  int elem_bytes;
+  std::vector<Copy2d> copies;
+};
+std::vector<CopyBatch> batch_copies(const std::vector<std::pair<int, Copy2d>>& q);
 
 }  // namespace rma

@@ -159,6 +159,18 @@ void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int6
                 int64_t n_k, int elem_bytes, stream_t stream);
 void copy2d_cpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int64_t n_o,
                 int64_t n_k, int elem_bytes);
+// Up to kCopy2dBatch independent copies of one element size in ONE launch
+// (the halo engine issues all packs of a dimension, then all its unpacks, as
+// one batch each). Empty copies are skipped.
+constexpr int kCopy2dBatch = 8;
+struct Copy2d {
+  void* dst;
+  int64_t dst_ld;
+  const void* src;
+  int64_t src_ld, n_o, n_k;
+};
+void copy2d_batch_gpu(const Copy2d* copies, int n, int elem_bytes, stream_t stream);
+void copy2d_batch_cpu(const Copy2d* copies, int n, int elem_bytes);
 
 // ---------------------------------------------------------------------------
 // Streaming roofline probes (same-box HBM ceiling for the T_eff comparison):

@@ -166,6 +166,16 @@ void copy2d_cpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int6
     std::memcpy(d + o * dst_ld * elem_bytes, s + o * src_ld * elem_bytes, n_k * elem_bytes);
 }
 
+void copy2d_batch_cpu(const Copy2d* copies, int n, int elem_bytes) {
+  RMA_CHECK_ARG(n >= 0 && n <= kCopy2dBatch, "copy2d batch of " << n);
+  for (int i = 0; i < n; ++i) {
+    const Copy2d& c = copies[i];
+    if (c.n_o <= 0 || c.n_k <= 0) continue;
+    RMA_CHECK_ARG(c.dst_ld >= c.n_k && c.src_ld >= c.n_k, "leading dims smaller than row length");
+    copy2d_cpu(c.dst, c.dst_ld, c.src, c.src_ld, c.n_o, c.n_k, elem_bytes);
+  }
+}
+
 double reduce_cpu(const double* A, int64_t n, int op) {
   double v = (op == kMax) ? -std::numeric_limits<double>::infinity()
                           : (op == kMin ? std::numeric_limits<double>::infinity() : 0.0);

@@ -6,13 +6,15 @@
 //  * init_random: synthetic random temperature field (BASELINE.json north
 //    star), counter-based and keyed by the global cell index so it is
 //    decomposition-invariant.
-//  * copy2d: the pack (K7) / unpack (K8) primitive of update_halo!: a strided
-//    plane <-> contiguous buffer copy; x-planes of a row-major (ny,nx) field
-//    are nx-strided, y-planes are contiguous (sent without packing).
+//  * copy2d: the pack (K7) / unpack (K8) primitive of update_halo!: strided
+//    plane <-> contiguous buffer copies, batched (one launch per halo
+//    dimension for its packs, one for its unpacks); x-planes of a row-major
+//    (ny,nx) field are nx-strided, y-planes are contiguous (sent unpacked).
 //  * reduce: sum / max / min / max|.| / non-finite count for verification and
 //    NaN guards.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "rma/hip_check.h"
@@ -95,29 +97,47 @@ __global__ void fill_scalar_kernel(double* __restrict__ A, int64_t n, double v) 
     A[i] = v;
 }
 
-template <typename E>
-__global__ void copy2d_kernel(E* __restrict__ dst, int64_t dst_ld, const E* __restrict__ src,
-                              int64_t src_ld, int64_t n_o, int64_t n_k) {
-  const int64_t n = n_o * n_k;
-  if (n < (int64_t(1) << 31)) {  // 32-bit index split (a 64-bit division is a long sequence)
-    const unsigned nk = (unsigned)n_k;
-    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n;
-         i += gridDim.x * blockDim.x) {
-      const unsigned o = i / nk, k = i - o * nk;
-      dst[(int64_t)o * dst_ld + k] = src[(int64_t)o * src_ld + k];
-    }
-    return;
-  }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t o = i / n_k, k = i - o * n_k;
-    dst[o * dst_ld + k] = src[o * src_ld + k];
-  }
-}
-
 struct alignas(16) E16 {
   uint64_t a, b;
 };
+
+// Batched strided 2D copy: blockIdx.y selects one of up to kCopy2dBatch copies
+// (all packs, or all unpacks, of one halo dimension in one launch). No
+// per-element index division: narrow rows (an x-plane row is K fp64) map
+// each thread to a fixed (row, column) once and stride over rows; wide rows
+// stride blocks over (row, 256-column chunk) with one scalar division per
+// 256 elements.
+struct Copy2dDev {
+  void* dst;
+  const void* src;
+  int64_t dst_ld, src_ld, n_o, n_k;  // in elements of the launch's E
+};
+struct Copy2dBatchArgs {
+  Copy2dDev c[kCopy2dBatch];
+};
+
+constexpr int kCopyBlock = 256;
+
+template <typename E>
+__global__ __launch_bounds__(kCopyBlock) void copy2d_batch_kernel(Copy2dBatchArgs b) {
+  const Copy2dDev c = b.c[blockIdx.y];
+  E* __restrict__ dst = static_cast<E*>(c.dst);
+  const E* __restrict__ src = static_cast<const E*>(c.src);
+  const unsigned t = threadIdx.x;
+  if (c.n_k * 2 <= kCopyBlock) {
+    const unsigned nk = (unsigned)c.n_k, R = kCopyBlock / nk;
+    if (t >= R * nk) return;
+    const unsigned r0 = t / nk, k = t - r0 * nk;
+    for (int64_t o = (int64_t)blockIdx.x * R + r0; o < c.n_o; o += (int64_t)gridDim.x * R)
+      dst[o * c.dst_ld + k] = src[o * c.src_ld + k];
+  } else {
+    const int64_t cpr = (c.n_k + kCopyBlock - 1) / kCopyBlock;
+    for (int64_t w = blockIdx.x; w < c.n_o * cpr; w += gridDim.x) {
+      const int64_t o = w / cpr, k = (w - o * cpr) * kCopyBlock + t;
+      if (k < c.n_k) dst[o * c.dst_ld + k] = src[o * c.src_ld + k];
+    }
+  }
+}
 
 constexpr int kRedBlock = 256;
 constexpr int kRedMaxBlocks = 1024;
@@ -285,40 +305,56 @@ void fill_gpu(double* A, int64_t n, double value, stream_t stream) {
   RMA_HIP_LAUNCH_CHECK();
 }
 
-void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int64_t n_o,
-                int64_t n_k, int elem_bytes, stream_t stream) {
-  if (n_o <= 0 || n_k <= 0) return;
-  RMA_CHECK_ARG(dst_ld >= n_k && src_ld >= n_k, "leading dims smaller than row length");
-  // 8-byte planes with even rows and 16-B aligned rows move as 16-byte
-  // elements (a width-K halo of fp64: K/2 dwordx4 per row instead of K dwords)
-  if (elem_bytes == 8 && n_k % 2 == 0 && dst_ld % 2 == 0 && src_ld % 2 == 0 &&
-      ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
-    elem_bytes = 16;
-    n_k /= 2;
-    dst_ld /= 2;
-    src_ld /= 2;
+void copy2d_batch_gpu(const Copy2d* copies, int n, int elem_bytes, stream_t stream) {
+  RMA_CHECK_ARG(n >= 0 && n <= kCopy2dBatch, "copy2d batch of " << n << " (max " << kCopy2dBatch << ")");
+  RMA_CHECK_ARG(elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16,
+                "unsupported element size " << elem_bytes);
+  Copy2dBatchArgs a{};
+  int m = 0;
+  // 8-byte planes whose rows are even and 16-B aligned move as 16-byte
+  // elements (a width-K halo of fp64: K/2 dwordx4 per row instead of K)
+  bool wide = elem_bytes == 8;
+  for (int i = 0; i < n; ++i) {
+    const Copy2d& c = copies[i];
+    if (c.n_o <= 0 || c.n_k <= 0) continue;
+    RMA_CHECK_ARG(c.dst_ld >= c.n_k && c.src_ld >= c.n_k, "leading dims smaller than row length");
+    RMA_CHECK_ARG(c.dst && c.src, "null copy2d pointer");
+    wide = wide && c.n_k % 2 == 0 && c.dst_ld % 2 == 0 && c.src_ld % 2 == 0 &&
+           ((reinterpret_cast<uintptr_t>(c.dst) | reinterpret_cast<uintptr_t>(c.src)) & 15) == 0;
+    a.c[m++] = {c.dst, c.src, c.dst_ld, c.src_ld, c.n_o, c.n_k};
   }
-  const unsigned g = grid_stride_blocks(n_o * n_k, 256);
+  if (m == 0) return;
+  if (wide) {
+    elem_bytes = 16;
+    for (int i = 0; i < m; ++i) {
+      a.c[i].dst_ld /= 2;
+      a.c[i].src_ld /= 2;
+      a.c[i].n_k /= 2;
+    }
+  }
+  int64_t bx = 1;  // blocks along x: what the largest copy can use, capped (grid-stride)
+  for (int i = 0; i < m; ++i) {
+    const Copy2dDev& c = a.c[i];
+    const int64_t need = c.n_k * 2 <= kCopyBlock
+                             ? (c.n_o + kCopyBlock / c.n_k - 1) / (kCopyBlock / c.n_k)
+                             : c.n_o * ((c.n_k + kCopyBlock - 1) / kCopyBlock);
+    bx = std::max(bx, need);
+  }
+  const dim3 grid((unsigned)std::min<int64_t>(bx, 256 * 8), (unsigned)m);
   hipStream_t s = as_stream(stream);
   switch (elem_bytes) {
-    case 2:
-      copy2d_kernel<uint16_t><<<g, 256, 0, s>>>((uint16_t*)dst, dst_ld, (const uint16_t*)src,
-                                                src_ld, n_o, n_k);
-      break;
-    case 4:
-      copy2d_kernel<uint32_t><<<g, 256, 0, s>>>((uint32_t*)dst, dst_ld, (const uint32_t*)src,
-                                                src_ld, n_o, n_k);
-      break;
-    case 8:
-      copy2d_kernel<uint64_t><<<g, 256, 0, s>>>((uint64_t*)dst, dst_ld, (const uint64_t*)src,
-                                                src_ld, n_o, n_k);
-      break;
-    case 16:
-      copy2d_kernel<E16><<<g, 256, 0, s>>>((E16*)dst, dst_ld, (const E16*)src, src_ld, n_o, n_k);
-      break;
-    default: RMA_CHECK_ARG(false, "unsupported element size " << elem_bytes);
+    case 2: copy2d_batch_kernel<uint16_t><<<grid, kCopyBlock, 0, s>>>(a); break;
+    case 4: copy2d_batch_kernel<uint32_t><<<grid, kCopyBlock, 0, s>>>(a); break;
+    case 8: copy2d_batch_kernel<uint64_t><<<grid, kCopyBlock, 0, s>>>(a); break;
+    default: copy2d_batch_kernel<E16><<<grid, kCopyBlock, 0, s>>>(a); break;
   }
   RMA_HIP_LAUNCH_CHECK();
+}
+
+void copy2d_gpu(void* dst, int64_t dst_ld, const void* src, int64_t src_ld, int64_t n_o,
+                int64_t n_k, int elem_bytes, stream_t stream) {
+  const Copy2d c{dst, dst_ld, src, src_ld, n_o, n_k};
+  copy2d_batch_gpu(&c, 1, elem_bytes, stream);
 }
 
 void stream_copy_gpu(double* b, const double* a, int64_t n, int nt, int blocks, stream_t stream) {

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rma/hip_check.h"
+#include "rma/kernels.h"
 #include "rma/topology.h"
 
 namespace rma {
@@ -49,6 +50,7 @@ namespace {
 char* at(const HaloField& f, const PlaneView& v) {
   return static_cast<char*>(f.ptr) + v.offset * f.elem_bytes;
 }
+
 }  // namespace
 
 void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stream,
@@ -58,16 +60,9 @@ void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stre
   const HaloPlan plan = plan_exchange(fields, nbr_, self_, self_via_comm_, dims_mask);
   for (size_t s = 0; s < plan.slot_bytes.size(); ++s) buffer(s, plan.slot_bytes[s]);
   for (const HaloDimPlan& dp : plan.dims) {
-    for (const HaloCopy& c : dp.copies) {
-      const HaloField& f = fields[c.field];
-      copy2d_gpu(at(f, c.dst), c.dst.ld, at(f, c.src), c.src.ld, c.src.n_o, c.src.n_k,
-                 f.elem_bytes, stream);
-    }
-    for (const HaloPack& p : dp.packs) {
-      const HaloField& f = fields[p.field];
-      copy2d_gpu(bufs_[p.slot], p.view.n_k, at(f, p.view), p.view.ld, p.view.n_o, p.view.n_k,
-                 f.elem_bytes, stream);
-    }
+    // self copies + packs in one batched launch, the group, unpacks in one
+    for (const CopyBatch& b : batch_copies(dim_copies(dp, fields, bufs_, 0)))
+      copy2d_batch_gpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes, stream);
     if (!dp.sends.empty() || !dp.recvs.empty()) {
       RMA_CHECK_ARG(comm_ != nullptr, "remote neighbour without communicator");
       comm_->group_start();
@@ -79,11 +74,8 @@ void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stre
                     stream);
       comm_->group_end();
     }
-    for (const HaloPack& u : dp.unpacks) {
-      const HaloField& f = fields[u.field];
-      copy2d_gpu(at(f, u.view), u.view.ld, bufs_[u.slot], u.view.n_k, u.view.n_o, u.view.n_k,
-                 f.elem_bytes, stream);
-    }
+    for (const CopyBatch& b : batch_copies(dim_copies(dp, fields, bufs_, 1)))
+      copy2d_batch_gpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes, stream);
   }
   bytes_last_ = plan.bytes_sent;
 }

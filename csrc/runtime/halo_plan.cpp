@@ -75,4 +75,60 @@ HaloPlan plan_exchange(const std::vector<HaloField>& fields,
   return plan;
 }
 
+namespace {
+char* plane_ptr(const HaloField& f, const PlaneView& v) {
+  return static_cast<char*>(f.ptr) + v.offset * f.elem_bytes;
+}
+}  // namespace
+
+std::vector<std::pair<int, Copy2d>> dim_copies(const HaloDimPlan& dp,
+                                               const std::vector<HaloField>& fields,
+                                               const std::vector<void*>& slots, int phase) {
+  std::vector<std::pair<int, Copy2d>> q;
+  auto slot = [&](int i) {
+    RMA_CHECK_ARG(i >= 0 && i < (int)slots.size() && slots[i], "halo buffer slot " << i);
+    return slots[i];
+  };
+  if (phase == 0) {
+    for (const HaloCopy& c : dp.copies) {
+      const HaloField& f = fields.at(c.field);
+      q.push_back({f.elem_bytes, {plane_ptr(f, c.dst), c.dst.ld, plane_ptr(f, c.src), c.src.ld,
+                                  c.src.n_o, c.src.n_k}});
+    }
+    for (const HaloPack& p : dp.packs) {
+      const HaloField& f = fields.at(p.field);
+      q.push_back({f.elem_bytes, {slot(p.slot), p.view.n_k, plane_ptr(f, p.view), p.view.ld,
+                                  p.view.n_o, p.view.n_k}});
+    }
+  } else {
+    for (const HaloPack& u : dp.unpacks) {
+      const HaloField& f = fields.at(u.field);
+      q.push_back({f.elem_bytes, {plane_ptr(f, u.view), u.view.ld, slot(u.slot), u.view.n_k,
+                                  u.view.n_o, u.view.n_k}});
+    }
+  }
+  return q;
+}
+
+std::vector<CopyBatch> batch_copies(const std::vector<std::pair<int, Copy2d>>& q) {
+  std::vector<CopyBatch> out;
+  std::vector<bool> done(q.size(), false);
+  for (size_t i = 0; i < q.size(); ++i) {
+    if (done[i]) continue;
+    const int eb = q[i].first;
+    CopyBatch b{eb, {}};
+    for (size_t j = i; j < q.size(); ++j) {
+      if (done[j] || q[j].first != eb) continue;
+      done[j] = true;
+      b.copies.push_back(q[j].second);
+      if ((int)b.copies.size() == kCopy2dBatch) {
+        out.push_back(std::move(b));
+        b = CopyBatch{eb, {}};
+      }
+    }
+    if (!b.copies.empty()) out.push_back(std::move(b));
+  }
+  return out;
+}
+
 }  // namespace rma

@@ -116,6 +116,9 @@ int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<in
     plans[r] = plan_exchange(fields[r], topo.neighbors(r), r, via_comm, 7);
     for (size_t b : plans[r].slot_bytes) bufs[r].push_back(std::vector<double>(b / 8, -9.0));
   }
+  std::vector<std::vector<void*>> slots(P);
+  for (int r = 0; r < P; ++r)
+    for (auto& b : bufs[r]) slots[r].push_back(b.data());
   auto at = [&](int r, int f, const PlaneView& v) {
     return reinterpret_cast<char*>(fields[r][f].ptr) + v.offset * 8;
   };
@@ -125,12 +128,9 @@ int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<in
     for (int r = 0; r < P; ++r) {
       if (plans[r].dims.size() != plans[0].dims.size()) return 101;
       const HaloDimPlan& dp = plans[r].dims[k];
-      for (const auto& c : dp.copies)
-        copy2d_cpu(at(r, c.field, c.dst), c.dst.ld, at(r, c.field, c.src), c.src.ld, c.src.n_o,
-                   c.src.n_k, 8);
-      for (const auto& p : dp.packs)
-        copy2d_cpu(bufs[r][p.slot].data(), p.view.n_k, at(r, p.field, p.view), p.view.ld,
-                   p.view.n_o, p.view.n_k, 8);
+      // the engine's batches (halo.cpp), executed by the CPU twin
+      for (const CopyBatch& b : batch_copies(dim_copies(dp, fields[r], slots[r], 0)))
+        copy2d_batch_cpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes);
       for (const auto& m : dp.sends) {
         const char* src = m.slot >= 0 ? reinterpret_cast<const char*>(bufs[r][m.slot].data())
                                       : at(r, m.field, m.view);
@@ -148,9 +148,8 @@ int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<in
         std::memcpy(dst, q.front().data(), m.bytes);
         q.pop_front();
       }
-      for (const auto& u : dp.unpacks)
-        copy2d_cpu(at(r, u.field, u.view), u.view.ld, bufs[r][u.slot].data(), u.view.n_k,
-                   u.view.n_o, u.view.n_k, 8);
+      for (const CopyBatch& b : batch_copies(dim_copies(dp, fields[r], slots[r], 1)))
+        copy2d_batch_cpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes);
     }
   }
   for (auto& kv : wire)
@@ -222,6 +221,37 @@ int main() {
   copy2d_cpu(col.data(), 1, T.data() + 3, nx, ny, 1, 8);
   copy2d_cpu(back.data() + 5, nx, col.data(), 1, ny, 1, 8);
   for (int64_t y = 0; y < ny; ++y) EXPECT(back[y * nx + 5] == T[y * nx + 3]);
+  // copy batching: plan order per element size, <= kCopy2dBatch per batch
+  {
+    std::vector<std::pair<int, Copy2d>> q;
+    std::vector<std::vector<uint32_t>> bufs(2 * kCopy2dBatch + 3, std::vector<uint32_t>(8, 0));
+    for (int i = 0; i < 2 * kCopy2dBatch + 3; ++i) {
+      for (auto& v : bufs[i]) v = (uint32_t)i;
+      // one 4-byte copy in every third slot, 8-byte copies otherwise
+      const int eb = i % 3 == 1 ? 4 : 8;
+      q.push_back({eb, {bufs[i].data() + 4, 1, bufs[i].data(), 1, 4 * 4 / eb, 1}});
+    }
+    const std::vector<CopyBatch> bs = batch_copies(q);
+    size_t total = 0;
+    int prev8 = -1;
+    for (const CopyBatch& b : bs) {
+      EXPECT(!b.copies.empty() && (int)b.copies.size() <= kCopy2dBatch);
+      total += b.copies.size();
+      for (const Copy2d& c : b.copies) {
+        EXPECT((b.elem_bytes == 4) == ((static_cast<const uint32_t*>(c.src))[0] % 3 == 1));
+        if (b.elem_bytes == 8) {  // plan order kept within an element size
+          const int idx = (int)(static_cast<const uint32_t*>(c.src))[0];
+          EXPECT(idx > prev8);
+          prev8 = idx;
+        }
+      }
+      copy2d_batch_cpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes);
+    }
+    EXPECT(total == q.size());
+    for (auto& b : bufs)
+      for (int k = 4; k < 8; ++k) EXPECT(b[k] == b[0]);
+    EXPECT(throws([&] { copy2d_batch_cpu(nullptr, kCopy2dBatch + 1, 8); }));
+  }
   // reductions
   EXPECT(reduce_cpu(T.data(), nx * ny, kMaxAbs) <= 1.0);
   T[11] = NAN;

@@ -162,3 +162,21 @@ def test_dead_peer_times_out_instead_of_hanging():
     out = run_loopback(2, spmd_dead_peer, timeout=2)
     assert out[1] == "died"
     assert "no message from 1" in out[0]
+
+
+def test_copy_planes_cpu_twin():
+    """The batched pack/unpack entry point on host tensors (CPU twin of the
+    GPU batch kernel): every copy of the batch lands, nothing else moves."""
+    from rocm_mpi_amd import ops
+
+    A = torch.arange(37 * 53, dtype=torch.float64).reshape(37, 53)
+    B = torch.zeros_like(A)
+    planes = [(slice(0, 37), slice(3, 5)), (slice(2, 6), slice(0, 53)), (slice(0, 0), slice(0, 2)),
+              (slice(10, 30), slice(20, 41))]
+    ops.copy_planes([(B[r, c], A[r, c]) for r, c in planes])
+    ref = torch.zeros_like(A)
+    for r, c in planes:
+        ref[r, c] = A[r, c]
+    assert torch.equal(B, ref)
+    with pytest.raises(ValueError):
+        ops.copy_planes([(B[:, :1], A[:, :1])] * 9)

@@ -168,6 +168,49 @@ def test_copy_plane_fp64_wide_rows(c0, w):
     assert float(B[:, :30].abs().sum()) == 0.0 and float(B[:, 30 + w:].abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32, torch.float16])
+def test_copy_planes_batch(dtype):
+    """One launch, copies of every shape class: narrow rows (n_k = 1, odd, K),
+    rows wider than a block, a contiguous plane, an empty copy, unaligned
+    columns (the batch falls back to 8-byte elements for all copies)."""
+    A = rand((301, 700), 12).to(dtype)
+    B = torch.zeros_like(A)
+    planes = [(slice(0, 301), slice(3, 4)), (slice(0, 301), slice(10, 17)),
+              (slice(0, 300), slice(40, 64)), (slice(5, 9), slice(0, 700)),
+              (slice(100, 140), slice(65, 365)), (slice(0, 0), slice(0, 5)),
+              (slice(200, 201), slice(1, 699)), (slice(7, 290), slice(400, 402))]
+    ops.copy_planes([(B[r, c], A[r, c]) for r, c in planes])
+    ref = torch.zeros_like(A)
+    for r, c in planes:
+        ref[r, c] = A[r, c]
+    assert torch.equal(B, ref)
+
+
+def test_copy_planes_halo_shapes_16b():
+    """The halo engine's fp64 batch at K = 24: two x-planes packed into
+    contiguous buffers (16-byte elements), unpacked into the halo columns."""
+    n, K = 4099, 24
+    T = rand((n, n + 1), 13)[:, :n]  # odd leading dim: 8-byte path
+    U = rand((n, n), 14)
+    for F in (T, U):
+        bl = torch.empty((n, K), dtype=torch.float64, device=DEV)
+        bh = torch.empty_like(bl)
+        ops.copy_planes([(bl, F[:, K:2 * K]), (bh, F[:, n - 2 * K:n - K])])
+        assert torch.equal(bl, F[:, K:2 * K]) and torch.equal(bh, F[:, n - 2 * K:n - K])
+        G = F.clone()
+        ops.copy_planes([(G[:, :K], bh), (G[:, n - K:], bl)])
+        assert torch.equal(G[:, :K], F[:, n - 2 * K:n - K]) and torch.equal(G[:, n - K:], F[:, K:2 * K])
+        assert torch.equal(G[:, K:n - K], F[:, K:n - K])
+
+
+def test_copy_planes_rejects_mixed_and_oversized():
+    A = rand((16, 16), 15)
+    with pytest.raises(ValueError):
+        ops.copy_planes([(A[:, :2], A[:, 4:6]), (A.float()[:, :2], A.float()[:, 4:6])])
+    with pytest.raises(ValueError):
+        ops.copy_planes([(A[:, :1], A[:, 1:2])] * 9)
+
+
 @pytest.mark.parametrize("op", ["sum", "max", "min", "maxabs", "nonfinite"])
 def test_reduce(op):
     A = rand((513, 257), 9) - 0.5
