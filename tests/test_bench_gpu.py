@@ -41,6 +41,7 @@ def test_bench_small_tile_with_self_rccl_halo_check():
     assert hc["transport"] == "rccl" and hc["self_rccl"] and hc["tiles_mismatched"] == 0
     pt = c["pass_timing"]
     assert pt["passes"] == len(plan) and pt["depths"] == plan and pt["interior_ms"] > 0
+    assert pt["overlap_fraction"] is None and "no neighbour" in pt["note"]  # nothing exchanged
     # no neighbour: solo == the run (a ~2 ms timed region: launch/clock noise only)
     assert c["weak_scaling_eff_same_run"] > 0.7
     assert c["teff_single_step_kernel_GBps"] > 0 and c["teff_bitwise_kstep_GBps"] > 0
