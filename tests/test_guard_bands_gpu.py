@@ -129,3 +129,22 @@ def test_copy_init_fill_reduce_stay_in_bounds():
     ops.copy_plane(A[:, 120:123], B[:, 2:5])
     assert guards_intact(b) and guards_intact(bB)
     assert torch.equal(A[:, 120:123], A[:, 10:13])
+
+
+@pytest.mark.parametrize("nx,w", [(130, 1), (130, 24), (1026, 300), (4098, 2048)])
+def test_batched_plane_copies_stay_in_bounds(nx, w):
+    """Batched pack / unpack (one launch per halo phase): narrow rows (thread ->
+    fixed row/column), rows wider than a block, 16-byte and 8-byte elements;
+    only the destination planes change."""
+    ny = 67
+    bA, A = guarded(ny, nx, 6)
+    bB, B = guarded(ny, w, 7)
+    bC, Cb = guarded(ny, w, 8)
+    before = A.clone()
+    ops.copy_planes([(B, A[:, 1:1 + w]), (Cb, A[:, nx - 1 - w:nx - 1])])  # 8-B (odd offset)
+    ops.copy_planes([(A[:, nx - w:], B), (A[:, :w], Cb)])  # 16-B when w is even
+    assert guards_intact(bA) and guards_intact(bB) and guards_intact(bC)
+    assert torch.equal(A[:, nx - w:], before[:, 1:1 + w])
+    assert torch.equal(A[:, :w], before[:, nx - 1 - w:nx - 1])
+    if nx > 2 * w:
+        assert torch.equal(A[:, w:nx - w], before[:, w:nx - w])
