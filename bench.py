@@ -293,7 +293,14 @@ def main(argv=None) -> int:
     if gpu:
         from rocm_mpi_amd._native import native
 
-        bus = native().device_pci_bus_id(torch.cuda.current_device())
+        try:
+            bus = native().device_pci_bus_id(torch.cuda.current_device())
+        except Exception as e:  # noqa: BLE001 - fall back to the device UUID
+            uuid = getattr(torch.cuda.get_device_properties(torch.cuda.current_device()),
+                           "uuid", None)
+            if uuid is None:
+                return fail(f"cannot identify the physical GPU (PCI bus id: {e})", rank)
+            bus = f"uuid-{uuid}"
     else:
         bus = f"cpu-rank-{rank}"
     buses = gather_obj(bus, world)
