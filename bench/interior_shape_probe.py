@@ -1,0 +1,78 @@
+"""Pass time of the K-step interior launch vs the rect it covers (288 GB tile):
+the owned rect of an open tile, of one with x / y / x+y neighbours, and the
+interior left by the frame strips, to see whether the rect's origin or
+extent (not the concurrent frame + exchange) makes a rank with neighbours
+slower.
+
+    python bench/interior_shape_probe.py --K 24 --out gpurun_out/shape.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from rocm_mpi_amd import ops  # noqa: E402
+from rocm_mpi_amd._native import native  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--K", type=int, default=24)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    n = a.n
+    if not n:
+        free, _ = torch.cuda.mem_get_info()
+        n = int(math.isqrt(int(0.8 * free / 24))) // 256 * 256
+    K = a.K
+    T = torch.empty((n, n), dtype=torch.float64, device="cuda")
+    T2 = torch.empty_like(T)
+    iCp = torch.empty_like(T)
+    geom = ops.TileGeometry(0, 0, n, n, 1.0, 1.0)
+    ops.init_random_(T, geom, seed=1)
+    ops.fill_(iCp, 1.0)
+    ops.fill_(T2, 0.0)
+    coef = ops.StencilCoef(-1.0, 1.0 / 0.01, 1.0 / 0.01, 1e-5)
+    kern, vec, ch = native().fast_kernel_k(K, n, tuple(coef))
+    names = {v: k for k, v in ops.KERNELS.items()}
+    tn = ops.StencilTuning(chunk_rows=ch, kernel=names[kern], vec=vec, xcd_remap=1)
+    f = 128 - 2 * K + K  # interior start next to an ol-wide frame strip (frame fill)
+    rects = {
+        "open": (1, n - 1, 1, n - 1),
+        "owned_x": (K, n - K, 1, n - 1),
+        "owned_y": (1, n - 1, K, n - K),
+        "owned_xy": (K, n - K, K, n - K),
+        "interior_x_strips": (f, n - f, 1, n - 1),
+        "interior_y_strips": (1, n - 1, 2 * K, n - 2 * K),
+        "interior_xy_strips": (f, n - f, 2 * K, n - 2 * K),
+        "open_shift_x8": (9, n - 1, 1, n - 1),
+    }
+    res = {"n": n, "K": K, "kernel": names[kern], "vec": vec, "chunk_rows": ch, "ms": {}}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for rep in range(a.reps):
+        for name, r in rects.items():
+            ops.stencilk_step(K, T2, T, iCp, coef, [r], tn)
+            torch.cuda.synchronize()
+            ev[0].record()
+            ops.stencilk_step(K, T2, T, iCp, coef, [r], tn)
+            ev[1].record()
+            torch.cuda.synchronize()
+            res["ms"].setdefault(name, []).append(round(ev[0].elapsed_time(ev[1]), 3))
+        print(json.dumps(res["ms"]), flush=True)
+    if a.out:
+        with open(a.out, "w") as fo:
+            json.dump(res, fo, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

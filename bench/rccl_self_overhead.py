@@ -32,18 +32,19 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
-        chunk2: int = 0) -> dict:
+        chunk2: int = 0, dims: str = "xy") -> dict:
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
     from rocm_mpi_amd.parallel import implicit_grid as gg
 
-    p = 1 if periodic else 0
-    gg.init_global_grid(n, n, 1, periodx=p, periody=p, quiet=True, transport="rccl",
+    px = 1 if periodic and "x" in dims else 0
+    py = 1 if periodic and "y" in dims else 0
+    gg.init_global_grid(n, n, 1, periodx=px, periody=py, quiet=True, transport="rccl",
                         overlaps=(max(2, 2 * K), max(2, 2 * K), 2), halowidths=(K, K, 1),
                         self_via_transport=periodic)
     m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=n, nt=steps, quiet=True,
-                                    init="random", periods=(p, p, 0), temporal=K,
+                                    init="random", periods=(px, py, 0), temporal=K,
                                     fast_math=K > 1, chunk2=chunk2))
     m.step(2 * K)
     m.synchronize()
@@ -74,6 +75,9 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=320)
     ap.add_argument("--variants", default="perf_hide")
     ap.add_argument("--chunk2", type=int, default=0, help="rows per task of the K-step passes (0: table)")
+    ap.add_argument("--periodic", default="xy", choices=["xy", "x", "y"],
+                    help="dimensions routed through RCCL-self in the periodic runs (x: the "
+                         "two x-neighbours of a middle rank of a 4x1 row, no y-neighbour)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -82,11 +86,12 @@ def main(argv=None) -> int:
     if not n:
         free, _ = torch.cuda.mem_get_info()
         n = int(math.isqrt(int(0.8 * free / 24))) // 256 * 256
-    out = {"tile": n, "K": a.K, "steps": a.steps, "variants": {}}
+    out = {"tile": n, "K": a.K, "steps": a.steps, "periodic_dims": a.periodic,
+           "frame_sides": os.environ.get("RMA_FRAME_SIDES", "neighbours"), "variants": {}}
     for variant in a.variants.split(","):
         rows = []
         for periodic in (False, True, False, True):
-            r = run(n, a.K, a.steps, periodic, variant, a.chunk2)
+            r = run(n, a.K, a.steps, periodic, variant, a.chunk2, a.periodic)
             r.update({"periodic_rccl_self": periodic,
                       "teff_GBps": 3 * n * n * 8 / 1e9 / (r["ms_per_step"] / 1e3)})
             rows.append(r)

@@ -20,12 +20,20 @@ using Neighbors = std::array<std::array<int, 2>, 3>;  // (dim, side) -> rank, -1
 // and interior is empty.
 void split_rect(const Rect& out, int64_t bwx, int64_t bwy, std::vector<Rect>& frame,
                 Rect& interior);
+// The same with one width per side (0: no frame rect on that side).
+void split_rect_sides(const Rect& out, int64_t xlo, int64_t xhi, int64_t ylo, int64_t yhi,
+                      std::vector<Rect>& frame, Rect& interior);
 
 // Cells a K-step pass owns: next to a neighbour the K cells [0,K) are halo
 // (level j of the pass is valid from column j on, so the pass outputs from
 // column K; the width-hw exchange refreshes [0,hw) afterwards), elsewhere the
 // fixed boundary cell 0 stays.
 Rect owned_rect(int64_t nx, int64_t ny, int K, const Neighbors& nbr);
+
+// Sides [dim][lo/hi] whose cells perf_hide computes ahead of the exchange:
+// those with a neighbour (their send planes), all four under
+// RMA_FRAME_SIDES=all (the r1-r2 layout, for A/B runs).
+std::array<std::array<bool, 2>, 2> frame_sides(const Neighbors& nbr);
 
 struct PassGeom {
   Rect out{};                // cells the pass writes
@@ -41,7 +49,7 @@ struct PassGeom {
 };
 
 // Geometry of one pass. hide: split into frame + interior so that the frame
-// holds the send planes [ol-hw, ol) of every side (width >= ol - out.x0, the
+// holds the send planes [ol-hw, ol) of every side with a neighbour (width >= ol - out.x0, the
 // reference's b_width >= overlap invariant); without any
 // neighbour there is nothing to overlap and the owned rect is one launch.
 // task_w / task_h > 0 (pipelined passes): output columns per strip and rows

@@ -105,13 +105,16 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
                               << "halowidths=K), got " << ol[d]);
   full_ = {1, nx - 1, 1, ny - 1};
   // perf_hide one-step updates: the frame must contain the send planes
-  // [ol-hw, ol) of every side, so it is at least ol-1 cells wide (the
+  // [ol-hw, ol) of every side with a neighbour, so it is at least ol-1 cells wide (the
   // reference's b_width >= overlap invariant); minimal frames
   // otherwise (width 1 for ol=2: thin x-frames run in the kernel's column mode)
   if (p.mode == Mode::kHide) {
     RMA_CHECK_ARG(p.bwx >= 1 && p.bwy >= 1,
                   "b_width must be >= 1 so the send planes belong to the boundary kernel");
-    split_rect(full_, std::max(p.bwx, p.olx - 1), std::max(p.bwy, p.oly - 1), frame_, interior_);
+    const int64_t fx = std::max(p.bwx, p.olx - 1), fy = std::max(p.bwy, p.oly - 1);
+    const auto side = frame_sides(nbr_);
+    split_rect_sides(full_, side[0][0] ? fx : 0, side[0][1] ? fx : 0, side[1][0] ? fy : 0,
+                     side[1][1] ? fy : 0, frame_, interior_);
   } else {
     interior_ = full_;
   }
@@ -296,7 +299,7 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
   rec(0, s_hi_);
   StencilTuning ft = p_.tune;
   ft.chunk_rows = std::min(ft.chunk_rows, 16);
-  {
+  if (!frame_.empty()) {  // no frame without a neighbour: the interior is the whole tile
     TraceRange tb("rma.boundary");
     stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, frame_.data(), (int)frame_.size(), c, ft, s_hi_);
   }

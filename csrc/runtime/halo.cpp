@@ -2,6 +2,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "rma/hip_check.h"
 #include "rma/kernels.h"
 #include "rma/topology.h"
@@ -51,6 +53,19 @@ char* at(const HaloField& f, const PlaneView& v) {
   return static_cast<char*>(f.ptr) + v.offset * f.elem_bytes;
 }
 
+// RMA_HALO_BATCH=0: one launch per plane copy (A/B and diagnosis)
+void launch_batches(const std::vector<CopyBatch>& bs, stream_t stream) {
+  static const char* e = std::getenv("RMA_HALO_BATCH");
+  const bool single = e && e[0] == '0';
+  for (const CopyBatch& b : bs) {
+    if (single) {
+      for (const Copy2d& c : b.copies) copy2d_batch_gpu(&c, 1, b.elem_bytes, stream);
+    } else {
+      copy2d_batch_gpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes, stream);
+    }
+  }
+}
+
 }  // namespace
 
 void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stream,
@@ -61,8 +76,7 @@ void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stre
   for (size_t s = 0; s < plan.slot_bytes.size(); ++s) buffer(s, plan.slot_bytes[s]);
   for (const HaloDimPlan& dp : plan.dims) {
     // self copies + packs in one batched launch, the group, unpacks in one
-    for (const CopyBatch& b : batch_copies(dim_copies(dp, fields, bufs_, 0)))
-      copy2d_batch_gpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes, stream);
+    launch_batches(batch_copies(dim_copies(dp, fields, bufs_, 0)), stream);
     if (!dp.sends.empty() || !dp.recvs.empty()) {
       RMA_CHECK_ARG(comm_ != nullptr, "remote neighbour without communicator");
       comm_->group_start();
@@ -74,8 +88,7 @@ void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stre
                     stream);
       comm_->group_end();
     }
-    for (const CopyBatch& b : batch_copies(dim_copies(dp, fields, bufs_, 1)))
-      copy2d_batch_gpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes, stream);
+    launch_batches(batch_copies(dim_copies(dp, fields, bufs_, 1)), stream);
   }
   bytes_last_ = plan.bytes_sent;
 }

@@ -8,22 +8,43 @@
 
 namespace rma {
 
-void split_rect(const Rect& out, int64_t bwx, int64_t bwy, std::vector<Rect>& frame,
-                Rect& interior) {
-  RMA_CHECK_ARG(bwx >= 0 && bwy >= 0, "frame widths " << bwx << "," << bwy);
+void split_rect_sides(const Rect& out, int64_t xlo, int64_t xhi, int64_t ylo, int64_t yhi,
+                      std::vector<Rect>& frame, Rect& interior) {
+  RMA_CHECK_ARG(xlo >= 0 && xhi >= 0 && ylo >= 0 && yhi >= 0,
+                "frame widths " << xlo << "," << xhi << "," << ylo << "," << yhi);
   frame.clear();
-  const int64_t xi0 = out.x0 + bwx, xi1 = out.x1 - bwx;
-  const int64_t yi0 = out.y0 + bwy, yi1 = out.y1 - bwy;
+  const int64_t xi0 = out.x0 + xlo, xi1 = out.x1 - xhi;
+  const int64_t yi0 = out.y0 + ylo, yi1 = out.y1 - yhi;
   if (xi0 >= xi1 || yi0 >= yi1) {
     interior = {0, 0, 0, 0};
     if (!out.empty()) frame.push_back(out);
     return;
   }
   interior = {xi0, xi1, yi0, yi1};
-  frame = {{out.x0, out.x1, out.y0, yi0},
-           {out.x0, out.x1, yi1, out.y1},
-           {out.x0, xi0, yi0, yi1},
-           {xi1, out.x1, yi0, yi1}};
+  if (ylo > 0) frame.push_back({out.x0, out.x1, out.y0, yi0});
+  if (yhi > 0) frame.push_back({out.x0, out.x1, yi1, out.y1});
+  if (xlo > 0) frame.push_back({out.x0, xi0, yi0, yi1});
+  if (xhi > 0) frame.push_back({xi1, out.x1, yi0, yi1});
+}
+
+void split_rect(const Rect& out, int64_t bwx, int64_t bwy, std::vector<Rect>& frame,
+                Rect& interior) {
+  RMA_CHECK_ARG(bwx >= 0 && bwy >= 0, "frame widths " << bwx << "," << bwy);
+  split_rect_sides(out, bwx, bwx, bwy, bwy, frame, interior);
+}
+
+std::array<std::array<bool, 2>, 2> frame_sides(const Neighbors& nbr) {
+  // Only a side that sends needs its cells before the exchange: a side
+  // without a neighbour (open boundary) is computed by the interior launch.
+  // RMA_FRAME_SIDES=all: every side once any neighbour exists (the r1-r2
+  // layout, kept for A/B runs).
+  static const char* fs = std::getenv("RMA_FRAME_SIDES");
+  const bool any = nbr[0][0] >= 0 || nbr[0][1] >= 0 || nbr[1][0] >= 0 || nbr[1][1] >= 0;
+  const bool all = any && fs && std::string(fs) == "all";
+  std::array<std::array<bool, 2>, 2> on{};
+  for (int d = 0; d < 2; ++d)
+    for (int s = 0; s < 2; ++s) on[d][s] = all || nbr[d][s] >= 0;
+  return on;
 }
 
 Rect owned_rect(int64_t nx, int64_t ny, int K, const Neighbors& nbr) {
@@ -58,20 +79,27 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
     // first / last strip column (tall strips): every frame cell is computed
     // once, with the same recompute as in one launch of the owned rect
     g.aligned = true;
+    const auto side = frame_sides(nbr);
     const int64_t V = std::max(1, vec);
     auto floor_v = [&](int64_t a) { return a - (((a % V) + V) % V); };
     // left strip: exactly the first strip of the owned rect's grid
-    const int64_t xl = floor_v(o.x0 - K) + K + task_w;
+    const int64_t xl = side[0][0] ? floor_v(o.x0 - K) + K + task_w : o.x0;
     // right strip: starts where a strip's origin (start - K) is V-aligned and
     // its output still reaches x1
-    int64_t xr = o.x1 - task_w;
-    xr += ((V - ((xr - K) % V + V) % V) % V);
-    g.frame_wide = {{o.x0, o.x1, o.y0, o.y0 + task_h}, {o.x0, o.x1, o.y1 - task_h, o.y1}};
-    g.frame_tall = {{o.x0, xl, o.y0 + task_h, o.y1 - task_h},
-                    {xr, o.x1, o.y0 + task_h, o.y1 - task_h}};
+    int64_t xr = o.x1;
+    if (side[0][1]) {
+      xr = o.x1 - task_w;
+      xr += ((V - ((xr - K) % V + V) % V) % V);
+    }
+    const int64_t yb = side[1][0] ? o.y0 + task_h : o.y0;
+    const int64_t yt = side[1][1] ? o.y1 - task_h : o.y1;
+    if (side[1][0]) g.frame_wide.push_back({o.x0, o.x1, o.y0, yb});
+    if (side[1][1]) g.frame_wide.push_back({o.x0, o.x1, yt, o.y1});
+    if (side[0][0]) g.frame_tall.push_back({o.x0, xl, yb, yt});
+    if (side[0][1]) g.frame_tall.push_back({xr, o.x1, yb, yt});
     g.frame = g.frame_wide;
     g.frame.insert(g.frame.end(), g.frame_tall.begin(), g.frame_tall.end());
-    g.interior = {xl, xr, o.y0 + task_h, o.y1 - task_h};
+    g.interior = {xl, xr, yb, yt};
     return g;
   }
   if (hide && any_nbr) {
@@ -83,7 +111,10 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
     static const char* ff = std::getenv("RMA_FRAME_FILL");
     if (K >= 5 && !(ff && ff[0] == '0'))
       fx = std::max<int64_t>(fx, std::min<int64_t>(128 - 2 * K, (g.out.x1 - g.out.x0) / 4));
-    split_rect(g.out, fx, std::max(bwy, oly - g.out.y0), g.frame, g.interior);
+    const int64_t fy = std::max(bwy, oly - g.out.y0);
+    const auto side = frame_sides(nbr);
+    split_rect_sides(g.out, side[0][0] ? fx : 0, side[0][1] ? fx : 0, side[1][0] ? fy : 0,
+                     side[1][1] ? fy : 0, g.frame, g.interior);
     for (const Rect& r : g.frame)
       (r.x1 - r.x0 >= r.y1 - r.y0 ? g.frame_wide : g.frame_tall).push_back(r);
   } else {

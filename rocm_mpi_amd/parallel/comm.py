@@ -388,15 +388,25 @@ class LoopbackComm(Communicator):
         return {"sum": sum, "max": max, "min": min}[op](vals)
 
     def gather(self, t, root=0):
-        vals = self.hub.collect(self.rank, t.detach().clone())
+        c = t.detach().clone()
+        if c.is_cuda:
+            # the root reads this copy from ITS thread and stream: the clone
+            # (and the steps before it on this rank's stream) must have run
+            # (without this the root intermittently read a rank's tile one
+            # step stale in the loopback GPU tests)
+            torch.cuda.current_stream(c.device).synchronize()
+        vals = self.hub.collect(self.rank, c)
         return vals if self.rank == root else None
 
     def exchange(self, ops):
-        if ops and any(o.tensor.is_cuda for o in ops):
+        cuda = bool(ops) and any(o.tensor.is_cuda for o in ops)
+        sends = [(o, o.tensor.detach().clone()) for o in ops if o.kind == "send"]
+        if cuda:
+            # the send copies (and the producers before them) must have run
+            # before a peer thread reads them on its own stream
             torch.cuda.current_stream().synchronize()
-        for o in ops:
-            if o.kind == "send":
-                self.hub.box(self.rank, o.peer, o.tag).put(o.tensor.detach().clone())
+        for o, c in sends:
+            self.hub.box(self.rank, o.peer, o.tag).put(c)
         for o in ops:
             if o.kind == "recv":
                 try:

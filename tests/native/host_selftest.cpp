@@ -286,14 +286,26 @@ int main() {
     EXPECT(fr.empty() && in.empty());
     EXPECT(throws([&] { split_rect({1, 9, 1, 9}, -1, 1, fr, in); }));
     const Neighbors none{{{-1, -1}, {-1, -1}, {-1, -1}}}, all{{{1, 1}, {2, 2}, {-1, -1}}},
-        self{{{0, 0}, {0, 0}, {-1, -1}}};
+        self{{{0, 0}, {0, 0}, {-1, -1}}}, xhi_ylo{{{-1, 3}, {4, -1}, {-1, -1}}},
+        xlo{{{5, -1}, {-1, -1}, {-1, -1}}};
+    // per-side frames: only sides with a neighbour
+    split_rect_sides({1, 99, 1, 49}, 0, 4, 3, 0, fr, in);
+    EXPECT(fr.size() == 2 && in.x0 == 1 && in.x1 == 95 && in.y0 == 4 && in.y1 == 49);
+    split_rect_sides({1, 99, 1, 49}, 0, 0, 0, 0, fr, in);
+    EXPECT(fr.empty() && in.x0 == 1 && in.x1 == 99 && in.y0 == 1 && in.y1 == 49);
+    {
+      const auto sd = frame_sides(xhi_ylo);
+      EXPECT(!sd[0][0] && sd[0][1] && sd[1][0] && !sd[1][1]);
+      const auto sn = frame_sides(none);
+      EXPECT(!sn[0][0] && !sn[0][1] && !sn[1][0] && !sn[1][1]);
+    }
     Rect o = owned_rect(100, 60, 16, all);
     EXPECT(o.x0 == 16 && o.x1 == 84 && o.y0 == 16 && o.y1 == 44);
     o = owned_rect(100, 60, 16, none);
     EXPECT(o.x0 == 1 && o.x1 == 99 && o.y0 == 1 && o.y1 == 59);
     EXPECT(throws([&] { owned_rect(20, 60, 10, all); }));  // minimal tile: nothing owned
     for (int K = 1; K <= 24; ++K) {
-      for (const Neighbors* nb : {&none, &all, &self})
+      for (const Neighbors* nb : {&none, &all, &self, &xhi_ylo, &xlo})
         for (int variant = 0; variant < 3; ++variant) {
         // variant 0: ol-wide frame strips on a small tile; 1, 2: frames of
         // whole pipelined tasks (aligned) on tiles large enough for them
@@ -310,7 +322,7 @@ int main() {
             const int64_t xa = (q.x0 - K) - ((((q.x0 - K) % vec) + vec) % vec);
             EXPECT(q.x1 <= xa + K + tw && q.x1 > q.x0);
           }
-          EXPECT(((pg.interior.x0 - K) % vec + vec) % vec == 0);
+          if ((*nb)[0][0] >= 0) EXPECT(((pg.interior.x0 - K) % vec + vec) % vec == 0);
         }
         int64_t c2 = pg.interior.cells();
         for (auto& q : pg.frame) {
@@ -330,8 +342,15 @@ int main() {
           EXPECT(q.x1 - q.x0 < q.y1 - q.y0);
         }
         EXPECT(c3 + pg.interior.cells() == pg.out.cells());
-        if (nb != &none && !pg.frame.empty()) {  // the frame holds the send planes [ol-hw, ol)
-          EXPECT(pg.interior.empty() || (pg.interior.x0 >= 48 && pg.interior.y0 >= 48));
+        if (nb != &none && !pg.frame.empty() && !pg.interior.empty()) {
+          // the frame holds the send planes [ol-hw, ol) of the sides with a
+          // neighbour; an open side belongs to the interior launch
+          const int64_t nxx = n0, nyy = n0 + 3;
+          const Neighbors& b = *nb;
+          EXPECT(b[0][0] >= 0 ? pg.interior.x0 >= 48 : pg.interior.x0 == pg.out.x0);
+          EXPECT(b[0][1] >= 0 ? pg.interior.x1 <= nxx - 48 : pg.interior.x1 == pg.out.x1);
+          EXPECT(b[1][0] >= 0 ? pg.interior.y0 >= 48 : pg.interior.y0 == pg.out.y0);
+          EXPECT(b[1][1] >= 0 ? pg.interior.y1 <= nyy - 48 : pg.interior.y1 == pg.out.y1);
         }
         }
     }
