@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
-        chunk2: int = 0, dims: str = "xy") -> dict:
+        chunk2: int = 0, dims: str = "xy", via_rccl: bool = True) -> dict:
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
@@ -42,7 +42,7 @@ def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
     py = 1 if periodic and "y" in dims else 0
     gg.init_global_grid(n, n, 1, periodx=px, periody=py, quiet=True, transport="rccl",
                         overlaps=(max(2, 2 * K), max(2, 2 * K), 2), halowidths=(K, K, 1),
-                        self_via_transport=periodic)
+                        self_via_transport=periodic and via_rccl)
     m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=n, nt=steps, quiet=True,
                                     init="random", periods=(px, py, 0), temporal=K,
                                     fast_math=K > 1, chunk2=chunk2))
@@ -78,6 +78,12 @@ def main(argv=None) -> int:
     ap.add_argument("--periodic", default="xy", choices=["xy", "x", "y"],
                     help="dimensions routed through RCCL-self in the periodic runs (x: the "
                          "two x-neighbours of a middle rank of a 4x1 row, no y-neighbour)")
+    ap.add_argument("--self-copies", action="store_true",
+                    help="periodic halos by local copies instead of RCCL send/recv to self "
+                         "(separates the exchange transport from the geometry)")
+    ap.add_argument("--pattern", default="opop",
+                    help="run order: o = open boundaries, p = periodic (each run allocates "
+                         "its own tile)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -87,18 +93,20 @@ def main(argv=None) -> int:
         free, _ = torch.cuda.mem_get_info()
         n = int(math.isqrt(int(0.8 * free / 24))) // 256 * 256
     out = {"tile": n, "K": a.K, "steps": a.steps, "periodic_dims": a.periodic,
+           "periodic_via": "local copies" if a.self_copies else "rccl self send/recv",
            "frame_sides": os.environ.get("RMA_FRAME_SIDES", "neighbours"), "variants": {}}
     for variant in a.variants.split(","):
         rows = []
-        for periodic in (False, True, False, True):
-            r = run(n, a.K, a.steps, periodic, variant, a.chunk2, a.periodic)
+        for periodic in (c == "p" for c in a.pattern):
+            r = run(n, a.K, a.steps, periodic, variant, a.chunk2, a.periodic, not a.self_copies)
             r.update({"periodic_rccl_self": periodic,
                       "teff_GBps": 3 * n * n * 8 / 1e9 / (r["ms_per_step"] / 1e3)})
             rows.append(r)
             print(json.dumps({"variant": variant, **r}), flush=True)
         op = [r["ms_per_step"] for r in rows if not r["periodic_rccl_self"]]
         pe = [r["ms_per_step"] for r in rows if r["periodic_rccl_self"]]
-        out["variants"][variant] = {"runs": rows, "overhead": min(pe) / min(op) - 1.0}
+        out["variants"][variant] = {"runs": rows,
+                                    "overhead": min(pe) / min(op) - 1.0 if pe and op else None}
     print(json.dumps(out), flush=True)
     if a.out:
         with open(a.out, "w") as f:
