@@ -27,6 +27,7 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--K", type=int, default=24)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--init", default="random", choices=["random", "gaussian"])
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     n = a.n
@@ -38,7 +39,10 @@ def main() -> int:
     T2 = torch.empty_like(T)
     iCp = torch.empty_like(T)
     geom = ops.TileGeometry(0, 0, n, n, 1.0, 1.0)
-    ops.init_random_(T, geom, seed=1)
+    if a.init == "random":
+        ops.init_random_(T, geom, seed=1)
+    else:
+        ops.init_gaussian_(T, geom, 10.0, 10.0)
     ops.fill_(iCp, 1.0)
     ops.fill_(T2, 0.0)
     coef = ops.StencilCoef(-1.0, 1.0 / 0.01, 1.0 / 0.01, 1e-5)
@@ -55,15 +59,18 @@ def main() -> int:
         "interior_y_strips": (1, n - 1, 2 * K, n - 2 * K),
         "interior_xy_strips": (f, n - f, 2 * K, n - 2 * K),
         "open_shift_x8": (9, n - 1, 1, n - 1),
+        "owned_x_split_y24": [(K, n - K, 1, K), (K, n - K, K, n - 1)],
+        "owned_y_split_x24": [(1, K, K, n - K), (K, n - 1, K, n - K)],
     }
-    res = {"n": n, "K": K, "kernel": names[kern], "vec": vec, "chunk_rows": ch, "ms": {}}
+    res = {"n": n, "K": K, "init": a.init, "kernel": names[kern], "vec": vec, "chunk_rows": ch, "ms": {}}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for rep in range(a.reps):
         for name, r in rects.items():
-            ops.stencilk_step(K, T2, T, iCp, coef, [r], tn)
+            rl = r if isinstance(r, list) else [r]
+            ops.stencilk_step(K, T2, T, iCp, coef, rl, tn)
             torch.cuda.synchronize()
             ev[0].record()
-            ops.stencilk_step(K, T2, T, iCp, coef, [r], tn)
+            ops.stencilk_step(K, T2, T, iCp, coef, rl, tn)
             ev[1].record()
             torch.cuda.synchronize()
             res["ms"].setdefault(name, []).append(round(ev[0].elapsed_time(ev[1]), 3))

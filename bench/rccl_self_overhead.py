@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
-        chunk2: int = 0, dims: str = "xy", via_rccl: bool = True) -> dict:
+        chunk2: int = 0, dims: str = "xy", via_rccl: bool = True, init: str = "random") -> dict:
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
@@ -44,7 +44,7 @@ def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
                         overlaps=(max(2, 2 * K), max(2, 2 * K), 2), halowidths=(K, K, 1),
                         self_via_transport=periodic and via_rccl)
     m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=n, nt=steps, quiet=True,
-                                    init="random", periods=(px, py, 0), temporal=K,
+                                    init=init, periods=(px, py, 0), temporal=K,
                                     fast_math=K > 1, chunk2=chunk2))
     m.step(2 * K)
     m.synchronize()
@@ -81,6 +81,7 @@ def main(argv=None) -> int:
     ap.add_argument("--self-copies", action="store_true",
                     help="periodic halos by local copies instead of RCCL send/recv to self "
                          "(separates the exchange transport from the geometry)")
+    ap.add_argument("--init", default="random", choices=["random", "gaussian"])
     ap.add_argument("--pattern", default="opop",
                     help="run order: o = open boundaries, p = periodic (each run allocates "
                          "its own tile)")
@@ -94,11 +95,13 @@ def main(argv=None) -> int:
         n = int(math.isqrt(int(0.8 * free / 24))) // 256 * 256
     out = {"tile": n, "K": a.K, "steps": a.steps, "periodic_dims": a.periodic,
            "periodic_via": "local copies" if a.self_copies else "rccl self send/recv",
+           "init": a.init,
            "frame_sides": os.environ.get("RMA_FRAME_SIDES", "neighbours"), "variants": {}}
     for variant in a.variants.split(","):
         rows = []
         for periodic in (c == "p" for c in a.pattern):
-            r = run(n, a.K, a.steps, periodic, variant, a.chunk2, a.periodic, not a.self_copies)
+            r = run(n, a.K, a.steps, periodic, variant, a.chunk2, a.periodic, not a.self_copies,
+                    a.init)
             r.update({"periodic_rccl_self": periodic,
                       "teff_GBps": 3 * n * n * 8 / 1e9 / (r["ms_per_step"] / 1e3)})
             rows.append(r)
