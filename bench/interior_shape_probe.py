@@ -59,6 +59,8 @@ def main() -> int:
         "interior_y_strips": (1, n - 1, 2 * K, n - 2 * K),
         "interior_xy_strips": (f, n - f, 2 * K, n - 2 * K),
         "open_shift_x8": (9, n - 1, 1, n - 1),
+        "owned_x_origin_only": (K, n - 1, 1, n - 1),
+        "owned_x_far_only": (1, n - K, 1, n - 1),
         "owned_x_split_y24": [(K, n - K, 1, K), (K, n - K, K, n - 1)],
         "owned_y_split_x24": [(1, K, K, n - K), (K, n - 1, K, n - K)],
     }
