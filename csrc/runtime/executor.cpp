@@ -247,6 +247,10 @@ StencilTuning DiffusionExecutor::pass_tuning(int K, int part) const {
 
 void DiffusionExecutor::exchange(double* A, stream_t s) {
   if (!halo_ || solo_) return;
+  // diagnosis only (profiles/SUMMARY_r2.md, x-neighbour pass cost): keep the
+  // geometry of a rank with neighbours but skip its exchange (wrong results)
+  static const char* skip = std::getenv("RMA_DIAG_SKIP_EXCHANGE");
+  if (skip && skip[0] == '1') return;
   HaloField f;
   f.ptr = A;
   f.size = {nx_, ny_, 1};
