@@ -13,4 +13,5 @@ step() {  # name timeout cmd...
   return $rc
 }
 RMA_DIAG_SKIP_EXCHANGE=1 step x_skip 400 python -u bench/rccl_self_overhead.py --K 24 --steps 240 --periodic x --variants perf --self-copies --init gaussian --out $OUT/x_skip.json &&
-step x_ref 400 python -u bench/rccl_self_overhead.py --K 24 --steps 240 --periodic x --variants perf --self-copies --init gaussian --out $OUT/x_ref.json
+step x_ref 400 python -u bench/rccl_self_overhead.py --K 24 --steps 240 --periodic x --variants perf --self-copies --init gaussian --out $OUT/x_ref.json &&
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
