@@ -17,34 +17,54 @@ are timed between barrier+device-sync pairs; the step time is the MAX over
 ranks; ``value`` is the whole-job aggregate = N x per-GPU T_eff (weak scaling:
 the local tile is the same for every N). Data: synthetic random-init field.
 
-A multi-rank run validates itself:
-* RCCL is mandatory (no fallback to the host-staged transport) and every rank
-  must drive a different physical GPU (PCI bus ids are compared); otherwise
-  the run exits non-zero before timing anything;
-* per-pass HIP-event timings of the frame kernel, the halo exchange (pack +
-  RCCL group + unpack) and the interior give halo ms, the exposed part of the
-  exchange and the overlap fraction, per rank (``config.pass_timing``);
-* each rank then re-times its own tile with the exchange disabled, all ranks
-  concurrently: ``weak_scaling_eff_same_run`` = solo time / multi-rank time;
-* after the timed run a small grid with the same process grid runs fast-math
-  and canonical passes through the same RCCL halo path; the tiles are gathered
-  on rank 0 and compared bitwise with a 1-rank run of the global grid on rank
-  0's GPU (``rccl_halo_bitwise_ok``); a mismatch fails the run.
+The run validates itself and says which rank is slow (VERDICT r1 item 1, r2
+items 1-3):
+* preflight, before the HBM-sized tile is allocated: the GPU-direct ring
+  send/recv of the reference's smoke test (scripts/rocmaware_test_selectdevice.jl:
+  16-23) over the halo transport (RCCL; RCCL to self on one GPU) and a tiny
+  halo check through the same path; a failure exits non-zero on every rank;
+* RCCL is mandatory at N > 1 (no fallback to the host-staged transport) and
+  every rank must drive a different physical GPU (PCI bus ids compared);
+* ``config.ranks_detail``: per rank its coordinates, neighbours, PCI bus id,
+  its OWN step time (taken before the closing barrier, so a slow GPU shows as
+  the one slow entry), its solo re-time with the exchange disabled, and its
+  per-pass HIP-event split (frame / halo / interior / exposed halo);
+* after the timed run: the fast-math drift bound of this run's length
+  (``fast_math_drift_max``: max |fast - canonical| on a small tile after
+  warmup + steps steps, every rank, must agree bitwise across GPUs), and the
+  halo check (a small grid with the bench's process grid through the real
+  halo path, gathered and compared bitwise with a 1-rank run; on one GPU the
+  grid is periodic and every halo goes through RCCL send/recv to itself).
+  Any error or mismatch on any rank makes EVERY rank exit non-zero and rank 0
+  still prints the record with the error; all check-phase collectives are
+  bounded (``--check-timeout``) and a watchdog ends a rank stuck in the GPU
+  runtime.
 """
 from __future__ import annotations
 
-import argparse
-import json
-import math
 import os
-import subprocess
-import sys
-import time
+
+# dmabuf IPC (the host driver supports no legacy IPC); before torch / HIP load
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import argparse  # noqa: E402
+import datetime  # noqa: E402
+import hashlib  # noqa: E402
+import json  # noqa: E402
+import math  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+import threading  # noqa: E402
+import time  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "T_eff (GB/s) + weak-scaling eff., 2D diffusion 1000 steps at 1/2/4/8 MI355X"
+# fast-math drift bound (max |fast - canonical| after the run's steps on a
+# random field in [0, 1)): diffusion is contractive, rounding differences do
+# not accumulate (3.3e-16 after 24..5000 steps, CPU twins, 514^2)
+DRIFT_BOUND = 1e-14
 
 
 def parse(argv=None):
@@ -91,12 +111,21 @@ def parse(argv=None):
     ap.add_argument("--solo-steps", type=int, default=-1,
                     help="steps re-timed with the exchange disabled for the same-run weak-scaling "
                          "efficiency (-1: = --steps; 0: skip)")
+    ap.add_argument("--preflight", type=int, default=1,
+                    help="ring send/recv + tiny halo check before the tile is allocated (1/0)")
     ap.add_argument("--check", type=int, default=-1,
-                    help="RCCL halo bitwise check after the run (1 on, 0 off, -1: on if N > 1)")
+                    help="halo bitwise check after the run (1 on, 0 off, -1: on with a GPU "
+                         "or N > 1)")
     ap.add_argument("--check-nx", type=int, default=0,
                     help="local tile of the halo check (0: 2050 on GPU, 130 on CPU)")
-    ap.add_argument("--check-self-rccl", action="store_true",
-                    help="one rank: run the halo check periodic with RCCL send/recv to self")
+    ap.add_argument("--check-self-rccl", type=int, nargs="?", const=1, default=-1,
+                    help="one rank: run the halo check periodic with RCCL send/recv to self "
+                         "(-1: on with a GPU)")
+    ap.add_argument("--check-timeout", type=float, default=300.0,
+                    help="seconds any check-phase collective (and the whole check phase, x3) "
+                         "may take before the run fails")
+    ap.add_argument("--drift-steps", type=int, default=-1,
+                    help="steps of the fast-math drift measurement (-1: warmup + steps; 0: off)")
     ap.add_argument("--shared-gpu-test", action="store_true",
                     help="functional test of the multi-process path on ONE GPU: ranks share "
                          "the card over the host-staged transport; the record says so and is "
@@ -119,13 +148,20 @@ def auto_tile(frac: float, cap: int) -> int:
     return max(n, 512)
 
 
-def fail(msg: str, rank: int) -> int:
+def log(rank: int, msg: str) -> None:
     print(f"bench.py rank {rank}: {msg}", file=sys.stderr, flush=True)
-    return 2
 
 
+class CheckFailed(RuntimeError):
+    """A correctness check failed (on this or another rank)."""
+
+
+# ---------------------------------------------------------------------------
+# bounded collectives over the gloo group (metadata only)
+# ---------------------------------------------------------------------------
 def gather_obj(obj, world: int):
-    """All-gather a small picklable object over the gloo group."""
+    """All-gather a small picklable object over the gloo group (main phase:
+    every rank reaches it; torchrun ends the job if one rank dies)."""
     if world == 1:
         return [obj]
     import torch.distributed as dist
@@ -137,19 +173,146 @@ def gather_obj(obj, world: int):
     return out
 
 
-def gather_to_root(obj, world: int):
-    """Gather a picklable object on rank 0 over the gloo group (others: None)."""
+def _wait(work, timeout_s: float, what: str) -> None:
+    try:
+        work.wait(timeout=datetime.timedelta(seconds=timeout_s))
+    except Exception as e:  # noqa: BLE001 - a peer is gone or stuck
+        raise CheckFailed(f"{what}: no answer from every rank within {timeout_s:.0f} s ({e})") \
+            from None
+
+
+def bounded_status(ok: bool, msg: str, world: int, timeout_s: float) -> list:
+    """All-gather (ok, message) from every rank, bounded: every rank learns
+    whether any rank failed and why, and nobody blocks longer than timeout_s."""
     if world == 1:
-        return [obj]
+        return [(ok, msg)]
+    import torch
     import torch.distributed as dist
 
     from rocm_mpi_amd.parallel import comm as C
 
-    out = [None] * world if dist.get_rank() == 0 else None
-    dist.gather_object(obj, out, dst=0, group=C._gloo_group())
-    return out
+    raw = msg.encode("utf-8", "replace")[:480]
+    buf = torch.zeros(512, dtype=torch.uint8)
+    buf[0] = 1 if ok else 0
+    buf[1] = len(raw) >> 8
+    buf[2] = len(raw) & 0xFF
+    if raw:
+        buf[3:3 + len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+    out = [torch.empty_like(buf) for _ in range(world)]
+    _wait(dist.all_gather(out, buf, group=C._gloo_group(), async_op=True), timeout_s,
+          "status exchange")
+    res = []
+    for b in out:
+        n = (int(b[1]) << 8) | int(b[2])
+        res.append((bool(b[0]), bytes(b[3:3 + n].tolist()).decode("utf-8", "replace")))
+    return res
 
 
+def agree(ok: bool, msg: str, world: int, timeout_s: float, what: str) -> None:
+    """Raise CheckFailed on EVERY rank if any rank failed (bounded)."""
+    st = bounded_status(ok, msg, world, timeout_s)
+    bad = [(r, m) for r, (o, m) in enumerate(st) if not o]
+    if bad:
+        raise CheckFailed(f"{what} failed on rank(s) " +
+                          "; ".join(f"{r}: {m}" for r, m in bad))
+
+
+def bounded_gather_tiles(field, world: int, timeout_s: float):
+    """The equal-shape tiles of every rank on rank 0 (host copies), bounded."""
+    host = field.detach().cpu().contiguous()
+    if world == 1:
+        return [host]
+    import torch
+    import torch.distributed as dist
+
+    from rocm_mpi_amd.parallel import comm as C
+
+    lst = [torch.empty_like(host) for _ in range(world)] if dist.get_rank() == 0 else None
+    _wait(dist.gather(host, lst, dst=0, group=C._gloo_group(), async_op=True), timeout_s,
+          "tile gather")
+    return lst
+
+
+_DONE_KEY = "rma/bench/rank0_reported"
+
+
+def signal_reported(world: int) -> None:
+    """Rank 0 has printed its record (or is about to exit without one)."""
+    if world > 1:
+        try:
+            import torch.distributed as dist
+
+            dist.distributed_c10d._get_default_store().set(_DONE_KEY, "1")
+        except Exception:  # noqa: BLE001 - best effort on an error path
+            pass
+
+
+def wait_reported(world: int, timeout_s: float) -> None:
+    """A failing rank > 0 waits (bounded) for rank 0's record before it exits:
+    torchrun ends the whole job as soon as one rank exits non-zero."""
+    if world > 1:
+        try:
+            import torch.distributed as dist
+
+            dist.distributed_c10d._get_default_store().wait(
+                [_DONE_KEY], datetime.timedelta(seconds=timeout_s))
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class Watchdog:
+    """Ends this rank if a phase outlives its deadline (a rank stuck inside
+    the GPU runtime, RCCL or a gloo receive cannot be interrupted from
+    Python): rank 0 first prints the record it has, with the failure, so the
+    run still reports; the other ranks give it time to do so."""
+
+    def __init__(self, rank: int, world: int, seconds: float, what: str, on_fire=None):
+        self.rank, self.world, self.what, self.on_fire = rank, world, what, on_fire
+        self._t = threading.Timer(seconds, self._fire)
+        self._t.daemon = True
+        self._t.start()
+
+    def _fire(self) -> None:
+        msg = f"watchdog: {self.what} did not finish in time"
+        log(self.rank, msg + "; exiting")
+        try:
+            if self.rank == 0 and self.on_fire is not None:
+                self.on_fire(msg)
+        finally:
+            finish_failed(self.rank, self.world, 6, 30.0)
+
+    def cancel(self) -> None:
+        self._t.cancel()
+
+
+def finish_failed(rank: int, world: int, rc: int, wait_s: float) -> None:
+    """Exit a failed run on this rank without touching the (possibly broken)
+    process groups: rank 0 after its record, the others after rank 0's."""
+    if rank == 0:
+        signal_reported(world)
+    else:
+        wait_reported(world, wait_s)
+    hard_exit(rank, rc)
+
+
+def hard_exit(rank: int, rc: int) -> None:
+    record_rc(rank, rc)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(rc)
+
+
+def record_rc(rank: int, rc: int) -> None:
+    """RMA_BENCH_RC_DIR: every rank writes its exit status (tests)."""
+    d = os.environ.get("RMA_BENCH_RC_DIR")
+    if d:
+        with open(os.path.join(d, f"rc{rank}"), "w") as f:
+            f.write(str(rc))
+
+
+# ---------------------------------------------------------------------------
+# checks
+# ---------------------------------------------------------------------------
 def summarize_timings(ts: list, exchange: bool = True) -> dict:
     """Mean per-pass frame / halo / interior / exposed-halo ms of one rank.
     Without a neighbour (exchange=False) the halo events bracket an empty
@@ -170,85 +333,180 @@ def summarize_timings(ts: list, exchange: bool = True) -> dict:
     return mean
 
 
-def halo_check(a, dims, K: int, dev: str, world: int, self_rccl: bool = False) -> tuple[bool, dict]:
+def _run_grid(nx, ny, dims_, K, steps_fast, steps_can, periodic, loopback=None, device=None,
+              via=False):
+    """A small grid through the production path: steps_fast fast-math steps,
+    then steps_can canonical steps. Returns (field, coords, nxyz_g, transport, plan)."""
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    ol = 2 * K
+    per = 1 if periodic else 0
+    kw = dict(dimx=dims_[0], dimy=dims_[1], overlaps=(ol, ol, 2), halowidths=(K, K, 1),
+              quiet=True, periodx=per, periody=per)
+    if loopback is not None:
+        kw.update(loopback=loopback, device=device)
+    elif via:
+        kw.update(transport="rccl", self_via_transport=True)
+    gg.init_global_grid(nx, ny, 1, **kw)
+    try:
+        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny,
+                                        nt=max(1, steps_fast + steps_can), init="random",
+                                        quiet=True, dims=(*dims_, 0), temporal=K,
+                                        periods=(per, per, 0), fast_math=True, device=device))
+        plan = m.plan(steps_fast)
+        m.step(steps_fast)
+        if steps_can:
+            m.set_temporal(K, fast_math=False)
+            m.step(steps_can)
+        m.synchronize()
+        out = (m.field.clone(), m.g.coords, m.g.nxyz_g, m.g.transport, plan)
+        m.close()
+    finally:
+        gg.finalize_global_grid(finalize_dist=False)
+    return out
+
+
+def _local_device(dev: str) -> str:
+    import torch
+
+    return dev if dev == "cpu" else f"cuda:{torch.cuda.current_device()}"
+
+
+def _restore_stream(dev: str):
+    """The loopback grid installs its own stream: put the caller's back."""
+    import torch
+
+    prev = torch.cuda.current_stream() if dev != "cpu" else None
+
+    class _R:
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *exc):
+            if prev is not None:
+                torch.cuda.set_stream(prev)
+            return False
+
+    return _R()
+
+
+def halo_check(n: int, dims, K: int, dev: str, world: int, rank: int, timeout_s: float,
+               self_rccl: bool = False, inject: bool = True) -> dict:
     """Run a small grid with the bench's process grid through the real halo
-    path (fast-math passes, then canonical passes), gather every rank's tile
-    on rank 0 and compare bitwise with a 1-rank run of the global grid on rank
-    0's device. Returns (ok on every rank, info).
+    path (37 fast-math steps, then 23 canonical), gather every rank's tile on
+    rank 0 and compare bitwise with a 1-rank run of the global grid on rank
+    0's device. Raises CheckFailed on every rank on any error or mismatch.
 
     self_rccl (one rank): the check grid is periodic and its halos go through
     RCCL send/recv to itself; the reference is the same periodic tile with
     local self copies (exercises this path with real RCCL traffic on 1 GPU)."""
     import numpy as np
-    import torch
 
-    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
     from rocm_mpi_amd.parallel import comm as C
-    from rocm_mpi_amd.parallel import implicit_grid as gg
 
-    n = a.check_nx or (2050 if dev != "cpu" else max(130, 6 * K + 2))
     n_fast, n_can = 37, 23
     ol = 2 * K
-    per = 1 if self_rccl else 0
+    t0 = time.perf_counter()
+    err = ""
+    field = coords = None
+    info = {"local_tile": [n, n], "steps": [n_fast, n_can], "self_rccl": self_rccl}
+    try:
+        fault = os.environ.get("RMA_BENCH_CHECK_RAISE", "") if inject and rank == world - 1 else ""
+        if fault == "before":  # peers then block in the exchange: the watchdog path
+            raise RuntimeError("injected halo-check failure before the run")
+        field, coords, nxyz_g, transport, plan = _run_grid(n, n, dims, K, n_fast, n_can,
+                                                           self_rccl, via=self_rccl)
+        if fault == "after":
+            raise RuntimeError("injected halo-check failure after the run")
+        info.update(global_grid=list(nxyz_g[:2]), transport=transport, fast_math_plan=plan)
+        if inject and os.environ.get("RMA_BENCH_CHECK_CORRUPT") == "1" and rank == world - 1:
+            field[n // 2, n // 2] += 1e-12  # negative test (tests/test_multiprocess_cpu.py)
+    except Exception as e:  # noqa: BLE001 - reported to every rank below
+        err = f"{type(e).__name__}: {e}"
+    agree(not err, err, world, timeout_s, "halo check run")
+    import torch
 
-    def run(nx, ny, dims_, loopback=None, device=None, via=False):
-        kw = dict(dimx=dims_[0], dimy=dims_[1], overlaps=(ol, ol, 2), halowidths=(K, K, 1),
-                  quiet=True, periodx=per, periody=per)
-        if loopback is not None:
-            kw.update(loopback=loopback, device=device)
-        elif via:
-            kw.update(transport="rccl", self_via_transport=True)
-        gg.init_global_grid(nx, ny, 1, **kw)
-        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=n_fast + n_can,
-                                        init="random", quiet=True, dims=(*dims_, 0), temporal=K,
-                                        periods=(per, per, 0), fast_math=True, device=device))
-        m.step(n_fast)
-        m.set_temporal(K, fast_math=False)
-        m.step(n_can)
-        m.synchronize()
-        field, coords, nxyz_g, transport = m.field.clone(), m.g.coords, m.g.nxyz_g, m.g.transport
-        plan = m.plan(n_fast)
-        m.close()
-        gg.finalize_global_grid(finalize_dist=False)
-        return field, coords, nxyz_g, transport, plan
+    cxy = torch.tensor([coords[0], coords[1]], dtype=torch.float64)
+    all_xy = bounded_gather_tiles(cxy, world, timeout_s)
+    tiles = bounded_gather_tiles(field, world, timeout_s)
+    bad, err = 0, ""
+    if rank == 0:
+        try:
+            with _restore_stream(dev):
+                rn = (n, n) if self_rccl else tuple(info["global_grid"])
+                ref = _run_grid(*rn, (1, 1), K, n_fast, n_can, self_rccl,
+                                loopback=(C.LoopbackHub(1), 0), device=_local_device(dev))[0]
+            ref = ref.cpu().numpy()
+            for xy, T in zip(all_xy, tiles):
+                gx0, gy0 = int(xy[0]) * (n - ol), int(xy[1]) * (n - ol)
+                if not np.array_equal(T.numpy(), ref[gy0:gy0 + n, gx0:gx0 + n]):
+                    bad += 1
+        except Exception as e:  # noqa: BLE001
+            err = f"reference run: {type(e).__name__}: {e}"
+    st = bounded_status(not err and bad == 0, err or f"{bad} tile(s) differ", world, timeout_s)
+    info["tiles_mismatched"] = bad if rank == 0 else None
+    info["seconds"] = round(time.perf_counter() - t0, 3)
+    if not st[0][0]:
+        info["tiles_mismatched"] = bad if rank == 0 else -1
+        raise CheckFailed(f"halo check: {st[0][1]}", info)
+    return info
+
+
+def drift_check(n: int, K: int, steps: int, dev: str, world: int, timeout_s: float) -> dict:
+    """max |fast - canonical| on an n x n random tile after `steps` steps
+    (every rank on its own GPU, 1-rank grid); the fast fields must agree
+    bitwise across ranks (same kernels, same data) and stay within DRIFT_BOUND."""
+    from rocm_mpi_amd.parallel import comm as C
 
     t0 = time.perf_counter()
-    field, coords, nxyz_g, transport, plan = run(n, n, dims, via=self_rccl)
-    if os.environ.get("RMA_BENCH_CHECK_CORRUPT") == "1" and int(os.environ.get("RANK", "0")) == world - 1:
-        field[n // 2, n // 2] += 1e-12  # negative test of the check (tests/test_multiprocess_cpu.py)
-    # tiles to rank 0 (host copies: at most a few hundred MB)
-    tiles = gather_to_root((coords, field.cpu().numpy()), world)
-    ok = True
-    info = {"local_tile": [n, n], "global_grid": list(nxyz_g[:2]), "transport": transport,
-            "steps": [n_fast, n_can], "fast_math_plan": plan, "self_rccl": self_rccl}
-    rank = int(os.environ.get("RANK", "0"))
-    if rank == 0:
-        import torch.cuda as tc
+    err, drift, digest = "", None, ""
+    try:
+        with _restore_stream(dev):
+            kw = dict(loopback=(C.LoopbackHub(1), 0), device=_local_device(dev))
+            fast = _run_grid(n, n, (1, 1), K, steps, 0, False, **kw)
+            can = _run_grid(n, n, (1, 1), K, 0, steps, False, **kw)
+        drift = float((fast[0] - can[0]).abs().max())
+        digest = hashlib.sha1(fast[0].cpu().numpy().tobytes()).hexdigest()[:16]
+        if not drift <= DRIFT_BOUND:
+            err = f"fast-math drift {drift:.3e} > bound {DRIFT_BOUND:.0e}"
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"
+    st = bounded_status(not err, err or f"{digest} {drift!r}", world, timeout_s)
+    bad = [f"{r}: {m}" for r, (o, m) in enumerate(st) if not o]
+    if not bad and len({m.split()[0] for _, m in st}) != 1:
+        bad = ["fast-math fields differ across GPUs: " + ", ".join(m for _, m in st)]
+    info = {"tile": [n, n], "steps": steps, "fast_math_drift_max": drift, "bound": DRIFT_BOUND,
+            "fast_field_sha1_16": digest, "seconds": round(time.perf_counter() - t0, 3)}
+    if bad:
+        raise CheckFailed("fast-math drift check: " + "; ".join(bad), info)
+    return info
 
-        hub = C.LoopbackHub(1)
-        device = dev if dev == "cpu" else f"cuda:{tc.current_device()}"
-        prev = tc.current_stream() if dev != "cpu" else None
-        rn = (n, n) if self_rccl else (nxyz_g[0], nxyz_g[1])
-        try:
-            ref = run(*rn, (1, 1), loopback=(hub, 0), device=device)[0]
-        finally:
-            if prev is not None:
-                tc.set_stream(prev)
-        ref = ref.cpu().numpy()
-        bad = 0
-        for (cx, cy, _), T in tiles:
-            gx0, gy0 = cx * (n - ol), cy * (n - ol)
-            if not np.array_equal(T, ref[gy0:gy0 + n, gx0:gx0 + n]):
-                bad += 1
-        ok = bad == 0
-        info["tiles_mismatched"] = bad
-    ok = bool(gather_obj(ok, world)[0])
+
+def preflight(dims, K: int, dev: str, world: int, rank: int, gpu: bool, n: int,
+              timeout_s: float) -> dict:
+    """Before the HBM-sized tile: the ring send/recv of the reference's smoke
+    test over the halo transport, then the halo check on a tiny grid."""
+    from rocm_mpi_amd.apps import rocmaware_test_selectdevice as smoke
+
+    t0 = time.perf_counter()
+    err = ""
+    transport = "rccl" if gpu and world == 1 else "auto"
+    try:
+        vals = smoke.run(4, transport=transport, verbose=False, self_ring=world == 1)
+        if any(v != float((rank - 1) % world) for v in vals):
+            err = f"ring received {vals}, expected {(rank - 1) % world}"
+    except Exception as e:  # noqa: BLE001
+        err = f"ring send/recv: {type(e).__name__}: {e}"
+    agree(not err, err, world, timeout_s, "preflight ring")
+    info = {"ring_ok": True, "ring_ranks": world}
+    info["halo"] = halo_check(n, dims, K, dev, world, rank, timeout_s,
+                              self_rccl=gpu and world == 1, inject=False)
     info["seconds"] = round(time.perf_counter() - t0, 3)
-    if dev != "cpu":
-        torch.cuda.synchronize()
-    return ok, info
+    return info
 
 
+# ---------------------------------------------------------------------------
 def main(argv=None) -> int:
     a = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -260,10 +518,18 @@ def main(argv=None) -> int:
                *(argv if argv is not None else sys.argv[1:])]
         return subprocess.call(cmd)
     rank = int(os.environ.get("RANK", "0"))
+    rc = run(a, world, rank)
+    record_rc(rank, rc)
+    return rc
+
+
+def run(a, world: int, rank: int) -> int:
     if world != a.gpus:
-        return fail(f"WORLD_SIZE={world} but --gpus {a.gpus}", rank)
+        log(rank, f"WORLD_SIZE={world} but --gpus {a.gpus}")
+        return 2
     if not 1 <= a.temporal <= 24:
-        return fail(f"--temporal must be 1..24, got {a.temporal}", rank)
+        log(rank, f"--temporal must be 1..24, got {a.temporal}")
+        return 2
 
     gpu = a.device == "cuda"
     shared = a.shared_gpu_test and gpu and world > 1
@@ -273,6 +539,15 @@ def main(argv=None) -> int:
         # a scaling point must never silently run on the host-staged transport
         os.environ["RMA_RCCL_STRICT"] = "1"
         os.environ["RMA_TRANSPORT"] = "rccl"
+    diag = {k: v for k, v in sorted(os.environ.items())
+            if k.startswith("RMA_DIAG") or k in ("RMA_FRAME_SIDES", "RMA_FRAME_ALIGNED",
+                                                 "RMA_PASS_COSTS", "RMA_HALO_BATCH",
+                                                 "RMA_FRAME_FILL", "RMA_EXEC_STREAMS")}
+    check_on = a.check == 1 or (a.check < 0 and (gpu or world > 1))
+    if check_on and os.environ.get("RMA_DIAG_SKIP_EXCHANGE", "0") == "1":
+        log(rank, "RMA_DIAG_SKIP_EXCHANGE=1 skips every halo exchange: refused with the halo "
+                  "check on (--check 0 for a diagnosis run)")
+        return 2
 
     import torch
 
@@ -280,13 +555,16 @@ def main(argv=None) -> int:
     from rocm_mpi_amd.parallel import comm as C
 
     if gpu and not torch.cuda.is_available():
-        return fail("needs an MI355X (no GPU visible)", rank)
+        log(rank, "needs an MI355X (no GPU visible)")
+        return 2
     if not gpu and not a.nx:
-        return fail("--device cpu needs --nx", rank)
+        log(rank, "--device cpu needs --nx")
+        return 2
     if world > 1:
         C.init_distributed(None if gpu and not shared else "gloo")
     local, _ = C.node_local_rank(rank, world)
     dev = str(C.select_device(local)) if gpu else "cpu"
+    tmo = a.check_timeout
 
     # one rank per PHYSICAL GPU: compare PCI bus ids (shared GPUs would make
     # the scaling point meaningless)
@@ -299,19 +577,68 @@ def main(argv=None) -> int:
             uuid = getattr(torch.cuda.get_device_properties(torch.cuda.current_device()),
                            "uuid", None)
             if uuid is None:
-                return fail(f"cannot identify the physical GPU (PCI bus id: {e})", rank)
+                log(rank, f"cannot identify the physical GPU (PCI bus id: {e})")
+                return 2
             bus = f"uuid-{uuid}"
     else:
         bus = f"cpu-rank-{rank}"
     buses = gather_obj(bus, world)
     n_gpus = len(set(buses)) if gpu else world
     if gpu and n_gpus != world and not shared:
-        return fail(f"{world} ranks share {n_gpus} physical GPU(s) (PCI bus ids {buses}); "
-                    "a scaling point needs one GPU per rank", rank)
+        log(rank, f"{world} ranks share {n_gpus} physical GPU(s) (PCI bus ids {buses}); "
+                  "a scaling point needs one GPU per rank")
+        return 2
 
     def sync():
         if gpu:
             torch.cuda.synchronize()
+
+    dims = tuple(int(v) for v in a.dims.split(",")) + (0,)
+    bw = tuple(int(v) for v in a.b_width.split(","))
+    K = a.temporal if a.variant != "kp" else 1
+    check_n = a.check_nx or (2050 if gpu else max(130, 6 * K + 2))
+    self_rccl = (a.check_self_rccl == 1 or (a.check_self_rccl < 0 and gpu)) and world == 1 and gpu
+
+    # the record is built up as the run goes: a failing phase still reports
+    out = {"metric": METRIC + (" [shared-GPU functional test]" if shared else ""),
+           "value": None, "unit": "GB/s", "n_gpus": n_gpus, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": None, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp64",
+           "data": "synthetic: counter-based uniform [0,1) random-init temperature field",
+           "config": {"model": f"diffusion_2D_{a.variant}", "ranks": world,
+                      "pci_bus_ids": buses if gpu else None, "shared_gpu_test": bool(shared),
+                      "diag_env": diag}}
+    printed = [False]
+
+    def emit(error: str | None = None) -> None:
+        if rank != 0 or printed[0]:
+            return
+        printed[0] = True
+        if error:
+            out["error"] = error[:2000]
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+
+    def fail_run(what: str, e: Exception, rc: int) -> int:
+        log(rank, f"{what}: {e}")
+        emit(f"{what}: {e}")
+        finish_failed(rank, world, rc, 3 * tmo + 30)
+        return rc  # not reached
+
+    # --- preflight: before the HBM-sized allocation --------------------------
+    if a.preflight and a.variant != "kp":
+        wd = Watchdog(rank, world, 3 * tmo, "preflight", emit)
+        try:
+            out["config"]["preflight"] = preflight(dims[:2], K, dev, world, rank, gpu,
+                                                   max(130, 6 * K + 2), tmo)
+        except CheckFailed as e:
+            out["config"]["preflight"] = {"error": str(e.args[0])}
+            return fail_run("preflight", e, 5)
+        finally:
+            wd.cancel()
 
     nx = a.nx or auto_tile(a.hbm_frac, a.max_tile)
     if world > 1 and not a.nx:
@@ -321,9 +648,6 @@ def main(argv=None) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=C._gloo_group())
         nx = int(t.item())
     ny = a.ny or nx
-    dims = tuple(int(v) for v in a.dims.split(",")) + (0,)
-    bw = tuple(int(v) for v in a.b_width.split(","))
-    K = a.temporal if a.variant != "kp" else 1
     cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup, device=dev,
                           warmup=a.warmup, init="random", b_width=bw, dims=dims,
                           chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
@@ -338,7 +662,8 @@ def main(argv=None) -> int:
     g = model.g
     comm = g.comm
     if gpu and world > 1 and g.transport != "rccl" and not shared:
-        return fail(f"halo transport is {g.transport!r}, a multi-GPU point needs RCCL", rank)
+        log(rank, f"halo transport is {g.transport!r}, a multi-GPU point needs RCCL")
+        return 2
     model.synchronize()
     comm.barrier()
     setup_s = time.perf_counter() - t_setup
@@ -354,9 +679,9 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     model.step(a.steps)
     sync()
+    own_s = time.perf_counter() - t0  # this rank's own time, before the closing barrier
     comm.barrier()
-    t1 = time.perf_counter()
-    local_s = t1 - t0
+    local_s = time.perf_counter() - t0
     wall = comm.allreduce(local_s, "max")
     nbrs = any(p >= 0 for side in g.neighbors[:2] for p in side)
     timings = summarize_timings(model.pass_timings(), exchange=nbrs)
@@ -364,7 +689,6 @@ def main(argv=None) -> int:
     bad = float(model.field[:: max(1, ny // 64), :: max(1, nx // 64)].isfinite().logical_not().sum())
     bad = comm.allreduce(bad, "sum")
     a_eff = 3 * nx * ny * 8 / 1e9
-    teff_ranks = gather_obj(a_eff / (local_s / a.steps), world)
 
     def side_teff(Kside, fast, steps):
         model.set_temporal(Kside, fast_math=fast)
@@ -380,9 +704,10 @@ def main(argv=None) -> int:
         return a_eff / (s1 / steps)
 
     # same-run weak-scaling reference: every rank re-times its tile without
-    # the exchange (one launch per pass), all ranks concurrently
+    # the exchange (one launch per pass), all ranks concurrently; each rank's
+    # own (pre-barrier) solo time identifies a slow GPU independently of the halo
     solo_steps = a.steps if a.solo_steps < 0 else a.solo_steps
-    solo = None
+    solo = solo_own = None
     if solo_steps > 0:
         model.set_solo(True)
         model.step(a.warmup)
@@ -392,9 +717,20 @@ def main(argv=None) -> int:
         s0 = time.perf_counter()
         model.step(solo_steps)
         sync()
+        solo_own = (time.perf_counter() - s0) / solo_steps
         comm.barrier()
         solo = comm.allreduce(time.perf_counter() - s0, "max") / solo_steps
         model.set_solo(False)
+
+    detail = {"rank": rank, "coords": list(g.coords[:2]),
+              "neighbors": [list(p) for p in g.neighbors[:2]], "pci_bus_id": bus,
+              "ms_per_step": round(own_s / a.steps * 1e3, 6),
+              "teff_GBps": round(a_eff / (own_s / a.steps), 2),
+              "solo_ms_per_step": round(solo_own * 1e3, 6) if solo_own else None,
+              "pass_timing": {k: (round(v, 4) if isinstance(v, float) else v)
+                              for k, v in timings.items() if k != "note"}}
+    ranks_detail = gather_obj(detail, world)
+    teff_ranks = [d["teff_GBps"] for d in ranks_detail]
 
     # side measurements on the same tile: the canonical (bitwise) K-step
     # passes and the one-step kernel (24 B/cell/step at the HBM roofline)
@@ -428,17 +764,9 @@ def main(argv=None) -> int:
             kinfo = {"kernel": names[kern], "vec": kvec, "chunk_rows": a.chunk2 or kch,
                      "stages": native().pipe_default_stages(depth) if kern >= 9 else None}
     model.close()
-
-    check_on = a.check == 1 or (a.check < 0 and world > 1)
-    check_ok, check_info = None, None
-    if check_on and a.variant != "kp":
-        try:
-            check_ok, check_info = halo_check(a, dims[:2], K, dev, world,
-                                              self_rccl=a.check_self_rccl and world == 1 and gpu)
-        except Exception as e:  # noqa: BLE001 - keep the timed record; say the check broke
-            check_ok, check_info = None, {"error": f"{type(e).__name__}: {e}"[:500]}
-            print(f"bench.py rank {rank}: halo check did not complete: {e}", file=sys.stderr,
-                  flush=True)
+    del model
+    if gpu:
+        torch.cuda.empty_cache()
 
     t_it = wall / a.steps
     teff_gpu = a_eff / t_it
@@ -452,79 +780,91 @@ def main(argv=None) -> int:
         par = f"halo: {tdesc}" + (", boundary frame + exchange on a high-priority stream "
                                   "overlapped with the interior" if a.variant == "perf_hide"
                                   else ", exchange after each pass")
-    eff_same = (solo / t_it) if solo else None
+    # without a neighbour the solo re-time IS the run: no same-run efficiency
+    eff_same = (solo / t_it) if solo and nbrs else None
     if shared:
         par = f"SHARED-GPU FUNCTIONAL TEST, {world} ranks on {n_gpus} GPU, not a scaling point; {par}"
-    out = {
-        "metric": METRIC + (" [shared-GPU functional test]" if shared else ""),
-        "value": round(total, 2),
-        "unit": "GB/s",
-        "n_gpus": n_gpus,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(t_it * 1e3, 6),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "fp64",
-        "data": "synthetic: counter-based uniform [0,1) random-init temperature field",
-        "config": {
-            "model": f"diffusion_2D_{a.variant}",
-            "global_batch": g.nxyz_g[0] * g.nxyz_g[1],
-            "seq_len": None,
-            "parallelism": f"2D domain decomposition dims {g.dims[0]}x{g.dims[1]} ({par})",
-            "ranks": world,
-            "local_grid": [nx, ny],
-            "global_grid": [g.nxyz_g[0], g.nxyz_g[1]],
-            "teff_per_gpu_GBps": round(teff_gpu, 2),
-            "teff_per_gpu_min_GBps": round(min(teff_ranks), 2),
-            "teff_per_gpu_max_GBps": round(max(teff_ranks), 2),
-            "a_eff_GB_per_step": round(a_eff, 6),
-            "max_steps_per_pass": K,
-            "passes_warmup": plan_warm,
-            "passes_timed": plan_timed,
-            "kstep_kernel": kinfo,
-            "fast_math": fast_used,
-            "pass_timing": timings,
-            "solo_ms_per_step": round(solo * 1e3, 6) if solo else None,
-            "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,
-            "rccl_halo_bitwise_ok": check_ok,
-            "halo_check": check_info,
-            "teff_note": ("T_eff = A_eff/t_step with A_eff = 3*nx*ny*8 B (reference "
-                          "perf.jl:55-58). With temporal blocking every step of every cell "
-                          "is computed, but HBM is read/written once per pass of up to "
-                          f"{K} steps, so T_eff exceeds the HBM bandwidth and is a time per "
-                          "step, not a memory throughput; teff_single_step_kernel_GBps is "
-                          "the one-step kernel on the same tile (the like-for-like memory "
-                          "number). fast_math: the passes evaluate the same fp64 update as "
-                          "a 5-point sum with one folded per-cell factor and FMAs "
-                          "(rounding-level deviation from the canonical update, bitwise "
-                          "equal to its CPU twin, tests/test_pipe_gpu.py); "
-                          "teff_bitwise_kstep_GBps is the canonical K-step kernel on the "
-                          "same tile") if K > 1 else "",
-            "teff_single_step_kernel_GBps": round(single, 2) if single else None,
-            "teff_bitwise_kstep_GBps": round(canonical, 2) if canonical else None,
-            "bitwise_kstep_steps_per_pass": kc if canonical else None,
-            "overlap": list(g.overlaps[:2]),
-            "transport": g.transport,
-            "pci_bus_ids": buses if gpu else None,
-            "hipgraph": bool(a.graph),
-            "setup_s": round(setup_s, 3),
-            "nonfinite_cells_sampled": int(bad),
-            "shared_gpu_test": bool(shared),
-        },
-    }
-    if rank == 0:
-        line = json.dumps(out)
-        print(line, flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                f.write(line + "\n")
+    out.update({"value": round(total, 2), "ms_per_step": round(t_it * 1e3, 6)})
+    out["config"].update({
+        "global_batch": g.nxyz_g[0] * g.nxyz_g[1],
+        "seq_len": None,
+        "parallelism": f"2D domain decomposition dims {g.dims[0]}x{g.dims[1]} ({par})",
+        "local_grid": [nx, ny],
+        "global_grid": [g.nxyz_g[0], g.nxyz_g[1]],
+        "teff_per_gpu_GBps": round(teff_gpu, 2),
+        "teff_per_gpu_min_GBps": round(min(teff_ranks), 2),
+        "teff_per_gpu_max_GBps": round(max(teff_ranks), 2),
+        "slowest_rank": int(max(range(world), key=lambda r: ranks_detail[r]["ms_per_step"])),
+        "a_eff_GB_per_step": round(a_eff, 6),
+        "max_steps_per_pass": K,
+        "passes_warmup": plan_warm,
+        "passes_timed": plan_timed,
+        "kstep_kernel": kinfo,
+        "fast_math": fast_used,
+        "pass_timing": timings,
+        "ranks_detail": ranks_detail,
+        "solo_ms_per_step": round(solo * 1e3, 6) if solo else None,
+        "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,
+        "rccl_halo_bitwise_ok": None,
+        "halo_check": None,
+        "fast_math_drift_max": None,
+        "drift_check": None,
+        "teff_note": ("T_eff = A_eff/t_step with A_eff = 3*nx*ny*8 B (reference "
+                      "perf.jl:55-58). With temporal blocking every step of every cell "
+                      "is computed, but HBM is read/written once per pass of up to "
+                      f"{K} steps, so T_eff exceeds the HBM bandwidth and is a time per "
+                      "step, not a memory throughput; teff_single_step_kernel_GBps is "
+                      "the one-step kernel on the same tile (the like-for-like memory "
+                      "number). fast_math: the passes evaluate the same fp64 update as "
+                      "a 5-point sum with one folded per-cell factor and FMAs "
+                      "(rounding-level deviation from the canonical update, bounded in "
+                      "fast_math_drift_max for this run's length; bitwise "
+                      "equal to its CPU twin, tests/test_pipe_gpu.py); "
+                      "teff_bitwise_kstep_GBps is the canonical K-step kernel on the "
+                      "same tile") if K > 1 else "",
+        "teff_single_step_kernel_GBps": round(single, 2) if single else None,
+        "teff_bitwise_kstep_GBps": round(canonical, 2) if canonical else None,
+        "bitwise_kstep_steps_per_pass": kc if canonical else None,
+        "overlap": list(g.overlaps[:2]),
+        "transport": g.transport,
+        "hipgraph": bool(a.graph),
+        "setup_s": round(setup_s, 3),
+        "nonfinite_cells_sampled": int(bad),
+    })
+
+    # --- correctness of this run's code paths (bounded; any failure fails all)
+    rc = 0 if bad == 0 else 3
+    drift_steps = (a.warmup + a.steps) if a.drift_steps < 0 else a.drift_steps
+    if (check_on or drift_steps) and a.variant != "kp":
+        wd = Watchdog(rank, world, 3 * tmo, "check phase", emit)
+        try:
+            if drift_steps and fast_used and K > 1:
+                try:
+                    di = drift_check(check_n, K, drift_steps, dev, world, tmo)
+                except CheckFailed as e:
+                    out["config"]["drift_check"] = e.args[1] if len(e.args) > 1 else None
+                    raise
+                out["config"]["drift_check"] = di
+                out["config"]["fast_math_drift_max"] = di["fast_math_drift_max"]
+            if check_on:
+                try:
+                    hc = halo_check(check_n, dims[:2], K, dev, world, rank, tmo,
+                                    self_rccl=self_rccl)
+                except CheckFailed as e:
+                    out["config"]["rccl_halo_bitwise_ok"] = False
+                    out["config"]["halo_check"] = dict(e.args[1] if len(e.args) > 1 else {},
+                                                       error=str(e.args[0]))
+                    raise
+                out["config"]["halo_check"] = hc
+                out["config"]["rccl_halo_bitwise_ok"] = True
+        except CheckFailed as e:
+            return fail_run("check", CheckFailed(e.args[0]), 4)
+        finally:
+            wd.cancel()
+    emit()
     if world > 1:
         C.shutdown_distributed()
-    if check_ok is False:
-        return 4
-    return 0 if bad == 0 else 3
+    return rc
 
 
 if __name__ == "__main__":

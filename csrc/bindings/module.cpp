@@ -363,7 +363,9 @@ PYBIND11_MODULE(_C, m) {
       .def("capturable", &HaloExchanger::capturable)
       .def("set_self_via_transport", &HaloExchanger::set_self_via_transport)
       .def_property_readonly("neighbors", &HaloExchanger::neighbors)
-      .def_property_readonly("bytes_sent_last", &HaloExchanger::bytes_sent_last);
+      .def_property_readonly("bytes_sent_last", &HaloExchanger::bytes_sent_last)
+      .def_property_readonly("plan_hits", &HaloExchanger::plan_hits)
+      .def_property_readonly("plan_misses", &HaloExchanger::plan_misses);
 
   // ---------------- executor ----------------
   m.def("pipe_chunk_rows", &pipe_chunk_rows, py::arg("K"), py::arg("ny"),
@@ -486,7 +488,26 @@ PYBIND11_MODULE(_C, m) {
                                return v;
                              })
       .def_property_readonly("interior_rect",
-                             [](const DiffusionExecutor& e) { return from_rect(e.interior_rect()); });
+                             [](const DiffusionExecutor& e) { return from_rect(e.interior_rect()); })
+      .def(
+          "geometry",
+          [](DiffusionExecutor& e, int K) {
+            const PassGeom& g = e.geometry(K);
+            auto rl = [](const std::vector<Rect>& v) {
+              std::vector<Rect4> o;
+              for (auto& r : v) o.push_back(from_rect(r));
+              return o;
+            };
+            py::dict d;
+            d["aligned"] = g.aligned;
+            d["out"] = from_rect(g.out);
+            d["frame"] = rl(g.frame);
+            d["frame_wide"] = rl(g.frame_wide);
+            d["frame_tall"] = rl(g.frame_tall);
+            d["interior"] = from_rect(g.interior);
+            return d;
+          },
+          py::arg("K"));
 
   // ---------------- tracing ----------------
   m.def("trace_enable", &trace_enable);

@@ -54,11 +54,31 @@ class HaloExchanger {
   }
   // Route self-neighbours (periodic, one process along a dim) through the
   // transport instead of a local copy (tests the P2P path on one GPU).
-  void set_self_via_transport(bool on) { self_via_comm_ = on && comm_ != nullptr; }
+  void set_self_via_transport(bool on) {
+    self_via_comm_ = on && comm_ != nullptr;
+    cache_.clear();
+  }
   const std::array<std::array<int, 2>, 3>& neighbors() const { return nbr_; }
   int64_t bytes_sent_last() const { return bytes_last_; }
+  // exchanges served from the plan cache / planned afresh (tests, diagnosis)
+  int64_t plan_hits() const { return hits_; }
+  int64_t plan_misses() const { return misses_; }
 
  private:
+  // One planned exchange: the host plan plus its copy batches with every
+  // pointer resolved (fields and pack buffers). The executor alternates
+  // between two fields (T, T2), so a few entries serve the steady state and
+  // an exchange costs only its launches and the RCCL group.
+  struct Planned {
+    std::vector<HaloField> fields;
+    int dims_mask = 0;
+    HaloPlan plan;
+    std::vector<std::array<std::vector<CopyBatch>, 2>> batches;  // per plan dim, phase 0 / 1
+    std::vector<std::vector<void*>> send_ptr, recv_ptr;          // per plan dim, message order
+    uint64_t used = 0;
+  };
+  static constexpr size_t kPlanCache = 4;
+  const Planned& planned(const std::vector<HaloField>& fields, int dims_mask);
   void* buffer(size_t slot, size_t bytes);
   P2PTransport* comm_;
   int self_;
@@ -67,6 +87,9 @@ class HaloExchanger {
   std::vector<void*> bufs_;
   std::vector<size_t> buf_bytes_;
   int64_t bytes_last_ = 0;
+  std::vector<Planned> cache_;
+  uint64_t tick_ = 0;
+  int64_t hits_ = 0, misses_ = 0;
 };
 
 }  // namespace rma

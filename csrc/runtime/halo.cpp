@@ -39,20 +39,67 @@ void* HaloExchanger::buffer(size_t slot, size_t bytes) {
     bufs_[slot] = nullptr;
     RMA_HIP_CHECK(hipMalloc(&bufs_[slot], bytes));
     buf_bytes_[slot] = bytes;
+    cache_.clear();  // cached batches point at the old buffer
   }
   return bufs_[slot];
 }
 
+namespace {
+bool same_fields(const std::vector<HaloField>& a, const std::vector<HaloField>& b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (a[i].ptr != b[i].ptr || a[i].size != b[i].size || a[i].elem_bytes != b[i].elem_bytes ||
+        a[i].ol != b[i].ol || a[i].hw != b[i].hw)
+      return false;
+  return true;
+}
+}  // namespace
+
+const HaloExchanger::Planned& HaloExchanger::planned(const std::vector<HaloField>& fields,
+                                                     int dims_mask) {
+  ++tick_;
+  for (Planned& c : cache_)
+    if (c.dims_mask == dims_mask && same_fields(c.fields, fields)) {
+      c.used = tick_;
+      ++hits_;
+      return c;
+    }
+  ++misses_;
+  Planned c;
+  c.fields = fields;
+  c.dims_mask = dims_mask;
+  // the order of operations is the host-only plan (halo_plan.cpp), which the
+  // sanitizer self test also executes on host memory
+  c.plan = plan_exchange(fields, nbr_, self_, self_via_comm_, dims_mask);
+  for (size_t s = 0; s < c.plan.slot_bytes.size(); ++s) buffer(s, c.plan.slot_bytes[s]);
+  auto ptr = [&](const HaloMsg& m) -> void* {
+    return m.slot >= 0 ? bufs_[m.slot]
+                       : static_cast<char*>(fields[m.field].ptr) + m.view.offset * fields[m.field].elem_bytes;
+  };
+  for (const HaloDimPlan& dp : c.plan.dims) {
+    c.batches.push_back({batch_copies(dim_copies(dp, fields, bufs_, 0)),
+                         batch_copies(dim_copies(dp, fields, bufs_, 1))});
+    c.send_ptr.emplace_back();
+    c.recv_ptr.emplace_back();
+    for (const HaloMsg& m : dp.sends) c.send_ptr.back().push_back(ptr(m));
+    for (const HaloMsg& m : dp.recvs) c.recv_ptr.back().push_back(ptr(m));
+  }
+  c.used = tick_;
+  if (cache_.size() >= kPlanCache) {
+    size_t lru = 0;
+    for (size_t i = 1; i < cache_.size(); ++i)
+      if (cache_[i].used < cache_[lru].used) lru = i;
+    cache_.erase(cache_.begin() + (std::ptrdiff_t)lru);
+  }
+  cache_.push_back(std::move(c));
+  return cache_.back();
+}
+
 void HaloExchanger::prepare(const std::vector<HaloField>& fields, int dims_mask) {
-  const HaloPlan plan = plan_exchange(fields, nbr_, self_, self_via_comm_, dims_mask);
-  for (size_t s = 0; s < plan.slot_bytes.size(); ++s) buffer(s, plan.slot_bytes[s]);
+  (void)planned(fields, dims_mask);
 }
 
 namespace {
-char* at(const HaloField& f, const PlaneView& v) {
-  return static_cast<char*>(f.ptr) + v.offset * f.elem_bytes;
-}
-
 // RMA_HALO_BATCH=0: one launch per plane copy (A/B and diagnosis)
 void launch_batches(const std::vector<CopyBatch>& bs, stream_t stream) {
   static const char* e = std::getenv("RMA_HALO_BATCH");
@@ -70,27 +117,23 @@ void launch_batches(const std::vector<CopyBatch>& bs, stream_t stream) {
 
 void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stream,
                              int dims_mask) {
-  // the order of operations is the host-only plan (halo_plan.cpp), which the
-  // sanitizer self test also executes on host memory
-  const HaloPlan plan = plan_exchange(fields, nbr_, self_, self_via_comm_, dims_mask);
-  for (size_t s = 0; s < plan.slot_bytes.size(); ++s) buffer(s, plan.slot_bytes[s]);
-  for (const HaloDimPlan& dp : plan.dims) {
+  const Planned& c = planned(fields, dims_mask);
+  for (size_t d = 0; d < c.plan.dims.size(); ++d) {
+    const HaloDimPlan& dp = c.plan.dims[d];
     // self copies + packs in one batched launch, the group, unpacks in one
-    launch_batches(batch_copies(dim_copies(dp, fields, bufs_, 0)), stream);
+    launch_batches(c.batches[d][0], stream);
     if (!dp.sends.empty() || !dp.recvs.empty()) {
       RMA_CHECK_ARG(comm_ != nullptr, "remote neighbour without communicator");
       comm_->group_start();
-      for (const HaloMsg& m : dp.sends)
-        comm_->send(m.slot >= 0 ? bufs_[m.slot] : at(fields[m.field], m.view), m.bytes, m.peer,
-                    stream);
-      for (const HaloMsg& m : dp.recvs)
-        comm_->recv(m.slot >= 0 ? bufs_[m.slot] : at(fields[m.field], m.view), m.bytes, m.peer,
-                    stream);
+      for (size_t i = 0; i < dp.sends.size(); ++i)
+        comm_->send(c.send_ptr[d][i], dp.sends[i].bytes, dp.sends[i].peer, stream);
+      for (size_t i = 0; i < dp.recvs.size(); ++i)
+        comm_->recv(c.recv_ptr[d][i], dp.recvs[i].bytes, dp.recvs[i].peer, stream);
       comm_->group_end();
     }
-    launch_batches(batch_copies(dim_copies(dp, fields, bufs_, 1)), stream);
+    launch_batches(c.batches[d][1], stream);
   }
-  bytes_last_ = plan.bytes_sent;
+  bytes_last_ = c.plan.bytes_sent;
 }
 
 }  // namespace rma

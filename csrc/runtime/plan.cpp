@@ -65,14 +65,15 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
   const Rect& o = g.out;
   const int64_t need_x = std::max(bwx, olx - o.x0), need_y = std::max(bwy, oly - o.y0);
   // RMA_FRAME_ALIGNED=0 / 1 forces the choice; by default aligned frames are
-  // used up to 1024-row chunks. Measured RCCL-self halo overhead per step at
-  // K=24 (profiles/frame_aligned_r2.json): 16384^2 5.7 -> 0.1 %, 32768^2
-  // 2.3-3.1 -> ~0 %, 65536^2 1.9-2.2 -> 0.1-0.4 %; at the 288 GB tile (3072-row
-  // chunks: ~6 % of the pass in the bands, ahead of the exchange) 1.3-1.5 %
-  // with ol-wide strips vs 1.6-1.9 % aligned, and bands shorter than a chunk
-  // were worse still (3.2-3.8 %).
+  // used up to 1536-row tasks (the executor caps a perf_hide rank with a
+  // neighbour at that, DiffusionExecutor::kAlignedMaxRows). Measured RCCL-self
+  // halo overhead per step at K=24 (profiles/frame_aligned_r2.json): 16384^2
+  // 5.7 -> 0.1 %, 32768^2 2.3-3.1 -> ~0 %, 65536^2 1.9-2.2 -> 0.1-0.4 %; at
+  // the 288 GB tile strips with 3072-row chunks vs aligned 1536-row tasks:
+  // x / y / xy periodic +3.8 / +2.4 / +2.5 % vs +2.6 / +2.2 / +0.5 %
+  // (profiles/SUMMARY_r2.md); bands shorter than a task were worse still.
   static const char* fa = std::getenv("RMA_FRAME_ALIGNED");
-  const bool want = fa && fa[0] ? fa[0] != '0' : task_h <= 1024;
+  const bool want = fa && fa[0] ? fa[0] != '0' : task_h <= 1536;
   if (want && hide && any_nbr && task_w >= need_x && task_h >= need_y &&
       o.x1 - o.x0 >= 3 * task_w && o.y1 - o.y0 >= 3 * task_h) {
     // frame = the interior launch's first / last chunk row (wide bands) and

@@ -42,11 +42,29 @@ def test_bench_small_tile_with_self_rccl_halo_check():
     pt = c["pass_timing"]
     assert pt["passes"] == len(plan) and pt["depths"] == plan and pt["interior_ms"] > 0
     assert pt["overlap_fraction"] is None and "no neighbour" in pt["note"]  # nothing exchanged
-    # no neighbour: solo == the run (a ~2 ms timed region: launch/clock noise only)
-    assert c["weak_scaling_eff_same_run"] > 0.7
+    # no neighbour: the solo re-time is the run itself (no same-run efficiency)
+    assert c["weak_scaling_eff_same_run"] is None and c["solo_ms_per_step"] > 0
+    # preflight over RCCL (ring to self + tiny periodic halo check), drift bound
+    pf = c["preflight"]
+    assert pf["ring_ok"] and pf["halo"]["transport"] == "rccl" and pf["halo"]["self_rccl"]
+    assert pf["halo"]["tiles_mismatched"] == 0
+    assert c["drift_check"]["steps"] == 25 and c["fast_math_drift_max"] <= 1e-14
+    rd = c["ranks_detail"]
+    assert len(rd) == 1 and rd[0]["pci_bus_id"] == c["pci_bus_ids"][0]
     assert c["teff_single_step_kernel_GBps"] > 0 and c["teff_bitwise_kstep_GBps"] > 0
     assert c["pci_bus_ids"] and len(c["pci_bus_ids"]) == 1
     assert c["nonfinite_cells_sampled"] == 0
+
+
+def test_bench_default_check_on_one_gpu():
+    """The driver's N=1 command shape: the RCCL-self halo check and the drift
+    bound run by default."""
+    d = bench("--steps", "48", "--warmup", "4", "--nx", "2048", "--single-step-steps", "0",
+              "--check-nx", "530")
+    c = d["config"]
+    assert c["rccl_halo_bitwise_ok"] is True and c["halo_check"]["self_rccl"]
+    assert c["halo_check"]["transport"] == "rccl"
+    assert c["drift_check"]["steps"] == 52 and c["fast_math_drift_max"] <= 1e-14
 
 
 def test_bench_two_processes_sharing_the_gpu(tmp_path):
@@ -61,3 +79,5 @@ def test_bench_two_processes_sharing_the_gpu(tmp_path):
     assert c["rccl_halo_bitwise_ok"] is True and c["halo_check"]["tiles_mismatched"] == 0
     assert c["pass_timing"]["passes"] == len(c["passes_timed"]) and sum(c["passes_timed"]) == 24
     assert len(c["pci_bus_ids"]) == 2 and c["nonfinite_cells_sampled"] == 0
+    assert [r["rank"] for r in c["ranks_detail"]] == [0, 1]
+    assert c["preflight"]["ring_ok"] and c["preflight"]["halo"]["transport"] == "staged"

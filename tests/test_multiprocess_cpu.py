@@ -107,7 +107,8 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     assert c["ranks"] == world and c["transport"] == "gloo"
     assert sum(c["passes_timed"]) == 20 and max(c["passes_timed"]) <= K
     assert c["fast_math"] is True  # the timed passes, not the canonical side run after them
-    assert c["teff_per_gpu_min_GBps"] <= c["teff_per_gpu_GBps"] * (1 + 1e-9) + 0.02
+    # per-rank own (pre-barrier) times: the job time is the slowest rank's
+    assert c["teff_per_gpu_GBps"] <= c["teff_per_gpu_min_GBps"] * (1 + 1e-9) + 0.02
     assert c["teff_per_gpu_min_GBps"] <= c["teff_per_gpu_max_GBps"]
     pt = c["pass_timing"]
     assert pt["passes"] == len(c["passes_timed"])
@@ -115,10 +116,29 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
         assert pt[k] >= 0
     assert pt["halo_ms"] > 0 and pt["overlap_fraction"] is not None
     assert 0 < c["weak_scaling_eff_same_run"] and c["solo_ms_per_step"] > 0
+    # every rank's detail
+    rd = c["ranks_detail"]
+    assert [r["rank"] for r in rd] == list(range(world))
+    assert sorted(tuple(r["coords"]) for r in rd) == sorted(
+        (x, y) for x in range(dims[0]) for y in range(dims[1]))
+    assert len({r["pci_bus_id"] for r in rd}) == world
+    for r in rd:
+        assert r["ms_per_step"] > 0 and r["solo_ms_per_step"] > 0
+        assert r["ms_per_step"] <= d["ms_per_step"] * (1 + 1e-6) + 1e-6
+        assert r["pass_timing"]["passes"] == len(c["passes_timed"])
+        assert r["pass_timing"]["halo_ms"] > 0
+    assert min(r["teff_GBps"] for r in rd) == c["teff_per_gpu_min_GBps"]
+    assert max(r["teff_GBps"] for r in rd) == c["teff_per_gpu_max_GBps"]
+    assert rd[c["slowest_rank"]]["ms_per_step"] == max(r["ms_per_step"] for r in rd)
+    # preflight ring + tiny halo check before the tile, then the in-run checks
+    assert c["preflight"]["ring_ok"] is True
+    assert c["preflight"]["halo"]["tiles_mismatched"] == 0
     assert c["rccl_halo_bitwise_ok"] is True
     hc = c["halo_check"]
     assert hc["tiles_mismatched"] == 0 and hc["transport"] == "gloo"
     assert hc["global_grid"] == [dims[0] * (130 - 2 * K) + 2 * K, dims[1] * (130 - 2 * K) + 2 * K]
+    dc = c["drift_check"]
+    assert dc["steps"] == 23 and 0 <= c["fast_math_drift_max"] <= dc["bound"]
 
 
 def test_bench_halo_check_detects_a_wrong_tile(tmp_path):
@@ -145,6 +165,70 @@ def test_bench_halo_check_detects_a_wrong_tile(tmp_path):
     assert len(lines) == 1, r.stdout + r.stderr[-2000:]
     c = json.loads(lines[0])["config"]
     assert c["rccl_halo_bitwise_ok"] is False and c["halo_check"]["tiles_mismatched"] == 1
+
+
+@pytest.mark.parametrize("where,tmo", [("after", 60), ("before", 8)])
+def test_bench_check_exception_fails_every_rank(tmp_path, where, tmo):
+    """A check that raises on one rank fails the run on EVERY rank (VERDICT r2
+    next 1b): 'after' the check grid ran, the ranks agree through a bounded
+    status exchange; 'before' it, the peers block in the halo exchange and the
+    check-phase watchdog (3 x --check-timeout) ends them. Either way rank 0
+    prints the record with rccl_halo_bitwise_ok false and the error."""
+    import json
+    import subprocess
+    import sys
+    import time
+
+    from helpers import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rcdir = tmp_path / "rc"
+    rcdir.mkdir()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "2",
+           "--device", "cpu", "--nx", "64", "--single-step-steps", "0", "--temporal", "4",
+           "--solo-steps", "0", "--drift-steps", "0", "--check-timeout", str(tmo)]
+    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_CHECK_RAISE=where,
+               RMA_BENCH_RC_DIR=str(rcdir))
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
+                       env=env)
+    assert r.returncode != 0
+    assert time.time() - t0 < 3 * tmo + 60
+    rcs = {p.name: int(p.read_text()) for p in rcdir.iterdir()}
+    assert set(rcs) == {"rc0", "rc1"} and all(v != 0 for v in rcs.values()), rcs
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert "error" in d
+    c = d["config"]
+    if where == "after":
+        assert c["rccl_halo_bitwise_ok"] is False
+        assert "injected" in c["halo_check"]["error"] and "rank(s) 1" in d["error"]
+    else:
+        assert "watchdog" in d["error"]
+
+
+def test_bench_preflight_runs_before_the_tile(tmp_path):
+    """One CPU rank: the preflight ring + tiny halo check and the drift bound
+    are in the record, the halo check is off by default without a GPU."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "30",
+                        "--warmup", "3", "--device", "cpu", "--nx", "80", "--temporal", "6",
+                        "--single-step-steps", "0"], capture_output=True, text=True,
+                       timeout=300, cwd=str(tmp_path), env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    c = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])["config"]
+    assert c["preflight"]["ring_ok"] is True and c["preflight"]["halo"]["tiles_mismatched"] == 0
+    assert c["halo_check"] is None and c["rccl_halo_bitwise_ok"] is None
+    assert c["weak_scaling_eff_same_run"] is None  # no neighbour: solo is the run
+    assert c["drift_check"]["steps"] == 33 and c["fast_math_drift_max"] <= 1e-14
+    assert c["ranks_detail"][0]["rank"] == 0
 
 
 def test_node_local_rank_from_hostnames(tmp_path):

@@ -321,3 +321,42 @@ def test_p2p_smoke_test_through_rccl_on_one_gpu(capsys):
     assert vals == [0.0] * 4
     out = capsys.readouterr().out
     assert "transport=rccl" in out and "recv_mesg on proc 0: [0.0, 0.0, 0.0, 0.0]" in out
+
+
+def spmd_aligned(rank, hub, nx, ny, nt, dims, K, fast):
+    """One rank of an open (non-periodic) grid: its pass geometry at depth K
+    and its field after nt steps; also the halo plan cache counters."""
+    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], overlaps=(2 * K, 2 * K, 2),
+                        halowidths=(K, K, 1), quiet=True, loopback=(hub, rank))
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=nt, init="random",
+                                    quiet=True, dims=dims, temporal=K, fast_math=fast))
+    geo = m.executor.geometry(K)
+    plan = m.plan(nt)
+    m.step(nt)
+    halo = m.g.halo
+    out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g, geo, plan,
+           halo.plan_hits, halo.plan_misses)
+    m.close()
+    gg.finalize_global_grid()
+    return out
+
+
+@pytest.mark.parametrize("dims", [(2, 1), (1, 2), (2, 2)])
+@pytest.mark.parametrize("K,fast,nt", [(24, True, 53), (12, False, 29)])
+def test_aligned_frames_on_partial_sides_bitwise(dims, K, fast, nt):
+    """tiles big enough for the aligned frame layout
+    (frame = whole tasks of the interior's grid) on ranks with neighbours on
+    only one to three sides: every tile == its window of a 1-rank run of the
+    global grid, bitwise; the deepest passes really are aligned. The halo plan
+    is built once per field (T, T2) and served from the cache afterwards."""
+    nx = ny = 1100
+    P = dims[0] * dims[1]
+    res = run_loopback(P, spmd_aligned, nx, ny, nt, dims, K, fast, timeout=180)
+    nxg, nyg, _ = res[0][2]
+    one = run_loopback(1, spmd_aligned, nxg, nyg, nt, (1, 1), K, fast, timeout=180)[0][1]
+    for coords, T, _, geo, plan, hits, misses in res:
+        assert geo["aligned"], (coords, geo)
+        assert len(geo["frame"]) == len(geo["frame_wide"]) + len(geo["frame_tall"]) >= 1
+        gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
+        assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
+        assert misses <= 2 and hits + misses == len(plan)
