@@ -1,0 +1,52 @@
+#!/bin/bash
+# Named GPU steps for one gpurun call (round 3 on), e.g.
+#   gpurun --timeout 900 -- bash scripts/gpu_steps.sh OUT=gpurun_out/r3a tests smoke bench20
+# Every step runs under its own time limit, logs to $OUT/<step>.log, and the
+# chain stops at the first failure, fault or timeout (no retries).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+OUT=gpurun_out/steps
+for a in "$@"; do case $a in OUT=*) OUT=${a#OUT=} ;; esac; done
+mkdir -p "$OUT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name start $(date +%T)"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(date +%T)"; tail -3 "$OUT/$name.log" | cut -c1-300
+  return $rc
+}
+prof() {  # name timeout rocprofv3-args... -- cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name start $(date +%T)"
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 "$t" rocprofv3 "$@" > "$R/$OUT/$name.log" 2>&1)
+  local rc=$?
+  echo "== $name rc=$rc $(date +%T)"; tail -3 "$OUT/$name.log" | cut -c1-300
+  return $rc
+}
+for s in "$@"; do
+  case $s in
+    OUT=*) ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 \
+             --timeout-method thread -p no:cacheprovider || exit 1 ;;
+    tests_new) step tests_new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+             tests/test_bench_gpu.py tests/test_drift_gpu.py \
+             "tests/test_multirank_gpu.py::test_aligned_frames_on_partial_sides_bitwise" || exit 1 ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
+             --json-out "$OUT/bench20.json" || exit 1 ;;
+    bench1000) step bench1000 300 python bench.py --json-out "$OUT/bench1000.json" || exit 1 ;;
+    nbr_x|nbr_y|nbr_xy) d=${s#nbr_}
+             step "$s" 400 python bench/rccl_self_overhead.py --K 24 --periodic "$d" --steps 320 \
+             --pattern opop --out "$OUT/$s.json" || exit 1 ;;
+    nbr_x_strips|nbr_y_strips|nbr_xy_strips) d=${s#nbr_}; d=${d%_strips}
+             RMA_FRAME_ALIGNED=0 step "$s" 400 python bench/rccl_self_overhead.py --K 24 \
+             --periodic "$d" --steps 320 --pattern opop --out "$OUT/$s.json" || exit 1 ;;
+    trace20) prof trace20 300 --kernel-trace --stats --output-format csv -d "$R/$OUT/trace20" \
+             -o run -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== all steps done"
