@@ -28,6 +28,12 @@ def main() -> int:
     ap.add_argument("--K", type=int, default=24)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--init", default="random", choices=["random", "gaussian"])
+    ap.add_argument("--coef", default="probe", choices=["probe", "physics"],
+                    help="physics: the run's coefficients (lx = 10, dt = dx^2/4.1)")
+    ap.add_argument("--alternate", type=int, default=0,
+                    help="P > 0: per rect, P passes alternating T <-> T2 (the executor's "
+                         "buffer sequence on an evolving field), timed one by one")
+    ap.add_argument("--rects", default="", help="comma list of rect names (default: all)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     n = a.n
@@ -46,6 +52,9 @@ def main() -> int:
     ops.fill_(iCp, 1.0)
     ops.fill_(T2, 0.0)
     coef = ops.StencilCoef(-1.0, 1.0 / 0.01, 1.0 / 0.01, 1e-5)
+    if a.coef == "physics":
+        dx = 10.0 / n
+        coef = ops.StencilCoef.from_physics(1.0, dx, dx, dx * dx / 4.1)
     kern, vec, ch = native().fast_kernel_k(K, n, tuple(coef))
     names = {v: k for k, v in ops.KERNELS.items()}
     tn = ops.StencilTuning(chunk_rows=ch, kernel=names[kern], vec=vec, xcd_remap=1)
@@ -64,8 +73,37 @@ def main() -> int:
         "owned_x_split_y24": [(K, n - K, 1, K), (K, n - K, K, n - 1)],
         "owned_y_split_x24": [(1, K, K, n - K), (K, n - 1, K, n - K)],
     }
-    res = {"n": n, "K": K, "init": a.init, "kernel": names[kern], "vec": vec, "chunk_rows": ch, "ms": {}}
+    if a.rects:
+        rects = {k: rects[k] for k in a.rects.split(",")}
+    res = {"n": n, "K": K, "init": a.init, "kernel": names[kern], "vec": vec, "chunk_rows": ch,
+           "coef": a.coef, "alternate": a.alternate, "ms": {}}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    if a.alternate:
+        # every rect starts from the same random field; passes alternate the
+        # buffers like the executor (halo cells keep their values: no exchange)
+        T0 = T.clone() if a.reps * len(rects) > 1 else None
+        for rep in range(a.reps):
+            for name, r in rects.items():
+                rl = r if isinstance(r, list) else [r]
+                if T0 is not None:
+                    T.copy_(T0)
+                    T2.copy_(T0)
+                src, dst = T, T2
+                ts = []
+                for _ in range(a.alternate):
+                    torch.cuda.synchronize()
+                    ev[0].record()
+                    ops.stencilk_step(K, dst, src, iCp, coef, rl, tn)
+                    ev[1].record()
+                    torch.cuda.synchronize()
+                    ts.append(round(ev[0].elapsed_time(ev[1]), 3))
+                    src, dst = dst, src
+                res["ms"].setdefault(name, []).append(ts)
+                print(json.dumps({name: ts}), flush=True)
+        if a.out:
+            with open(a.out, "w") as fo:
+                json.dump(res, fo, indent=1)
+        return 0
     for rep in range(a.reps):
         for name, r in rects.items():
             rl = r if isinstance(r, list) else [r]

@@ -44,6 +44,15 @@ for s in "$@"; do
     nbr_x_strips|nbr_y_strips|nbr_xy_strips) d=${s#nbr_}; d=${d%_strips}
              RMA_FRAME_ALIGNED=0 step "$s" 400 python bench/rccl_self_overhead.py --K 24 \
              --periodic "$d" --steps 320 --pattern opop --out "$OUT/$s.json" || exit 1 ;;
+    host4096|host2048) n=${s#host}
+             step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 1 --variants perf_hide \
+             --steps 400 --pattern opop --out "$OUT/$s.json" || exit 1 ;;
+    shape_alt) step shape_alt 400 python bench/interior_shape_probe.py --K 24 --coef physics \
+             --alternate 12 --reps 2 --rects open,owned_x,owned_y,owned_xy \
+             --out "$OUT/shape_alt.json" || exit 1 ;;
+    shape_alt_g) step shape_alt_g 400 python bench/interior_shape_probe.py --K 24 --coef physics \
+             --init gaussian --alternate 12 --reps 2 --rects open,owned_x,owned_y,owned_xy \
+             --out "$OUT/shape_alt_g.json" || exit 1 ;;
     trace20) prof trace20 300 --kernel-trace --stats --output-format csv -d "$R/$OUT/trace20" \
              -o run -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
