@@ -45,10 +45,13 @@ def main() -> int:
     T2 = torch.empty_like(T)
     iCp = torch.empty_like(T)
     geom = ops.TileGeometry(0, 0, n, n, 1.0, 1.0)
-    if a.init == "random":
-        ops.init_random_(T, geom, seed=1)
-    else:
-        ops.init_gaussian_(T, geom, 10.0, 10.0)
+    def init(A):
+        if a.init == "random":
+            ops.init_random_(A, geom, seed=1)
+        else:
+            ops.init_gaussian_(A, geom, 10.0, 10.0)
+
+    init(T)
     ops.fill_(iCp, 1.0)
     ops.fill_(T2, 0.0)
     coef = ops.StencilCoef(-1.0, 1.0 / 0.01, 1.0 / 0.01, 1e-5)
@@ -81,13 +84,11 @@ def main() -> int:
     if a.alternate:
         # every rect starts from the same random field; passes alternate the
         # buffers like the executor (halo cells keep their values: no exchange)
-        T0 = T.clone() if a.reps * len(rects) > 1 else None
         for rep in range(a.reps):
             for name, r in rects.items():
                 rl = r if isinstance(r, list) else [r]
-                if T0 is not None:
-                    T.copy_(T0)
-                    T2.copy_(T0)
+                init(T)  # no room for a saved copy at the 288 GB tile
+                T2.copy_(T)
                 src, dst = T, T2
                 ts = []
                 for _ in range(a.alternate):
