@@ -15,7 +15,7 @@
 //   temporal=K>1 (kPerf/kHide): run(n) plans passes of 1..K steps
 //           (plan_passes: e.g. 20 steps = one 20-step pass, never 16 + 4);
 //           a pass of k steps runs the k-step kernel (stencil_tb.hip k=2,
-//           stencil_tbk.hip / stencil_pipe.h otherwise) on the "owned" rect
+//           stencil_kstep.hip / stencil_pipe.h otherwise) on the "owned" rect
 //           (the k cells next to a neighbour are left to the exchange), then
 //           one exchange of width K (overlap 2K).
 //

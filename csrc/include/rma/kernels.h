@@ -53,7 +53,7 @@ void stencil2_rects_gpu(double* T2, const double* T, const double* iCp, int64_t 
 void stencil2_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
                         const Rect* rects, int nrects, const StencilCoef& c);
 
-// K steps per pass (K = 2..4, stencil_tbk.hip): T2[r] = f^K(T)[r], the
+// K steps per pass (K = 2, 3, 4, 6, 8: stencil_kstep.hip kernel 3; others: csrc/lab): T2[r] = f^K(T)[r], the
 // intermediate levels being f on the interior and T elsewhere; face fluxes
 // shared between neighbouring cells (same rounding). Bitwise equal to K
 // one-step launches.
@@ -78,7 +78,7 @@ constexpr int kPipeMaxK = 24;
 int pipe_default_stages(int K);
 bool pipe_has(int K, int stages, int arith = 0);
 // Column waves per stage: 2 = blocks of 2 x stages waves over ~500 columns
-// (V = 4 only, fast5 K = 16/20/24, stencil_pipe_e.hip, an experiment: slower
+// (V = 4 only, fast5 K = 16/20/24, csrc/lab/stencil_pipe_lab.hip, an experiment: slower
 // than 1); pipe_has_cols says whether (K, S, arith, cols) is instantiated,
 // pipe_default_cols is what a tuning of cols = 0 runs.
 bool pipe_has_cols(int K, int stages, int arith, int cols);

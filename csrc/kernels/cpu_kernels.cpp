@@ -74,7 +74,7 @@ bool fast5_ok(const StencilCoef& c) {
          std::isfinite(c.dt * ax);
 }
 
-// fast5 arithmetic (stencil_tbk.hip kernel 5, stencil_pipe.h): the 5-point sum
+// fast5 arithmetic (csrc/lab/stencil_kstep_lab.hip kernel 5, stencil_pipe.h): the 5-point sum
 // with the constants folded into one per-cell factor g = dt*lam/dx^2 * 1/Cp,
 //   T2 = fma(g, fma(r, U+D, fma(-2(1+r), c, R+L)), c),  r = (lam/dy^2)/(lam/dx^2).
 // std::fma rounds once like v_fma_f64, so this twin is bitwise equal to the

@@ -174,7 +174,7 @@ inline int64_t plan_rects(RectList& L, const Rect* rects, int nrects, int V, int
   return total;
 }
 
-// Planner of the stage-pipelined K-step kernels (stencil_tbk.hip kernels 6-8,
+// Planner of the stage-pipelined K-step kernels (lab kernels 6-8,
 // stencil_pipe.h kernels 9/10):
 // one block per (strip, chunk) task, strips as in plan_rects with halo > 0;
 // block b of a rect is (chunk = lb / strips, strip = lb % strips).

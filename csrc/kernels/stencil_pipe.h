@@ -11,7 +11,7 @@
 // stores. One barrier per row iteration. Measured: profiles/SUMMARY_r2.md,
 // profiles/pmc_pipe_r2.md (what was tried and not kept is listed there).
 //
-// Generalises kernels 6-8 of stencil_tbk.hip (fixed K in {8,12,16}, H = K/S)
+// Generalises kernels 6-8 of csrc/lab/stencil_kstep_lab.hip (fixed K in {8,12,16}, H = K/S)
 // so that the executor's pass planner (executor.cpp plan_passes) can run a
 // pass of any depth: e.g. the 20 timed steps of the driver's bench command as
 // ONE 20-step pass (~70 ms) instead of 16 + 4 (each pass costs at least one
@@ -22,7 +22,7 @@
 // DPP on the VALU, an energy / issue experiment, profiles/SUMMARY_r2.md):
 //   false  fast5: T2 = fma(g, fma(r, U+D, fma(-2(1+r), c, L+R)), c), g = dt*lam/dx^2/Cp
 //          (LDS ring holds g, zero outside the interior). Bitwise equal to
-//          stencil_tbk.hip kernel 5 and to the CPU twin stencilk5_rects_cpu.
+//          kernel 5 (csrc/lab) and to the CPU twin stencilk5_rects_cpu.
 //   true   the canonical flux form of rma/common.h (scripts/diffusion_2D_perf.jl:8-10
 //          with 1/Cp): x face flux shared with the left lane, y face flux
 //          carried from the previous row; bitwise equal to K one-step launches.
@@ -425,14 +425,13 @@ void launch(const PipeLaunch& a) {
       a.T2, a.T, a.iCp, a.nx, a.ny, L, a.k, a.chunk_rows, a.remap);
 }
 
-// Each stencil_pipe_*.hip unit instantiates a range of (K, S) and answers
-// for it: returns false if it does not hold (K, S, V, arithmetic).
+// Each stencil_pipe_{a,b,c}.hip unit instantiates a range of (K, S) of the
+// default stage split and answers for it: returns false if it does not hold
+// (K, S, V, arithmetic). Alternative splits, the ds_bpermute variant and the
+// two-column blocks are in the lab library (csrc/lab/stencil_pipe_lab.hip).
 bool dispatch_a(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_b(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
-bool dispatch_d(int K, int S, int V, int ar, const PipeLaunch& a);
-// two column waves per stage (V = 4 only), stencil_pipe_e.hip
-bool dispatch_e(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe
 }  // namespace rma

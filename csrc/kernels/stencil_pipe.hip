@@ -1,12 +1,14 @@
 // Host side of the any-K stage-pipelined kernel (stencil_pipe.h): argument
 // checks, strip/chunk planning and the (K, S, V, arithmetic) dispatch over the
-// instantiation units stencil_pipe_{a,b,c,d}.hip.
+// instantiation units stencil_pipe_{a,b,c}.hip (default stage split); any
+// other (K, S, V, C, arithmetic) goes to the lab library (lab_hooks.h).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 
 #include "rma/hip_check.h"
 #include "rma/kernels.h"
+#include "lab_hooks.h"
 #include "stencil_pipe.h"
 
 namespace rma {
@@ -28,7 +30,7 @@ bool pipe_has(int K, int S, int arith) {
   if (K < 1 || K > kPipeMaxK) return false;
   if (arith == pipe::kArFast5Perm) return S == 4 && (K == 16 || K == 20 || K == 24);
   if (S == pipe_default_stages(K)) return true;
-  // alternative stage splits instantiated for sweeps (stencil_pipe_d.hip)
+  // alternative stage splits instantiated for sweeps (csrc/lab/stencil_pipe_lab.hip)
   return (K == 12 && S == 3) || (K == 16 && S == 8) || (K == 24 && S == 8) ||
          (K == 8 && S == 4) || (K == 8 && S == 1);
 }
@@ -39,7 +41,7 @@ bool pipe_has_cols(int K, int S, int arith, int cols) {
 }
 
 int pipe_default_cols(int K, int S, int arith) {
-  // one column wave: the 2-column blocks (stencil_pipe_e.hip) do 8 % less
+  // one column wave: the 2-column blocks (csrc/lab/stencil_pipe_lab.hip) do 8 % less
   // arithmetic at K=24 but run one block per CU and lose 5-20 % to the
   // unhidden per-row barrier (profiles/pass_sweep_cols2_r2.json)
   (void)K;
@@ -86,10 +88,12 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, rects, nrects, c, tune.chunk_rows, remap,
                      as_stream(stream)};
-  const bool ok =
-      C == 2 ? pipe::dispatch_e(K, S, V, arith, a)
-             : (pipe::dispatch_a(K, S, V, arith, a) || pipe::dispatch_b(K, S, V, arith, a) ||
-                pipe::dispatch_c(K, S, V, arith, a) || pipe::dispatch_d(K, S, V, arith, a));
+  bool ok = C == 1 && (pipe::dispatch_a(K, S, V, arith, a) || pipe::dispatch_b(K, S, V, arith, a) ||
+                       pipe::dispatch_c(K, S, V, arith, a));
+  if (!ok) {  // alternative stage splits, pipeb, two-column blocks: librma_lab.so
+    if (!lab_hooks().pipe) lab_missing("this pipelined kernel variant (stages / arithmetic / cols)");
+    ok = lab_hooks().pipe(K, S, V, C, arith, a);
+  }
   RMA_CHECK_ARG(ok, "pipelined kernel K=" << K << " S=" << S << " V=" << V << " C=" << C
                                            << " arithmetic=" << arith << " not instantiated");
   RMA_HIP_LAUNCH_CHECK();

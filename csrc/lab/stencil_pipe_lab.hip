@@ -1,0 +1,53 @@
+// librma_lab.so, pipelined unit: members of the any-K pipelined family
+// (stencil_pipe.h) that the executor never runs, kept for sweeps:
+//   * alternative stage splits (K=12 S=3, K=16/24 S=8, K=8 S=4/1), fast5;
+//   * kernel 11 "pipeb": fast5 with the lane moves by ds_bpermute on the LDS
+//     pipe instead of DPP (an energy / issue experiment, K = 16, 20, 24);
+//   * two column waves per stage (C = 2, V = 4, fast5 K = 16, 20, 24): 8-wave
+//     blocks of ~500 input columns whose inner stage boundary recomputes 2*Hp
+//     columns instead of a second strip's 2K. 8 % less arithmetic at K=24 but
+//     one block per CU (152 KB LDS), whose per-row barrier no second block
+//     hides: 85.2 vs 80.9 ms per K=24 pass at 101376^2, 65.7 vs 55.4 ms at
+//     K=16 (profiles/pass_sweep_cols2_r2.json).
+#include "../kernels/lab_hooks.h"
+
+namespace rma {
+namespace pipe {
+namespace {
+
+bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
+  RMA_PIPE_CASE(12, 3, kArFast5)
+  RMA_PIPE_CASE(16, 8, kArFast5)
+  RMA_PIPE_CASE(24, 8, kArFast5)
+  RMA_PIPE_CASE(8, 4, kArFast5)
+  RMA_PIPE_CASE(8, 1, kArFast5)
+  RMA_PIPE_CASE(16, 4, kArFast5Perm)
+  RMA_PIPE_CASE(20, 4, kArFast5Perm)
+  RMA_PIPE_CASE(24, 4, kArFast5Perm)
+  return false;
+}
+
+
+#define RMA_PIPE2_CASE(KK, SS, CC)          \
+  if (K == KK && S == SS && ar == CC) {     \
+    if (V != 4) return false;               \
+    launch<KK, SS, 4, CC, 2>(a);            \
+    return true;                            \
+  }
+
+bool dispatch_cols2(int K, int S, int V, int ar, const PipeLaunch& a) {
+  RMA_PIPE2_CASE(16, 4, kArFast5)
+  RMA_PIPE2_CASE(20, 4, kArFast5)
+  RMA_PIPE2_CASE(24, 4, kArFast5)
+  return false;
+}
+
+}  // namespace
+}  // namespace pipe
+
+namespace lab {
+bool pipe(int K, int S, int V, int C, int arith, const pipe::PipeLaunch& a) {
+  return C == 2 ? pipe::dispatch_cols2(K, S, V, arith, a) : pipe::dispatch_alt(K, S, V, arith, a);
+}
+}  // namespace lab
+}  // namespace rma

@@ -15,11 +15,23 @@ Usage::
 Objects go to ``build/native`` and are rebuilt when their source or any header
 under ``csrc/include`` is newer. All device code is compiled with
 ``-ffp-contract=off`` so the stencil is bit-reproducible against NumPy.
+
+Two libraries: ``librma_core.so`` holds every kernel the executor and the ops
+run plus the runtime and the C ABI; ``librma_lab.so`` (``csrc/lab``) holds the
+superseded and experimental kernels kept as test oracles and for sweeps. The
+lab library is loaded only on request (``_native.load_lab()``) and installs
+its kernels in the core's dispatchers.
+
+A stamp next to the libraries (``.build_stamp``) records a hash of every
+source and header, the compile flags and the offload arch: a snapshot whose
+stamp matches is used as is (no rebuild on a GPU box, whatever the file
+mtimes); otherwise the objects are rebuilt incrementally by mtime.
 """
 from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -35,8 +47,11 @@ PKG = ROOT / "rocm_mpi_amd"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RMA_OFFLOAD_ARCH", "gfx950")
 
-# librma_core.so: every kernel + the runtime + the C ABI (usable without Python)
+# librma_core.so: every kernel the executor / ops run + the runtime + the C ABI
+# (usable without Python)
 HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "runtime").glob("*.cpp"))
+# librma_lab.so: superseded / experimental kernels (test oracles, sweeps)
+LAB_SOURCES = sorted((CSRC / "lab").glob("*.hip"))
 CORE_HOST_SOURCES = sorted((CSRC / "kernels").glob("*.cpp"))
 # _C*.so: the pybind11 bindings, linked against librma_core.so ($ORIGIN rpath)
 BIND_SOURCES = [CSRC / "bindings" / "module.cpp"]
@@ -51,6 +66,13 @@ def ext_path() -> Path:
 
 def core_path() -> Path:
     return PKG / "librma_core.so"
+
+
+def lab_path() -> Path:
+    return PKG / "librma_lab.so"
+
+
+STAMP = PKG / ".build_stamp"
 
 
 def _pybind_include() -> str:
@@ -82,6 +104,20 @@ def _host_cmd(src: Path, obj: Path) -> list[str]:
     return [cxx, *COMMON, "-c", str(src), "-o", str(obj)]
 
 
+def _headers() -> list[Path]:
+    return sorted(list(INC.rglob("*.h")) + list((CSRC / "kernels").glob("*.h")))
+
+
+def source_stamp() -> str:
+    """Hash of every source and header, the flags and the arch."""
+    h = hashlib.sha1()
+    h.update(" ".join(COMMON + [ARCH, sysconfig.get_config_var("EXT_SUFFIX") or ""]).encode())
+    for p in sorted(set(HIP_SOURCES + LAB_SOURCES + HOST_SOURCES + EXAMPLES + TOOLS + _headers())):
+        h.update(str(p.relative_to(ROOT)).encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
 def _stale(src: Path, obj: Path, newest_header: float) -> bool:
     if not obj.exists():
         return True
@@ -93,26 +129,25 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
     """Compile (incrementally) and link ``rocm_mpi_amd/_C*.so``; returns its path."""
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
-    headers = list(INC.rglob("*.h")) + list((CSRC / "kernels").glob("*.h"))
+    headers = _headers()
     newest_header = max((p.stat().st_mtime for p in headers), default=0.0)
-    out, core = ext_path(), core_path()
-    if not clean and out.exists() and core.exists():
-        # the shipped libraries are newer than every source: nothing to do (a
-        # repository snapshot on a GPU box carries the .so files but not the
-        # object files, which would otherwise force a full rebuild there)
-        newest_src = max([newest_header] + [p.stat().st_mtime for p in
-                                            HIP_SOURCES + HOST_SOURCES + EXAMPLES + TOOLS])
-        if min(out.stat().st_mtime, core.stat().st_mtime) >= newest_src:
-            return out
+    out, core, lab = ext_path(), core_path(), lab_path()
+    stamp = source_stamp()
+    if not clean and out.exists() and core.exists() and lab.exists() and STAMP.exists() \
+            and STAMP.read_text().strip() == stamp:
+        # the libraries were built from exactly these sources, flags and arch
+        # (a repository snapshot on a GPU box carries the .so files and the
+        # stamp but not the object files)
+        return out
     BUILD.mkdir(parents=True, exist_ok=True)
     jobs = jobs or min(16, os.cpu_count() or 4)
     todo = []
     objs = []
-    for src in HIP_SOURCES + HOST_SOURCES:
+    for src in HIP_SOURCES + LAB_SOURCES + HOST_SOURCES:
         obj = BUILD / (src.parent.name + "_" + src.name + ".o")
         objs.append(obj)
         if _stale(src, obj, newest_header):
-            cmd = _hip_cmd(src, obj) if src in HIP_SOURCES else _host_cmd(src, obj)
+            cmd = _host_cmd(src, obj) if src in HOST_SOURCES else _hip_cmd(src, obj)
             todo.append((src, cmd))
 
     def run(item):
@@ -129,8 +164,10 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
             for src in ex.map(run, todo):
                 print(f"[rocm_mpi_amd build] compiled {src.relative_to(ROOT)}", flush=True)
     core = core_path()
-    core_objs = [o for o, src in zip(objs, HIP_SOURCES + HOST_SOURCES) if src not in BIND_SOURCES]
-    bind_objs = [o for o, src in zip(objs, HIP_SOURCES + HOST_SOURCES) if src in BIND_SOURCES]
+    pairs = list(zip(objs, HIP_SOURCES + LAB_SOURCES + HOST_SOURCES))
+    core_objs = [o for o, src in pairs if src not in BIND_SOURCES and src not in LAB_SOURCES]
+    lab_objs = [o for o, src in pairs if src in LAB_SOURCES]
+    bind_objs = [o for o, src in pairs if src in BIND_SOURCES]
 
     def newer(target: Path, deps) -> bool:
         return not target.exists() or any(d.stat().st_mtime > target.stat().st_mtime for d in deps)
@@ -150,6 +187,10 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
         link(core, [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, core_objs),
                     "-Wl,-soname,librma_core.so", f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64",
                     "-ldl", "-lpthread", f"-Wl,-rpath,{ROCM / 'lib'}"])
+    if newer(lab, lab_objs + [core]):
+        link(lab, [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, lab_objs),
+                   "-Wl,-soname,librma_lab.so", f"-L{PKG}", "-lrma_core", "-Wl,-rpath,$ORIGIN",
+                   f"-L{ROCM / 'lib'}", "-lamdhip64", f"-Wl,-rpath,{ROCM / 'lib'}"])
     out = ext_path()
     if newer(out, bind_objs + [core]):
         link(out, ["g++", "-shared", "-fPIC", *map(str, bind_objs), f"-L{PKG}", "-lrma_core",
@@ -177,6 +218,7 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
             if r.returncode != 0:
                 raise RuntimeError(f"tool build failed: {src}\n{r.stdout}\n{r.stderr}")
             print(f"[rocm_mpi_amd build] built {exe.relative_to(ROOT)}", flush=True)
+    STAMP.write_text(stamp + "\n")
     return out
 
 

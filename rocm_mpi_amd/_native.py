@@ -60,3 +60,27 @@ def native():
 def native_path() -> str | None:
     _load()
     return getattr(_mod, "__file__", None)
+
+
+_lab = None
+
+
+def load_lab():
+    """Load librma_lab.so (csrc/lab: the superseded / experimental kernels kept
+    as test oracles and for sweeps); it installs them in the core's K-step
+    dispatchers. Idempotent; loud failure if the library is missing."""
+    global _lab
+    native()  # the core first: the lab library binds to this process's librma_core.so
+    with _lock:
+        if _lab is None:
+            import ctypes
+
+            path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librma_lab.so")
+            if not os.path.exists(path):
+                raise RuntimeError(f"{path} is missing: run `python -m rocm_mpi_amd._build`")
+            _lab = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    return _lab
+
+
+def lab_loaded() -> bool:
+    return _lab is not None

@@ -24,19 +24,44 @@ from .._native import has_native, native
 
 Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 
-# K-step kernels also: 2 = dpp, 3 = lds_dpp (default), 4 = fast (reassociated, FMA; not
-# bitwise), 5 = fast5 (5-point sum with one folded per-cell factor; not bitwise, lam != 0);
-# 6 / 7 / 8 = fast5p2 / fast5p4 / fast5p8: the same arithmetic with the levels of one strip
-# split over 2 / 4 / 8 pipelined waves (K = 8, 12, 16; fast5p8: K = 8, 16); 9 = pipe: the
-# stage-pipelined fast5 kernel for ANY K in 1..24 (csrc/kernels/stencil_pipe.h, the executor's
-# fast-math kernel); 10 = pipec: the same pipeline with the canonical arithmetic (bitwise equal
-# to K one-step updates), any K in 1..24; 11 = pipeb: pipe with the lane moves on the LDS
-# pipe (ds_bpermute) instead of DPP (K = 16, 20, 24; an experiment).
+# Kernel ids (StencilTuning.kernel names). The core library (librma_core.so)
+# holds what the executor and the ops run by default:
+#   one-step:  "march" (0, the fused one-step kernel), "lds" (1, LDS-tiled baseline);
+#   K-step:    "lds_dpp" (3: canonical, K = 2, 3, 4, 6, 8; LDS 1/Cp ring + DPP),
+#              "pipe" (9: the stage-pipelined fast-math kernel, ANY K in 1..24,
+#              csrc/kernels/stencil_pipe.h), "pipec" (10: the same pipeline with the
+#              canonical arithmetic, bitwise equal to K one-step updates).
+# LAB_KERNELS live in librma_lab.so (csrc/lab: superseded / experimental kernels kept as
+# test oracles and for sweeps), loaded on first use: K-step "march"/"lds"/"dpp" (0/1/2:
+# canonical variants of kernel 3), "fast" (4: reassociated, not bitwise), "fast5" (5: the
+# 5-point sum with one folded per-cell factor, the GPU oracle of "pipe"), "fast5p2/p4/p8"
+# (6/7/8: fixed-K pipelined fast5), "pipeb" (11: pipe with ds_bpermute lane moves), and
+# the pipelined kernels' non-default stage splits and two-column blocks.
 FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe", "pipeb")
 PIPE = ("pipe", "pipec", "pipeb")
 PIPE_MAX_K = 24
-KERNELS = {"march": 0, "lds": 1, "dpp": 2, "lds_dpp": 3, "fast": 4, "fast5": 5, "fast5p2": 6,
-           "fast5p4": 7, "fast5p8": 8, "pipe": 9, "pipec": 10, "pipeb": 11}
+KERNELS = {"march": 0, "lds": 1, "lds_dpp": 3, "pipe": 9, "pipec": 10}
+LAB_KERNELS = {"dpp": 2, "fast": 4, "fast5": 5, "fast5p2": 6, "fast5p4": 7, "fast5p8": 8,
+               "pipeb": 11}
+KSTEP_CORE = ("lds_dpp", "pipe", "pipec")
+
+
+def kernel_id(name: str) -> int:
+    """Numeric id of a kernel name (core or lab)."""
+    if name in KERNELS:
+        return KERNELS[name]
+    if name in LAB_KERNELS:
+        return LAB_KERNELS[name]
+    raise ValueError(f"unknown kernel {name!r}: one of {sorted(KERNELS) + sorted(LAB_KERNELS)}")
+
+
+def _kstep_needs_lab(K: int, tn: "StencilTuning") -> bool:
+    """Does this K-step launch run a librma_lab.so kernel?"""
+    if tn.kernel not in KSTEP_CORE or tn.cols == 2:
+        return True
+    if tn.kernel in PIPE and tn.stages and has_native():
+        return tn.stages != native().pipe_default_stages(K)
+    return False
 
 
 class StencilCoef(NamedTuple):
@@ -169,7 +194,7 @@ def stencil_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: Ste
     tn = tuning or StencilTuning()
     if T.is_cuda:
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
-                               tn.chunk_rows, int(tn.nontemporal), KERNELS[tn.kernel],
+                               tn.chunk_rows, int(tn.nontemporal), kernel_id(tn.kernel),
                                stream_handle(T), True, tn.unroll, tn.vec, tn.xcd_remap)
     elif _use_native_cpu():
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
@@ -210,7 +235,7 @@ def stencil2_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: St
 def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
                   coef: StencilCoef, rects: Sequence[Rect] | None = None,
                   tuning: StencilTuning | None = None) -> None:
-    """K time steps in one pass (csrc/kernels/stencil_tbk.hip, stencil_pipe.h):
+    """K time steps in one pass (csrc/kernels/stencil_kstep.hip, stencil_pipe.h; lab kernels: csrc/lab):
     T2[r] = f^K(T)[r], the intermediate levels being f on the interior and T
     on boundary/halo cells. Kernels: K = 2, 3, 4, 6, 8 for march/lds/dpp/lds_dpp/
     fast/fast5 (12, 16 also fast5 and the fast5p* variants); ANY K in 1..24 for
@@ -245,13 +270,17 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
         raise ValueError("kernel 'fast5' folds dy^-2/dx^-2 into one factor: needs lam != 0 "
                          f"and finite coefficients, got {tuple(coef)}")
     if T.is_cuda:
+        if _kstep_needs_lab(K, tn):
+            from .._native import load_lab
+
+            load_lab()
         native().stencilk_rects(K, _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                 tn.chunk_rows, int(tn.nontemporal), stream_handle(T), True,
-                                tn.xcd_remap, tn.vec, KERNELS[tn.kernel], int(tn.stages),
+                                tn.xcd_remap, tn.vec, kernel_id(tn.kernel), int(tn.stages),
                                 int(tn.cols))
     elif _use_native_cpu():
         native().stencilk_rects(K, _ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
-                                16, 0, 0, False, -1, 2, KERNELS[tn.kernel], 0)
+                                16, 0, 0, False, -1, 2, kernel_id(tn.kernel), 0)
     elif tn.kernel in FAST5:
         a = T.clone()
         for _ in range(K - 1):
@@ -280,10 +309,8 @@ def fast5_constants(coef: StencilCoef) -> tuple[float, float, float]:
 def stencil5_torch(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, c: StencilCoef,
                    rects: Iterable[Rect]) -> None:
     """Torch twin of ONE fast5 step (CPU without the extension). torch has no
-    fused multiply-add for float64 tensors, so each fma is evaluated exactly
-    with a double-double product (Dekker/Veltkamp split) and rounded once:
-    bitwise equal to std::fma / v_fma_f64 unless an intermediate under- or
-    overflows."""
+    fused multiply-add for float64 tensors: each fma is emulated with
+    fma_exact (error-free product and sum, see its caveats)."""
     ry, mkc, gs = fast5_constants(c)
     for x0, x1, y0, y1 in rects:
         cu = T[y0:y1, x0:x1]
@@ -308,18 +335,18 @@ def _two_prod(a: torch.Tensor, b: torch.Tensor):
 
 
 def fma_exact(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
-    """round(a*b + c) for float64 tensors: a*b = p + e exactly (two_prod); the
-    sum p + e + c is formed with error-free two_sum steps and rounded once
-    (the residual is added last with round-to-odd style correction: the
-    partial sum s and its error terms are combined so that only the final
-    addition rounds)."""
+    """Emulated fma(a, b, c) for float64 tensors (the no-extension CPU fallback
+    of the fast5 twin only): a*b = p + e exactly (Dekker two_prod) and p + c =
+    s + err exactly (two_sum); the result s + (err + e) rounds twice, so it is
+    NOT always the correctly rounded fma: it differs when err + e is inexact
+    (near-ties after cancellation) and the Veltkamp split overflows for |a| or
+    |b| above ~2^996. On the fields the tests use it matches std::fma bitwise
+    (tests/test_fast5_cpu.py); the GPU kernels and the native CPU twins use a
+    real fma."""
     p, e = _two_prod(a, b)
     s = p + c  # two_sum(p, c)
     bp = s - p
     err = (p - (s - bp)) + (c - bp)
-    # s + (err + e): err + e is exact unless tiny cancellation; the final
-    # addition is the single rounding of the exact sum in all but tie cases,
-    # which tests pin against std::fma (tests/test_fast5_cpu.py)
     return s + (err + e)
 
 

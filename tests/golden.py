@@ -44,7 +44,7 @@ def run(nxg, nyg, nt, lx=10.0, ly=10.0, lam=1.0, Cp0=1.0, T0=None):
 
 
 # ---------------------------------------------------------------------------
-# fast5 arithmetic (csrc/kernels/stencil_pipe.h, stencil_tbk.hip kernel 5): the
+# fast5 arithmetic (csrc/kernels/stencil_pipe.h, csrc/lab/stencil_kstep_lab.hip kernel 5): the
 # 5-point sum with one folded per-cell factor,
 #   T2 = fma(g, fma(ry, U+D, fma(-2(1+ry), c, R+L)), c),  g = dt*lam/dx^2 * iCp,
 # evaluated with EXACT rational fused multiply-adds (fractions.Fraction; int /
