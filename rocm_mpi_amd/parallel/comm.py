@@ -415,6 +415,11 @@ class LoopbackComm(Communicator):
                     raise RuntimeError(
                         f"loopback rank {self.rank}: no message from {o.peer} tag {o.tag} "
                         f"within {self.hub.timeout_s}s") from None
+                if v.is_cuda:
+                    # the clone was allocated on the peer's stream and is read
+                    # on this one: keep its block from the caching allocator
+                    # until this stream's copy has run
+                    v.record_stream(torch.cuda.current_stream(v.device))
                 o.tensor.copy_(v)
 
 
