@@ -84,6 +84,7 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("set_rank_for_errors", &set_rank_for_errors);
   m.def("rccl_version", &rccl_version);
+  m.def("rccl_library", &rccl_library);
   m.def("device_pci_bus_id", &device_pci_bus_id, py::arg("device"));
   m.def(
       "stencil_strip_cells",

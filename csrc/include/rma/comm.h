@@ -90,6 +90,8 @@ class RcclComm : public P2PTransport {
 };
 
 int rccl_version();
+// "linked" or the path RMA_RCCL_LIB loaded the native communicators' RCCL from
+std::string rccl_library();
 // PCI bus id ("0000:05:00.0") of a HIP device: tells whether two ranks drive
 // the same physical GPU (bench.py refuses that for a scaling point).
 std::string device_pci_bus_id(int device);

@@ -8,19 +8,91 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <thread>
+#include <type_traits>
+
+#include <dlfcn.h>
 
 #include "rma/hip_check.h"
 
 namespace rma {
+
+namespace {
+// ---------------------------------------------------------------------------
+// RCCL entry points. By default the library this core is linked against,
+// which in a torch process resolves to torch's bundled RCCL (it is loaded
+// first, into the global scope). RMA_RCCL_LIB=system (or a path) loads
+// /opt/rocm/lib/librccl.so.1 privately instead (RTLD_LOCAL | RTLD_DEEPBIND:
+// its internal calls bind to itself; it shares the process's HIP runtime) for
+// the native communicators only -- torch's own process groups keep theirs.
+// Used to test RCCL P2P under hipGraph capture with the system RCCL
+// (bench/rccl_graph_probe.py).
+struct RcclApi {
+  decltype(&ncclGetErrorString) GetErrorString = &ncclGetErrorString;
+  decltype(&ncclGetLastError) GetLastError = &ncclGetLastError;
+  decltype(&ncclGetVersion) GetVersion = &ncclGetVersion;
+  decltype(&ncclGetUniqueId) GetUniqueId = &ncclGetUniqueId;
+  decltype(&ncclCommInitRankConfig) CommInitRankConfig = &ncclCommInitRankConfig;
+  decltype(&ncclCommInitRank) CommInitRank = &ncclCommInitRank;
+  decltype(&ncclCommAbort) CommAbort = &ncclCommAbort;
+  decltype(&ncclCommGetAsyncError) CommGetAsyncError = &ncclCommGetAsyncError;
+  decltype(&ncclCommDestroy) CommDestroy = &ncclCommDestroy;
+  decltype(&ncclCommSplit) CommSplit = &ncclCommSplit;
+  decltype(&ncclGroupStart) GroupStart = &ncclGroupStart;
+  decltype(&ncclGroupEnd) GroupEnd = &ncclGroupEnd;
+  decltype(&ncclSend) Send = &ncclSend;
+  decltype(&ncclRecv) Recv = &ncclRecv;
+  decltype(&ncclAllReduce) AllReduce = &ncclAllReduce;
+  decltype(&ncclBroadcast) Broadcast = &ncclBroadcast;
+  std::string source = "linked";
+};
+
+RcclApi load_rccl_api() {
+  RcclApi a;
+  const char* e = std::getenv("RMA_RCCL_LIB");
+  if (!e || !*e || std::string(e) == "linked") return a;
+  const std::string path = std::string(e) == "system" ? "/opt/rocm/lib/librccl.so.1" : e;
+  void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+  if (!h) throw_error("RMA_RCCL_LIB: dlopen failed", __FILE__, __LINE__, dlerror());
+  auto sym = [&](auto& fp, const char* name) {
+    void* p = dlsym(h, name);
+    if (!p) throw_error("RMA_RCCL_LIB: missing symbol", __FILE__, __LINE__, name);
+    fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(p);
+  };
+  sym(a.GetErrorString, "ncclGetErrorString");
+  sym(a.GetLastError, "ncclGetLastError");
+  sym(a.GetVersion, "ncclGetVersion");
+  sym(a.GetUniqueId, "ncclGetUniqueId");
+  sym(a.CommInitRankConfig, "ncclCommInitRankConfig");
+  sym(a.CommInitRank, "ncclCommInitRank");
+  sym(a.CommAbort, "ncclCommAbort");
+  sym(a.CommGetAsyncError, "ncclCommGetAsyncError");
+  sym(a.CommDestroy, "ncclCommDestroy");
+  sym(a.CommSplit, "ncclCommSplit");
+  sym(a.GroupStart, "ncclGroupStart");
+  sym(a.GroupEnd, "ncclGroupEnd");
+  sym(a.Send, "ncclSend");
+  sym(a.Recv, "ncclRecv");
+  sym(a.AllReduce, "ncclAllReduce");
+  sym(a.Broadcast, "ncclBroadcast");
+  a.source = path;
+  return a;
+}
+
+const RcclApi& rccl() {
+  static const RcclApi a = load_rccl_api();
+  return a;
+}
+}  // namespace
 
 #define RMA_NCCL_CHECK(expr)                                                              \
   do {                                                                                    \
     ncclResult_t _r = (expr);                                                             \
     if (_r != ncclSuccess && _r != ncclInProgress) {                                      \
       ::rma::throw_error("RCCL call failed: " #expr, __FILE__, __LINE__,                  \
-                         std::string(ncclGetErrorString(_r)) + " / " +                    \
-                             (ncclGetLastError(nullptr) ? ncclGetLastError(nullptr) : "")); \
+                         std::string(rccl().GetErrorString(_r)) + " / " +                    \
+                             (rccl().GetLastError(nullptr) ? rccl().GetLastError(nullptr) : "")); \
     }                                                                                     \
   } while (0)
 
@@ -51,9 +123,11 @@ ncclRedOp_t to_nccl(RedOp o) {
 
 int rccl_version() {
   int v = 0;
-  ncclGetVersion(&v);
+  rccl().GetVersion(&v);
   return v;
 }
+
+std::string rccl_library() { return rccl().source; }
 
 std::string device_pci_bus_id(int device) {
   char buf[64] = {0};
@@ -63,7 +137,7 @@ std::string device_pci_bus_id(int device) {
 
 std::string RcclComm::unique_id() {
   ncclUniqueId id;
-  RMA_NCCL_CHECK(ncclGetUniqueId(&id));
+  RMA_NCCL_CHECK(rccl().GetUniqueId(&id));
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
@@ -82,7 +156,7 @@ RcclComm::RcclComm(int nranks, int rank, const std::string& uid, int device,
     timeout_s_ = init_timeout_s;
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
-    RMA_NCCL_CHECK(ncclCommInitRankConfig(&c, nranks, id, rank, &cfg));
+    RMA_NCCL_CHECK(rccl().CommInitRankConfig(&c, nranks, id, rank, &cfg));
     comm_ = c;
     poll_ready(comm_, "ncclCommInitRankConfig (did every rank join?)");
     // opt-in: a blocking data communicator split from this one. Measured
@@ -92,7 +166,7 @@ RcclComm::RcclComm(int nranks, int rank, const std::string& uid, int device,
     const char* db = std::getenv("RMA_RCCL_DATA_BLOCKING");
     if (db && db[0] == '1') split_blocking(rank);
   } else {
-    RMA_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+    RMA_NCCL_CHECK(rccl().CommInitRank(&c, nranks, id, rank));
     comm_ = c;
   }
   RMA_HIP_CHECK(hipMalloc(&scratch_, 2 * sizeof(double)));
@@ -107,14 +181,14 @@ void RcclComm::split_blocking(int rank) {
   ncclConfig_t bc = NCCL_CONFIG_INITIALIZER;
   bc.blocking = 1;
   ncclComm_t child = nullptr;
-  const ncclResult_t r = ncclCommSplit(C(comm_), 0, rank, &child, &bc);
+  const ncclResult_t r = rccl().CommSplit(C(comm_), 0, rank, &child, &bc);
   auto give_up = [&](const std::string& why) {
-    if (child) (void)ncclCommAbort(child);
+    if (child) (void)rccl().CommAbort(child);
     fprintf(stderr, "[rocm_mpi_amd rank %d] RCCL: no blocking data communicator (%s); "
             "group ends are polled\n", rank, why.c_str());
   };
   if (r != ncclSuccess && r != ncclInProgress) {
-    give_up(ncclGetErrorString(r));
+    give_up(rccl().GetErrorString(r));
     return;
   }
   // a non-blocking parent completes the split asynchronously
@@ -122,17 +196,17 @@ void RcclComm::split_blocking(int rank) {
   const double limit = std::min(timeout_s_, 120.0);
   for (int spins = 0;; ++spins) {
     ncclResult_t st = ncclSuccess;
-    (void)ncclCommGetAsyncError(C(comm_), &st);
+    (void)rccl().CommGetAsyncError(C(comm_), &st);
     if (st == ncclSuccess && child) {
       ncclResult_t cs = ncclSuccess;
-      (void)ncclCommGetAsyncError(child, &cs);
+      (void)rccl().CommGetAsyncError(child, &cs);
       if (cs == ncclSuccess) break;
       if (cs != ncclInProgress) {
-        give_up(ncclGetErrorString(cs));
+        give_up(rccl().GetErrorString(cs));
         return;
       }
     } else if (st != ncclSuccess && st != ncclInProgress) {
-      give_up(ncclGetErrorString(st));
+      give_up(rccl().GetErrorString(st));
       return;
     }
     if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
@@ -153,13 +227,13 @@ void RcclComm::poll_ready(void* comm, const char* what) {
   int spins = 0;
   for (;;) {
     ncclResult_t st = ncclSuccess;
-    const ncclResult_t r = ncclCommGetAsyncError(C(comm), &st);
+    const ncclResult_t r = rccl().CommGetAsyncError(C(comm), &st);
     if (r != ncclSuccess) st = r;
     if (st == ncclSuccess) return;
     if (st != ncclInProgress) {
       abort();
       throw_error("RCCL asynchronous error", __FILE__, __LINE__,
-                  std::string(what) + ": " + ncclGetErrorString(st));
+                  std::string(what) + ": " + rccl().GetErrorString(st));
     }
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (el > timeout_s_) {
@@ -184,8 +258,8 @@ void RcclComm::settle(const char* what) {
 RcclComm::~RcclComm() {
   if (scratch_) (void)hipFree(scratch_);
   if (aborted_) return;  // already torn down by abort()
-  if (comm_) (void)ncclCommDestroy(C(comm_));
-  if (parent_) (void)ncclCommDestroy(C(parent_));
+  if (comm_) (void)rccl().CommDestroy(C(comm_));
+  if (parent_) (void)rccl().CommDestroy(C(parent_));
 }
 
 bool RcclComm::capturable() const {
@@ -194,65 +268,65 @@ bool RcclComm::capturable() const {
 }
 
 void RcclComm::group_start() {
-  RMA_NCCL_CHECK(ncclGroupStart());
+  RMA_NCCL_CHECK(rccl().GroupStart());
   ++group_depth_;
 }
 void RcclComm::group_end() {
   --group_depth_;
-  RMA_NCCL_CHECK(ncclGroupEnd());
+  RMA_NCCL_CHECK(rccl().GroupEnd());
   if (group_depth_ == 0) settle("ncclGroupEnd");
 }
 
 void RcclComm::send(const void* buf, size_t bytes, int peer, stream_t stream) {
   RMA_CHECK_ARG(peer >= 0 && peer < nranks_, "peer " << peer);
-  RMA_NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, C(comm_), as_stream(stream)));
+  RMA_NCCL_CHECK(rccl().Send(buf, bytes, ncclUint8, peer, C(comm_), as_stream(stream)));
   if (group_depth_ == 0) settle("ncclSend");
 }
 
 void RcclComm::recv(void* buf, size_t bytes, int peer, stream_t stream) {
   RMA_CHECK_ARG(peer >= 0 && peer < nranks_, "peer " << peer);
-  RMA_NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, C(comm_), as_stream(stream)));
+  RMA_NCCL_CHECK(rccl().Recv(buf, bytes, ncclUint8, peer, C(comm_), as_stream(stream)));
   if (group_depth_ == 0) settle("ncclRecv");
 }
 
 void RcclComm::allreduce(const void* sendbuf, void* recvbuf, size_t count, DType dt, RedOp op,
                          stream_t stream) {
   RMA_NCCL_CHECK(
-      ncclAllReduce(sendbuf, recvbuf, count, to_nccl(dt), to_nccl(op), C(comm_), as_stream(stream)));
+      rccl().AllReduce(sendbuf, recvbuf, count, to_nccl(dt), to_nccl(op), C(comm_), as_stream(stream)));
   settle("ncclAllReduce");
 }
 
 void RcclComm::broadcast(const void* sendbuf, void* recvbuf, size_t count, DType dt, int root,
                          stream_t stream) {
   RMA_NCCL_CHECK(
-      ncclBroadcast(sendbuf, recvbuf, count, to_nccl(dt), root, C(comm_), as_stream(stream)));
+      rccl().Broadcast(sendbuf, recvbuf, count, to_nccl(dt), root, C(comm_), as_stream(stream)));
   settle("ncclBroadcast");
 }
 
 void RcclComm::gather(const void* sendbuf, void* recvbuf, size_t bytes, int root,
                       stream_t stream) {
   hipStream_t s = as_stream(stream);
-  RMA_NCCL_CHECK(ncclGroupStart());
+  RMA_NCCL_CHECK(rccl().GroupStart());
   if (rank_ == root) {
     for (int r = 0; r < nranks_; ++r) {
       char* dst = static_cast<char*>(recvbuf) + (size_t)r * bytes;
       if (r == root) {
         RMA_HIP_CHECK(hipMemcpyAsync(dst, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
       } else {
-        RMA_NCCL_CHECK(ncclRecv(dst, bytes, ncclUint8, r, C(comm_), s));
+        RMA_NCCL_CHECK(rccl().Recv(dst, bytes, ncclUint8, r, C(comm_), s));
       }
     }
   } else {
-    RMA_NCCL_CHECK(ncclSend(sendbuf, bytes, ncclUint8, root, C(comm_), s));
+    RMA_NCCL_CHECK(rccl().Send(sendbuf, bytes, ncclUint8, root, C(comm_), s));
   }
-  RMA_NCCL_CHECK(ncclGroupEnd());
+  RMA_NCCL_CHECK(rccl().GroupEnd());
   settle("gather");
 }
 
 void RcclComm::barrier(stream_t stream, double timeout_s) {
   hipStream_t s = as_stream(stream);
   RMA_HIP_CHECK(hipMemsetAsync(scratch_, 0, sizeof(double), s));
-  RMA_NCCL_CHECK(ncclAllReduce(scratch_, scratch_ + 1, 1, ncclFloat64, ncclSum, C(comm_), s));
+  RMA_NCCL_CHECK(rccl().AllReduce(scratch_, scratch_ + 1, 1, ncclFloat64, ncclSum, C(comm_), s));
   settle("barrier");
   wait(stream, timeout_s);
 }
@@ -260,10 +334,10 @@ void RcclComm::barrier(stream_t stream, double timeout_s) {
 void RcclComm::check_async() {
   if (aborted_) throw_error("communicator was aborted", __FILE__, __LINE__, "");
   ncclResult_t ar = ncclSuccess;
-  RMA_NCCL_CHECK(ncclCommGetAsyncError(C(comm_), &ar));
+  RMA_NCCL_CHECK(rccl().CommGetAsyncError(C(comm_), &ar));
   if (ar != ncclSuccess && ar != ncclInProgress) {
     abort();
-    throw_error("RCCL asynchronous error", __FILE__, __LINE__, ncclGetErrorString(ar));
+    throw_error("RCCL asynchronous error", __FILE__, __LINE__, rccl().GetErrorString(ar));
   }
 }
 
@@ -293,8 +367,8 @@ void RcclComm::wait(stream_t stream, double timeout_s) {
 void RcclComm::abort() {
   if (aborted_ || !comm_) return;
   aborted_ = true;
-  (void)ncclCommAbort(C(comm_));
-  if (parent_) (void)ncclCommAbort(C(parent_));
+  (void)rccl().CommAbort(C(comm_));
+  if (parent_) (void)rccl().CommAbort(C(parent_));
 }
 
 }  // namespace rma
