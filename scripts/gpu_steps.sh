@@ -53,6 +53,8 @@ for s in "$@"; do
     shape_alt_g) step shape_alt_g 400 python bench/interior_shape_probe.py --K 24 --coef physics \
              --init gaussian --alternate 12 --reps 2 --rects open,owned_x,owned_y,owned_xy \
              --out "$OUT/shape_alt_g.json" || exit 1 ;;
+    rccl_graph) step rccl_graph 500 python bench/rccl_graph_probe.py --n 4096 --steps 400 \
+             --out "$OUT/rccl_graph.json" || exit 1 ;;
     trace20) prof trace20 300 --kernel-trace --stats --output-format csv -d "$R/$OUT/trace20" \
              -o run -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
