@@ -34,6 +34,11 @@ def main() -> int:
                     help="P > 0: per rect, P passes alternating T <-> T2 (the executor's "
                          "buffer sequence on an evolving field), timed one by one")
     ap.add_argument("--rects", default="", help="comma list of rect names (default: all)")
+    ap.add_argument("--nosync", action="store_true",
+                    help="with --alternate: enqueue the P passes back to back (events only)")
+    ap.add_argument("--stream", default="default", choices=["default", "low", "high"],
+                    help="run the passes on a new stream of this priority (the executor's "
+                         "interior runs on a low-priority stream)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     n = a.n
@@ -81,6 +86,13 @@ def main() -> int:
     res = {"n": n, "K": K, "init": a.init, "kernel": names[kern], "vec": vec, "chunk_rows": ch,
            "coef": a.coef, "alternate": a.alternate, "ms": {}}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    stream = torch.cuda.current_stream()
+    if a.stream != "default":  # torch: lower number = higher priority
+        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") \
+            else (0, -1)
+        stream = torch.cuda.Stream(priority=lo if a.stream == "low" else hi)
+    res["stream"] = a.stream
+    res["nosync"] = a.nosync
     if a.alternate:
         # every rect starts from the same random field; passes alternate the
         # buffers like the executor (halo cells keep their values: no exchange)
@@ -90,15 +102,19 @@ def main() -> int:
                 init(T)  # no room for a saved copy at the 288 GB tile
                 T2.copy_(T)
                 src, dst = T, T2
-                ts = []
-                for _ in range(a.alternate):
-                    torch.cuda.synchronize()
-                    ev[0].record()
-                    ops.stencilk_step(K, dst, src, iCp, coef, rl, tn)
-                    ev[1].record()
-                    torch.cuda.synchronize()
-                    ts.append(round(ev[0].elapsed_time(ev[1]), 3))
-                    src, dst = dst, src
+                torch.cuda.synchronize()
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                       for _ in range(a.alternate)]
+                with torch.cuda.stream(stream):
+                    for e0, e1 in evs:
+                        if not a.nosync:
+                            torch.cuda.synchronize()
+                        e0.record()
+                        ops.stencilk_step(K, dst, src, iCp, coef, rl, tn)
+                        e1.record()
+                        src, dst = dst, src
+                torch.cuda.synchronize()
+                ts = [round(e0.elapsed_time(e1), 3) for e0, e1 in evs]
                 res["ms"].setdefault(name, []).append(ts)
                 print(json.dumps({name: ts}), flush=True)
         if a.out:

@@ -53,6 +53,22 @@ for s in "$@"; do
     shape_alt_g) step shape_alt_g 400 python bench/interior_shape_probe.py --K 24 --coef physics \
              --init gaussian --alternate 12 --reps 2 --rects open,owned_x,owned_y,owned_xy \
              --out "$OUT/shape_alt_g.json" || exit 1 ;;
+    shape_alt_lowns) step shape_alt_lowns 400 python bench/interior_shape_probe.py --K 24 \
+             --coef physics --alternate 12 --reps 2 --rects open,owned_x,owned_y,owned_xy \
+             --nosync --stream low --out "$OUT/shape_alt_lowns.json" || exit 1 ;;
+    nbr_x_plain) RMA_EXEC_STREAMS=plain step nbr_x_plain 400 python bench/rccl_self_overhead.py \
+             --K 24 --periodic x --steps 320 --pattern opop --out "$OUT/nbr_x_plain.json" || exit 1 ;;
+    nbr_x_perf) step nbr_x_perf 400 python bench/rccl_self_overhead.py --K 24 --periodic x \
+             --variants perf --steps 320 --pattern opop --out "$OUT/nbr_x_perf.json" || exit 1 ;;
+    pmc_x_perf_a) prof pmc_x_perf_a 240 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+             SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM GRBM_GUI_ACTIVE \
+             --output-format csv -d "$R/$OUT/pmc_x_perf_a" -o run -- python3 \
+             "$R/bench/rccl_self_overhead.py" --K 24 --periodic x --variants perf --steps 96 \
+             --pattern op || exit 1 ;;
+    pmc_x_perf_b) prof pmc_x_perf_b 240 --pmc FETCH_SIZE SQ_ACTIVE_INST_VALU SQ_INST_LEVEL_VMEM \
+             TCP_TCC_READ_REQ_sum GRBM_COUNT --output-format csv -d "$R/$OUT/pmc_x_perf_b" -o run \
+             -- python3 "$R/bench/rccl_self_overhead.py" --K 24 --periodic x --variants perf \
+             --steps 96 --pattern op || exit 1 ;;
     rccl_graph) step rccl_graph 500 python bench/rccl_graph_probe.py --n 4096 --steps 400 \
              --out "$OUT/rccl_graph.json" || exit 1 ;;
     trace20) prof trace20 300 --kernel-trace --stats --output-format csv -d "$R/$OUT/trace20" \
