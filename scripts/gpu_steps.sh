@@ -60,13 +60,13 @@ for s in "$@"; do
              --K 24 --periodic x --steps 320 --pattern opop --out "$OUT/nbr_x_plain.json" || exit 1 ;;
     nbr_x_perf) step nbr_x_perf 400 python bench/rccl_self_overhead.py --K 24 --periodic x \
              --variants perf --steps 320 --pattern opop --out "$OUT/nbr_x_perf.json" || exit 1 ;;
-    pmc_x_perf_a) prof pmc_x_perf_a 240 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
-             SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM GRBM_GUI_ACTIVE \
+    pmc_x_perf_a) prof pmc_x_perf_a 240 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+             SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CU_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE \
              --output-format csv -d "$R/$OUT/pmc_x_perf_a" -o run -- python3 \
              "$R/bench/rccl_self_overhead.py" --K 24 --periodic x --variants perf --steps 96 \
              --pattern op || exit 1 ;;
-    pmc_x_perf_b) prof pmc_x_perf_b 240 --pmc FETCH_SIZE SQ_ACTIVE_INST_VALU SQ_INST_LEVEL_VMEM \
-             TCP_TCC_READ_REQ_sum GRBM_COUNT --output-format csv -d "$R/$OUT/pmc_x_perf_b" -o run \
+    pmc_x_perf_b) prof pmc_x_perf_b 240 --pmc FETCH_SIZE SQ_WAVES SQ_INSTS_VMEM SQ_INSTS_SALU \
+             GRBM_COUNT --output-format csv -d "$R/$OUT/pmc_x_perf_b" -o run \
              -- python3 "$R/bench/rccl_self_overhead.py" --K 24 --periodic x --variants perf \
              --steps 96 --pattern op || exit 1 ;;
     rccl_graph) step rccl_graph 500 python bench/rccl_graph_probe.py --n 4096 --steps 400 \
