@@ -32,7 +32,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
-        chunk2: int = 0, dims: str = "xy", via_rccl: bool = True, init: str = "random") -> dict:
+        chunk2: int = 0, dims: str = "xy", via_rccl: bool = True, init: str = "random",
+        spacing=None) -> dict:
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
@@ -45,7 +46,7 @@ def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
                         self_via_transport=periodic and via_rccl)
     m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=n, nt=steps, quiet=True,
                                     init=init, periods=(px, py, 0), temporal=K,
-                                    fast_math=K > 1, chunk2=chunk2))
+                                    fast_math=K > 1, chunk2=chunk2, spacing=spacing))
     m.step(2 * K)
     m.synchronize()
     t0 = time.perf_counter()
@@ -85,6 +86,12 @@ def main(argv=None) -> int:
     ap.add_argument("--pattern", default="opop",
                     help="run order: o = open boundaries, p = periodic (each run allocates "
                          "its own tile)")
+    ap.add_argument("--spacing", default="grid", choices=["grid", "equal", "anisotropic"],
+                    help="grid: dx = 10/nx_g, dy = 10/ny_g of each run (a periodic dim has "
+                         "nx_g = n - 2K, so dx != dy and the coefficients differ from the open "
+                         "run's); equal: dx = dy = 10/n in every run (same coefficients, the "
+                         "halo path alone); anisotropic: dx = 10/(n - 2K), dy = 10/n in every "
+                         "run (the x-periodic coefficients everywhere)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -93,7 +100,10 @@ def main(argv=None) -> int:
     if not n:
         free, _ = torch.cuda.mem_get_info()
         n = int(math.isqrt(int(0.8 * free / 24))) // 256 * 256
+    spacing = {"grid": None, "equal": (10.0 / n, 10.0 / n),
+               "anisotropic": (10.0 / (n - 2 * a.K), 10.0 / n)}[a.spacing]
     out = {"tile": n, "K": a.K, "steps": a.steps, "periodic_dims": a.periodic,
+           "spacing": a.spacing,
            "periodic_via": "local copies" if a.self_copies else "rccl self send/recv",
            "init": a.init,
            "frame_sides": os.environ.get("RMA_FRAME_SIDES", "neighbours"), "variants": {}}
@@ -101,7 +111,7 @@ def main(argv=None) -> int:
         rows = []
         for periodic in (c == "p" for c in a.pattern):
             r = run(n, a.K, a.steps, periodic, variant, a.chunk2, a.periodic, not a.self_copies,
-                    a.init)
+                    a.init, spacing)
             r.update({"periodic_rccl_self": periodic,
                       "teff_GBps": 3 * n * n * 8 / 1e9 / (r["ms_per_step"] / 1e3)})
             rows.append(r)

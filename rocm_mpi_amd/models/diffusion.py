@@ -109,6 +109,11 @@ class DiffusionConfig:
     # equal to the canonical expression, bitwise equal to its C++ CPU twin
     # (which the CPU path then runs)
     fast_math: bool = False
+    # (dx, dy) instead of (lx/nx_g, ly/ny_g): probes that compare decompositions
+    # at equal coefficients (the pass energy, hence the power-capped clock,
+    # depends on them: ry = (dx/dy)^2 = 1 makes two of the three fast-math
+    # multipliers trivial; profiles/SUMMARY_r3.md)
+    spacing: tuple | None = None
 
     def validate(self) -> None:
         if self.variant not in VARIANTS:
@@ -152,8 +157,8 @@ class Diffusion2D:
             raise ValueError(f"global grid local size {g.nxyz} != config {(cfg.nx, cfg.ny)}")
         self.device = g.device
         nx, ny = cfg.nx, cfg.ny
-        self.dx = cfg.lx / gg.nx_g()
-        self.dy = cfg.ly / gg.ny_g()
+        self.dx = cfg.lx / gg.nx_g() if cfg.spacing is None else float(cfg.spacing[0])
+        self.dy = cfg.ly / gg.ny_g() if cfg.spacing is None else float(cfg.spacing[1])
         self.dt = min(self.dx * self.dx, self.dy * self.dy) * cfg.Cp0 / cfg.lam / 4.1
         self.coef = ops.StencilCoef.from_physics(cfg.lam, self.dx, self.dy, self.dt)
         dev = self.device

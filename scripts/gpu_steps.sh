@@ -44,6 +44,14 @@ for s in "$@"; do
     nbr_x_strips|nbr_y_strips|nbr_xy_strips) d=${s#nbr_}; d=${d%_strips}
              RMA_FRAME_ALIGNED=0 step "$s" 400 python bench/rccl_self_overhead.py --K 24 \
              --periodic "$d" --steps 320 --pattern opop --out "$OUT/$s.json" || exit 1 ;;
+    eq_x|eq_y|eq_xy) d=${s#eq_}
+             step "$s" 400 python bench/rccl_self_overhead.py --K 24 --periodic "$d" --steps 320 \
+             --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    eq_x_strips|eq_y_strips|eq_xy_strips) d=${s#eq_}; d=${d%_strips}
+             RMA_FRAME_ALIGNED=0 step "$s" 400 python bench/rccl_self_overhead.py --K 24 \
+             --periodic "$d" --steps 320 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    coef_ry) step coef_ry 400 python bench/rccl_self_overhead.py --K 24 --periodic x --steps 320 \
+             --pattern oo --spacing anisotropic --variants perf --out "$OUT/coef_ry.json" || exit 1 ;;
     host4096|host2048) n=${s#host}
              step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 1 --variants perf_hide \
              --steps 400 --pattern opop --out "$OUT/$s.json" || exit 1 ;;
