@@ -50,6 +50,10 @@ for s in "$@"; do
     eq_x_strips|eq_y_strips|eq_xy_strips) d=${s#eq_}; d=${d%_strips}
              RMA_FRAME_ALIGNED=0 step "$s" 400 python bench/rccl_self_overhead.py --K 24 \
              --periodic "$d" --steps 320 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    eq_x_a3072|eq_y_a3072|eq_xy_a3072) d=${s#eq_}; d=${d%_a3072}
+             RMA_FRAME_ALIGNED=1 step "$s" 400 python bench/rccl_self_overhead.py --K 24 \
+             --periodic "$d" --steps 320 --pattern opop --spacing equal --chunk2 3072 \
+             --out "$OUT/$s.json" || exit 1 ;;
     coef_ry) step coef_ry 400 python bench/rccl_self_overhead.py --K 24 --periodic x --steps 320 \
              --pattern oo --spacing anisotropic --variants perf --out "$OUT/coef_ry.json" || exit 1 ;;
     host4096|host2048) n=${s#host}
