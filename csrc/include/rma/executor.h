@@ -122,9 +122,6 @@ class DiffusionExecutor {
   // owned rect, frame (aligned: whole tasks of the interior's grid) and
   // interior (plan.h pass_geometry); cached per K.
   const PassGeom& geometry(int K);
-  // A perf_hide rank with a neighbour runs its K-step passes in tasks of at
-  // most this many rows, so the frame can be whole tasks (aligned layout).
-  static constexpr int kAlignedMaxRows = 1536;
 
  private:
   void enqueue_step(double* Tin, double* Tout);
@@ -132,7 +129,6 @@ class DiffusionExecutor {
   // kernel tuning of a K-step launch: part 0 = the interior / whole tile,
   // 1 = wide (y) frame strips, 2 = tall (x) frame strips
   StencilTuning pass_tuning(int K, int part = 0) const;
-  bool has_neighbor() const;
   void multi_step(int K, double* Tin, double* Tout, const double* iCp, int64_t nx, int64_t ny,
                   const Rect* rects, int n, const StencilTuning& tn, void* stream) const;
   void exchange(double* A, stream_t s);

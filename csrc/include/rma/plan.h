@@ -42,9 +42,10 @@ struct PassGeom {
   // the frame split by shape: wide (y-frames: full width, ~ol rows) and tall
   // (x-frames: ~ol columns, full height) strips run with different tunings
   std::vector<Rect> frame_wide, frame_tall;
-  // aligned: the frame is whole (strip, chunk) tasks of the interior's own
-  // task grid (task_w x task_h given), so frame + interior do the work of ONE
-  // launch; frame launches then use the interior tuning
+  // aligned: the tall frames are whole strip columns of the interior's own
+  // task grid (task_w given) and the bands whole task rows (task_h <= 1024)
+  // or the ol-K rows the exchange needs (taller tasks), so frame + interior do
+  // the work of ONE launch; frame launches then use the interior tuning
   bool aligned = false;
 };
 

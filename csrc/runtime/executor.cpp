@@ -222,27 +222,10 @@ std::vector<int> DiffusionExecutor::plan(int64_t nsteps) const {
   return plan_passes(nsteps, cost_);
 }
 
-bool DiffusionExecutor::has_neighbor() const {
-  return nbr_[0][0] >= 0 || nbr_[0][1] >= 0 || nbr_[1][0] >= 0 || nbr_[1][1] >= 0;
-}
-
 StencilTuning DiffusionExecutor::pass_tuning(int K, int part) const {
   StencilTuning t = fast5() ? fast_tune_k(K, ny_, p_.coef) : canonical_tune_k(K, ny_);
   t.nontemporal = p_.tune2.nontemporal;
-  if (p_.chunk_rows2 > 0) {
-    t.chunk_rows = p_.chunk_rows2;
-  } else if (p_.mode == Mode::kHide && t.kernel >= 9 && t.chunk_rows > kAlignedMaxRows &&
-             has_neighbor()) {
-    // The frame layout follows the neighbour configuration (VERDICT r2 item
-    // 5): a rank with a neighbour runs 1536-row tasks so its frame is whole
-    // tasks of the interior's grid (plan.cpp, aligned); a rank without one
-    // (and the solo re-time) keeps the longer chunks of the table. 288 GB
-    // tile, K=24, RCCL-self overhead vs open boundaries: x / y / xy periodic
-    // +3.8 / +2.4 / +2.5 % with ol-wide strips and 3072-row chunks, +2.6 /
-    // +2.2 / +0.5 % aligned (profiles/SUMMARY_r2.md, frame layout).
-    static const char* fa = std::getenv("RMA_FRAME_ALIGNED");
-    if (!(fa && fa[0] == '0')) t.chunk_rows = kAlignedMaxRows;
-  }
+  if (p_.chunk_rows2 > 0) t.chunk_rows = p_.chunk_rows2;
   if (K == 2 && !fast5()) t.unroll = p_.tune2.unroll;
   if (part == 0) return t;
   if (t.kernel >= 9 && part == 1) {

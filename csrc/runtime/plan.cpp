@@ -64,21 +64,31 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
   const bool any_nbr = nbr[0][0] >= 0 || nbr[0][1] >= 0 || nbr[1][0] >= 0 || nbr[1][1] >= 0;
   const Rect& o = g.out;
   const int64_t need_x = std::max(bwx, olx - o.x0), need_y = std::max(bwy, oly - o.y0);
-  // RMA_FRAME_ALIGNED=0 / 1 forces the choice; by default aligned frames are
-  // used up to 1536-row tasks (the executor caps a perf_hide rank with a
-  // neighbour at that, DiffusionExecutor::kAlignedMaxRows). Measured RCCL-self
-  // halo overhead per step at K=24 (profiles/frame_aligned_r2.json): 16384^2
-  // 5.7 -> 0.1 %, 32768^2 2.3-3.1 -> ~0 %, 65536^2 1.9-2.2 -> 0.1-0.4 %; at
-  // the 288 GB tile strips with 3072-row chunks vs aligned 1536-row tasks:
-  // x / y / xy periodic +3.8 / +2.4 / +2.5 % vs +2.6 / +2.2 / +0.5 %
-  // (profiles/SUMMARY_r2.md); bands shorter than a task were worse still.
+  // Frame layout (perf_hide with a neighbour). Tall x-frames are whole strip
+  // columns of the interior launch's task grid ("aligned": every frame cell
+  // is computed once, with the interior's tuning and recompute). The y-bands
+  // are whole task rows when tasks are short (<= 1024 rows) and only the ol-K
+  // rows the exchange needs otherwise: a 3072-row task row would put 6 % of
+  // the pass ahead of the exchange on the high-priority stream, and capping
+  // the tasks at 1536 rows costs a rank ~1 % on its own. Measured RCCL-self
+  // overhead at K=24 and EQUAL coefficients (dx = dy; the coefficients alone
+  // move the power-capped pass by ~2 %, profiles/SUMMARY_r3.md), 288 GB tile:
+  // x-periodic 0.35 % (tall task columns, 3072-row tasks) vs 1.3 % (1536-row
+  // tasks) vs 1.7 % (128-column strips); y 0.4-0.7 % (ol-wide bands) vs
+  // 1.6 % (task-row bands); smaller tiles (profiles/frame_aligned_r2.json):
+  // 16384^2 5.7 -> 0.1 %, 32768^2 2.3-3.1 -> ~0 %, 65536^2 1.9-2.2 -> 0.1-0.4 %.
+  // RMA_FRAME_ALIGNED=0 / 1 forces the layout (0: ol-wide strips everywhere);
+  // RMA_FRAME_BANDS=task / ol forces the band height.
   static const char* fa = std::getenv("RMA_FRAME_ALIGNED");
-  const bool want = fa && fa[0] ? fa[0] != '0' : task_h <= 1536;
-  if (want && hide && any_nbr && task_w >= need_x && task_h >= need_y &&
-      o.x1 - o.x0 >= 3 * task_w && o.y1 - o.y0 >= 3 * task_h) {
-    // frame = the interior launch's first / last chunk row (wide bands) and
-    // first / last strip column (tall strips): every frame cell is computed
-    // once, with the same recompute as in one launch of the owned rect
+  static const char* fb = std::getenv("RMA_FRAME_BANDS");
+  const bool want = fa && fa[0] ? fa[0] != '0' : true;
+  const bool task_bands = fb && fb[0] ? fb[0] == 't' : task_h <= 1024;
+  const int64_t band = task_bands ? task_h : need_y;  // y-band height
+  if (want && hide && any_nbr && task_w >= need_x && task_h >= 1 && band >= need_y &&
+      o.x1 - o.x0 >= 3 * task_w && o.y1 - o.y0 >= (task_bands ? 3 * task_h : 2 * band + 1)) {
+    // frame = the interior launch's first / last strip column (tall strips)
+    // and its first / last task row, or the ol-K rows the exchange needs
+    // (bands): every frame cell is computed once
     g.aligned = true;
     const auto side = frame_sides(nbr);
     const int64_t V = std::max(1, vec);
@@ -92,8 +102,8 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
       xr = o.x1 - task_w;
       xr += ((V - ((xr - K) % V + V) % V) % V);
     }
-    const int64_t yb = side[1][0] ? o.y0 + task_h : o.y0;
-    const int64_t yt = side[1][1] ? o.y1 - task_h : o.y1;
+    const int64_t yb = side[1][0] ? o.y0 + band : o.y0;
+    const int64_t yt = side[1][1] ? o.y1 - band : o.y1;
     if (side[1][0]) g.frame_wide.push_back({o.x0, o.x1, o.y0, yb});
     if (side[1][1]) g.frame_wide.push_back({o.x0, o.x1, yt, o.y1});
     if (side[0][0]) g.frame_tall.push_back({o.x0, xl, yb, yt});

@@ -306,16 +306,22 @@ int main() {
     EXPECT(throws([&] { owned_rect(20, 60, 10, all); }));  // minimal tile: nothing owned
     for (int K = 1; K <= 24; ++K) {
       for (const Neighbors* nb : {&none, &all, &self, &xhi_ylo, &xlo})
-        for (int variant = 0; variant < 3; ++variant) {
+        for (int variant = 0; variant < 4; ++variant) {
         // variant 0: ol-wide frame strips on a small tile; 1, 2: frames of
-        // whole pipelined tasks (aligned) on tiles large enough for them
+        // whole pipelined tasks (aligned) on tiles large enough for them; 3:
+        // tasks taller than 1024 rows: whole strip columns + ol-K-row bands
         const int64_t n0 = variant == 0 ? 2 * (2 * 24) + 8 : 2000 + 17 * variant;
         const int vec = variant == 2 ? 2 : 4;
-        const int64_t tw = (64 * vec - 2 * K) / vec * vec, th = 64 * variant;
+        const int64_t tw = (64 * vec - 2 * K) / vec * vec, th = variant == 3 ? 2048 : 64 * variant;
         PassGeom pg = pass_geometry(n0, n0 + 3, K, *nb, true, 1, 1, 48, 48,
                                     variant ? tw : 0, variant ? th : 0, vec);
-        if (variant && nb != &none && K >= 1) {
+        if (variant && variant < 3 && nb != &none && K >= 1) {
           EXPECT(pg.aligned == (tw >= 48 - pg.out.x0 && th >= 48 - pg.out.y0));
+        }
+        if (variant == 3 && nb != &none) {
+          EXPECT(pg.aligned == (tw >= 48 - pg.out.x0));
+          if (pg.aligned)
+            for (auto& q : pg.frame_wide) EXPECT(q.y1 - q.y0 == std::max<int64_t>(1, 48 - pg.out.y0));
         }
         if (pg.aligned) {  // every frame strip is one strip column of the grid
           for (auto& q : pg.frame_tall) {

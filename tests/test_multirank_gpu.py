@@ -360,3 +360,34 @@ def test_aligned_frames_on_partial_sides_bitwise(dims, K, fast, nt):
         gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
         assert misses <= 2 and hits + misses == len(plan)
+
+
+def spmd_bands(rank, hub, nx, ny, nt, dims, K, chunk2):
+    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], overlaps=(2 * K, 2 * K, 2),
+                        halowidths=(K, K, 1), quiet=True, loopback=(hub, rank))
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=nt, init="random",
+                                    quiet=True, dims=dims, temporal=K, fast_math=True,
+                                    chunk2=chunk2))
+    geo = m.executor.geometry(K)
+    m.step(nt)
+    out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g, geo)
+    m.close()
+    gg.finalize_global_grid()
+    return out
+
+
+@pytest.mark.parametrize("dims", [(1, 2), (2, 2)])
+def test_aligned_frames_with_ol_bands_bitwise(dims):
+    """Tasks taller than 1024 rows (the 288 GB tile's 3072): the tall frames
+    are whole strip columns of the interior's grid, the bands only the ol-K
+    rows the exchange needs; every tile == the 1-rank run, bitwise."""
+    K, nx, ny, nt = 8, 700, 2600, 19
+    res = run_loopback(dims[0] * dims[1], spmd_bands, nx, ny, nt, dims, K, 1100, timeout=180)
+    nxg, nyg, _ = res[0][2]
+    one = run_loopback(1, spmd_bands, nxg, nyg, nt, (1, 1), K, 1100, timeout=180)[0][1]
+    for coords, T, _, geo in res:
+        assert geo["aligned"], (coords, geo)
+        for r in geo["frame_wide"]:
+            assert r[3] - r[2] == K  # ol - K rows (overlap 2K, owned rect from K)
+        gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
+        assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
