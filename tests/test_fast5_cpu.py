@@ -82,3 +82,44 @@ def test_fast_math_decomposition_invariant_on_cpu(P, dims, K, nt):
     for coords, T, _, _ in res:
         gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx])
+
+
+def test_fma_exact_against_correct_rounding():
+    """fma_exact (the no-extension fallback's fma emulation) vs the
+    correctly rounded fma computed in exact rationals (float(Fraction) rounds
+    to nearest even): equal on random operands of mixed magnitude and under
+    near-total cancellation; on constructed near-ties (exact result within a
+    tiny distance of a rounding boundary) at most one ulp away, as its
+    docstring states."""
+    import fractions
+    import random
+
+    import torch
+
+    from rocm_mpi_amd.ops import fma_exact
+
+    F = fractions.Fraction
+    rng = random.Random(7)
+    n = 3000
+
+    def exact(a, b, c):
+        return torch.tensor([float(F(x) * F(y) + F(z)) for x, y, z in
+                             zip(a.tolist(), b.tolist(), c.tolist())], dtype=torch.float64)
+
+    a = torch.tensor([rng.uniform(-1, 1) for _ in range(n)], dtype=torch.float64)
+    b = torch.tensor([rng.uniform(-1, 1) * 10 ** rng.randint(-3, 3) for _ in range(n)],
+                     dtype=torch.float64)
+    c = torch.tensor([rng.uniform(-1, 1) * 10 ** rng.randint(-3, 3) for _ in range(n)],
+                     dtype=torch.float64)
+    assert torch.equal(fma_exact(a, b, c), exact(a, b, c))
+    c2 = -(a * b) * (1 + torch.tensor([rng.uniform(-1e-15, 1e-15) for _ in range(n)],
+                                      dtype=torch.float64))
+    assert torch.equal(fma_exact(a, b, c2), exact(a, b, c2))
+    # near-ties: c = -round(a*b) + half an ulp of the product (+- a hair)
+    p = a * b
+    half = torch.nextafter(p.abs(), torch.full_like(p, float("inf"))) - p.abs()
+    c3 = half / 2 * torch.sign(p) + torch.tensor([rng.choice((-1, 1)) * 2.0 ** -80
+                                                  for _ in range(n)], dtype=torch.float64)
+    r3, e3 = fma_exact(a, b, c3), exact(a, b, c3)
+    ulp = torch.nextafter(e3.abs(), torch.full_like(e3, float("inf"))) - e3.abs()
+    assert bool(((r3 - e3).abs() <= ulp).all())
