@@ -80,6 +80,12 @@ def main() -> int:
         "owned_x_far_only": (1, n - K, 1, n - 1),
         "owned_x_split_y24": [(K, n - K, 1, K), (K, n - K, K, n - 1)],
         "owned_y_split_x24": [(1, K, K, n - K), (K, n - 1, K, n - K)],
+        # r3 interior rects of the aligned layouts (K = 24, vec 4: strip 208 columns)
+        "al_x": (K + 208, n - K - 208, 1, n - 1),
+        "band_y": (1, n - 1, 2 * K, n - 2 * K),
+        "hyb_xy": (K + 208, n - K - 208, 2 * K, n - 2 * K),
+        "al1536_xy": (K + 208, n - K - 208, K + 1536, n - K - 1536),
+        "hyb_xy_rowphase": (K + 208, n - K - 208, 1 + 3072, n - 1 - 3072),
     }
     if a.rects:
         rects = {k: rects[k] for k in a.rects.split(",")}

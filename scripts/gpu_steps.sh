@@ -66,6 +66,12 @@ for s in "$@"; do
     shape_alt_g) step shape_alt_g 400 python bench/interior_shape_probe.py --K 24 --coef physics \
              --init gaussian --alternate 12 --reps 2 --rects open,owned_x,owned_y,owned_xy \
              --out "$OUT/shape_alt_g.json" || exit 1 ;;
+    shape_r3) step shape_r3 400 python bench/interior_shape_probe.py --K 24 --coef physics \
+             --alternate 8 --reps 2 --rects open,al_x,band_y,hyb_xy,al1536_xy,hyb_xy_rowphase \
+             --out "$OUT/shape_r3.json" || exit 1 ;;
+    eq_xy_bandtask) RMA_FRAME_BANDS=task step eq_xy_bandtask 400 python bench/rccl_self_overhead.py \
+             --K 24 --periodic xy --steps 320 --pattern opop --spacing equal \
+             --out "$OUT/eq_xy_bandtask.json" || exit 1 ;;
     shape_alt_lowns) step shape_alt_lowns 400 python bench/interior_shape_probe.py --K 24 \
              --coef physics --alternate 12 --reps 2 --rects open,owned_x,owned_y,owned_xy \
              --nosync --stream low --out "$OUT/shape_alt_lowns.json" || exit 1 ;;
