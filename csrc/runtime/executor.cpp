@@ -391,7 +391,15 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   if (!g.frame.empty()) {
     TraceRange tb("rma.boundary");
     if (g.aligned) {  // whole tasks of the interior grid: one launch, its tuning
-      multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame.data(), (int)g.frame.size(), tn, s_hi_);
+      // ...but round-robin over the XCDs: with ol-K-row bands the launch
+      // mixes ~1000 short band tasks with the tall frames' few dozen long
+      // task-column tasks, and the interior's XCD-contiguous order would put
+      // all long ones on the last XCD, which then finishes its share of the
+      // interior one task-wave late (+3 ms per K=24 pass at the 288 GB tile
+      // with x and y neighbours; profiles/SUMMARY_r3.md)
+      StencilTuning ft = tn;
+      ft.xcd_remap = 0;
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame.data(), (int)g.frame.size(), ft, s_hi_);
     } else {
       if (!g.frame_wide.empty())
         multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_wide.data(), (int)g.frame_wide.size(),
