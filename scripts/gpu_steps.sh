@@ -55,6 +55,9 @@ for s in "$@"; do
              RMA_FRAME_ALIGNED=1 step "$s" 400 python bench/rccl_self_overhead.py --K 24 \
              --periodic "$d" --steps 320 --pattern opop --spacing equal --chunk2 3072 \
              --out "$OUT/$s.json" || exit 1 ;;
+    eq16k_x|eq16k_y|eq16k_xy) d=${s#eq16k_}
+             step "$s" 300 python bench/rccl_self_overhead.py --n 16384 --K 24 --periodic "$d" \
+             --steps 960 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     coef_ry) step coef_ry 400 python bench/rccl_self_overhead.py --K 24 --periodic x --steps 320 \
              --pattern oo --spacing anisotropic --variants perf --out "$OUT/coef_ry.json" || exit 1 ;;
     host4096|host2048) n=${s#host}
