@@ -58,9 +58,11 @@ for s in "$@"; do
     eq16k_x|eq16k_y|eq16k_xy) d=${s#eq16k_}
              step "$s" 300 python bench/rccl_self_overhead.py --n 16384 --K 24 --periodic "$d" \
              --steps 960 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
-    eq4096_x|eq4096_xy|eq2048_xy) n=${s#eq}; n=${n%_*}; d=${s##*_}
-             step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 --periodic "$d" \
-             --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    eqn*) # eqn<N>_<dims>[_strips]: N^2 tile, K=24, equal coefficients
+             t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""
+             case $t in *_strips) fa=0 ;; esac
+             RMA_FRAME_ALIGNED=$fa step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
+             --periodic "$d" --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     coef_ry) step coef_ry 400 python bench/rccl_self_overhead.py --K 24 --periodic x --steps 320 \
              --pattern oo --spacing anisotropic --variants perf --out "$OUT/coef_ry.json" || exit 1 ;;
     host4096|host2048) n=${s#host}
