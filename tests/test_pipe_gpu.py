@@ -193,3 +193,34 @@ def test_pipe_limits():
     with pytest.raises(RuntimeError):  # no such stage split instantiated
         ops.stencilk_step(16, out, T, T, coef(), None, ops.StencilTuning(kernel="pipe", stages=5))
     assert native().pipe_max_k() == 24
+
+
+def test_lab_kernels_fail_loudly_until_loaded():
+    """The superseded / experimental K-step kernels live in librma_lab.so: in a
+    fresh process that has not loaded it, asking the core for one is a loud
+    error naming the library; after load_lab() the same launch runs."""
+    import subprocess
+    import sys
+
+    code = r'''
+import torch
+from rocm_mpi_amd._native import native, load_lab, lab_loaded
+from rocm_mpi_amd import ops
+T = torch.rand(64, 256, dtype=torch.float64, device="cuda")
+T2 = torch.zeros_like(T); iCp = torch.ones_like(T)
+s = torch.cuda.current_stream().cuda_stream
+args = (8, T2.data_ptr(), T.data_ptr(), iCp.data_ptr(), 256, 64, [(1, 255, 1, 63)],
+        (-1.0, 10.0, 10.0, 1e-4), 16, 3, s, True, -1, 2, ops.kernel_id("fast5"), 0, 0)
+assert not lab_loaded()
+try:
+    native().stencilk_rects(*args)
+    raise SystemExit("no error")
+except RuntimeError as e:
+    assert "librma_lab.so" in str(e), str(e)
+load_lab()
+native().stencilk_rects(*args)
+torch.cuda.synchronize()
+print("OK")
+'''
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr[-2000:]
