@@ -391,3 +391,54 @@ def test_aligned_frames_with_ol_bands_bitwise(dims):
             assert r[3] - r[2] < 2 * K  # the rows the exchange needs, not a 1100-row task row
         gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
+
+
+def test_halo_plan_cache_hits_evicts_and_stays_correct():
+    """HaloExchanger caches the plan + resolved copy batches per field
+    geometry: alternating T/T2 exchanges hit after the
+    first of each; a field needing larger pack buffers reallocates them and
+    drops the cache (stale pointers), and an LRU of 4 entries bounds it. Every
+    exchange (x periodic through RCCL send/recv to self: strided planes are
+    packed) leaves the halo columns equal to the periodic copies."""
+    from rocm_mpi_amd._native import native
+    from rocm_mpi_amd.parallel import comm as C
+
+    n = native()
+    rc = C.RcclComm(torch.device("cuda", torch.cuda.current_device()))
+    halo = n.HaloExchanger(rc.native, 0, [[0, 0], [-1, -1], [-1, -1]])
+    halo.set_self_via_transport(True)
+    s = torch.cuda.current_stream().cuda_stream
+
+    def field(ny, nx, seed):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        return torch.rand(ny, nx, generator=g, dtype=torch.float64).cuda()
+
+    def check(T, hw, ol):
+        ref = T.clone()
+        nx = T.shape[1]
+        ref[:, :hw] = T[:, nx - ol:nx - ol + hw]
+        ref[:, nx - hw:] = T[:, ol - hw:ol]
+        return ref
+
+    def run(T, hw=1, ol=2):
+        ref = check(T, hw, ol)
+        halo.exchange([(T.data_ptr(), (T.shape[1], T.shape[0], 1), 8, (ol, ol, 2), (hw, hw, 1))],
+                      s, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(T, ref)
+
+    A, B = field(40, 64, 1), field(40, 64, 2)
+    for T in (A, B, A, B, A):
+        run(T)
+    assert (halo.plan_misses, halo.plan_hits) == (2, 3)
+    Cbig = field(40, 64, 3)
+    run(Cbig, hw=3, ol=6)  # larger pack buffers: reallocated, cache dropped
+    run(A)
+    assert halo.plan_misses == 4
+    fs = [field(40, 64, 10 + i) for i in range(5)]
+    m0 = halo.plan_misses
+    for _ in range(2):
+        for T in fs:  # 5 fields cycling through a 4-entry LRU: every one misses
+            run(T)
+    assert halo.plan_misses - m0 == 10
+    rc.finalize()
