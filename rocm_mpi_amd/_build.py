@@ -213,7 +213,7 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
         if newer(exe, [src]):
             tooldir.mkdir(parents=True, exist_ok=True)
             cmd = [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", str(src),
-                   "-o", str(exe)]
+                   "-o", str(exe), f"-L{ROCM / 'lib'}", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"tool build failed: {src}\n{r.stdout}\n{r.stderr}")

@@ -96,6 +96,7 @@ for s in "$@"; do
              GRBM_COUNT --output-format csv -d "$R/$OUT/pmc_x_perf_b" -o run \
              -- python3 "$R/bench/rccl_self_overhead.py" --K 24 --periodic x --variants perf \
              --steps 96 --pattern op || exit 1 ;;
+    rccl_capture) step rccl_capture 120 build/bench/rccl_capture_probe 1048576 0 || exit 1 ;;
     rccl_graph) step rccl_graph 500 python bench/rccl_graph_probe.py --n 4096 --steps 400 \
              --out "$OUT/rccl_graph.json" || exit 1 ;;
     trace20) prof trace20 300 --kernel-trace --stats --output-format csv -d "$R/$OUT/trace20" \
