@@ -622,10 +622,12 @@ def run(a, world: int, rank: int) -> int:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
 
-    def fail_run(what: str, e: Exception, rc: int) -> int:
+    def fail_run(what: str, e: Exception, rc: int, wait_s: float | None = None) -> int:
         log(rank, f"{what}: {e}")
         emit(f"{what}: {e}")
-        finish_failed(rank, world, rc, 3 * tmo + 30)
+        # in the bounded check protocol rank 0 reports within 3 x timeout; after
+        # an unexpected error elsewhere it may be blocked in a collective
+        finish_failed(rank, world, rc, 3 * tmo + 30 if wait_s is None else wait_s)
         return rc  # not reached
 
     # --- preflight: before the HBM-sized allocation --------------------------
@@ -640,227 +642,235 @@ def run(a, world: int, rank: int) -> int:
         finally:
             wd.cancel()
 
-    nx = a.nx or auto_tile(a.hbm_frac, a.max_tile)
-    if world > 1 and not a.nx:
-        import torch.distributed as dist
+    try:
+        nx = a.nx or auto_tile(a.hbm_frac, a.max_tile)
+        if world > 1 and not a.nx:
+            import torch.distributed as dist
 
-        t = torch.tensor([nx], dtype=torch.int64)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=C._gloo_group())
-        nx = int(t.item())
-    ny = a.ny or nx
-    cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup, device=dev,
-                          warmup=a.warmup, init="random", b_width=bw, dims=dims,
-                          chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
-                          unroll=a.unroll, vec=a.vec, temporal=K, chunk2=a.chunk2,
-                          unroll2=a.unroll2, use_graph=a.graph, quiet=True,
-                          fast_math=a.fast_math and a.variant != "kp")
-    t_setup = time.perf_counter()
-    gkw = {}
-    if a.overlap:
-        gkw = {"overlaps": (a.overlap, a.overlap, 2), "halowidths": (K, K, 1)}
-    model = Diffusion2D(cfg, grid_kwargs=gkw)
-    g = model.g
-    comm = g.comm
-    if gpu and world > 1 and g.transport != "rccl" and not shared:
-        log(rank, f"halo transport is {g.transport!r}, a multi-GPU point needs RCCL")
-        return 2
-    model.synchronize()
-    comm.barrier()
-    setup_s = time.perf_counter() - t_setup
-
-    fast_used = bool(model.cfg.fast_math)  # the side measurements below switch it off
-    plan_warm = model.plan(a.warmup)
-    plan_timed = model.plan(a.steps)
-    model.step(a.warmup)
-    model.synchronize()
-    comm.barrier()
-    model.enable_pass_timing(True)  # 5 event records per pass (~us against ~70 ms passes)
-    sync()
-    t0 = time.perf_counter()
-    model.step(a.steps)
-    sync()
-    own_s = time.perf_counter() - t0  # this rank's own time, before the closing barrier
-    comm.barrier()
-    local_s = time.perf_counter() - t0
-    wall = comm.allreduce(local_s, "max")
-    nbrs = any(p >= 0 for side in g.neighbors[:2] for p in side)
-    timings = summarize_timings(model.pass_timings(), exchange=nbrs)
-    model.enable_pass_timing(False)
-    bad = float(model.field[:: max(1, ny // 64), :: max(1, nx // 64)].isfinite().logical_not().sum())
-    bad = comm.allreduce(bad, "sum")
-    a_eff = 3 * nx * ny * 8 / 1e9
-
-    def side_teff(Kside, fast, steps):
-        model.set_temporal(Kside, fast_math=fast)
-        model.step(2 * Kside)
+            t = torch.tensor([nx], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=C._gloo_group())
+            nx = int(t.item())
+        ny = a.ny or nx
+        cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup, device=dev,
+                              warmup=a.warmup, init="random", b_width=bw, dims=dims,
+                              chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
+                              unroll=a.unroll, vec=a.vec, temporal=K, chunk2=a.chunk2,
+                              unroll2=a.unroll2, use_graph=a.graph, quiet=True,
+                              fast_math=a.fast_math and a.variant != "kp")
+        t_setup = time.perf_counter()
+        gkw = {}
+        if a.overlap:
+            gkw = {"overlaps": (a.overlap, a.overlap, 2), "halowidths": (K, K, 1)}
+        model = Diffusion2D(cfg, grid_kwargs=gkw)
+        g = model.g
+        comm = g.comm
+        if gpu and world > 1 and g.transport != "rccl" and not shared:
+            log(rank, f"halo transport is {g.transport!r}, a multi-GPU point needs RCCL")
+            return 2
         model.synchronize()
         comm.barrier()
-        sync()
-        s0 = time.perf_counter()
-        model.step(steps)
-        sync()
-        comm.barrier()
-        s1 = comm.allreduce(time.perf_counter() - s0, "max")
-        return a_eff / (s1 / steps)
+        setup_s = time.perf_counter() - t_setup
 
-    # same-run weak-scaling reference: every rank re-times its tile without
-    # the exchange (one launch per pass), all ranks concurrently; each rank's
-    # own (pre-barrier) solo time identifies a slow GPU independently of the halo
-    solo_steps = a.steps if a.solo_steps < 0 else a.solo_steps
-    solo = solo_own = None
-    if solo_steps > 0:
-        model.set_solo(True)
+        fast_used = bool(model.cfg.fast_math)  # the side measurements below switch it off
+        plan_warm = model.plan(a.warmup)
+        plan_timed = model.plan(a.steps)
         model.step(a.warmup)
         model.synchronize()
         comm.barrier()
+        model.enable_pass_timing(True)  # 5 event records per pass (~us against ~70 ms passes)
         sync()
-        s0 = time.perf_counter()
-        model.step(solo_steps)
+        t0 = time.perf_counter()
+        model.step(a.steps)
         sync()
-        solo_own = (time.perf_counter() - s0) / solo_steps
+        own_s = time.perf_counter() - t0  # this rank's own time, before the closing barrier
         comm.barrier()
-        solo = comm.allreduce(time.perf_counter() - s0, "max") / solo_steps
-        model.set_solo(False)
+        local_s = time.perf_counter() - t0
+        wall = comm.allreduce(local_s, "max")
+        nbrs = any(p >= 0 for side in g.neighbors[:2] for p in side)
+        timings = summarize_timings(model.pass_timings(), exchange=nbrs)
+        model.enable_pass_timing(False)
+        bad = float(model.field[:: max(1, ny // 64), :: max(1, nx // 64)].isfinite().logical_not().sum())
+        bad = comm.allreduce(bad, "sum")
+        a_eff = 3 * nx * ny * 8 / 1e9
 
-    detail = {"rank": rank, "coords": list(g.coords[:2]),
-              "neighbors": [list(p) for p in g.neighbors[:2]], "pci_bus_id": bus,
-              "ms_per_step": round(own_s / a.steps * 1e3, 6),
-              "teff_GBps": round(a_eff / (own_s / a.steps), 2),
-              "solo_ms_per_step": round(solo_own * 1e3, 6) if solo_own else None,
-              "pass_timing": {k: (round(v, 4) if isinstance(v, float) else v)
-                              for k, v in timings.items() if k != "note"}}
-    ranks_detail = gather_obj(detail, world)
-    teff_ranks = [d["teff_GBps"] for d in ranks_detail]
+        def side_teff(Kside, fast, steps):
+            model.set_temporal(Kside, fast_math=fast)
+            model.step(2 * Kside)
+            model.synchronize()
+            comm.barrier()
+            sync()
+            s0 = time.perf_counter()
+            model.step(steps)
+            sync()
+            comm.barrier()
+            s1 = comm.allreduce(time.perf_counter() - s0, "max")
+            return a_eff / (s1 / steps)
 
-    # side measurements on the same tile: the canonical (bitwise) K-step
-    # passes and the one-step kernel (24 B/cell/step at the HBM roofline)
-    single = canonical = None
-    kc = 1
-    if K > 1:  # the canonical depth <= K with the lowest measured cost per step
-        from rocm_mpi_amd._native import has_native, native
+        # same-run weak-scaling reference: every rank re-times its tile without
+        # the exchange (one launch per pass), all ranks concurrently; each rank's
+        # own (pre-barrier) solo time identifies a slow GPU independently of the halo
+        solo_steps = a.steps if a.solo_steps < 0 else a.solo_steps
+        solo = solo_own = None
+        if solo_steps > 0:
+            model.set_solo(True)
+            model.step(a.warmup)
+            model.synchronize()
+            comm.barrier()
+            sync()
+            s0 = time.perf_counter()
+            model.step(solo_steps)
+            sync()
+            solo_own = (time.perf_counter() - s0) / solo_steps
+            comm.barrier()
+            solo = comm.allreduce(time.perf_counter() - s0, "max") / solo_steps
+            model.set_solo(False)
 
-        if has_native():
-            cc = native().default_pass_costs(K, False, float(nx) * float(ny))
-            kc = min(range(1, K + 1), key=lambda k: cc[k] / k)
-        else:
-            kc = min(K, 8)
-    if a.single_step_steps > 0 and K > 1:
-        if a.fast_math:
-            canonical = side_teff(kc, False, a.canonical_steps or 2 * kc)
-        single = side_teff(1, False, a.single_step_steps)
+        detail = {"rank": rank, "coords": list(g.coords[:2]),
+                  "neighbors": [list(p) for p in g.neighbors[:2]], "pci_bus_id": bus,
+                  "ms_per_step": round(own_s / a.steps * 1e3, 6),
+                  "teff_GBps": round(a_eff / (own_s / a.steps), 2),
+                  "solo_ms_per_step": round(solo_own * 1e3, 6) if solo_own else None,
+                  "pass_timing": {k: (round(v, 4) if isinstance(v, float) else v)
+                                  for k, v in timings.items() if k != "note"}}
+        ranks_detail = gather_obj(detail, world)
+        teff_ranks = [d["teff_GBps"] for d in ranks_detail]
 
-    kinfo = None
-    if K > 1:
-        from rocm_mpi_amd import ops
-        from rocm_mpi_amd._native import has_native, native
+        # side measurements on the same tile: the canonical (bitwise) K-step
+        # passes and the one-step kernel (24 B/cell/step at the HBM roofline)
+        single = canonical = None
+        kc = 1
+        if K > 1:  # the canonical depth <= K with the lowest measured cost per step
+            from rocm_mpi_amd._native import has_native, native
 
-        if has_native():
-            depth = max(plan_timed)
-            if a.fast_math:
-                kern, kvec, kch = native().fast_kernel_k(depth, ny, tuple(model.coef))
+            if has_native():
+                cc = native().default_pass_costs(K, False, float(nx) * float(ny))
+                kc = min(range(1, K + 1), key=lambda k: cc[k] / k)
             else:
-                kern, kvec, kch = native().canonical_kernel_k(depth, ny)
-            names = {v: k for k, v in ops.KERNELS.items()}
-            kinfo = {"kernel": names[kern], "vec": kvec, "chunk_rows": a.chunk2 or kch,
-                     "stages": native().pipe_default_stages(depth) if kern >= 9 else None}
-    model.close()
-    del model
-    if gpu:
-        torch.cuda.empty_cache()
+                kc = min(K, 8)
+        if a.single_step_steps > 0 and K > 1:
+            if a.fast_math:
+                canonical = side_teff(kc, False, a.canonical_steps or 2 * kc)
+            single = side_teff(1, False, a.single_step_steps)
 
-    t_it = wall / a.steps
-    teff_gpu = a_eff / t_it
-    total = teff_gpu * world
-    if not nbrs:
-        par = "single rank, no halo exchange (one launch per pass)"
-    else:
-        tdesc = {"rccl": "RCCL send/recv over xGMI", "staged": "host-staged copies + gloo",
-                 "gloo": "gloo (CPU twin)", "loopback": "in-process loopback",
-                 "self": "periodic self copies"}.get(g.transport, g.transport)
-        par = f"halo: {tdesc}" + (", boundary frame + exchange on a high-priority stream "
-                                  "overlapped with the interior" if a.variant == "perf_hide"
-                                  else ", exchange after each pass")
-    # without a neighbour the solo re-time IS the run: no same-run efficiency
-    eff_same = (solo / t_it) if solo and nbrs else None
-    if shared:
-        par = f"SHARED-GPU FUNCTIONAL TEST, {world} ranks on {n_gpus} GPU, not a scaling point; {par}"
-    out.update({"value": round(total, 2), "ms_per_step": round(t_it * 1e3, 6)})
-    out["config"].update({
-        "global_batch": g.nxyz_g[0] * g.nxyz_g[1],
-        "seq_len": None,
-        "parallelism": f"2D domain decomposition dims {g.dims[0]}x{g.dims[1]} ({par})",
-        "local_grid": [nx, ny],
-        "global_grid": [g.nxyz_g[0], g.nxyz_g[1]],
-        "teff_per_gpu_GBps": round(teff_gpu, 2),
-        "teff_per_gpu_min_GBps": round(min(teff_ranks), 2),
-        "teff_per_gpu_max_GBps": round(max(teff_ranks), 2),
-        "slowest_rank": int(max(range(world), key=lambda r: ranks_detail[r]["ms_per_step"])),
-        "a_eff_GB_per_step": round(a_eff, 6),
-        "max_steps_per_pass": K,
-        "passes_warmup": plan_warm,
-        "passes_timed": plan_timed,
-        "kstep_kernel": kinfo,
-        "fast_math": fast_used,
-        "pass_timing": timings,
-        "ranks_detail": ranks_detail,
-        "solo_ms_per_step": round(solo * 1e3, 6) if solo else None,
-        "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,
-        "rccl_halo_bitwise_ok": None,
-        "halo_check": None,
-        "fast_math_drift_max": None,
-        "drift_check": None,
-        "teff_note": ("T_eff = A_eff/t_step with A_eff = 3*nx*ny*8 B (reference "
-                      "perf.jl:55-58). With temporal blocking every step of every cell "
-                      "is computed, but HBM is read/written once per pass of up to "
-                      f"{K} steps, so T_eff exceeds the HBM bandwidth and is a time per "
-                      "step, not a memory throughput; teff_single_step_kernel_GBps is "
-                      "the one-step kernel on the same tile (the like-for-like memory "
-                      "number). fast_math: the passes evaluate the same fp64 update as "
-                      "a 5-point sum with one folded per-cell factor and FMAs "
-                      "(rounding-level deviation from the canonical update, bounded in "
-                      "fast_math_drift_max for this run's length; bitwise "
-                      "equal to its CPU twin, tests/test_pipe_gpu.py); "
-                      "teff_bitwise_kstep_GBps is the canonical K-step kernel on the "
-                      "same tile") if K > 1 else "",
-        "teff_single_step_kernel_GBps": round(single, 2) if single else None,
-        "teff_bitwise_kstep_GBps": round(canonical, 2) if canonical else None,
-        "bitwise_kstep_steps_per_pass": kc if canonical else None,
-        "overlap": list(g.overlaps[:2]),
-        "transport": g.transport,
-        "hipgraph": bool(a.graph),
-        "setup_s": round(setup_s, 3),
-        "nonfinite_cells_sampled": int(bad),
-    })
+        kinfo = None
+        if K > 1:
+            from rocm_mpi_amd import ops
+            from rocm_mpi_amd._native import has_native, native
 
-    # --- correctness of this run's code paths (bounded; any failure fails all)
-    rc = 0 if bad == 0 else 3
-    drift_steps = (a.warmup + a.steps) if a.drift_steps < 0 else a.drift_steps
-    if (check_on or drift_steps) and a.variant != "kp":
-        wd = Watchdog(rank, world, 3 * tmo, "check phase", emit)
-        try:
-            if drift_steps and fast_used and K > 1:
-                try:
-                    di = drift_check(check_n, K, drift_steps, dev, world, tmo)
-                except CheckFailed as e:
-                    out["config"]["drift_check"] = e.args[1] if len(e.args) > 1 else None
-                    raise
-                out["config"]["drift_check"] = di
-                out["config"]["fast_math_drift_max"] = di["fast_math_drift_max"]
-            if check_on:
-                try:
-                    hc = halo_check(check_n, dims[:2], K, dev, world, rank, tmo,
-                                    self_rccl=self_rccl)
-                except CheckFailed as e:
-                    out["config"]["rccl_halo_bitwise_ok"] = False
-                    out["config"]["halo_check"] = dict(e.args[1] if len(e.args) > 1 else {},
-                                                       error=str(e.args[0]))
-                    raise
-                out["config"]["halo_check"] = hc
-                out["config"]["rccl_halo_bitwise_ok"] = True
-        except CheckFailed as e:
-            return fail_run("check", CheckFailed(e.args[0]), 4)
-        finally:
-            wd.cancel()
+            if has_native():
+                depth = max(plan_timed)
+                if a.fast_math:
+                    kern, kvec, kch = native().fast_kernel_k(depth, ny, tuple(model.coef))
+                else:
+                    kern, kvec, kch = native().canonical_kernel_k(depth, ny)
+                names = {v: k for k, v in ops.KERNELS.items()}
+                kinfo = {"kernel": names[kern], "vec": kvec, "chunk_rows": a.chunk2 or kch,
+                         "stages": native().pipe_default_stages(depth) if kern >= 9 else None}
+        model.close()
+        del model
+        if gpu:
+            torch.cuda.empty_cache()
+
+        t_it = wall / a.steps
+        teff_gpu = a_eff / t_it
+        total = teff_gpu * world
+        if not nbrs:
+            par = "single rank, no halo exchange (one launch per pass)"
+        else:
+            tdesc = {"rccl": "RCCL send/recv over xGMI", "staged": "host-staged copies + gloo",
+                     "gloo": "gloo (CPU twin)", "loopback": "in-process loopback",
+                     "self": "periodic self copies"}.get(g.transport, g.transport)
+            par = f"halo: {tdesc}" + (", boundary frame + exchange on a high-priority stream "
+                                      "overlapped with the interior" if a.variant == "perf_hide"
+                                      else ", exchange after each pass")
+        # without a neighbour the solo re-time IS the run: no same-run efficiency
+        eff_same = (solo / t_it) if solo and nbrs else None
+        if shared:
+            par = f"SHARED-GPU FUNCTIONAL TEST, {world} ranks on {n_gpus} GPU, not a scaling point; {par}"
+        out.update({"value": round(total, 2), "ms_per_step": round(t_it * 1e3, 6)})
+        out["config"].update({
+            "global_batch": g.nxyz_g[0] * g.nxyz_g[1],
+            "seq_len": None,
+            "parallelism": f"2D domain decomposition dims {g.dims[0]}x{g.dims[1]} ({par})",
+            "local_grid": [nx, ny],
+            "global_grid": [g.nxyz_g[0], g.nxyz_g[1]],
+            "teff_per_gpu_GBps": round(teff_gpu, 2),
+            "teff_per_gpu_min_GBps": round(min(teff_ranks), 2),
+            "teff_per_gpu_max_GBps": round(max(teff_ranks), 2),
+            "slowest_rank": int(max(range(world), key=lambda r: ranks_detail[r]["ms_per_step"])),
+            "a_eff_GB_per_step": round(a_eff, 6),
+            "max_steps_per_pass": K,
+            "passes_warmup": plan_warm,
+            "passes_timed": plan_timed,
+            "kstep_kernel": kinfo,
+            "fast_math": fast_used,
+            "pass_timing": timings,
+            "ranks_detail": ranks_detail,
+            "solo_ms_per_step": round(solo * 1e3, 6) if solo else None,
+            "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,
+            "rccl_halo_bitwise_ok": None,
+            "halo_check": None,
+            "fast_math_drift_max": None,
+            "drift_check": None,
+            "teff_note": ("T_eff = A_eff/t_step with A_eff = 3*nx*ny*8 B (reference "
+                          "perf.jl:55-58). With temporal blocking every step of every cell "
+                          "is computed, but HBM is read/written once per pass of up to "
+                          f"{K} steps, so T_eff exceeds the HBM bandwidth and is a time per "
+                          "step, not a memory throughput; teff_single_step_kernel_GBps is "
+                          "the one-step kernel on the same tile (the like-for-like memory "
+                          "number). fast_math: the passes evaluate the same fp64 update as "
+                          "a 5-point sum with one folded per-cell factor and FMAs "
+                          "(rounding-level deviation from the canonical update, bounded in "
+                          "fast_math_drift_max for this run's length; bitwise "
+                          "equal to its CPU twin, tests/test_pipe_gpu.py); "
+                          "teff_bitwise_kstep_GBps is the canonical K-step kernel on the "
+                          "same tile") if K > 1 else "",
+            "teff_single_step_kernel_GBps": round(single, 2) if single else None,
+            "teff_bitwise_kstep_GBps": round(canonical, 2) if canonical else None,
+            "bitwise_kstep_steps_per_pass": kc if canonical else None,
+            "overlap": list(g.overlaps[:2]),
+            "transport": g.transport,
+            "hipgraph": bool(a.graph),
+            "setup_s": round(setup_s, 3),
+            "nonfinite_cells_sampled": int(bad),
+        })
+
+        # --- correctness of this run's code paths (bounded; any failure fails all)
+        rc = 0 if bad == 0 else 3
+        drift_steps = (a.warmup + a.steps) if a.drift_steps < 0 else a.drift_steps
+        if (check_on or drift_steps) and a.variant != "kp":
+            wd = Watchdog(rank, world, 3 * tmo, "check phase", emit)
+            try:
+                if drift_steps and fast_used and K > 1:
+                    try:
+                        di = drift_check(check_n, K, drift_steps, dev, world, tmo)
+                    except CheckFailed as e:
+                        out["config"]["drift_check"] = e.args[1] if len(e.args) > 1 else None
+                        raise
+                    out["config"]["drift_check"] = di
+                    out["config"]["fast_math_drift_max"] = di["fast_math_drift_max"]
+                if check_on:
+                    try:
+                        hc = halo_check(check_n, dims[:2], K, dev, world, rank, tmo,
+                                        self_rccl=self_rccl)
+                    except CheckFailed as e:
+                        out["config"]["rccl_halo_bitwise_ok"] = False
+                        out["config"]["halo_check"] = dict(e.args[1] if len(e.args) > 1 else {},
+                                                           error=str(e.args[0]))
+                        raise
+                    out["config"]["halo_check"] = hc
+                    out["config"]["rccl_halo_bitwise_ok"] = True
+            except CheckFailed as e:
+                return fail_run("check", CheckFailed(e.args[0]), 4)
+            except Exception as e:  # noqa: BLE001 - an unexpected error is a failed check
+                return fail_run("check", RuntimeError(f"{type(e).__name__}: {e}"), 4)
+            finally:
+                wd.cancel()
+    except Exception as e:  # noqa: BLE001 - this rank reports and fails; torchrun ends the rest
+        import traceback
+
+        traceback.print_exc()
+        return fail_run("run", RuntimeError(f"{type(e).__name__}: {e}"), 5, wait_s=10.0)
     emit()
     if world > 1:
         C.shutdown_distributed()
