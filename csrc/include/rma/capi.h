@@ -87,6 +87,17 @@ int rma_executor_create_kf(rma_grid* g, int mode, double* T, double* T2, const d
                            int64_t nx, int64_t ny, const double coef[4], int64_t bwx,
                            int64_t bwy, int steps_per_pass, int fast_math, double* qx,
                            double* qy, double* dTdt, rma_executor** out);
+// Same with `graph_steps` > 0: steps are replayed from a hipGraph capturing
+// `graph_steps` steps (the host enqueue cost of a step drops to a graph launch);
+// needs a capturable halo transport (RCCL: RMA_RCCL_GRAPH=1, see README).
+int rma_executor_create_g(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
+                          int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
+                          int steps_per_pass, int fast_math, int graph_steps, double* qx,
+                          double* qy, double* dTdt, rma_executor** out);
+/* Single-rank grid: route the periodic self-neighbours through a 1-rank RCCL
+ * communicator (send/recv to itself) instead of local copies -- the GPU-direct
+ * P2P path on one GPU (tests, probes). Call before creating executors. */
+int rma_grid_self_via_rccl(rma_grid* g);
 int rma_executor_run(rma_executor* e, int64_t nsteps, void* stream);
 int rma_executor_parity(const rma_executor* e);
 int rma_executor_destroy(rma_executor* e);

@@ -246,6 +246,46 @@ int rma_executor_create_kf(rma_grid* g, int mode, double* T, double* T2, const d
   });
 }
 
+int rma_executor_create_g(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
+                          int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
+                          int steps_per_pass, int fast_math, int graph_steps, double* qx,
+                          double* qy, double* dTdt, rma_executor** out) {
+  return guard([&] {
+    RMA_CHECK_ARG(g && out && mode >= 0 && mode <= 2, "bad executor arguments");
+    rma::ExecParams p;
+    p.mode = static_cast<rma::Mode>(mode);
+    p.coef = {coef[0], coef[1], coef[2], coef[3]};
+    p.bwx = bwx;
+    p.bwy = bwy;
+    p.temporal = steps_per_pass;
+    p.olx = g->overlaps[0];
+    p.oly = g->overlaps[1];
+    p.tune2 = rma::default_tune_k(steps_per_pass, ny);
+    p.fast_math = fast_math ? 1 : 0;
+    p.use_graph = graph_steps > 0 ? 1 : 0;
+    p.graph_steps = graph_steps > 0 ? graph_steps : 0;
+    auto e = std::make_unique<rma_executor>();
+    e->ex = std::make_unique<rma::DiffusionExecutor>(T, T2, iCp, nx, ny, p, g->halo.get(), qx, qy,
+                                                     dTdt);
+    *out = e.release();
+  });
+}
+
+int rma_grid_self_via_rccl(rma_grid* g) {
+  return guard([&] {
+    RMA_CHECK_ARG(g != nullptr, "grid is NULL");
+    RMA_CHECK_ARG(g->nprocs == 1, "self via RCCL is for a single-rank grid");
+    if (!g->comm) {
+      const std::string uid = rma::RcclComm::unique_id();
+      const char* tb = std::getenv("RMA_RCCL_BLOCKING");
+      const double init_timeout = (tb && tb[0] == '1') ? 0.0 : 300.0;
+      g->comm = std::make_unique<rma::RcclComm>(1, 0, uid, g->device, init_timeout);
+    }
+    g->halo = std::make_unique<rma::HaloExchanger>(g->comm.get(), 0, g->topo->neighbors(0));
+    g->halo->set_self_via_transport(true);
+  });
+}
+
 int rma_executor_create(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
                         int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
                         double* qx, double* qy, double* dTdt, rma_executor** out) {

@@ -97,6 +97,10 @@ for s in "$@"; do
              -- python3 "$R/bench/rccl_self_overhead.py" --K 24 --periodic x --variants perf \
              --steps 96 --pattern op || exit 1 ;;
     rccl_capture) step rccl_capture 120 build/bench/rccl_capture_probe 1048576 0 || exit 1 ;;
+    capi_graph) RMA_RCCL_GRAPH=1 RMA_RCCL_BLOCKING=1 step capi_graph 180 \
+             build/examples/rccl_graph_capi 4096 400 1 || exit 1 ;;
+    capi_graph_k24) RMA_RCCL_GRAPH=1 RMA_RCCL_BLOCKING=1 step capi_graph_k24 180 \
+             build/examples/rccl_graph_capi 4096 2400 24 || exit 1 ;;
     rccl_graph) step rccl_graph 500 python bench/rccl_graph_probe.py --n 4096 --steps 400 \
              --out "$OUT/rccl_graph.json" || exit 1 ;;
     trace20) prof trace20 300 --kernel-trace --stats --output-format csv -d "$R/$OUT/trace20" \
