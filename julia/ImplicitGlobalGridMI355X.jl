@@ -114,17 +114,22 @@ end
 # steps_per_pass = K (1..24): at most K steps per kernel pass; run! plans the
 # passes (csrc/runtime/plan.cpp). fast_math=true: every pass uses the
 # 5-point-sum arithmetic (rounding-level difference from the canonical update,
-# bitwise equal to its C++ CPU twin).
+# bitwise equal to its C++ CPU twin). graph_steps > 0: replay steps from a
+# hipGraph of that many steps (rma_executor_create_g; needs a capturable halo
+# transport).
 function DiffusionExecutor(T, T2, iCp, coef::NTuple{4,Float64}; mode::Integer=1,
-                           steps_per_pass::Integer=1, b_width=(1, 1), fast_math::Bool=false)
+                           steps_per_pass::Integer=1, b_width=(1, 1), fast_math::Bool=false,
+                           graph_steps::Integer=0)
     out = Ref{Ptr{Cvoid}}(C_NULL)
     c = collect(coef)
     nx, ny = size(T, 1), size(T, 2)
-    check(ccall(sym(:rma_executor_create_kf), Cint,
+    check(ccall(sym(:rma_executor_create_g), Cint,
                 (Ptr{Cvoid}, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Ptr{Float64},
-                 Int64, Int64, Cint, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                 Int64, Int64, Cint, Cint, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid},
+                 Ptr{Ptr{Cvoid}}),
                 GRID[], mode, pointer(T), pointer(T2), pointer(iCp), nx, ny, c, b_width[1],
-                b_width[2], steps_per_pass, Cint(fast_math), C_NULL, C_NULL, C_NULL, out))
+                b_width[2], steps_per_pass, Cint(fast_math), Cint(graph_steps), C_NULL, C_NULL,
+                C_NULL, out))
     ex = DiffusionExecutor(out[], T, T2)
     finalizer(e -> ccall(sym(:rma_executor_destroy), Cint, (Ptr{Cvoid},), e.ptr), ex)
     return ex
