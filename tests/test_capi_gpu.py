@@ -166,3 +166,40 @@ def test_capi_error_reporting():
                                  ctypes.c_int64(1), 25, None, None, None, ctypes.byref(ex))
     assert rc != 0 and b"temporal" in L.rma_last_error()
     ck(L, L.rma_finalize_global_grid(g))
+
+
+@pytest.mark.parametrize("K,via_rccl", [(1, False), (8, False), (8, True)])
+def test_capi_graph_executor_and_self_via_rccl(K, via_rccl):
+    """rma_executor_create_g: a periodic single-rank perf_hide tile replayed
+    from hipGraphs (local periodic copies are capturable) == the eager run;
+    rma_grid_self_via_rccl routes the halos through RCCL send/recv to itself
+    (eager: RCCL is not captured in a torch process) == the same field."""
+    L = lib()
+    nx, ny, nt = 514, 300, 43
+    s = torch.cuda.current_stream().cuda_stream
+
+    def run(graph_steps, rccl):
+        g = grid(L, nx, ny, K, periods=(1, 1, 0))
+        if rccl:
+            ck(L, L.rma_grid_self_via_rccl(g))
+        T = torch.from_numpy(golden.initial(nx, ny)).cuda()
+        T2 = T.clone()
+        iCp = torch.ones_like(T)
+        ex = ctypes.c_void_p()
+        ck(L, L.rma_executor_create_g(g, 1, ctypes.c_void_p(T.data_ptr()),
+                                      ctypes.c_void_p(T2.data_ptr()),
+                                      ctypes.c_void_p(iCp.data_ptr()), ctypes.c_int64(nx),
+                                      ctypes.c_int64(ny), coef4(L, g, nx, ny), ctypes.c_int64(1),
+                                      ctypes.c_int64(1), K, 0, graph_steps, None, None, None,
+                                      ctypes.byref(ex)))
+        ck(L, L.rma_executor_run(ex, ctypes.c_int64(nt), ctypes.c_void_p(s)))
+        par = L.rma_executor_parity(ex)
+        torch.cuda.synchronize()
+        out = (T2 if par else T).cpu().numpy()
+        ck(L, L.rma_executor_destroy(ex))
+        ck(L, L.rma_finalize_global_grid(g))
+        return out
+
+    eager = run(0, False)
+    other = run(0, True) if via_rccl else run(10, False)
+    assert np.array_equal(eager, other)
