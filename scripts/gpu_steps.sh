@@ -63,6 +63,10 @@ for s in "$@"; do
              case $t in *_strips) fa=0 ;; esac
              RMA_FRAME_ALIGNED=$fa step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
              --periodic "$d" --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    chunk_sweep) step chunk_sweep 400 python bench/pass_sweep.py --pipe 20,24 --pipec "" \
+             --ldsdpp "" --old "" --alt "" --rounds 3 \
+             --chunks "20:2048/3072/4096/6144,24:2048/3072/4096/6144" \
+             --out "$OUT/chunk_sweep.json" || exit 1 ;;
     coef_ry) step coef_ry 400 python bench/rccl_self_overhead.py --K 24 --periodic x --steps 320 \
              --pattern oo --spacing anisotropic --variants perf --out "$OUT/coef_ry.json" || exit 1 ;;
     host4096|host2048) n=${s#host}
