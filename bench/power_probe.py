@@ -8,6 +8,12 @@ second, and reports the median pass time with the median power and clock of
 the samples taken inside that window. Prints one JSON document.
 
     python bench/power_probe.py --configs pipe:16,pipe:20,pipe:24,pipeb:20 --seconds 6
+    python bench/power_probe.py --configs pipe:24:iso,pipe:24:aniso,pipe:24:pow2
+
+A third field picks the coefficients: iso (dx = dy = 10/n: ry = (dx/dy)^2 = 1, the
+default), aniso (dx = 10/(n - 48), dy = 10/n: a single x-periodic rank's ry), pow2
+(dx = 10/(2n) = dy/2 exactly: ry = 0.25, a power of two) -- the pass energy at the
+power cap depends on the constant multipliers (profiles/SUMMARY_r3.md section 1).
 """
 from __future__ import annotations
 
@@ -75,8 +81,11 @@ def main(argv=None) -> int:
     T2 = T.clone()
     iCp = torch.empty_like(T)
     ops.fill_(iCp, 1.0)
-    dx = 10.0 / n
-    coef = ops.StencilCoef.from_physics(1.0, dx, dx, dx * dx / 4.1)
+    def coef_of(which: str) -> ops.StencilCoef:
+        dy = 10.0 / n
+        dx = {"iso": dy, "aniso": 10.0 / (n - 48), "pow2": 10.0 / (2 * n)}[which]
+        return ops.StencilCoef.from_physics(1.0, dx, dy, min(dx * dx, dy * dy) / 4.1)
+
     rect = [ops.interior_rect(n, n)]
     samples: list = []
     stop = threading.Event()
@@ -94,8 +103,10 @@ def main(argv=None) -> int:
     cap = smi_power_cap()
     rows = []
     for item in a.configs.split(","):
-        kind, K = item.split(":")
+        kind, K, *rest = item.split(":")
         K = int(K)
+        which = rest[0] if rest else "iso"
+        coef = coef_of(which)
         if kind == "march":
             def launch():
                 ops.stencil_step(T2, T, iCp, coef, rect, ops.StencilTuning())
@@ -120,7 +131,9 @@ def main(argv=None) -> int:
         win = [s for s in samples if t0 + 1.0 <= s["t"] <= t1]
         pw = [s["power_W"] for s in win if "power_W" in s]
         ck = [s["sclk_MHz"] for s in win if "sclk_MHz" in s]
-        rows.append({"kernel": kind, "K": K, "ms_per_pass": round(statistics.median(times), 3),
+        rows.append({"kernel": kind, "K": K, "coef": which,
+                     "ry": ops.fast5_constants(coef)[0],
+                     "ms_per_pass": round(statistics.median(times), 3),
                      "ms_per_step": round(statistics.median(times) / K, 4), "launches": len(times),
                      "power_W": statistics.median(pw) if pw else None,
                      "sclk_MHz": statistics.median(ck) if ck else None, "samples": len(win)})

@@ -67,6 +67,9 @@ for s in "$@"; do
              --ldsdpp "" --old "" --alt "" --rounds 3 \
              --chunks "20:2048/3072/4096/6144,24:2048/3072/4096/6144" \
              --out "$OUT/chunk_sweep.json" || exit 1 ;;
+    power_coef) step power_coef 400 python bench/power_probe.py --seconds 5 \
+             --configs pipe:24:iso,pipe:24:aniso,pipe:24:pow2,pipe:24:iso,pipe:24:aniso,pipe:24:pow2 \
+             --out "$OUT/power_coef.json" || exit 1 ;;
     coef_ry) step coef_ry 400 python bench/rccl_self_overhead.py --K 24 --periodic x --steps 320 \
              --pattern oo --spacing anisotropic --variants perf --out "$OUT/coef_ry.json" || exit 1 ;;
     host4096|host2048) n=${s#host}
