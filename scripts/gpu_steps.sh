@@ -35,6 +35,8 @@ for s in "$@"; do
              tests/test_bench_gpu.py tests/test_drift_gpu.py \
              "tests/test_multirank_gpu.py::test_aligned_frames_on_partial_sides_bitwise" \
              "tests/test_multirank_gpu.py::test_aligned_frames_with_ol_bands_bitwise" || exit 1 ;;
+    tests_capi) step tests_capi 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+             tests/test_capi_gpu.py || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
