@@ -111,7 +111,10 @@ def _headers() -> list[Path]:
 def source_stamp() -> str:
     """Hash of every source and header, the flags and the arch."""
     h = hashlib.sha1()
-    h.update(" ".join(COMMON + [ARCH, sysconfig.get_config_var("EXT_SUFFIX") or ""]).encode())
+    # flags with the checkout's absolute path taken out: a snapshot of the same
+    # tree under another directory (a GPU box) has the same stamp
+    flags = " ".join(COMMON + [ARCH, sysconfig.get_config_var("EXT_SUFFIX") or ""])
+    h.update(flags.replace(str(ROOT), "<root>").encode())
     for p in sorted(set(HIP_SOURCES + LAB_SOURCES + HOST_SOURCES + EXAMPLES + TOOLS + _headers())):
         h.update(str(p.relative_to(ROOT)).encode())
         h.update(p.read_bytes())

@@ -442,3 +442,24 @@ def test_halo_plan_cache_hits_evicts_and_stays_correct():
             run(T)
     assert halo.plan_misses - m0 == 10
     rc.finalize()
+
+
+@pytest.mark.parametrize("K,gs,nt", [(8, 10, 43), (8, 8, 43), (6, 10, 43), (4, 10, 43), (8, 20, 61)])
+@pytest.mark.parametrize("fast", [False, True])
+def test_graph_replay_matches_eager_periodic(K, gs, nt, fast):
+    """hipGraph replay of planned mixed-depth passes (a captured plan of gs
+    steps replayed, the remainder eager) == the eager run, on a periodic
+    single-rank tile (local periodic copies: capturable)."""
+    def run(graph):
+        gg.init_global_grid(514, 300, 1, periodx=1, periody=1, overlaps=(2 * K, 2 * K, 2),
+                            halowidths=(K, K, 1), quiet=True)
+        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=514, ny=300, nt=nt,
+                                        init="random", quiet=True, periods=(1, 1, 0),
+                                        temporal=K, fast_math=fast, use_graph=graph,
+                                        graph_steps=gs))
+        m.step(nt)
+        f = m.field.cpu().clone()
+        m.close()
+        gg.finalize_global_grid()
+        return f
+    assert torch.equal(run(True), run(False))
