@@ -47,6 +47,9 @@ def main(argv=None):
     ap.add_argument("--chunksc", default="", help="pipec K:c1/c2/..., chunk-row variants")
     ap.add_argument("--pipe2", default="", help="depths of the 2-column-wave pipe kernel")
     ap.add_argument("--chunks2", default="", help="pipe2 K:c1/c2/..., chunk-row variants")
+    ap.add_argument("--pipe5", default="", help="depths of the pipe kernel at 5 cells per lane "
+                    "(needs n % 5 == 0)")
+    ap.add_argument("--chunks5", default="", help="pipe5 K:c1/c2/..., chunk-row variants")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -75,7 +78,7 @@ def main(argv=None):
         # the executor's rows per task for this kernel and depth
         if c or a.chunk:
             return c or a.chunk
-        if kind in ("pipe", "pipe2", "pipeb"):
+        if kind in ("pipe", "pipe2", "pipeb", "pipe5"):
             return N.pipe_chunk_rows(K, n, False) or N.default_chunk_k(max(K, 3), n)
         if kind == "pipec":
             return N.pipe_chunk_rows(K, n, True) or N.default_chunk_k(max(K, 3), n)
@@ -101,6 +104,11 @@ def main(argv=None):
         for c in cs.split("/"):
             cfgs.append(("pipec", int(K), 0, int(c)))
     cfgs += [("pipe2", K, 0) for K in krange(a.pipe2)]
+    cfgs += [("pipe5", K, 0) for K in krange(a.pipe5)]
+    for item in filter(None, a.chunks5.split(",")):
+        K, cs = item.split(":")
+        for c in cs.split("/"):
+            cfgs.append(("pipe5", int(K), 0, int(c)))
     for item in filter(None, a.chunks2.split(",")):
         K, cs = item.split(":")
         for c in cs.split("/"):
@@ -114,9 +122,9 @@ def main(argv=None):
         elif kind == "two_step":
             ops.stencil2_step(T2, T, iCp, coef, rect, ops.StencilTuning(chunk_rows=16, unroll=2))
         else:
-            vec = 2 if kind in ("lds_dpp", "fast5") else 4
+            vec = 2 if kind in ("lds_dpp", "fast5") else 5 if kind == "pipe5" else 4
             tn = ops.StencilTuning(chunk_rows=chunk(K, c, kind),
-                                   kernel="pipe" if kind == "pipe2" else kind,
+                                   kernel="pipe" if kind in ("pipe2", "pipe5") else kind,
                                    vec=vec, xcd_remap=1, stages=S, cols=2 if kind == "pipe2" else 0)
             ops.stencilk_step(K, T2, T, iCp, coef, rect, tn)
 
@@ -142,10 +150,11 @@ def main(argv=None):
         kind, K, S = c[:3]
         med = statistics.median(times[c])
         rows.append({"kernel": kind, "K": K, "stages": S or (native().pipe_default_stages(K)
-                                                             if kind in ops.PIPE + ("pipe2",)
+                                                             if kind in ops.PIPE + ("pipe2", "pipe5")
                                                              else 0),
                      "chunk_rows": (chunk(K, c[3] if len(c) > 3 else 0, kind)
                                     if kind not in ("march", "two_step") else None),
+                     "vec": (N.pipe_vec(K, S, 0, n, 5, True) if kind == "pipe5" else None),
                      "ms_per_pass": round(med, 3), "ms_min": round(min(times[c]), 3),
                      "ms_per_step": round(med / K, 4), "rel": round(med / base, 4),
                      "teff_equiv_GBps": round(K * 24 * n * n / 1e9 / (med / 1e3), 1)})

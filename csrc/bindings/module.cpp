@@ -381,6 +381,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("arith") = 0);
   m.def("pipe_has_cols", &pipe_has_cols, py::arg("K"), py::arg("stages"), py::arg("arith"),
         py::arg("cols"));
+  m.def("pipe_vec", &pipe_vec, py::arg("K"), py::arg("stages"), py::arg("arith"), py::arg("nx"),
+        py::arg("requested"), py::arg("aligned16") = true);
   m.def("pipe_max_k", []() { return kPipeMaxK; });
   m.def(
       "pass_geometry",

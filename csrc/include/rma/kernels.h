@@ -83,6 +83,11 @@ bool pipe_has(int K, int stages, int arith = 0);
 // pipe_default_cols is what a tuning of cols = 0 runs.
 bool pipe_has_cols(int K, int stages, int arith, int cols);
 int pipe_default_cols(int K, int stages, int arith);
+// Cells per lane the pipelined kernel runs for a requested tuning.vec: 5
+// (fast5, K = 16..20, nx % 5 == 0: lanes never straddle the array edge; 8-B
+// aligned accesses), else 4 / 2 with 16-B aligned arrays and nx % 4 / % 2,
+// else 1. The executor's frame geometry uses the same answer.
+int pipe_vec(int K, int stages, int arith, int64_t nx, int requested, bool aligned16);
 // arith: 0 fast5, 1 canonical, 2 fast5 with ds_bpermute lane moves (kernel 11)
 void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const double* T,
                             const double* iCp, int64_t nx, int64_t ny, const Rect* rects,

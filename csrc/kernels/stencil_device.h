@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "rma/kernels.h"
 
@@ -17,6 +18,13 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int64_t kColMaxWidth = 8;  // rects at most this wide run in column mode
 typedef double dbl2 __attribute__((ext_vector_type(2)));  // native 16-byte vector
+// 16-byte vector at 8-byte alignment: 5 cells per lane put every other lane's
+// pairs on an odd cell (global_load/store_dwordx4 take dword alignment)
+typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
+
+// the 16-byte vector type of a V-cell row access (odd V: 8-byte aligned)
+template <int V>
+using dbl2v = typename std::conditional<V % 2 == 0, dbl2, dbl2u>::type;
 
 struct RectList {
   Rect r[kMaxRects];
@@ -36,11 +44,12 @@ __device__ __forceinline__ void load_row(double (&out)[V], const double* __restr
   } else {
 #pragma unroll
     for (int h = 0; h < V / 2; ++h) {
-      const dbl2* q = reinterpret_cast<const dbl2*>(p) + h;
-      const dbl2 t = NTL ? __builtin_nontemporal_load(q) : *q;
+      const dbl2v<V>* q = reinterpret_cast<const dbl2v<V>*>(p + 2 * h);
+      const dbl2v<V> t = NTL ? __builtin_nontemporal_load(q) : *q;
       out[2 * h] = t.x;
       out[2 * h + 1] = t.y;
     }
+    if constexpr (V % 2 == 1) out[V - 1] = NTL ? __builtin_nontemporal_load(p + V - 1) : p[V - 1];
   }
 }
 
@@ -54,14 +63,21 @@ __device__ __forceinline__ void store_row(double* __restrict__ p, const double (
     if (all) {
 #pragma unroll
       for (int h = 0; h < V / 2; ++h) {
-        dbl2 t;
+        dbl2v<V> t;
         t.x = v[2 * h];
         t.y = v[2 * h + 1];
-        dbl2* q = reinterpret_cast<dbl2*>(p) + h;
+        dbl2v<V>* q = reinterpret_cast<dbl2v<V>*>(p + 2 * h);
         if constexpr (NT) {
           __builtin_nontemporal_store(t, q);
         } else {
           *q = t;
+        }
+      }
+      if constexpr (V % 2 == 1) {
+        if constexpr (NT) {
+          __builtin_nontemporal_store(v[V - 1], p + V - 1);
+        } else {
+          p[V - 1] = v[V - 1];
         }
       }
       return;

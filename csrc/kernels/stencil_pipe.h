@@ -49,6 +49,28 @@ struct Plan {
   static_assert(S >= 1 && HL >= 1 && HL <= H, "bad stage split");
 };
 
+// Five cells per lane (fast5, one column wave): 320-column windows recompute
+// 2K of 320 columns instead of 2K of 256 (K=24: 1.185x vs 1.231x, K=20:
+// 1.143x vs 1.185x fp64 work) and move 4 lane values per 5 cells instead of
+// per 4. Two blocks per CU need <= 80 KiB of LDS per block, so at V = 5:
+//  * LDS rows are v-major (cell v of lane l at v*64 + l): every access is a
+//    contiguous 512-B ds_*_b64 per v (no bank conflicts at 40-B lane pitch),
+//    and rows sit on 512-B multiples, so one base VGPR with immediate
+//    offsets (ds_read2st64_b64) reaches every row of the ring;
+//  * stage 0 writes its factor row one iteration late (row i-1 at iteration
+//    i, levels 1/2 use the factors of rows i/i-1 from registers), which saves
+//    one ring row: R = K + S - 2 (K=20: 22 + 4 mirrors + 6 hand-off rows =
+//    exactly 80 KiB; without mirrors the level loop takes one immediate-
+//    offset path whenever the stage's rows do not wrap).
+// Registers bound the depth: K <= 20 (236 VGPRs at K = 20; the 6-level
+// stages of K >= 21 spill, stencil_pipe_d.hip).
+template <int V>
+constexpr bool kDelayedRing = V == 5;
+template <int K, int S, int V>
+constexpr int ring_rows() {
+  return Plan<K, S>::R - (kDelayedRing<V> ? 1 : 0);
+}
+
 // Block geometry with C column waves per stage (C = 1: one 64V-column window
 // per strip). With C > 1 the C waves of a stage sit D = 64V - 2*Hp columns
 // apart (Hp = H rounded up to even) and all exchange through the block-wide
@@ -76,7 +98,9 @@ constexpr int kArFast5 = 0, kArCanon = 1, kArFast5Perm = 2;
 template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int occupancy(int lds) {
   const int by_lds = (160 * 1024) / lds * S * C / 4;
-  const int vgpr = Canon ? 8 * Plan<K, S>::H * V + 8 * V + 64 : 6 * Plan<K, S>::H * V + 8 * V + 40;
+  // (V = 5: 142-150 VGPRs measured at K = 20/24, the V <= 4 estimate would claim 1 wave)
+  const int vgpr = Canon ? 8 * Plan<K, S>::H * V + 8 * V + 64
+                         : (V == 5 ? 5 : 6) * Plan<K, S>::H * V + 8 * V + 40;
   const int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
   const int w = by_lds < by_vgpr ? by_lds : by_vgpr;
   return w < 1 ? 1 : (w > 8 ? 8 : w);
@@ -91,7 +115,7 @@ constexpr int occupancy(int lds) {
 template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int mirror_rows() {
   constexpr int H = Plan<K, S>::H, row = Geo<K, S, V, C>::WB * 8;
-  constexpr int base = (Plan<K, S>::R + 2 * (S > 1 ? S - 1 : 1)) * row;
+  constexpr int base = (ring_rows<K, S, V>() + 2 * (S > 1 ? S - 1 : 1)) * row;
   return occupancy<K, S, V, Canon, C>(base + (H - 1) * row) ==
                  occupancy<K, S, V, Canon, C>(base)
              ? H - 1
@@ -101,7 +125,7 @@ constexpr int mirror_rows() {
 // LDS bytes of one block (ring + mirrors + double-buffered hand-off rows)
 template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int lds_bytes() {
-  return (Plan<K, S>::R + mirror_rows<K, S, V, Canon, C>() + 2 * (S > 1 ? S - 1 : 1)) *
+  return (ring_rows<K, S, V>() + mirror_rows<K, S, V, Canon, C>() + 2 * (S > 1 ? S - 1 : 1)) *
          Geo<K, S, V, C>::WB * 8;
 }
 
@@ -141,7 +165,9 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm;
   using G = Geo<K, S, V, C>;
-  constexpr int H = P::H, HL = P::HL, R = P::R, M = mirror_rows<K, S, V, Canon, C>();
+  constexpr int H = P::H, HL = P::HL, R = ring_rows<K, S, V>(), M = mirror_rows<K, S, V, Canon, C>();
+  constexpr bool kDelay = kDelayedRing<V>;
+  static_assert(V != 5 || (C == 1 && Ar == kArFast5), "5 cells per lane: fast5, one column wave");
   constexpr int W = G::W, WB = G::WB, D = G::D;
   constexpr int kStep = G::kStep;  // output columns per strip (plan_strip_tasks, sw = WB)
   constexpr int NH = S > 1 ? S - 1 : 1;
@@ -220,6 +246,9 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   auto rd2 = [&](const double* row, double (&out)[V]) {
     if constexpr (V == 1) {
       out[0] = row[lane];
+    } else if constexpr (V == 5) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) out[v] = row[v * kWave + lane];
     } else {
 #pragma unroll
       for (int h = 0; h < V / 2; ++h) {
@@ -232,6 +261,9 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   auto wr2 = [&](double* row, const double (&in)[V]) {
     if constexpr (V == 1) {
       row[lane] = in[0];
+    } else if constexpr (V == 5) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) row[v * kWave + lane] = in[v];
     } else {
 #pragma unroll
       for (int h = 0; h < V / 2; ++h) {
@@ -244,6 +276,9 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     }
   };
   int slot0 = 0;  // ring slot of row i (stage 0's level-1 row)
+  double gp[V];   // delayed ring: stage 0's factors of row i-1
+#pragma unroll
+  for (int v = 0; v < V; ++v) gp[v] = 0.0;
   int par = 0;
   const int lag = stage * (H + 1);  // rows behind stage 0
 
@@ -265,9 +300,17 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 #pragma unroll
         for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? (Canon ? pC[v] : gs * pC[v]) : 0.0;
       }
-      wr2(ring + (slot0 + M) * WB, g);
-      if constexpr (M > 0) {
-        if (slot0 >= R - M) wr2(ring + (slot0 - (R - M)) * WB, g);
+      if constexpr (kDelay) {  // row i-1's factors, kept from the previous iteration
+        const int sp = slot0 == 0 ? R - 1 : slot0 - 1;
+        wr2(ring + (sp + M) * WB, gp);
+        if constexpr (M > 0) {
+          if (sp >= R - M) wr2(ring + (sp - (R - M)) * WB, gp);
+        }
+      } else {
+        wr2(ring + (slot0 + M) * WB, g);
+        if constexpr (M > 0) {
+          if (slot0 >= R - M) wr2(ring + (slot0 - (R - M)) * WB, g);
+        }
       }
 #pragma unroll
       for (int v = 0; v < V; ++v) {
@@ -282,8 +325,15 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     int sbase = slot0 - (S0 ? 0 : lag);
     sbase = sbase < 0 ? sbase + R : sbase;
     const double* rbase = ring + (sbase + M) * WB;
+    // NW (no mirrors, delayed ring): the stage's NL slots do not wrap this
+    // iteration, so every level's row is one base + an immediate offset
+    const double* rlow = ring + (sbase - (NL - 1)) * WB;
+    auto levels = [&](auto NWc) {
+    constexpr bool NW = decltype(NWc)::value;
     auto ring_row = [&](int j) {  // factor row of local level j (slot sbase - (j-1))
-      if constexpr (M > 0) {
+      if constexpr (NW) {
+        return rlow + (NL - j) * WB;
+      } else if constexpr (M > 0) {
         return rbase - (j - 1) * WB;  // j - 1 <= H - 1 = M: inside the mirrors
       } else {
         const int sl = sbase - (j - 1) < 0 ? sbase - (j - 1) + R : sbase - (j - 1);
@@ -291,7 +341,16 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       }
     };
     // factors read one level ahead (LDS latency under the previous level's
-    // arithmetic); stage 0's level-1 factors are still in registers
+    // arithmetic); stage 0's level-1 factors are still in registers (with the
+    // delayed ring also its level-2 factors: row i-1, gp)
+    auto fetch = [&](int j, double (&out)[V]) {
+      if (S0 && kDelay && j == 2) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) out[v] = gp[v];
+      } else {
+        rd2(ring_row(j), out);
+      }
+    };
     double gn[V];
     if constexpr (S0) {
 #pragma unroll
@@ -305,7 +364,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       double gl[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) gl[v] = gn[v];
-      if (j < NL) rd2(ring_row(j + 1), gn);
+      if (j < NL) fetch(j + 1, gn);
       const double(&c)[V] = w[j - 1][PC];
       const double(&dn)[V] = w[j - 1][Pr];
       double res[V];
@@ -359,6 +418,19 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       } else if (row >= ya32 && row < yb32) {
         store_row<V, true>(T2 + (int64_t)row * nx + x, res, m);
       }
+    }
+    };
+    if constexpr (M == 0 && kDelay) {
+      if (sbase >= NL - 1)
+        levels(std::true_type{});
+      else
+        levels(std::false_type{});
+    } else {
+      levels(std::false_type{});
+    }
+    if constexpr (S0 && kDelay) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) gp[v] = g[v];
     }
     slot0 = slot0 + 1 == R ? 0 : slot0 + 1;
     par ^= 1;
@@ -432,6 +504,9 @@ void launch(const PipeLaunch& a) {
 bool dispatch_a(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_b(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
+// 5 cells per lane (stencil_pipe_d.hip): fast5, S = 4, K = 16..20
+bool dispatch_d(int K, int S, int V, int ar, const PipeLaunch& a);
+bool pipe_has_v5(int K, int S, int ar);
 
 }  // namespace pipe
 }  // namespace rma

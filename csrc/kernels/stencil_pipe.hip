@@ -50,6 +50,13 @@ int pipe_default_cols(int K, int S, int arith) {
   return 1;
 }
 
+int pipe_vec(int K, int stages, int arith, int64_t nx, int requested, bool aligned16) {
+  const int S = stages > 0 ? stages : pipe_default_stages(K);
+  if (requested == 5 && nx % 5 == 0 && pipe::pipe_has_v5(K, S, arith)) return 5;
+  if (aligned16 && nx % 2 == 0) return (requested >= 4 && nx % 4 == 0) ? 4 : 2;
+  return 1;
+}
+
 void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const double* T,
                             const double* iCp, int64_t nx, int64_t ny, const Rect* rects,
                             int nrects, const StencilCoef& c, const StencilTuning& tune,
@@ -78,8 +85,7 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   const bool aligned = ((reinterpret_cast<uintptr_t>(T) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(T2) & 15) == 0) &&
                        ((reinterpret_cast<uintptr_t>(iCp) & 15) == 0);
-  int V = 1;
-  if (aligned && nx % 2 == 0) V = (tune.vec == 4 && nx % 4 == 0) ? 4 : 2;
+  const int V = pipe_vec(K, S, arith, nx, tune.vec, aligned);
   int C = tune.cols > 0 ? tune.cols : pipe_default_cols(K, S, arith);
   RMA_CHECK_ARG(pipe_has_cols(K, S, arith, C), "no pipelined kernel with " << C
                                                    << " column waves for K=" << K << " S=" << S
@@ -88,8 +94,9 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, rects, nrects, c, tune.chunk_rows, remap,
                      as_stream(stream)};
-  bool ok = C == 1 && (pipe::dispatch_a(K, S, V, arith, a) || pipe::dispatch_b(K, S, V, arith, a) ||
-                       pipe::dispatch_c(K, S, V, arith, a));
+  // V = 5 first: the other units' cases take any V other than 4 and 2 as 1
+  bool ok = C == 1 && (pipe::dispatch_d(K, S, V, arith, a) || pipe::dispatch_a(K, S, V, arith, a) ||
+                       pipe::dispatch_b(K, S, V, arith, a) || pipe::dispatch_c(K, S, V, arith, a));
   if (!ok) {  // alternative stage splits, pipeb, two-column blocks: librma_lab.so
     if (!lab_hooks().pipe) lab_missing("this pipelined kernel variant (stages / arithmetic / cols)");
     ok = lab_hooks().pipe(K, S, V, C, arith, a);

@@ -82,7 +82,8 @@ class StencilTuning:
     """Knobs of the march kernel (defaults = the fastest measured on MI355X,
     profiles/sweep_16k.md): rows per wave-task, rows whose loads are issued
     together, non-temporal bitmask (1: T2 stores, 2: 1/Cp loads), cells per
-    lane (2 or 4), and the kernel family ("march" or the "lds" baseline).
+    lane (2 or 4; the fast5 ``pipe`` kernel also 5 at K = 16..20 when nx % 5 == 0,
+    see ``native().pipe_vec``), and the kernel family ("march" or the "lds" baseline).
     Bit 2 of the non-temporal mask also streams T loads (implies bits 0-1)."""
 
     chunk_rows: int = 4

@@ -37,6 +37,10 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_aligned_frames_with_ol_bands_bitwise" || exit 1 ;;
     tests_capi) step tests_capi 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py || exit 1 ;;
+    tests_pipe) step tests_pipe 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+             tests/test_pipe_gpu.py -p no:cacheprovider || exit 1 ;;
+    sweep5) step sweep5 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 16,20,24 \
+             --pipe5 16-20 --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweep5.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;

@@ -224,3 +224,60 @@ print("OK")
 '''
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("nx", [515, 520, 1285, 2050])
+@pytest.mark.parametrize("K", [16, 17, 18, 19, 20])
+def test_pipe_five_cells_per_lane_bitwise(nx, K):
+    """5 cells per lane (320-column strips, v-major LDS rows, delayed factor
+    ring, no-wrap immediate-offset path): bitwise equal to the CPU twin,
+    also on rect lists whose strips end mid-window and on the x edges."""
+    assert native().pipe_vec(K, 0, 0, nx, 5, True) == 5
+    ny = 131
+    T, iCp = rand((ny, nx), 21 + K), rand((ny, nx), 22, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    assert torch.equal(gpu_run(K, T, iCp, rects, "pipe", chunk=37, vec=5),
+                       cpu_ref(K, T, iCp, rects, "pipe"))
+    sub = [(K + 3, nx - K - 7, K + 2, ny - K - 5), (1, K + 3, 1, ny - 1)]
+    assert torch.equal(gpu_run(K, T, iCp, sub, "pipe", chunk=23, vec=5, xcd=0),
+                       cpu_ref(K, T, iCp, sub, "pipe"))
+
+
+def test_pipe_five_cells_falls_back():
+    """vec=5 where it does not apply (nx % 5 != 0, K outside 16..20, the
+    canonical arithmetic) runs 4 / 2 / 1 cells per lane, still bitwise."""
+    assert native().pipe_vec(20, 0, 0, 1028, 5, True) == 4
+    assert native().pipe_vec(24, 0, 0, 1280, 5, True) == 4
+    assert native().pipe_vec(20, 0, 1, 1280, 5, True) == 4
+    assert native().pipe_vec(20, 0, 0, 1285, 5, False) == 5  # 8-B accesses only
+    ny = 97
+    for K, nx, kernel in ((20, 1028, "pipe"), (24, 1280, "pipe"), (20, 1280, "pipec")):
+        T, iCp = rand((ny, nx), 23), rand((ny, nx), 24, 0.5, 1.0)
+        rects = [ops.interior_rect(nx, ny)]
+        assert torch.equal(gpu_run(K, T, iCp, rects, kernel, chunk=41, vec=5),
+                           cpu_ref(K, T, iCp, rects, kernel))
+
+
+@pytest.mark.parametrize("K,nx", [(20, 1285), (16, 520), (18, 2050)])
+def test_pipe_five_cells_guard_bands(K, nx):
+    ny = 197
+    bufs, fields = [], []
+    for seed in (25, 26, 27):
+        b = torch.full((G + ny * nx + G,), CANARY, dtype=torch.float64, device=DEV)
+        f = b[G:G + ny * nx].view(ny, nx)
+        f.copy_(rand((ny, nx), seed, 0.5, 1.0))
+        bufs.append(b)
+        fields.append(f)
+    T, iCp, out = fields
+    before = out.clone()
+    rects = [(K, nx - K, K, ny - K)]
+    ops.stencilk_step(K, out, T, iCp, coef(), rects,
+                      ops.StencilTuning(kernel="pipe", chunk_rows=29, vec=5))
+    torch.cuda.synchronize()
+    for b in bufs:
+        assert bool((b[:G] == CANARY).all()) and bool((b[-G:] == CANARY).all())
+    mask = torch.ones((ny, nx), dtype=torch.bool, device=DEV)
+    mask[K:ny - K, K:nx - K] = False
+    assert torch.equal(out[mask], before[mask])
+    ref = cpu_ref(K, T.cpu(), iCp.cpu(), rects, "pipe")
+    assert torch.equal(out.cpu()[~mask.cpu()], ref[~mask.cpu()])
