@@ -50,6 +50,8 @@ def main(argv=None):
     ap.add_argument("--pipe5", default="", help="depths of the pipe kernel at 5 cells per lane "
                     "(needs n % 5 == 0)")
     ap.add_argument("--chunks5", default="", help="pipe5 K:c1/c2/..., chunk-row variants")
+    ap.add_argument("--kinds", default="", help="other K-step kernels by name, kernel:K,... "
+                    "(e.g. piper:24,pipe_diag1:24; 4 cells per lane)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -78,7 +80,7 @@ def main(argv=None):
         # the executor's rows per task for this kernel and depth
         if c or a.chunk:
             return c or a.chunk
-        if kind in ("pipe", "pipe2", "pipeb", "pipe5"):
+        if kind in ("pipe", "pipe2", "pipeb", "pipe5", "piper", "pipe_diag1"):
             return N.pipe_chunk_rows(K, n, False) or N.default_chunk_k(max(K, 3), n)
         if kind == "pipec":
             return N.pipe_chunk_rows(K, n, True) or N.default_chunk_k(max(K, 3), n)
@@ -105,6 +107,9 @@ def main(argv=None):
             cfgs.append(("pipec", int(K), 0, int(c)))
     cfgs += [("pipe2", K, 0) for K in krange(a.pipe2)]
     cfgs += [("pipe5", K, 0) for K in krange(a.pipe5)]
+    for item in filter(None, a.kinds.split(",")):
+        k, K = item.split(":")
+        cfgs.append((k, int(K), 0))
     for item in filter(None, a.chunks5.split(",")):
         K, cs = item.split(":")
         for c in cs.split("/"):

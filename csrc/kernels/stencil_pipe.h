@@ -93,7 +93,11 @@ struct Geo {
 // 3 rows x V cells x 2 dwords per level, stage 0's two-row prefetch, ~40 for
 // addressing and temporaries; canonical also the carried y flux and the x
 // fluxes (checked: no spills at any K, V, scripts/check_isa.py).
-constexpr int kArFast5 = 0, kArCanon = 1, kArFast5Perm = 2;
+constexpr int kArFast5 = 0, kArCanon = 1, kArFast5Perm = 2, kArFast5Reg = 3;
+// diagnosis only (lab, WRONG results): every level of a stage uses the factor
+// row of its level 1, i.e. one LDS ring row read per stage and iteration
+// instead of H; measures what the ring reads cost (energy / time)
+constexpr int kArDiagOneRow = 4;
 
 template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int occupancy(int lds) {
@@ -134,6 +138,26 @@ constexpr int waves_per_simd() {
   return occupancy<K, S, V, Canon, C>(lds_bytes<K, S, V, Canon, C>());
 }
 
+// Register-resident factors (Ar = kArFast5Reg, "piper"): no factor ring. A
+// stage keeps the factor rows of its H levels in registers; level j at row
+// phase q uses the row born at phase q-j+1 (names mod 6 = the row loop's
+// unroll, so any H <= 6), and each stage hands the row it retires to the
+// next stage through a double-buffered LDS row, like the T hand-off. LDS
+// read bytes per cell update: the ring's one factor row per level -> one
+// factor row per stage (H levels); LDS per block: 4 (S-1) rows.
+template <int K, int S, int V>
+constexpr int lds_bytes_reg() {
+  return 4 * (S > 1 ? S - 1 : 1) * Geo<K, S, V, 1>::WB * 8;
+}
+template <int K, int S, int V, int Ar, int C>
+constexpr int kernel_waves() {
+  if constexpr (Ar == kArFast5Reg) {
+    return occupancy<K, S, V, false, C>(lds_bytes_reg<K, S, V>());
+  } else {
+    return waves_per_simd<K, S, V, Ar == kArCanon, C>();
+  }
+}
+
 template <bool kDpp = true>
 __device__ __forceinline__ double from_next_lane(double v) {
   if constexpr (kDpp) {
@@ -163,9 +187,12 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
                                           const RectList& L, const StencilCoef& k, int chunk_rows,
                                           int remap) {
   using P = Plan<K, S>;
-  constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm;
+  constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = Ar == kArFast5Reg;
+  static_assert(!kRegG || (C == 1 && V != 5 && (K + S - 1) / S <= 6), "register factors: H <= 6");
+  constexpr int U = kRegG ? 6 : 3;  // row-loop unroll: w rotates mod 3, register factors mod 6
   using G = Geo<K, S, V, C>;
-  constexpr int H = P::H, HL = P::HL, R = ring_rows<K, S, V>(), M = mirror_rows<K, S, V, Canon, C>();
+  constexpr int H = P::H, HL = P::HL, R = ring_rows<K, S, V>();
+  constexpr int M = kRegG ? 0 : mirror_rows<K, S, V, Canon, C>();
   constexpr bool kDelay = kDelayedRing<V>;
   static_assert(V != 5 || (C == 1 && Ar == kArFast5), "5 cells per lane: fast5, one column wave");
   constexpr int W = G::W, WB = G::WB, D = G::D;
@@ -232,10 +259,19 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
   }
   // physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R)
-  __shared__ double ring[(R + M) * WB];
+  constexpr int kRing = kRegG ? 1 : (R + M) * WB, kGh = kRegG ? 2 * NH * WB : 1;
+  __shared__ double ring[kRing];
   __shared__ double hand[2][NH][WB];
-  for (int t = threadIdx.x; t < (R + M) * WB; t += S * C * kWave) ring[t] = 0.0;
+  __shared__ double ghand[kGh];  // register factors: [2][NH][WB] factor hand-off rows
+  for (int t = threadIdx.x; t < kRing; t += S * C * kWave) ring[t] = 0.0;
   for (int t = threadIdx.x; t < 2 * NH * WB; t += S * C * kWave) (&hand[0][0][0])[t] = 0.0;
+  for (int t = threadIdx.x; t < kGh; t += S * C * kWave) ghand[t] = 0.0;
+  double gr[kRegG ? 6 : 1][V];  // register factors: the row born at phase q in gr[q]
+#pragma unroll
+  for (int q = 0; q < (kRegG ? 6 : 1); ++q)
+#pragma unroll
+    for (int v = 0; v < V; ++v) gr[q][v] = 0.0;
+  auto gh = [&](int pb, int st) { return &ghand[(pb * NH + st) * WB]; };
   __syncthreads();
   // LDS rows hold cell pairs interleaved by parity (pair p at dbl2 slot
   // (p & 1) * WB/4 + p/2): a wave window starting at an even pair (D % 4 == 0)
@@ -282,8 +318,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   int par = 0;
   const int lag = stage * (H + 1);  // rows behind stage 0
 
-  auto iter = [&](auto Pc, auto S0c, auto LASTc) {
-    constexpr int Pr = decltype(Pc)::value;
+  auto iter = [&](auto Qc, auto S0c, auto LASTc) {
+    constexpr int Q = decltype(Qc)::value;  // row phase mod U
+    constexpr int Pr = Q % 3;
+    constexpr int QR = (Q - H + 12) % 6;  // register factors: the row this stage retires
     constexpr bool S0 = decltype(S0c)::value;
     constexpr bool LAST = decltype(LASTc)::value;
     constexpr int NL = LAST ? HL : H;  // levels of this stage
@@ -300,7 +338,11 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 #pragma unroll
         for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? (Canon ? pC[v] : gs * pC[v]) : 0.0;
       }
-      if constexpr (kDelay) {  // row i-1's factors, kept from the previous iteration
+      if constexpr (kRegG) {
+        if constexpr (!LAST) wr2(gh(par, 0), gr[QR]);
+#pragma unroll
+        for (int v = 0; v < V; ++v) gr[Q][v] = g[v];
+      } else if constexpr (kDelay) {  // row i-1's factors, kept from the previous iteration
         const int sp = slot0 == 0 ? R - 1 : slot0 - 1;
         wr2(ring + (sp + M) * WB, gp);
         if constexpr (M > 0) {
@@ -321,6 +363,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
     } else {
       rd2(&hand[par ^ 1][stage - 1][0], w[0][Pr]);
+      if constexpr (kRegG) {
+        if constexpr (!LAST) wr2(gh(par, stage), gr[QR]);
+        rd2(gh(par ^ 1, stage - 1), gr[Q]);
+      }
     }
     int sbase = slot0 - (S0 ? 0 : lag);
     sbase = sbase < 0 ? sbase + R : sbase;
@@ -352,7 +398,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       }
     };
     double gn[V];
-    if constexpr (S0) {
+    if constexpr (kRegG) {
+    } else if constexpr (S0) {
 #pragma unroll
       for (int v = 0; v < V; ++v) gn[v] = g[v];
     } else {
@@ -362,9 +409,14 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     for (int j = 1; j <= NL; ++j) {
       const int row = i - (S0 ? 0 : lag) - (j - 1);
       double gl[V];
+      if constexpr (kRegG) {
 #pragma unroll
-      for (int v = 0; v < V; ++v) gl[v] = gn[v];
-      if (j < NL) fetch(j + 1, gn);
+        for (int v = 0; v < V; ++v) gl[v] = gr[(Q - (j - 1) + 12) % 6][v];
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) gl[v] = gn[v];
+        if (j < NL && Ar != kArDiagOneRow) fetch(j + 1, gn);
+      }
       const double(&c)[V] = w[j - 1][PC];
       const double(&dn)[V] = w[j - 1][Pr];
       double res[V];
@@ -446,6 +498,14 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       if (++i > iend) break;
       iter(std::integral_constant<int, 2>{}, S0c, LASTc);
       if (++i > iend) break;
+      if constexpr (U == 6) {
+        iter(std::integral_constant<int, 3>{}, S0c, LASTc);
+        if (++i > iend) break;
+        iter(std::integral_constant<int, 4>{}, S0c, LASTc);
+        if (++i > iend) break;
+        iter(std::integral_constant<int, 5>{}, S0c, LASTc);
+        if (++i > iend) break;
+      }
     }
   };
   if constexpr (S == 1) {
@@ -462,7 +522,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 
 template <int K, int S, int V, int Ar, int C>
 __global__ __launch_bounds__(kWave * S * C) __attribute__((amdgpu_waves_per_eu(
-    waves_per_simd<K, S, V, Ar == kArCanon, C>()))) void pipe_kernel(double* __restrict__ T2,
+    kernel_waves<K, S, V, Ar, C>()))) void pipe_kernel(double* __restrict__ T2,
                                                       const double* __restrict__ T,
                                                       const double* __restrict__ iCp,
                                                       int64_t nx, int64_t ny, RectList L,
@@ -507,6 +567,8 @@ bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
 // 5 cells per lane (stencil_pipe_d.hip): fast5, S = 4, K = 16..20
 bool dispatch_d(int K, int S, int V, int ar, const PipeLaunch& a);
 bool pipe_has_v5(int K, int S, int ar);
+// register-resident factors (stencil_pipe_r.hip): fast5, S = 4, K = 12, 16, 20, 24
+bool dispatch_r(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe
 }  // namespace rma

@@ -29,6 +29,8 @@ int pipe_default_stages(int K) {
 bool pipe_has(int K, int S, int arith) {
   if (K < 1 || K > kPipeMaxK) return false;
   if (arith == pipe::kArFast5Perm) return S == 4 && (K == 16 || K == 20 || K == 24);
+  if (arith == pipe::kArFast5Reg) return S == 4 && (K == 12 || K == 16 || K == 20 || K == 24);
+  if (arith == pipe::kArDiagOneRow) return S == 4 && (K == 20 || K == 24);
   if (S == pipe_default_stages(K)) return true;
   // alternative stage splits instantiated for sweeps (csrc/lab/stencil_pipe_lab.hip)
   return (K == 12 && S == 3) || (K == 16 && S == 8) || (K == 24 && S == 8) ||
@@ -66,7 +68,7 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
                 "pipelined K-step kernel: 1 <= K <= " << kPipeMaxK << ", got " << K);
   RMA_CHECK_ARG(pipe_has(K, S, arith), "no pipelined kernel instantiated for K=" << K << " S=" << S
                                                                              << " arithmetic " << arith);
-  RMA_CHECK_ARG(arith >= 0 && arith <= 2, "pipelined kernel arithmetic " << arith);
+  RMA_CHECK_ARG(arith >= 0 && arith <= 4, "pipelined kernel arithmetic " << arith);
   const bool canonical = arith == pipe::kArCanon;
   RMA_CHECK_ARG(canonical || fast5_ok(c),
                 "the fast5 arithmetic folds dy^-2/dx^-2 into one factor: needs lam != 0 and "
@@ -95,7 +97,8 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, rects, nrects, c, tune.chunk_rows, remap,
                      as_stream(stream)};
   // V = 5 first: the other units' cases take any V other than 4 and 2 as 1
-  bool ok = C == 1 && (pipe::dispatch_d(K, S, V, arith, a) || pipe::dispatch_a(K, S, V, arith, a) ||
+  bool ok = C == 1 && (pipe::dispatch_d(K, S, V, arith, a) || pipe::dispatch_r(K, S, V, arith, a) ||
+                       pipe::dispatch_a(K, S, V, arith, a) ||
                        pipe::dispatch_b(K, S, V, arith, a) || pipe::dispatch_c(K, S, V, arith, a));
   if (!ok) {  // alternative stage splits, pipeb, two-column blocks: librma_lab.so
     if (!lab_hooks().pipe) lab_missing("this pipelined kernel variant (stages / arithmetic / cols)");

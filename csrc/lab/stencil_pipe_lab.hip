@@ -24,6 +24,8 @@ bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(16, 4, kArFast5Perm)
   RMA_PIPE_CASE(20, 4, kArFast5Perm)
   RMA_PIPE_CASE(24, 4, kArFast5Perm)
+  RMA_PIPE_CASE(20, 4, kArDiagOneRow)
+  RMA_PIPE_CASE(24, 4, kArDiagOneRow)
   return false;
 }
 

@@ -37,13 +37,13 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 # 5-point sum with one folded per-cell factor, the GPU oracle of "pipe"), "fast5p2/p4/p8"
 # (6/7/8: fixed-K pipelined fast5), "pipeb" (11: pipe with ds_bpermute lane moves), and
 # the pipelined kernels' non-default stage splits and two-column blocks.
-FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe", "pipeb")
-PIPE = ("pipe", "pipec", "pipeb")
+FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe", "pipeb", "piper")
+PIPE = ("pipe", "pipec", "pipeb", "piper", "pipe_diag1")
 PIPE_MAX_K = 24
-KERNELS = {"march": 0, "lds": 1, "lds_dpp": 3, "pipe": 9, "pipec": 10}
+KERNELS = {"march": 0, "lds": 1, "lds_dpp": 3, "pipe": 9, "pipec": 10, "piper": 12}
 LAB_KERNELS = {"dpp": 2, "fast": 4, "fast5": 5, "fast5p2": 6, "fast5p4": 7, "fast5p8": 8,
-               "pipeb": 11}
-KSTEP_CORE = ("lds_dpp", "pipe", "pipec")
+               "pipeb": 11, "pipe_diag1": 13}
+KSTEP_CORE = ("lds_dpp", "pipe", "pipec", "piper")
 
 
 def kernel_id(name: str) -> int:

@@ -41,6 +41,14 @@ for s in "$@"; do
              tests/test_pipe_gpu.py -p no:cacheprovider || exit 1 ;;
     sweep5) step sweep5 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 16,20,24 \
              --pipe5 16-20 --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweep5.json" || exit 1 ;;
+    sweep5b) step sweep5b 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 20,24 \
+             --pipe5 20 --chunks5 20:1536/2048/4096 --kinds piper:20,piper:24,pipe_diag1:20,pipe_diag1:24 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweep5b.json" || exit 1 ;;
+    pmc5a) prof pmc5a 300 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+             SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CU_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+             --output-format csv -d "$R/$OUT/pmc5a" -o run -- python3 "$R/bench/pass_sweep.py" \
+             --n 101120 --rounds 2 --pipe 20,24 --pipe5 20 --kinds pipe_diag1:24 --pipec "" \
+             --ldsdpp "" --old "" --alt "" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
