@@ -139,12 +139,12 @@ constexpr int waves_per_simd() {
 }
 
 // Register-resident factors (Ar = kArFast5Reg, "piper"): no factor ring. A
-// stage keeps the factor rows of its H levels in registers; level j at row
-// phase q uses the row born at phase q-j+1 (names mod 6 = the row loop's
-// unroll, so any H <= 6), and each stage hands the row it retires to the
-// next stage through a double-buffered LDS row, like the T hand-off. LDS
-// read bytes per cell update: the ring's one factor row per level -> one
-// factor row per stage (H levels); LDS per block: 4 (S-1) rows.
+// stage keeps the factor rows of its H levels in registers (a shift register:
+// level j+1 uses next row iteration the row level j uses now), and each stage
+// hands the row it retires to the next stage through a double-buffered LDS
+// row, like the T hand-off. LDS read bytes per cell update: the ring's one
+// factor row per level -> one factor row per stage (H levels); LDS per
+// block: 4 (S-1) rows.
 template <int K, int S, int V>
 constexpr int lds_bytes_reg() {
   return 4 * (S > 1 ? S - 1 : 1) * Geo<K, S, V, 1>::WB * 8;
@@ -152,7 +152,12 @@ constexpr int lds_bytes_reg() {
 template <int K, int S, int V, int Ar, int C>
 constexpr int kernel_waves() {
   if constexpr (Ar == kArFast5Reg) {
-    return occupancy<K, S, V, false, C>(lds_bytes_reg<K, S, V>());
+    // + the H factor rows (measured 158 / 233 / 256 VGPRs at K = 12 / 20 / 24, V = 4)
+    constexpr int H = Plan<K, S>::H;
+    constexpr int vgpr = 8 * H * V + 8 * V + 40;
+    constexpr int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
+    constexpr int w = occupancy<K, S, V, false, C>(lds_bytes_reg<K, S, V>());
+    return by_vgpr < 2 ? 2 : (by_vgpr < w ? by_vgpr : w);
   } else {
     return waves_per_simd<K, S, V, Ar == kArCanon, C>();
   }
@@ -188,8 +193,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
                                           int remap) {
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = Ar == kArFast5Reg;
-  static_assert(!kRegG || (C == 1 && V != 5 && (K + S - 1) / S <= 6), "register factors: H <= 6");
-  constexpr int U = kRegG ? 6 : 3;  // row-loop unroll: w rotates mod 3, register factors mod 6
+  static_assert(!kRegG || (C == 1 && V != 5), "register factors: V <= 4, one column wave");
+  // stage 0 prefetches T / 1/Cp two rows ahead; one row ahead where the
+  // register factors would otherwise not fit 2 waves per SIMD (K = 21..24, V = 4)
+  constexpr bool kPre1 = kRegG && V == 4 && Plan<K, S>::H >= 6;
   using G = Geo<K, S, V, C>;
   constexpr int H = P::H, HL = P::HL, R = ring_rows<K, S, V>();
   constexpr int M = kRegG ? 0 : mirror_rows<K, S, V, Canon, C>();
@@ -255,23 +262,36 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     load_row<V>(w[0][2], T + rowc(i) * nx + xl);
     load_row<V>(pT, T + rowc(i + 1) * nx + xl);
     load_row<V>(pC, iCp + rowc(i) * nx + xl);
-    load_row<V>(qT, T + rowc(i + 2) * nx + xl);
-    load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
+    if constexpr (!kPre1) {
+      load_row<V>(qT, T + rowc(i + 2) * nx + xl);
+      load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
+    }
   }
   // physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R)
-  constexpr int kRing = kRegG ? 1 : (R + M) * WB, kGh = kRegG ? 2 * NH * WB : 1;
+  // register factors: the same LDS array holds the [2][NH][WB] factor hand-off rows
+  constexpr int kRing = kRegG ? 2 * NH * WB : (R + M) * WB;
   __shared__ double ring[kRing];
   __shared__ double hand[2][NH][WB];
-  __shared__ double ghand[kGh];  // register factors: [2][NH][WB] factor hand-off rows
   for (int t = threadIdx.x; t < kRing; t += S * C * kWave) ring[t] = 0.0;
   for (int t = threadIdx.x; t < 2 * NH * WB; t += S * C * kWave) (&hand[0][0][0])[t] = 0.0;
-  for (int t = threadIdx.x; t < kGh; t += S * C * kWave) ghand[t] = 0.0;
-  double gr[kRegG ? 6 : 1][V];  // register factors: the row born at phase q in gr[q]
+  // register factors: gr[j-1] = the factor row of level j, shifted one level
+  // per row iteration (level j+1 computes next iteration the row level j
+  // computes now); the shift is SSA renaming, the loop back-edge costs the
+  // register allocator a few row copies per 3 rows (the row loop stays
+  // unrolled by 3: unrolling by 6 for static names raised the VGPR count of
+  // the plain kernel from 213 to 270)
+  double gr[kRegG ? H : 1][V];
 #pragma unroll
-  for (int q = 0; q < (kRegG ? 6 : 1); ++q)
+  for (int q = 0; q < (kRegG ? H : 1); ++q)
 #pragma unroll
     for (int v = 0; v < V; ++v) gr[q][v] = 0.0;
-  auto gh = [&](int pb, int st) { return &ghand[(pb * NH + st) * WB]; };
+  auto gh = [&](int pb, int st) { return &ring[(pb * NH + st) * WB]; };
+  auto gshift = [&]() {
+#pragma unroll
+    for (int q = (kRegG ? H : 1) - 1; q > 0; --q)
+#pragma unroll
+      for (int v = 0; v < V; ++v) gr[q][v] = gr[q - 1][v];
+  };
   __syncthreads();
   // LDS rows hold cell pairs interleaved by parity (pair p at dbl2 slot
   // (p & 1) * WB/4 + p/2): a wave window starting at an even pair (D % 4 == 0)
@@ -318,10 +338,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   int par = 0;
   const int lag = stage * (H + 1);  // rows behind stage 0
 
-  auto iter = [&](auto Qc, auto S0c, auto LASTc) {
-    constexpr int Q = decltype(Qc)::value;  // row phase mod U
-    constexpr int Pr = Q % 3;
-    constexpr int QR = (Q - H + 12) % 6;  // register factors: the row this stage retires
+  auto iter = [&](auto Pc, auto S0c, auto LASTc) {
+    constexpr int Pr = decltype(Pc)::value;
     constexpr bool S0 = decltype(S0c)::value;
     constexpr bool LAST = decltype(LASTc)::value;
     constexpr int NL = LAST ? HL : H;  // levels of this stage
@@ -338,10 +356,11 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 #pragma unroll
         for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? (Canon ? pC[v] : gs * pC[v]) : 0.0;
       }
-      if constexpr (kRegG) {
-        if constexpr (!LAST) wr2(gh(par, 0), gr[QR]);
+      if constexpr (kRegG) {  // retire level H's row to stage 1, shift, take row i
+        if constexpr (!LAST) wr2(gh(par, 0), gr[H - 1]);
+        gshift();
 #pragma unroll
-        for (int v = 0; v < V; ++v) gr[Q][v] = g[v];
+        for (int v = 0; v < V; ++v) gr[0][v] = g[v];
       } else if constexpr (kDelay) {  // row i-1's factors, kept from the previous iteration
         const int sp = slot0 == 0 ? R - 1 : slot0 - 1;
         wr2(ring + (sp + M) * WB, gp);
@@ -356,16 +375,24 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       }
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        pT[v] = qT[v];
-        pC[v] = qC[v];
+        if constexpr (!kPre1) {
+          pT[v] = qT[v];
+          pC[v] = qC[v];
+        }
       }
-      load_row<V>(qT, T + rowc(i + 3) * nx + xl);
-      load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
+      if constexpr (kPre1) {
+        load_row<V>(pT, T + rowc(i + 2) * nx + xl);
+        load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
+      } else {
+        load_row<V>(qT, T + rowc(i + 3) * nx + xl);
+        load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
+      }
     } else {
       rd2(&hand[par ^ 1][stage - 1][0], w[0][Pr]);
       if constexpr (kRegG) {
-        if constexpr (!LAST) wr2(gh(par, stage), gr[QR]);
-        rd2(gh(par ^ 1, stage - 1), gr[Q]);
+        if constexpr (!LAST) wr2(gh(par, stage), gr[H - 1]);
+        gshift();
+        rd2(gh(par ^ 1, stage - 1), gr[0]);
       }
     }
     int sbase = slot0 - (S0 ? 0 : lag);
@@ -411,7 +438,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       double gl[V];
       if constexpr (kRegG) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) gl[v] = gr[(Q - (j - 1) + 12) % 6][v];
+        for (int v = 0; v < V; ++v) gl[v] = gr[j - 1][v];
       } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) gl[v] = gn[v];
@@ -498,14 +525,6 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       if (++i > iend) break;
       iter(std::integral_constant<int, 2>{}, S0c, LASTc);
       if (++i > iend) break;
-      if constexpr (U == 6) {
-        iter(std::integral_constant<int, 3>{}, S0c, LASTc);
-        if (++i > iend) break;
-        iter(std::integral_constant<int, 4>{}, S0c, LASTc);
-        if (++i > iend) break;
-        iter(std::integral_constant<int, 5>{}, S0c, LASTc);
-        if (++i > iend) break;
-      }
     }
   };
   if constexpr (S == 1) {

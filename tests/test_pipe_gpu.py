@@ -281,3 +281,19 @@ def test_pipe_five_cells_guard_bands(K, nx):
     assert torch.equal(out[mask], before[mask])
     ref = cpu_ref(K, T.cpu(), iCp.cpu(), rects, "pipe")
     assert torch.equal(out.cpu()[~mask.cpu()], ref[~mask.cpu()])
+
+
+@pytest.mark.parametrize("nx", [515, 518, 520, 1028])
+@pytest.mark.parametrize("K", [12, 16, 20, 24])
+def test_piper_register_factors_bitwise(nx, K):
+    """piper (factor rows in registers, shifted one level per row, one LDS
+    hand-off row per stage boundary): bitwise equal to the CPU twin and to
+    pipe, also on rect lists (1, 2 and 4 cells per lane)."""
+    ny = 157
+    T, iCp = rand((ny, nx), 31 + K), rand((ny, nx), 32, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, "pipe")
+    assert torch.equal(gpu_run(K, T, iCp, rects, "piper", chunk=43), ref)
+    sub = [(K + 3, nx - K - 7, K + 2, ny - K - 5), (1, K + 3, 1, ny - 1)]
+    assert torch.equal(gpu_run(K, T, iCp, sub, "piper", chunk=19, xcd=0),
+                       cpu_ref(K, T, iCp, sub, "pipe"))
