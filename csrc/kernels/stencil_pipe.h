@@ -194,8 +194,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = Ar == kArFast5Reg;
   static_assert(!kRegG || (C == 1 && V != 5), "register factors: V <= 4, one column wave");
-  // stage 0 prefetches T / 1/Cp two rows ahead; one row ahead where the
-  // register factors would otherwise not fit 2 waves per SIMD (K = 21..24, V = 4)
+  // stage 0 prefetches T / 1/Cp two rows ahead; 1/Cp only one row ahead where
+  // the register factors would otherwise not fit 2 waves per SIMD (H = 6,
+  // V = 4; T one row ahead too: 92.7 vs 81.6 ms per K=24 pass, the HBM
+  // latency is longer than one row iteration)
   constexpr bool kPre1 = kRegG && V == 4 && Plan<K, S>::H >= 6;
   using G = Geo<K, S, V, C>;
   constexpr int H = P::H, HL = P::HL, R = ring_rows<K, S, V>();
@@ -233,6 +235,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     cin[v] = (x + v >= 1) && (x + v <= nx - 2);
   }
   const int64_t xl = min(max(x, (int64_t)0), nx - V);
+  // 32-bit lane offsets from a uniform row pointer (SGPR base + VGPR offset
+  // addressing instead of 64-bit VGPR address arithmetic); xso wraps only for
+  // lanes left of the array, which never store (m[] false)
+  const uint32_t xo = (uint32_t)xl, xso = (uint32_t)x;
   const bool xin = xw >= 1 && xw + W - 1 <= nx - 2;  // no x-boundary cell in the window
 
   // fast5 constants (the host guarantees fast5_ok); canonical uses k directly
@@ -259,13 +265,11 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   const int iend = yb32 + K - 3 + S;
   auto rowc = [&](int y) { return (int64_t)min(max(y, 0), ny32 - 1); };
   if (stage == 0) {
-    load_row<V>(w[0][2], T + rowc(i) * nx + xl);
-    load_row<V>(pT, T + rowc(i + 1) * nx + xl);
-    load_row<V>(pC, iCp + rowc(i) * nx + xl);
-    if constexpr (!kPre1) {
-      load_row<V>(qT, T + rowc(i + 2) * nx + xl);
-      load_row<V>(qC, iCp + rowc(i + 1) * nx + xl);
-    }
+    load_row<V>(w[0][2], T + rowc(i) * nx + xo);
+    load_row<V>(pT, T + rowc(i + 1) * nx + xo);
+    load_row<V>(pC, iCp + rowc(i) * nx + xo);
+    load_row<V>(qT, T + rowc(i + 2) * nx + xo);
+    if constexpr (!kPre1) load_row<V>(qC, iCp + rowc(i + 1) * nx + xo);
   }
   // physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R)
   // register factors: the same LDS array holds the [2][NH][WB] factor hand-off rows
@@ -346,6 +350,9 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     constexpr int PC = (Pr + 2) % 3, PU = (Pr + 1) % 3;
     double g[V];
     if constexpr (S0) {
+      // register factors: retire level H's row to stage 1 before row i's
+      // factors exist (one factor row fewer live)
+      if constexpr (kRegG && !LAST) wr2(gh(par, 0), gr[H - 1]);
       const bool rin1 = i >= 1 && i <= ny32 - 2;
 #pragma unroll
       for (int v = 0; v < V; ++v) w[0][Pr][v] = pT[v];
@@ -356,8 +363,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 #pragma unroll
         for (int v = 0; v < V; ++v) g[v] = (rin1 && cin[v]) ? (Canon ? pC[v] : gs * pC[v]) : 0.0;
       }
-      if constexpr (kRegG) {  // retire level H's row to stage 1, shift, take row i
-        if constexpr (!LAST) wr2(gh(par, 0), gr[H - 1]);
+      if constexpr (kRegG) {  // shift, take row i
         gshift();
 #pragma unroll
         for (int v = 0; v < V; ++v) gr[0][v] = g[v];
@@ -375,17 +381,14 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       }
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        if constexpr (!kPre1) {
-          pT[v] = qT[v];
-          pC[v] = qC[v];
-        }
+        pT[v] = qT[v];
+        if constexpr (!kPre1) pC[v] = qC[v];
       }
+      load_row<V>(qT, T + rowc(i + 3) * nx + xo);
       if constexpr (kPre1) {
-        load_row<V>(pT, T + rowc(i + 2) * nx + xl);
-        load_row<V>(pC, iCp + rowc(i + 1) * nx + xl);
+        load_row<V>(pC, iCp + rowc(i + 1) * nx + xo);
       } else {
-        load_row<V>(qT, T + rowc(i + 3) * nx + xl);
-        load_row<V>(qC, iCp + rowc(i + 2) * nx + xl);
+        load_row<V>(qC, iCp + rowc(i + 2) * nx + xo);
       }
     } else {
       rd2(&hand[par ^ 1][stage - 1][0], w[0][Pr]);
@@ -495,7 +498,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       } else if constexpr (!LAST) {
         wr2(&hand[par][S0 ? 0 : stage][0], res);
       } else if (row >= ya32 && row < yb32) {
-        store_row<V, true>(T2 + (int64_t)row * nx + x, res, m);
+        store_row<V, true>(T2 + (int64_t)row * nx + xso, res, m);
       }
     }
     };

@@ -52,6 +52,9 @@ for s in "$@"; do
     sweepr) step sweepr 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 12,16,20,24 \
              --pipe5 20 --kinds piper:12,piper:16,piper:20,piper:24,pipe_diag1:24 \
              --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepr.json" || exit 1 ;;
+    sweepr2) step sweepr2 600 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe 16,20,24 \
+             --pipe5 20 --kinds piper:20,piper:24 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepr2.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
