@@ -305,9 +305,11 @@ def hard_exit(rank: int, rc: int) -> None:
 def record_rc(rank: int, rc: int) -> None:
     """RMA_BENCH_RC_DIR: every rank writes its exit status (tests)."""
     d = os.environ.get("RMA_BENCH_RC_DIR")
-    if d:
-        with open(os.path.join(d, f"rc{rank}"), "w") as f:
+    if d:  # atomically: torchrun may end this rank right after (a half-written file)
+        tmp = os.path.join(d, f".rc{rank}.tmp")
+        with open(tmp, "w") as f:
             f.write(str(rc))
+        os.replace(tmp, os.path.join(d, f"rc{rank}"))
 
 
 # ---------------------------------------------------------------------------
@@ -542,7 +544,12 @@ def run(a, world: int, rank: int) -> int:
     diag = {k: v for k, v in sorted(os.environ.items())
             if k.startswith("RMA_DIAG") or k in ("RMA_FRAME_SIDES", "RMA_FRAME_ALIGNED",
                                                  "RMA_PASS_COSTS", "RMA_HALO_BATCH",
-                                                 "RMA_FRAME_FILL", "RMA_EXEC_STREAMS")}
+                                                 "RMA_FRAME_FILL", "RMA_EXEC_STREAMS",
+                                                 "RMA_PIPE_FAST")}
+    if gpu and os.environ.get("RMA_PIPE_FAST") == "pipe5":  # an A/B of the lab kernel
+        from rocm_mpi_amd._native import load_lab
+
+        load_lab()
     check_on = a.check == 1 or (a.check < 0 and (gpu or world > 1))
     if check_on and os.environ.get("RMA_DIAG_SKIP_EXCHANGE", "0") == "1":
         log(rank, "RMA_DIAG_SKIP_EXCHANGE=1 skips every halo exchange: refused with the halo "
@@ -764,6 +771,8 @@ def run(a, world: int, rank: int) -> int:
                 else:
                     kern, kvec, kch = native().canonical_kernel_k(depth, ny)
                 names = {v: k for k, v in ops.KERNELS.items()}
+                if kern >= 9:  # the cells per lane the kernel runs (vec 5 needs nx % 5 == 0)
+                    kvec = native().pipe_vec(depth, 0, kern - 9, nx, kvec, True)
                 kinfo = {"kernel": names[kern], "vec": kvec, "chunk_rows": a.chunk2 or kch,
                          "stages": native().pipe_default_stages(depth) if kern >= 9 else None}
         model.close()

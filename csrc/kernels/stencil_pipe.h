@@ -63,7 +63,8 @@ struct Plan {
 //    exactly 80 KiB; without mirrors the level loop takes one immediate-
 //    offset path whenever the stage's rows do not wrap).
 // Registers bound the depth: K <= 20 (236 VGPRs at K = 20; the 6-level
-// stages of K >= 21 spill, stencil_pipe_d.hip).
+// stages of K >= 21 spill). An experiment in the lab library
+// (csrc/lab/stencil_pipe5_lab.hip): 0.8-1.6 % per K=20 pass.
 template <int V>
 constexpr bool kDelayedRing = V == 5;
 template <int K, int S, int V>
@@ -586,10 +587,12 @@ void launch(const PipeLaunch& a) {
 bool dispatch_a(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_b(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
-// 5 cells per lane (stencil_pipe_d.hip): fast5, S = 4, K = 16..20
-bool dispatch_d(int K, int S, int V, int ar, const PipeLaunch& a);
-bool pipe_has_v5(int K, int S, int ar);
-// register-resident factors (stencil_pipe_r.hip): fast5, S = 4, K = 12, 16, 20, 24
+// 5 cells per lane: fast5, S = 4, K = 16..20, in the lab library
+// (csrc/lab/stencil_pipe5_lab.hip)
+inline bool pipe_has_v5(int K, int S, int ar) {
+  return ar == kArFast5 && S == 4 && K >= 16 && K <= 20;
+}
+// register-resident factors (stencil_pipe_r.hip): fast5, S = 4, K = 17..20
 bool dispatch_r(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe

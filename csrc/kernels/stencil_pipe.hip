@@ -29,7 +29,7 @@ int pipe_default_stages(int K) {
 bool pipe_has(int K, int S, int arith) {
   if (K < 1 || K > kPipeMaxK) return false;
   if (arith == pipe::kArFast5Perm) return S == 4 && (K == 16 || K == 20 || K == 24);
-  if (arith == pipe::kArFast5Reg) return S == 4 && (K == 12 || K == 16 || K == 20 || K == 24);
+  if (arith == pipe::kArFast5Reg) return S == 4 && K >= 17 && K <= 20;
   if (arith == pipe::kArDiagOneRow) return S == 4 && (K == 20 || K == 24);
   if (S == pipe_default_stages(K)) return true;
   // alternative stage splits instantiated for sweeps (csrc/lab/stencil_pipe_lab.hip)
@@ -96,12 +96,13 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, rects, nrects, c, tune.chunk_rows, remap,
                      as_stream(stream)};
-  // V = 5 first: the other units' cases take any V other than 4 and 2 as 1
-  bool ok = C == 1 && (pipe::dispatch_d(K, S, V, arith, a) || pipe::dispatch_r(K, S, V, arith, a) ||
-                       pipe::dispatch_a(K, S, V, arith, a) ||
-                       pipe::dispatch_b(K, S, V, arith, a) || pipe::dispatch_c(K, S, V, arith, a));
-  if (!ok) {  // alternative stage splits, pipeb, two-column blocks: librma_lab.so
-    if (!lab_hooks().pipe) lab_missing("this pipelined kernel variant (stages / arithmetic / cols)");
+  // V = 5 only in the lab (the core units' cases take any V other than 4 and 2 as 1)
+  bool ok = C == 1 && V != 5 &&
+            (pipe::dispatch_r(K, S, V, arith, a) || pipe::dispatch_a(K, S, V, arith, a) ||
+             pipe::dispatch_b(K, S, V, arith, a) || pipe::dispatch_c(K, S, V, arith, a));
+  if (!ok) {  // alternative stage splits, pipeb, two-column blocks, 5 cells: librma_lab.so
+    if (!lab_hooks().pipe)
+      lab_missing("this pipelined kernel variant (stages / arithmetic / cols / 5 cells per lane)");
     ok = lab_hooks().pipe(K, S, V, C, arith, a);
   }
   RMA_CHECK_ARG(ok, "pipelined kernel K=" << K << " S=" << S << " V=" << V << " C=" << C

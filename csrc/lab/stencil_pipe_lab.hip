@@ -8,7 +8,10 @@
 //     columns instead of a second strip's 2K. 8 % less arithmetic at K=24 but
 //     one block per CU (152 KB LDS), whose per-row barrier no second block
 //     hides: 85.2 vs 80.9 ms per K=24 pass at 101376^2, 65.7 vs 55.4 ms at
-//     K=16 (profiles/pass_sweep_cols2_r2.json).
+//     K=16 (profiles/pass_sweep_cols2_r2.json);
+//   * 5 cells per lane (fast5, K = 16..20, stencil_pipe5_lab.hip);
+//   * a diagnosis variant with one factor-ring read per stage and row (wrong
+//     results; what the ring reads cost: -5 % per K=24 pass, SUMMARY_r3).
 #include "../kernels/lab_hooks.h"
 
 namespace rma {
@@ -45,11 +48,15 @@ bool dispatch_cols2(int K, int S, int V, int ar, const PipeLaunch& a) {
 }
 
 }  // namespace
+
+bool dispatch_v5(int K, int S, int V, int ar, const PipeLaunch& a);  // stencil_pipe5_lab.hip
+
 }  // namespace pipe
 
 namespace lab {
 bool pipe(int K, int S, int V, int C, int arith, const pipe::PipeLaunch& a) {
-  return C == 2 ? pipe::dispatch_cols2(K, S, V, arith, a) : pipe::dispatch_alt(K, S, V, arith, a);
+  if (C == 2) return pipe::dispatch_cols2(K, S, V, arith, a);
+  return V == 5 ? pipe::dispatch_v5(K, S, V, arith, a) : pipe::dispatch_alt(K, S, V, arith, a);
 }
 }  // namespace lab
 }  // namespace rma

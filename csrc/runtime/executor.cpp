@@ -59,6 +59,15 @@ StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c) {
   t.kernel = 9;  // stage-pipelined fast5, any K (stencil_pipe.h)
   t.vec = 4;
   if (const int ch = pipe_chunk_rows(K, ny, false)) t.chunk_rows = ch;
+  // K = 17..20: factor rows in registers instead of the LDS ring ("piper",
+  // 5-level stages; 1.3-2.1 % per K=20 pass at 101120^2, profiles/SUMMARY_r3.md)
+  if (pipe_has(K, pipe_default_stages(K), 3)) t.kernel = 12;
+  // RMA_PIPE_FAST=pipe | pipe5 forces the ring kernel at every depth (A/B runs;
+  // pipe5 = 5 cells per lane, lab library, K = 16..20 and nx % 5 == 0)
+  static const char* e = std::getenv("RMA_PIPE_FAST");
+  const std::string force = e ? e : "";
+  if (force == "pipe" || force == "pipe5") t.kernel = 9;
+  if (force == "pipe5") t.vec = 5;
   return t;
 }
 
@@ -206,12 +215,15 @@ const PassGeom& DiffusionExecutor::geometry(int K) {
     // pipelined passes: the frame is whole tasks of the interior's grid
     const StencilTuning t = pass_tuning(K, 0);
     int64_t tw = 0, th = 0;
+    int vec = t.vec;
     if (t.kernel >= 9) {
-      tw = (64 * t.vec - 2 * K) / t.vec * t.vec;
+      // the cells per lane the kernel will run (its strip step), not the request
+      vec = pipe_vec(K, t.stages, t.kernel - 9, nx_, t.vec, true);
+      tw = (64 * vec - 2 * K) / vec * vec;
       th = t.chunk_rows;
     }
     geom_[K] = pass_geometry(nx_, ny_, K, nbr_, p_.mode == Mode::kHide, p_.bwx, p_.bwy, p_.olx,
-                             p_.oly, tw, th, t.vec);
+                             p_.oly, tw, th, vec);
     geom_ok_[K] = 1;
   }
   return geom_[K];

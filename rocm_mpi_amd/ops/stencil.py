@@ -30,13 +30,16 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 #   K-step:    "lds_dpp" (3: canonical, K = 2, 3, 4, 6, 8; LDS 1/Cp ring + DPP),
 #              "pipe" (9: the stage-pipelined fast-math kernel, ANY K in 1..24,
 #              csrc/kernels/stencil_pipe.h), "pipec" (10: the same pipeline with the
-#              canonical arithmetic, bitwise equal to K one-step updates).
+#              canonical arithmetic, bitwise equal to K one-step updates), "piper"
+#              (12: "pipe" with the factor rows in registers instead of the LDS
+#              ring, K = 17..20, the executor's kernel at those depths).
 # LAB_KERNELS live in librma_lab.so (csrc/lab: superseded / experimental kernels kept as
 # test oracles and for sweeps), loaded on first use: K-step "march"/"lds"/"dpp" (0/1/2:
 # canonical variants of kernel 3), "fast" (4: reassociated, not bitwise), "fast5" (5: the
 # 5-point sum with one folded per-cell factor, the GPU oracle of "pipe"), "fast5p2/p4/p8"
 # (6/7/8: fixed-K pipelined fast5), "pipeb" (11: pipe with ds_bpermute lane moves), and
-# the pipelined kernels' non-default stage splits and two-column blocks.
+# the pipelined kernels' non-default stage splits, two-column blocks and 5 cells per lane,
+# and "pipe_diag1" (13: a diagnosis, WRONG results: one factor-ring read per stage and row).
 FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe", "pipeb", "piper")
 PIPE = ("pipe", "pipec", "pipeb", "piper", "pipe_diag1")
 PIPE_MAX_K = 24
@@ -57,7 +60,7 @@ def kernel_id(name: str) -> int:
 
 def _kstep_needs_lab(K: int, tn: "StencilTuning") -> bool:
     """Does this K-step launch run a librma_lab.so kernel?"""
-    if tn.kernel not in KSTEP_CORE or tn.cols == 2:
+    if tn.kernel not in KSTEP_CORE or tn.cols == 2 or (tn.kernel == "pipe" and tn.vec == 5):
         return True
     if tn.kernel in PIPE and tn.stages and has_native():
         return tn.stages != native().pipe_default_stages(K)
@@ -82,8 +85,9 @@ class StencilTuning:
     """Knobs of the march kernel (defaults = the fastest measured on MI355X,
     profiles/sweep_16k.md): rows per wave-task, rows whose loads are issued
     together, non-temporal bitmask (1: T2 stores, 2: 1/Cp loads), cells per
-    lane (2 or 4; the fast5 ``pipe`` kernel also 5 at K = 16..20 when nx % 5 == 0,
-    see ``native().pipe_vec``), and the kernel family ("march" or the "lds" baseline).
+    lane (2 or 4; the fast5 ``pipe`` kernel also 5 at K = 16..20 when nx % 5 == 0, a
+    lab-library experiment, see ``native().pipe_vec``), and the kernel family ("march"
+    or the "lds" baseline).
     Bit 2 of the non-temporal mask also streams T loads (implies bits 0-1)."""
 
     chunk_rows: int = 4

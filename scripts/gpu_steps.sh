@@ -55,6 +55,14 @@ for s in "$@"; do
     sweepr2) step sweepr2 600 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe 16,20,24 \
              --pipe5 20 --kinds piper:20,piper:24 \
              --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepr2.json" || exit 1 ;;
+    bench20_pipe|bench20_piper|bench20_pipe5) v=${s#bench20_}
+             RMA_PIPE_FAST=$v step "$s" 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
+             --json-out "$OUT/$s.json" || exit 1 ;;
+    bench1000_pipe|bench1000_piper) v=${s#bench1000_}
+             RMA_PIPE_FAST=$v step "$s" 300 python bench.py --json-out "$OUT/$s.json" || exit 1 ;;
+    sweepr3) step sweepr3 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 17,18,19,20,24 \
+             --kinds piper:17,piper:18,piper:19,piper:20 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepr3.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;

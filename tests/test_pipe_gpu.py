@@ -284,7 +284,7 @@ def test_pipe_five_cells_guard_bands(K, nx):
 
 
 @pytest.mark.parametrize("nx", [515, 518, 520, 1028])
-@pytest.mark.parametrize("K", [12, 16, 20, 24])
+@pytest.mark.parametrize("K", [17, 18, 19, 20])
 def test_piper_register_factors_bitwise(nx, K):
     """piper (factor rows in registers, shifted one level per row, one LDS
     hand-off row per stage boundary): bitwise equal to the CPU twin and to
