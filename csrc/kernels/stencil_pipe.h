@@ -147,8 +147,8 @@ constexpr int waves_per_simd() {
 // factor row per level -> one factor row per stage (H levels); LDS per
 // block: 4 (S-1) rows.
 template <int K, int S, int V>
-constexpr int lds_bytes_reg() {
-  return 4 * (S > 1 ? S - 1 : 1) * Geo<K, S, V, 1>::WB * 8;
+constexpr int lds_bytes_reg() {  // T + factor hand-off rows, LDS-DMA staging (V = 2, 4)
+  return (4 * (S > 1 ? S - 1 : 1) + (V == 2 || V == 4 ? 6 : 0)) * Geo<K, S, V, 1>::WB * 8 + 8;
 }
 template <int K, int S, int V, int Ar, int C>
 constexpr int kernel_waves() {
@@ -195,11 +195,15 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = Ar == kArFast5Reg;
   static_assert(!kRegG || (C == 1 && V != 5), "register factors: V <= 4, one column wave");
-  // stage 0 prefetches T / 1/Cp two rows ahead; 1/Cp only one row ahead where
-  // the register factors would otherwise not fit 2 waves per SIMD (H = 6,
-  // V = 4; T one row ahead too: 92.7 vs 81.6 ms per K=24 pass, the HBM
-  // latency is longer than one row iteration)
-  constexpr bool kPre1 = kRegG && V == 4 && Plan<K, S>::H >= 6;
+  // register factors, 2 or 4 cells per lane: stage 0 prefetches T / 1/Cp two
+  // rows ahead by LDS-DMA (global_load_lds_dwordx4 into three staging rows per
+  // array) instead of into 4 rows of registers, which the register factors
+  // need (K=24: 256 VGPRs + 6 spilled with register prefetch; with T one row
+  // ahead 251 VGPRs but the HBM latency shows: 92.7 vs 81.6 ms per pass). The
+  // row barrier is then a raw s_barrier after lgkmcnt(0): __syncthreads()
+  // would also wait vmcnt(0) and drain the prefetch every row.
+  constexpr bool kGlds = kRegG && (V == 2 || V == 4);
+  constexpr bool kPre1 = false;
   using G = Geo<K, S, V, C>;
   constexpr int H = P::H, HL = P::HL, R = ring_rows<K, S, V>();
   constexpr int M = kRegG ? 0 : mirror_rows<K, S, V, Canon, C>();
@@ -267,18 +271,27 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   auto rowc = [&](int y) { return (int64_t)min(max(y, 0), ny32 - 1); };
   if (stage == 0) {
     load_row<V>(w[0][2], T + rowc(i) * nx + xo);
-    load_row<V>(pT, T + rowc(i + 1) * nx + xo);
-    load_row<V>(pC, iCp + rowc(i) * nx + xo);
-    load_row<V>(qT, T + rowc(i + 2) * nx + xo);
-    if constexpr (!kPre1) load_row<V>(qC, iCp + rowc(i + 1) * nx + xo);
+    if constexpr (!kGlds) {
+      load_row<V>(pT, T + rowc(i + 1) * nx + xo);
+      load_row<V>(pC, iCp + rowc(i) * nx + xo);
+      load_row<V>(qT, T + rowc(i + 2) * nx + xo);
+      if constexpr (!kPre1) load_row<V>(qC, iCp + rowc(i + 1) * nx + xo);
+    }
   }
   // physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R)
   // register factors: the same LDS array holds the [2][NH][WB] factor hand-off rows
-  constexpr int kRing = kRegG ? 2 * NH * WB : (R + M) * WB;
+  // register factors: no ring; the factor hand-off rows follow the T hand-off
+  // rows in `hand` ([2][NH][WB] each), and the LDS-DMA staging rows are an
+  // array of their own (T rows 0..2, 1/Cp rows 3..5), declared only where used:
+  // the compiler's LDS-DMA hazard check then sees the hand-off writes and the
+  // DMA on distinct objects and waits for no DMA before them
+  constexpr int kRing = kRegG ? 1 : (R + M) * WB, kHand = kRegG ? 4 : 2;
   __shared__ double ring[kRing];
-  __shared__ double hand[2][NH][WB];
-  for (int t = threadIdx.x; t < kRing; t += S * C * kWave) ring[t] = 0.0;
-  for (int t = threadIdx.x; t < 2 * NH * WB; t += S * C * kWave) (&hand[0][0][0])[t] = 0.0;
+  __shared__ double hand[kHand][NH][WB];
+  __shared__ double staging[kGlds ? 6 * WB : 1];  // referenced by kGlds code only
+  if constexpr (!kRegG)
+    for (int t = threadIdx.x; t < kRing; t += S * C * kWave) ring[t] = 0.0;
+  for (int t = threadIdx.x; t < kHand * NH * WB; t += S * C * kWave) (&hand[0][0][0])[t] = 0.0;
   // register factors: gr[j-1] = the factor row of level j, shifted one level
   // per row iteration (level j+1 computes next iteration the row level j
   // computes now); the shift is SSA renaming, the loop back-edge costs the
@@ -290,7 +303,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   for (int q = 0; q < (kRegG ? H : 1); ++q)
 #pragma unroll
     for (int v = 0; v < V; ++v) gr[q][v] = 0.0;
-  auto gh = [&](int pb, int st) { return &ring[(pb * NH + st) * WB]; };
+  auto gh = [&](int pb, int st) { return &hand[2 + pb][st][0]; };
   auto gshift = [&]() {
 #pragma unroll
     for (int q = (kRegG ? H : 1) - 1; q > 0; --q)
@@ -298,6 +311,26 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       for (int v = 0; v < V; ++v) gr[q][v] = gr[q - 1][v];
   };
   __syncthreads();
+  // LDS-DMA staging row of T (a = 0) / 1/Cp (a = 1) for relative row r (mod 3):
+  // instruction h, lane l loads the cell pair 2l+h of the lane's window, which
+  // lands at dbl2 slot h*64 + l: the pair-interleaved row layout rd2 reads
+  auto stg = [&](int a, int r) { return &staging[(3 * a + r) * WB]; };
+  auto glds_row = [&](int a, int y, int r) {
+    const double* src = (a ? iCp : T) + rowc(y) * nx + xo;
+#pragma unroll
+    for (int h = 0; h < V / 2; ++h)
+      __builtin_amdgcn_global_load_lds(src + 2 * h, stg(a, r) + h * 2 * kWave, 16, 0, 0);
+  };
+  if constexpr (kGlds) {
+    if (stage == 0) {  // rows i+1..i+3 of T and i..i+2 of 1/Cp, in the order they are waited for
+      glds_row(0, i + 1, 0);
+      glds_row(1, i, 0);
+      glds_row(0, i + 2, 1);
+      glds_row(1, i + 1, 1);
+      glds_row(0, i + 3, 2);
+      glds_row(1, i + 2, 2);
+    }
+  }
   // LDS rows hold cell pairs interleaved by parity (pair p at dbl2 slot
   // (p & 1) * WB/4 + p/2): a wave window starting at an even pair (D % 4 == 0)
   // reads/writes each of its two pairs per lane as one contiguous 1 KiB
@@ -355,6 +388,22 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       // factors exist (one factor row fewer live)
       if constexpr (kRegG && !LAST) wr2(gh(par, 0), gr[H - 1]);
       const bool rin1 = i >= 1 && i <= ny32 - 2;
+      if constexpr (kGlds) {
+        // three rows ahead: the staging slot of this iteration's rows (T i+1,
+        // 1/Cp i) is the unrolled phase (the loop starts at phase 0), and their
+        // DMA (issued three iterations ago, at this phase of the previous loop
+        // trip) has landed when at most the two later iterations' 2 x V
+        // instructions are outstanding. Same-phase slots keep every DMA -> read
+        // pair across the loop back-edge, where the compiler's LDS-DMA hazard
+        // check adds no vmcnt(0) (a read of a slot DMA'd earlier in the same
+        // trip got one, whatever the counted wait before it). The builtin
+        // (gfx9 encoding: vmcnt bits 3:0, expcnt 6:4 and lgkmcnt 11:8 at their
+        // maxima = no wait) plus an empty asm keeps the reads below the wait.
+        __builtin_amdgcn_s_waitcnt(0x0F70 | (V == 4 ? 8 : 4));
+        asm volatile("" ::: "memory");
+        rd2(stg(0, Pr), pT);
+        rd2(stg(1, Pr), pC);
+      }
 #pragma unroll
       for (int v = 0; v < V; ++v) w[0][Pr][v] = pT[v];
       if (rin1 && xin) {  // wave-uniform: no per-cell selects away from the x edges
@@ -380,16 +429,18 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
           if (slot0 >= R - M) wr2(ring + (slot0 - (R - M)) * WB, g);
         }
       }
+      if constexpr (!kGlds) {
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        pT[v] = qT[v];
-        if constexpr (!kPre1) pC[v] = qC[v];
-      }
-      load_row<V>(qT, T + rowc(i + 3) * nx + xo);
-      if constexpr (kPre1) {
-        load_row<V>(pC, iCp + rowc(i + 1) * nx + xo);
-      } else {
-        load_row<V>(qC, iCp + rowc(i + 2) * nx + xo);
+        for (int v = 0; v < V; ++v) {
+          pT[v] = qT[v];
+          if constexpr (!kPre1) pC[v] = qC[v];
+        }
+        load_row<V>(qT, T + rowc(i + 3) * nx + xo);
+        if constexpr (kPre1) {
+          load_row<V>(pC, iCp + rowc(i + 1) * nx + xo);
+        } else {
+          load_row<V>(qC, iCp + rowc(i + 2) * nx + xo);
+        }
       }
     } else {
       rd2(&hand[par ^ 1][stage - 1][0], w[0][Pr]);
@@ -517,7 +568,19 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     }
     slot0 = slot0 + 1 == R ? 0 : slot0 + 1;
     par ^= 1;
-    __syncthreads();  // hand-off and ring rows visible; this iteration's reads done
+    if constexpr (kGlds) {  // no vmcnt(0): the staging DMA stays in flight across rows
+      if constexpr (S0) {
+        // the staging reads above are complete (lgkmcnt(0)) before the DMA of
+        // T row i+4 / 1/Cp row i+3 overwrites the same slots
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        asm volatile("" ::: "memory");
+        glds_row(0, i + 4, Pr);
+        glds_row(1, i + 3, Pr);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      __syncthreads();  // hand-off and ring rows visible; this iteration's reads done
+    }
   };
   // one row loop per stage role (stage is wave-uniform; every copy passes the
   // same barriers): stage 0 carries the HBM prefetch registers, the others not
@@ -540,6 +603,11 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       run(std::false_type{}, std::true_type{});
     else if constexpr (S > 2)
       run(std::false_type{}, std::false_type{});
+  }
+  // the staging DMA issued past the last row must land before the block's LDS
+  // is released to the next block on this CU
+  if constexpr (kGlds) {
+    if (stage == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
 

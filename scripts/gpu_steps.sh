@@ -63,6 +63,9 @@ for s in "$@"; do
     sweepr3) step sweepr3 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 17,18,19,20,24 \
              --kinds piper:17,piper:18,piper:19,piper:20 \
              --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepr3.json" || exit 1 ;;
+    sweepg) step sweepg 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 20,21,22,23,24 \
+             --kinds piper:20,piper:21,piper:22,piper:23,piper:24,pipe_diag1:24 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepg.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;

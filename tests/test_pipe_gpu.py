@@ -284,11 +284,12 @@ def test_pipe_five_cells_guard_bands(K, nx):
 
 
 @pytest.mark.parametrize("nx", [515, 518, 520, 1028])
-@pytest.mark.parametrize("K", [17, 18, 19, 20])
+@pytest.mark.parametrize("K", [17, 20, 21, 24])
 def test_piper_register_factors_bitwise(nx, K):
     """piper (factor rows in registers, shifted one level per row, one LDS
-    hand-off row per stage boundary): bitwise equal to the CPU twin and to
-    pipe, also on rect lists (1, 2 and 4 cells per lane)."""
+    hand-off row per stage boundary; at 2 and 4 cells per lane stage 0's T /
+    1/Cp prefetch by LDS-DMA three rows ahead): bitwise equal to the CPU twin,
+    also on rect lists and short chunks (1, 2 and 4 cells per lane)."""
     ny = 157
     T, iCp = rand((ny, nx), 31 + K), rand((ny, nx), 32, 0.5, 1.0)
     rects = [ops.interior_rect(nx, ny)]
