@@ -66,6 +66,11 @@ for s in "$@"; do
     sweepg) step sweepg 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 20,21,22,23,24 \
              --kinds piper:20,piper:21,piper:22,piper:23,piper:24,pipe_diag1:24 \
              --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepg.json" || exit 1 ;;
+    pmcg) prof pmcg 300 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+             SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CU_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+             --output-format csv -d "$R/$OUT/pmcg" -o run -- python3 "$R/bench/pass_sweep.py" \
+             --n 101120 --rounds 1 --pipe 20,24 --kinds piper:20,piper:24,pipe_diag1:24 --pipec "" \
+             --ldsdpp "" --old "" --alt "" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
