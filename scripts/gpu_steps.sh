@@ -71,6 +71,12 @@ for s in "$@"; do
              --output-format csv -d "$R/$OUT/pmcg" -o run -- python3 "$R/bench/pass_sweep.py" \
              --n 101120 --rounds 1 --pipe 20,24 --kinds piper:20,piper:24,pipe_diag1:24 --pipec "" \
              --ldsdpp "" --old "" --alt "" || exit 1 ;;
+    sweepg_small) step sweepg_small 600 python bench/pass_sweep.py --n 16384 --rounds 7 \
+             --pipe 17,20,24 --kinds piper:17,piper:20,piper:24 --pipec "" --ldsdpp "" --old "" \
+             --alt "" --out "$OUT/sweepg_16384.json" && \
+             step sweepg_4096 600 python bench/pass_sweep.py --n 4096 --rounds 9 \
+             --pipe 17,20,24 --kinds piper:17,piper:20,piper:24 --pipec "" --ldsdpp "" --old "" \
+             --alt "" --out "$OUT/sweepg_4096.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
