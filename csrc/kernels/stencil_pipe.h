@@ -195,15 +195,15 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = Ar == kArFast5Reg;
   static_assert(!kRegG || (C == 1 && V != 5), "register factors: V <= 4, one column wave");
-  // register factors, 2 or 4 cells per lane: stage 0 prefetches T / 1/Cp two
+  // register factors, 2 or 4 cells per lane: stage 0 prefetches T / 1/Cp three
   // rows ahead by LDS-DMA (global_load_lds_dwordx4 into three staging rows per
-  // array) instead of into 4 rows of registers, which the register factors
-  // need (K=24: 256 VGPRs + 6 spilled with register prefetch; with T one row
-  // ahead 251 VGPRs but the HBM latency shows: 92.7 vs 81.6 ms per pass). The
-  // row barrier is then a raw s_barrier after lgkmcnt(0): __syncthreads()
-  // would also wait vmcnt(0) and drain the prefetch every row.
+  // array) instead of two rows ahead into 4 rows of registers, which the
+  // register factors need (K=24: 256 VGPRs + 6 spilled with the register
+  // prefetch; with T one row ahead 251 VGPRs but the HBM latency shows: 92.7 vs
+  // 81.6 ms per pass; with LDS-DMA 234 VGPRs). The row barrier is then a raw
+  // s_barrier after lgkmcnt(0): __syncthreads() would also wait vmcnt(0) and
+  // drain the prefetch every row.
   constexpr bool kGlds = kRegG && (V == 2 || V == 4);
-  constexpr bool kPre1 = false;
   using G = Geo<K, S, V, C>;
   constexpr int H = P::H, HL = P::HL, R = ring_rows<K, S, V>();
   constexpr int M = kRegG ? 0 : mirror_rows<K, S, V, Canon, C>();
@@ -275,7 +275,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       load_row<V>(pT, T + rowc(i + 1) * nx + xo);
       load_row<V>(pC, iCp + rowc(i) * nx + xo);
       load_row<V>(qT, T + rowc(i + 2) * nx + xo);
-      if constexpr (!kPre1) load_row<V>(qC, iCp + rowc(i + 1) * nx + xo);
+      load_row<V>(qC, iCp + rowc(i + 1) * nx + xo);
     }
   }
   // physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R)
@@ -433,14 +433,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           pT[v] = qT[v];
-          if constexpr (!kPre1) pC[v] = qC[v];
+          pC[v] = qC[v];
         }
         load_row<V>(qT, T + rowc(i + 3) * nx + xo);
-        if constexpr (kPre1) {
-          load_row<V>(pC, iCp + rowc(i + 1) * nx + xo);
-        } else {
-          load_row<V>(qC, iCp + rowc(i + 2) * nx + xo);
-        }
+        load_row<V>(qC, iCp + rowc(i + 2) * nx + xo);
       }
     } else {
       rd2(&hand[par ^ 1][stage - 1][0], w[0][Pr]);
