@@ -50,8 +50,8 @@ def main(argv=None):
     ap.add_argument("--pipe5", default="", help="depths of the pipe kernel at 5 cells per lane "
                     "(needs n % 5 == 0)")
     ap.add_argument("--chunks5", default="", help="pipe5 K:c1/c2/..., chunk-row variants")
-    ap.add_argument("--kinds", default="", help="other K-step kernels by name, kernel:K,... "
-                    "(e.g. piper:24,pipe_diag1:24; 4 cells per lane)")
+    ap.add_argument("--kinds", default="", help="other K-step kernels by name, kernel:K[:chunk],"
+                    "... (e.g. piper:24,piper:24:4096,pipe_diag1:24; 4 cells per lane)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -108,8 +108,8 @@ def main(argv=None):
     cfgs += [("pipe2", K, 0) for K in krange(a.pipe2)]
     cfgs += [("pipe5", K, 0) for K in krange(a.pipe5)]
     for item in filter(None, a.kinds.split(",")):
-        k, K = item.split(":")
-        cfgs.append((k, int(K), 0))
+        k, K, *c = item.split(":")  # kernel:K[:chunk_rows]
+        cfgs.append((k, int(K), 0, int(c[0])) if c else (k, int(K), 0))
     for item in filter(None, a.chunks5.split(",")):
         K, cs = item.split(":")
         for c in cs.split("/"):

@@ -77,6 +77,11 @@ for s in "$@"; do
              step sweepg_4096 600 python bench/pass_sweep.py --n 4096 --rounds 9 \
              --pipe 17,20,24 --kinds piper:17,piper:20,piper:24 --pipec "" --ldsdpp "" --old "" \
              --alt "" --out "$OUT/sweepg_4096.json" || exit 1 ;;
+    sweepc) step sweepc 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 20,24 \
+             --kinds piper:20,piper:20:2048,piper:20:4096,piper:20:6144,piper:24,piper:24:2048,piper:24:4096,piper:24:6144 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepc.json" || exit 1 ;;
+    prof20) prof prof20 300 --kernel-trace --stats -d "$R/$OUT/prof20" -o run -- python3 \
+             "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --json-out "$R/$OUT/prof20.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
