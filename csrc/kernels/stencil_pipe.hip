@@ -29,7 +29,7 @@ int pipe_default_stages(int K) {
 bool pipe_has(int K, int S, int arith) {
   if (K < 1 || K > kPipeMaxK) return false;
   if (arith == pipe::kArFast5Perm) return S == 4 && (K == 16 || K == 20 || K == 24);
-  if (arith == pipe::kArFast5Reg) return S == 4 && K >= 17 && K <= 24;
+  if (arith == pipe::kArFast5Reg) return S == 4 && K >= 10 && K <= 24;
   if (arith == pipe::kArDiagOneRow) return S == 4 && (K == 20 || K == 24);
   if (S == pipe_default_stages(K)) return true;
   // alternative stage splits instantiated for sweeps (csrc/lab/stencil_pipe_lab.hip)

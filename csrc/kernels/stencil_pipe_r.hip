@@ -14,6 +14,13 @@ namespace pipe {
 
 bool dispatch_r(int K, int S, int V, int ar, const PipeLaunch& a) {
   if (ar != kArFast5Reg) return false;
+  RMA_PIPE_CASE(10, 4, kArFast5Reg)
+  RMA_PIPE_CASE(11, 4, kArFast5Reg)
+  RMA_PIPE_CASE(12, 4, kArFast5Reg)
+  RMA_PIPE_CASE(13, 4, kArFast5Reg)
+  RMA_PIPE_CASE(14, 4, kArFast5Reg)
+  RMA_PIPE_CASE(15, 4, kArFast5Reg)
+  RMA_PIPE_CASE(16, 4, kArFast5Reg)
   RMA_PIPE_CASE(17, 4, kArFast5Reg)
   RMA_PIPE_CASE(18, 4, kArFast5Reg)
   RMA_PIPE_CASE(19, 4, kArFast5Reg)

@@ -61,7 +61,7 @@ StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c) {
   if (const int ch = pipe_chunk_rows(K, ny, false)) t.chunk_rows = ch;
   // K = 17..20: factor rows in registers instead of the LDS ring ("piper",
   // 5-level stages; 1.3-2.1 % per K=20 pass at 101120^2, profiles/SUMMARY_r3.md)
-  if (pipe_has(K, pipe_default_stages(K), 3)) t.kernel = 12;
+  if (K >= 17 && pipe_has(K, pipe_default_stages(K), 3)) t.kernel = 12;
   // RMA_PIPE_FAST=pipe | pipe5 forces the ring kernel at every depth (A/B runs;
   // pipe5 = 5 cells per lane, lab library, K = 16..20 and nx % 5 == 0)
   static const char* e = std::getenv("RMA_PIPE_FAST");

@@ -82,6 +82,12 @@ for s in "$@"; do
              --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepc.json" || exit 1 ;;
     prof20) prof prof20 300 --kernel-trace --stats -d "$R/$OUT/prof20" -o run -- python3 \
              "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --json-out "$R/$OUT/prof20.json" || exit 1 ;;
+    sweeplo) step sweeplo 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe 10,12,14,16,17,18 \
+             --kinds piper:10,piper:12,piper:14,piper:16,piper:17,piper:18 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweeplo.json" && \
+             step sweeplo16k 600 python bench/pass_sweep.py --n 16384 --rounds 7 --pipe 10,12,14,16 \
+             --kinds piper:10,piper:12,piper:14,piper:16 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweeplo16k.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;

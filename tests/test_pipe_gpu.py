@@ -284,7 +284,7 @@ def test_pipe_five_cells_guard_bands(K, nx):
 
 
 @pytest.mark.parametrize("nx", [515, 518, 520, 1028])
-@pytest.mark.parametrize("K", [17, 20, 21, 24])
+@pytest.mark.parametrize("K", [10, 13, 16, 17, 20, 21, 24])
 def test_piper_register_factors_bitwise(nx, K):
     """piper (factor rows in registers, shifted one level per row, one LDS
     hand-off row per stage boundary; at 2 and 4 cells per lane stage 0's T /
