@@ -64,8 +64,8 @@ struct ExecParams {
 // the tile height (they amortise the 2K-1 rows recomputed per chunk).
 StencilTuning default_tune_k(int K, int64_t ny);
 // Kernel of a K-step pass: fast_math (and fast5_ok) -> the pipelined fast5
-// kernel (9) with 4 cells per lane, at K = 17..20 its register-factor variant
-// (12, "piper"); canonical -> kernel 3 at K in
+// kernel (9) with 4 cells per lane, at K >= 14 (K >= 10 from 65536 rows on) its
+// register-factor variant (12, "piper"); canonical -> kernel 3 at K in
 // {3,4,6,8}, the canonical pipelined kernel (10) at other K >= 3 (K = 1 and
 // 2 have their own one- and two-step kernels).
 StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c);

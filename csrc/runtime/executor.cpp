@@ -59,9 +59,12 @@ StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c) {
   t.kernel = 9;  // stage-pipelined fast5, any K (stencil_pipe.h)
   t.vec = 4;
   if (const int ch = pipe_chunk_rows(K, ny, false)) t.chunk_rows = ch;
-  // K = 17..20: factor rows in registers instead of the LDS ring ("piper",
-  // 5-level stages; 1.3-2.1 % per K=20 pass at 101120^2, profiles/SUMMARY_r3.md)
-  if (K >= 17 && pipe_has(K, pipe_default_stages(K), 3)) t.kernel = 12;
+  // factor rows in registers instead of the LDS ring, stage-0 prefetch by
+  // LDS-DMA ("piper"): per pass at 101120^2 K=10..24 -0.7..-7 % (K=20 -2.2 %,
+  // K=24 -1.5 %); at 16384^2 K=14..20 -0.7..-8.5 % but K=10 / 12 +12 / +7 %
+  // (profiles/SUMMARY_r3.md), so K = 10..13 only on the large tile classes
+  if ((K >= 14 || (K >= 10 && ny >= 65536)) && pipe_has(K, pipe_default_stages(K), 3))
+    t.kernel = 12;
   // RMA_PIPE_FAST=pipe | pipe5 forces the ring kernel at every depth (A/B runs;
   // pipe5 = 5 cells per lane, lab library, K = 16..20 and nx % 5 == 0)
   static const char* e = std::getenv("RMA_PIPE_FAST");

@@ -85,8 +85,8 @@ def test_pipe_chunk_rows_by_tile_class():
 
 def test_fast_kernel_choice_by_depth():
     """The executor's fast-math kernel per pass depth: the register-factor
-    pipelined kernel ("piper", 12) at K = 17..24, the ring kernel ("pipe", 9)
-    below; cells per lane as the kernel will run them (pipe_vec: 5 only for the
+    pipelined kernel ("piper", 12) from K = 14 (from K = 10 on tiles of >= 65536
+    rows), the ring kernel ("pipe", 9) below; cells per lane as the kernel will run them (pipe_vec: 5 only for the
     lab's fast5 K = 16..20 on nx % 5 == 0, else 4 / 2 / 1 by alignment)."""
     nat = pytest.importorskip("rocm_mpi_amd._native")
     try:
@@ -95,8 +95,11 @@ def test_fast_kernel_choice_by_depth():
         pytest.skip(f"native core not built: {e}")
     coef = (-1.0, 10.0, 10.0, 1e-3)
     kern = {K: N.fast_kernel_k(K, 101376, coef)[0] for K in range(3, 25)}
-    assert all(kern[K] == 12 for K in range(17, 25)), kern
-    assert all(kern[K] == 9 for K in range(3, 17)), kern
+    assert all(kern[K] == 12 for K in range(10, 25)), kern
+    assert all(kern[K] == 9 for K in range(3, 10)), kern
+    small = {K: N.fast_kernel_k(K, 16384, coef)[0] for K in range(3, 25)}
+    assert all(small[K] == 12 for K in range(14, 25)), small
+    assert all(small[K] == 9 for K in range(3, 14)), small
     assert N.pipe_vec(20, 0, 0, 101120, 5, True) == 5
     assert N.pipe_vec(20, 0, 0, 101376, 5, True) == 4      # nx % 5 != 0
     assert N.pipe_vec(24, 0, 0, 101120, 5, True) == 4      # K > 20
