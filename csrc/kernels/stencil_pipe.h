@@ -278,17 +278,17 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       load_row<V>(qC, iCp + rowc(i + 1) * nx + xo);
     }
   }
-  // physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R)
-  // register factors: the same LDS array holds the [2][NH][WB] factor hand-off rows
-  // register factors: no ring; the factor hand-off rows follow the T hand-off
+  // ring: physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R).
+  // Register factors: no ring; the factor hand-off rows follow the T hand-off
   // rows in `hand` ([2][NH][WB] each), and the LDS-DMA staging rows are an
-  // array of their own (T rows 0..2, 1/Cp rows 3..5), declared only where used:
-  // the compiler's LDS-DMA hazard check then sees the hand-off writes and the
-  // DMA on distinct objects and waits for no DMA before them
+  // array of their own (T rows 0..2, 1/Cp rows 3..5; referenced by kGlds code
+  // only, so other instantiations allocate nothing for it): the compiler's
+  // LDS-DMA hazard check then sees the hand-off writes and the DMA on distinct
+  // objects and waits for no DMA before them
   constexpr int kRing = kRegG ? 1 : (R + M) * WB, kHand = kRegG ? 4 : 2;
   __shared__ double ring[kRing];
   __shared__ double hand[kHand][NH][WB];
-  __shared__ double staging[kGlds ? 6 * WB : 1];  // referenced by kGlds code only
+  __shared__ double staging[kGlds ? 6 * WB : 1];
   if constexpr (!kRegG)
     for (int t = threadIdx.x; t < kRing; t += S * C * kWave) ring[t] = 0.0;
   for (int t = threadIdx.x; t < kHand * NH * WB; t += S * C * kWave) (&hand[0][0][0])[t] = 0.0;
