@@ -244,6 +244,12 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   // addressing instead of 64-bit VGPR address arithmetic); xso wraps only for
   // lanes left of the array, which never store (m[] false)
   const uint32_t xo = (uint32_t)xl, xso = (uint32_t)x;
+  // byte offsets in 32 bits: uniform 64-bit row base + zero-extended 32-bit
+  // offset is the SGPR-base + VGPR-offset (saddr) addressing form
+  const uint32_t xob = xo * 8u, xsob = xso * 8u;
+  auto at = [](const double* base, uint32_t boff) {
+    return reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + boff);
+  };
   const bool xin = xw >= 1 && xw + W - 1 <= nx - 2;  // no x-boundary cell in the window
 
   // fast5 constants (the host guarantees fast5_ok); canonical uses k directly
@@ -269,13 +275,14 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   int i = ya32 - K;
   const int iend = yb32 + K - 3 + S;
   auto rowc = [&](int y) { return (int64_t)min(max(y, 0), ny32 - 1); };
+  auto rowp = [&](const double* a, int y) { return at(a + rowc(y) * nx, xob); };
   if (stage == 0) {
-    load_row<V>(w[0][2], T + rowc(i) * nx + xo);
+    load_row<V>(w[0][2], rowp(T, i));
     if constexpr (!kGlds) {
-      load_row<V>(pT, T + rowc(i + 1) * nx + xo);
-      load_row<V>(pC, iCp + rowc(i) * nx + xo);
-      load_row<V>(qT, T + rowc(i + 2) * nx + xo);
-      load_row<V>(qC, iCp + rowc(i + 1) * nx + xo);
+      load_row<V>(pT, rowp(T, i + 1));
+      load_row<V>(pC, rowp(iCp, i));
+      load_row<V>(qT, rowp(T, i + 2));
+      load_row<V>(qC, rowp(iCp, i + 1));
     }
   }
   // ring: physical row M + s holds slot s; rows [0, M) mirror slots [R-M, R).
@@ -316,10 +323,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   // lands at dbl2 slot h*64 + l: the pair-interleaved row layout rd2 reads
   auto stg = [&](int a, int r) { return &staging[(3 * a + r) * WB]; };
   auto glds_row = [&](int a, int y, int r) {
-    const double* src = (a ? iCp : T) + rowc(y) * nx + xo;
+    const double* rb = (a ? iCp : T) + rowc(y) * nx;
 #pragma unroll
     for (int h = 0; h < V / 2; ++h)
-      __builtin_amdgcn_global_load_lds(src + 2 * h, stg(a, r) + h * 2 * kWave, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(at(rb, xob + 16u * h), stg(a, r) + h * 2 * kWave, 16, 0, 0);
   };
   if constexpr (kGlds) {
     if (stage == 0) {  // rows i+1..i+3 of T and i..i+2 of 1/Cp, in the order they are waited for
@@ -435,8 +442,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
           pT[v] = qT[v];
           pC[v] = qC[v];
         }
-        load_row<V>(qT, T + rowc(i + 3) * nx + xo);
-        load_row<V>(qC, iCp + rowc(i + 2) * nx + xo);
+        load_row<V>(qT, rowp(T, i + 3));
+        load_row<V>(qC, rowp(iCp, i + 2));
       }
     } else {
       rd2(&hand[par ^ 1][stage - 1][0], w[0][Pr]);
@@ -546,7 +553,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       } else if constexpr (!LAST) {
         wr2(&hand[par][S0 ? 0 : stage][0], res);
       } else if (row >= ya32 && row < yb32) {
-        store_row<V, true>(T2 + (int64_t)row * nx + xso, res, m);
+        store_row<V, true>(const_cast<double*>(at(T2 + (int64_t)row * nx, xsob)), res, m);
       }
     }
     };
