@@ -58,6 +58,39 @@ def tables(path: str):
     return d["tile"], fast, fill(can)
 
 
+def piper_ratios(paths) -> dict:
+    """Per-depth piper / pipe pass-time ratios from same-run sweeps (round 3:
+    the executor's fast kernel from K = 10 on the 288 GB tile class)."""
+    r = {}
+    for path in paths:
+        rows = json.load(open(path))["rows"]
+        pipe = {x["K"]: x["ms_per_pass"] for x in rows if x["kernel"] == "pipe"}
+        for x in rows:
+            if x["kernel"] == "piper" and x["K"] in pipe and x.get("chunk_rows") == next(
+                    y["chunk_rows"] for y in rows if y["kernel"] == "pipe" and y["K"] == x["K"]):
+                r[x["K"]] = x["ms_per_pass"] / pipe[x["K"]]
+    return r
+
+
+def apply_ratios(fast: list, ratios: dict, kmin: int) -> list:
+    """Scale the fast5 table by the piper ratios at K >= kmin (depths between
+    measured ones interpolated)."""
+    ks = sorted(k for k in ratios if k >= kmin)
+    out = list(fast)
+    for K in range(kmin, KMAX + 1):
+        if K in ratios:
+            f = ratios[K]
+        else:
+            lo = max([k for k in ks if k < K], default=ks[0])
+            hi = min([k for k in ks if k > K], default=ks[-1])
+            f = ratios[lo] if lo == hi else ratios[lo] + (ratios[hi] - ratios[lo]) * (K - lo) / (hi - lo)
+        out[K - 1] = fast[K - 1] * f
+    return out
+
+
+PIPER_SWEEPS_101376 = ["r3/pass_sweep_piper_lowK_101120.json", "r3/pass_sweep_piper_glds_boxE.json"]
+
+
 def fmt(name, vals):
     body = ", ".join(f"{v:.3f}" for v in vals)
     return f"    {{{body}}},  // {name}"

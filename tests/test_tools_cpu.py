@@ -25,8 +25,12 @@ def test_planner_tables_come_from_the_committed_sweeps(tile):
         N = native()
     except Exception as e:  # noqa: BLE001
         pytest.skip(f"native core not built: {e}")
-    n, fast, can = load("fit_pass_costs").tables(os.path.join(P, f"pass_sweep_{tile}_r2_final.json"))
+    fpc = load("fit_pass_costs")
+    n, fast, can = fpc.tables(os.path.join(P, f"pass_sweep_{tile}_r2_final.json"))
     assert n == tile
+    if tile == 101376:  # round 3: piper from K = 10, scaled by its measured ratios to pipe
+        fast = fpc.apply_ratios(fast, fpc.piper_ratios(
+            [os.path.join(P, q) for q in fpc.PIPER_SWEEPS_101376]), 10)
     cells = float(tile) * tile
     got_f = list(N.default_pass_costs(24, True, cells))[1:]
     got_c = list(N.default_pass_costs(24, False, cells))[1:]
