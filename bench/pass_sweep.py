@@ -80,8 +80,6 @@ def main(argv=None):
         # the executor's rows per task for this kernel and depth
         if c or a.chunk:
             return c or a.chunk
-        if kind == "pipecr":
-            return N.pipe_chunk_rows(K, n, True) or N.default_chunk_k(max(K, 3), n)
         if kind in ("pipe", "pipe2", "pipeb", "pipe5", "piper", "pipe_diag1"):
             return N.pipe_chunk_rows(K, n, False) or N.default_chunk_k(max(K, 3), n)
         if kind == "pipec":

@@ -95,8 +95,6 @@ struct Geo {
 // addressing and temporaries; canonical also the carried y flux and the x
 // fluxes (checked: no spills at any K, V, scripts/check_isa.py).
 constexpr int kArFast5 = 0, kArCanon = 1, kArFast5Perm = 2, kArFast5Reg = 3;
-// canonical arithmetic with register-resident factors (1/Cp rows) and the LDS-DMA prefetch
-constexpr int kArCanonReg = 5;
 // diagnosis only (lab, WRONG results): every level of a stage uses the factor
 // row of its level 1, i.e. one LDS ring row read per stage and iteration
 // instead of H; measures what the ring reads cost (energy / time)
@@ -154,7 +152,7 @@ constexpr int lds_bytes_reg() {  // T + factor hand-off rows, LDS-DMA staging (V
 }
 template <int K, int S, int V, int Ar, int C>
 constexpr int kernel_waves() {
-  if constexpr (Ar == kArFast5Reg || Ar == kArCanonReg) {
+  if constexpr (Ar == kArFast5Reg) {
     // + the H factor rows (measured 158 / 233 / 256 VGPRs at K = 12 / 20 / 24, V = 4)
     constexpr int H = Plan<K, S>::H;
     constexpr int vgpr = 8 * H * V + 8 * V + 40;
@@ -195,8 +193,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
                                           const RectList& L, const StencilCoef& k, int chunk_rows,
                                           int remap) {
   using P = Plan<K, S>;
-  constexpr bool Canon = Ar == kArCanon || Ar == kArCanonReg, kDpp = Ar != kArFast5Perm;
-  constexpr bool kRegG = Ar == kArFast5Reg || Ar == kArCanonReg;
+  constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = Ar == kArFast5Reg;
   static_assert(!kRegG || (C == 1 && V != 5), "register factors: V <= 4, one column wave");
   // register factors, 2 or 4 cells per lane: stage 0 prefetches T / 1/Cp three
   // rows ahead by LDS-DMA (global_load_lds_dwordx4 into three staging rows per
@@ -666,7 +663,7 @@ bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
 inline bool pipe_has_v5(int K, int S, int ar) {
   return ar == kArFast5 && S == 4 && K >= 16 && K <= 20;
 }
-// register-resident factors (stencil_pipe_r.hip): fast5 and canonical, S = 4, K = 10..24
+// register-resident factors (stencil_pipe_r.hip): fast5, S = 4, K = 17..20
 bool dispatch_r(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe

@@ -32,8 +32,7 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 #              csrc/kernels/stencil_pipe.h), "pipec" (10: the same pipeline with the
 #              canonical arithmetic, bitwise equal to K one-step updates), "piper"
 #              (12: "pipe" with the factor rows in registers instead of the LDS
-#              ring and an LDS-DMA prefetch, K = 10..24, the executor's fast kernel
-#              from K = 14), "pipecr" (14: the same for the canonical arithmetic).
+#              ring, K = 17..20, the executor's kernel at those depths).
 # LAB_KERNELS live in librma_lab.so (csrc/lab: superseded / experimental kernels kept as
 # test oracles and for sweeps), loaded on first use: K-step "march"/"lds"/"dpp" (0/1/2:
 # canonical variants of kernel 3), "fast" (4: reassociated, not bitwise), "fast5" (5: the
@@ -42,13 +41,12 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 # the pipelined kernels' non-default stage splits, two-column blocks and 5 cells per lane,
 # and "pipe_diag1" (13: a diagnosis, WRONG results: one factor-ring read per stage and row).
 FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe", "pipeb", "piper")
-PIPE = ("pipe", "pipec", "pipeb", "piper", "pipe_diag1", "pipecr")
+PIPE = ("pipe", "pipec", "pipeb", "piper", "pipe_diag1")
 PIPE_MAX_K = 24
-KERNELS = {"march": 0, "lds": 1, "lds_dpp": 3, "pipe": 9, "pipec": 10, "piper": 12,
-           "pipecr": 14}
+KERNELS = {"march": 0, "lds": 1, "lds_dpp": 3, "pipe": 9, "pipec": 10, "piper": 12}
 LAB_KERNELS = {"dpp": 2, "fast": 4, "fast5": 5, "fast5p2": 6, "fast5p4": 7, "fast5p8": 8,
                "pipeb": 11, "pipe_diag1": 13}
-KSTEP_CORE = ("lds_dpp", "pipe", "pipec", "piper", "pipecr")
+KSTEP_CORE = ("lds_dpp", "pipe", "pipec", "piper")
 
 
 def kernel_id(name: str) -> int:

@@ -88,9 +88,6 @@ for s in "$@"; do
              step sweeplo16k 600 python bench/pass_sweep.py --n 16384 --rounds 7 --pipe 10,12,14,16 \
              --kinds piper:10,piper:12,piper:14,piper:16 \
              --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweeplo16k.json" || exit 1 ;;
-    sweepcr) step sweepcr 600 python bench/pass_sweep.py --n 101120 --rounds 3 --pipe "" \
-             --pipec 8,10,12,16,20,24 --kinds pipecr:10,pipecr:12,pipecr:16,pipecr:20,pipecr:24 \
-             --ldsdpp "" --old "" --alt "" --out "$OUT/sweepcr.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;

@@ -298,17 +298,3 @@ def test_piper_register_factors_bitwise(nx, K):
     sub = [(K + 3, nx - K - 7, K + 2, ny - K - 5), (1, K + 3, 1, ny - 1)]
     assert torch.equal(gpu_run(K, T, iCp, sub, "piper", chunk=19, xcd=0),
                        cpu_ref(K, T, iCp, sub, "pipe"))
-
-
-@pytest.mark.parametrize("nx", [515, 518, 520, 1028])
-@pytest.mark.parametrize("K", [10, 13, 16, 20, 24])
-def test_pipecr_canonical_register_factors_bitwise(nx, K):
-    """pipecr (canonical arithmetic, 1/Cp rows in registers, LDS-DMA prefetch):
-    bitwise equal to the canonical CPU twin (= K one-step updates)."""
-    ny = 143
-    T, iCp = rand((ny, nx), 41 + K), rand((ny, nx), 42, 0.5, 1.0)
-    rects = [ops.interior_rect(nx, ny)]
-    assert torch.equal(gpu_run(K, T, iCp, rects, "pipecr", chunk=39), cpu_ref(K, T, iCp, rects, "pipec"))
-    sub = [(K + 3, nx - K - 7, K + 2, ny - K - 5), (1, K + 3, 1, ny - 1)]
-    assert torch.equal(gpu_run(K, T, iCp, sub, "pipecr", chunk=17, xcd=0),
-                       cpu_ref(K, T, iCp, sub, "pipec"))
