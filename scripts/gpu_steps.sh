@@ -88,6 +88,9 @@ for s in "$@"; do
              step sweeplo16k 600 python bench/pass_sweep.py --n 16384 --rounds 7 --pipe 10,12,14,16 \
              --kinds piper:10,piper:12,piper:14,piper:16 \
              --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweeplo16k.json" || exit 1 ;;
+    prof_host4096) prof prof_host4096 300 --kernel-trace --output-format csv -d "$R/$OUT/prof_host4096" \
+             -o run -- python3 "$R/bench/rccl_self_overhead.py" --n 4096 --K 1 --variants perf_hide \
+             --steps 200 --pattern op --out "$R/$OUT/prof_host4096.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
