@@ -545,7 +545,7 @@ def run(a, world: int, rank: int) -> int:
             if k.startswith("RMA_DIAG") or k in ("RMA_FRAME_SIDES", "RMA_FRAME_ALIGNED",
                                                  "RMA_PASS_COSTS", "RMA_HALO_BATCH",
                                                  "RMA_FRAME_FILL", "RMA_EXEC_STREAMS",
-                                                 "RMA_PIPE_FAST")}
+                                                 "RMA_PIPE_FAST", "RMA_HALO_CROSS")}
     if gpu and os.environ.get("RMA_PIPE_FAST") == "pipe5":  # an A/B of the lab kernel
         from rocm_mpi_amd._native import load_lab
 

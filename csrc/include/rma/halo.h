@@ -39,6 +39,13 @@ class HaloExchanger {
   // Enqueue the full exchange of all fields on `stream` (asynchronous).
   // dims_mask bit d enables dimension d.
   void exchange(const std::vector<HaloField>& fields, stream_t stream, int dims_mask = 7);
+  // The same messages with ONE RCCL group for all dimensions (packs of every
+  // dimension first, unpacks after the group). Only the halo cells that lie in
+  // one dimension's halo are exact; corner cells (in two dimensions' halos)
+  // may hold a stale value. For cross-shaped (5-point) stencils whose next
+  // update reads no corner halo cell (one-step passes): one group instead of
+  // one per dimension, i.e. one RCCL enqueue and one RCCL kernel per exchange.
+  void exchange_cross(const std::vector<HaloField>& fields, stream_t stream, int dims_mask = 7);
   // Pre-allocate the pack buffers for this field set (call before capture).
   void prepare(const std::vector<HaloField>& fields, int dims_mask = 7);
 

@@ -280,7 +280,19 @@ void DiffusionExecutor::exchange(double* A, stream_t s) {
   f.elem_bytes = 8;
   f.ol = {p_.olx, p_.oly, 2};
   f.hw = {hwx_, hwy_, 1};
-  halo_->exchange({f}, s, 3);
+  // one-step passes only (temporal = 1): the 5-point update never reads a
+  // corner halo cell, so all dimensions go in ONE RCCL group (one enqueue and
+  // one RCCL kernel per exchange instead of two; RMA_HALO_CROSS=0: per dimension).
+  // K-step passes read the corners (diagonal dependencies) and keep the
+  // dimension-ordered exchange.
+  static const bool cross_ok = [] {
+    const char* e = std::getenv("RMA_HALO_CROSS");
+    return !(e && e[0] == '0');
+  }();
+  if (cross_ok && p_.temporal == 1 && p_.mode != Mode::kKp)
+    halo_->exchange_cross({f}, s, 3);
+  else
+    halo_->exchange({f}, s, 3);
 }
 
 void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {

@@ -136,4 +136,28 @@ void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stre
   bytes_last_ = c.plan.bytes_sent;
 }
 
+void HaloExchanger::exchange_cross(const std::vector<HaloField>& fields, stream_t stream,
+                                   int dims_mask) {
+  const Planned& c = planned(fields, dims_mask);
+  // packs and self copies dimension by dimension (stream-ordered launches:
+  // deterministic where two dimensions' self copies meet at a corner)
+  for (size_t d = 0; d < c.plan.dims.size(); ++d) launch_batches(c.batches[d][0], stream);
+  bool any = false;
+  for (const HaloDimPlan& dp : c.plan.dims) any = any || !dp.sends.empty() || !dp.recvs.empty();
+  if (any) {
+    RMA_CHECK_ARG(comm_ != nullptr, "remote neighbour without communicator");
+    comm_->group_start();
+    for (size_t d = 0; d < c.plan.dims.size(); ++d) {
+      const HaloDimPlan& dp = c.plan.dims[d];
+      for (size_t i = 0; i < dp.sends.size(); ++i)
+        comm_->send(c.send_ptr[d][i], dp.sends[i].bytes, dp.sends[i].peer, stream);
+      for (size_t i = 0; i < dp.recvs.size(); ++i)
+        comm_->recv(c.recv_ptr[d][i], dp.recvs[i].bytes, dp.recvs[i].peer, stream);
+    }
+    comm_->group_end();
+  }
+  for (size_t d = 0; d < c.plan.dims.size(); ++d) launch_batches(c.batches[d][1], stream);
+  bytes_last_ = c.plan.bytes_sent;
+}
+
 }  // namespace rma

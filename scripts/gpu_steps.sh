@@ -91,6 +91,9 @@ for s in "$@"; do
     prof_host4096) prof prof_host4096 300 --kernel-trace --output-format csv -d "$R/$OUT/prof_host4096" \
              -o run -- python3 "$R/bench/rccl_self_overhead.py" --n 4096 --K 1 --variants perf_hide \
              --steps 200 --pattern op --out "$R/$OUT/prof_host4096.json" || exit 1 ;;
+    host4096_nocross) RMA_HALO_CROSS=0 step host4096_nocross 300 python bench/rccl_self_overhead.py \
+             --n 4096 --K 1 --variants perf_hide --steps 400 --pattern opop \
+             --out "$OUT/host4096_nocross.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
