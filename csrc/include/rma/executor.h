@@ -133,6 +133,7 @@ class DiffusionExecutor {
   void multi_step(int K, double* Tin, double* Tout, const double* iCp, int64_t nx, int64_t ny,
                   const Rect* rects, int n, const StencilTuning& tn, void* stream) const;
   void exchange(double* A, stream_t s);
+  bool cross_pass_ = false;  // this pass may use the one-group cross exchange (run_eager)
   void build_graph(int64_t steps, int reps);
   void run_eager(int64_t nsteps);
   bool fast5() const;

@@ -289,7 +289,9 @@ void DiffusionExecutor::exchange(double* A, stream_t s) {
     const char* e = std::getenv("RMA_HALO_CROSS");
     return !(e && e[0] == '0');
   }();
-  if (cross_ok && p_.temporal == 1 && p_.mode != Mode::kKp)
+  // The last pass of a run() exchanges per dimension, so the arrays a run
+  // leaves behind have consistent corner halos (IGG update_halo! semantics).
+  if (cross_ok && cross_pass_ && p_.temporal == 1 && p_.mode != Mode::kKp)
     halo_->exchange_cross({f}, s, 3);
   else
     halo_->exchange({f}, s, 3);
@@ -557,7 +559,9 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
   }
   const std::vector<int> passes =
       cost_.empty() ? std::vector<int>((size_t)nsteps, 1) : plan_passes(nsteps, cost_);
-  for (const int K : passes) {
+  for (size_t pi = 0; pi < passes.size(); ++pi) {
+    const int K = passes[pi];
+    cross_pass_ = pi + 1 < passes.size();  // corners exact after the last pass
     double* Tin = parity_ ? T2_ : T_;
     double* Tout = parity_ ? T_ : T2_;
     if (K == 1 && !fast5()) {
@@ -571,6 +575,7 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
     ++passes_;
     parity_ ^= 1;
   }
+  cross_pass_ = false;
 }
 
 void DiffusionExecutor::build_graph(int64_t steps, int reps) {
