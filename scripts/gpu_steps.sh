@@ -94,6 +94,10 @@ for s in "$@"; do
     host4096_nocross) RMA_HALO_CROSS=0 step host4096_nocross 300 python bench/rccl_self_overhead.py \
              --n 4096 --K 1 --variants perf_hide --steps 400 --pattern opop \
              --out "$OUT/host4096_nocross.json" || exit 1 ;;
+    host4096_ch4|host4096_ch8|host4096_ch16) c=${s#host4096_ch}
+             NCCL_MIN_P2P_NCHANNELS=$c NCCL_MAX_P2P_NCHANNELS=$c step "$s" 300 python \
+             bench/rccl_self_overhead.py --n 4096 --K 1 --variants perf_hide --steps 400 --pattern opop \
+             --out "$OUT/$s.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
