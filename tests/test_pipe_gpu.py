@@ -157,9 +157,10 @@ G = 4096
 CANARY = -1.2345678901234567e300
 
 
-@pytest.mark.parametrize("kernel", ["pipe", "pipec"])
-@pytest.mark.parametrize("K,vec,nx", [(16, 4, 1024), (16, 2, 1026), (16, 4, 1027), (24, 4, 776),
-                                      (20, 2, 514), (5, 4, 300)])
+@pytest.mark.parametrize("kernel,K,vec,nx", [(k, *c) for k in ("pipe", "pipec") for c in (
+    (16, 4, 1024), (16, 2, 1026), (16, 4, 1027), (24, 4, 776), (20, 2, 514), (5, 4, 300))] + [
+    ("piper", 24, 4, 776), ("piper", 20, 2, 514), ("piper", 17, 4, 1027), ("piper", 10, 4, 1024),
+    ("piper", 14, 2, 1026)])
 def test_pipe_guard_bands(kernel, K, vec, nx):
     """No write outside the output rects or the arrays (GPU ASan is not
     available on the pool): canaries around every array, untouched cells
@@ -183,6 +184,18 @@ def test_pipe_guard_bands(kernel, K, vec, nx):
     mask = torch.ones((ny, nx), dtype=torch.bool, device=DEV)
     mask[K:ny - K, K:nx - K] = False
     assert torch.equal(out[mask], before[mask])
+
+
+def test_piper_tiny_tiles_and_short_chunks():
+    """piper (register factors, LDS-DMA staging three rows ahead) where the
+    prefetch runs past the last row, the tile is narrower than a strip, and
+    chunks are shorter than the pipeline: clamped rows/columns, bitwise."""
+    for ny, nx in ((9, 260), (70, 4), (41, 1028), (200, 64)):
+        T, iCp = rand((ny, nx), 51), rand((ny, nx), 52, 0.5, 1.0)
+        for K in (10, 17, 24):
+            for chunk in (1, 5, 64):
+                assert torch.equal(gpu_run(K, T, iCp, None, "piper", chunk=chunk),
+                                   cpu_ref(K, T, iCp, [ops.interior_rect(nx, ny)], "pipe"))
 
 
 def test_pipe_limits():
