@@ -48,9 +48,12 @@ bool throws(F&& f) {
 // field; one halo exchange executed from the plan on host memory (copy2d_cpu
 // for copies / packs / unpacks, per-pair FIFO queues matching sends and
 // receives in order, like RCCL). Afterwards every tile must equal its window
-// of the global field.
+// of the global field. cross: the order of HaloExchanger::exchange_cross
+// (packs of every dimension, ONE group with all sends and receives, unpacks):
+// every cell must match except corners (cells in two dimensions' halos).
 int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<int, 3> n,
-              std::array<int, 3> ol, std::array<int, 3> hw, int stagger_x, bool via_comm) {
+              std::array<int, 3> ol, std::array<int, 3> hw, int stagger_x, bool via_comm,
+              bool cross = false) {
   const int P = dims[0] * dims[1] * dims[2];
   CartTopology topo(P, dims, periods);
   std::array<int64_t, 3> ng;
@@ -124,7 +127,37 @@ int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<in
   };
   // dimension by dimension on every rank (the plans list the same dims)
   std::map<std::pair<int, int>, std::deque<std::vector<char>>> wire;
-  for (size_t k = 0; k < plans[0].dims.size(); ++k) {
+  if (cross) {
+    for (int r = 0; r < P; ++r) {
+      if (plans[r].dims.size() != plans[0].dims.size()) return 101;
+      for (const HaloDimPlan& dp : plans[r].dims)
+        for (const CopyBatch& b : batch_copies(dim_copies(dp, fields[r], slots[r], 0)))
+          copy2d_batch_cpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes);
+    }
+    for (int r = 0; r < P; ++r)  // the one group: every dimension's sends, then receives
+      for (const HaloDimPlan& dp : plans[r].dims)
+        for (const auto& m : dp.sends) {
+          const char* src = m.slot >= 0 ? reinterpret_cast<const char*>(bufs[r][m.slot].data())
+                                        : at(r, m.field, m.view);
+          wire[{r, m.peer}].emplace_back(src, src + m.bytes);
+        }
+    for (int r = 0; r < P; ++r)
+      for (const HaloDimPlan& dp : plans[r].dims)
+        for (const auto& m : dp.recvs) {
+          auto& q = wire[{m.peer, r}];
+          if (q.empty()) return 102;
+          if (q.front().size() != m.bytes) return 103;
+          char* dst = m.slot >= 0 ? reinterpret_cast<char*>(bufs[r][m.slot].data())
+                                  : at(r, m.field, m.view);
+          std::memcpy(dst, q.front().data(), m.bytes);
+          q.pop_front();
+        }
+    for (int r = 0; r < P; ++r)
+      for (const HaloDimPlan& dp : plans[r].dims)
+        for (const CopyBatch& b : batch_copies(dim_copies(dp, fields[r], slots[r], 1)))
+          copy2d_batch_cpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes);
+  }
+  for (size_t k = 0; !cross && k < plans[0].dims.size(); ++k) {
     for (int r = 0; r < P; ++r) {
       if (plans[r].dims.size() != plans[0].dims.size()) return 101;
       const HaloDimPlan& dp = plans[r].dims[k];
@@ -157,9 +190,20 @@ int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<in
   for (int r = 0; r < P; ++r)
     for (int f = 0; f < 2; ++f) {
       const auto& sz = tiles[r].size[f];
+      const auto nb = topo.neighbors(r);
       for (int64_t z = 0; z < sz[2]; ++z)
         for (int64_t y = 0; y < sz[1]; ++y)
           for (int64_t x = 0; x < sz[0]; ++x) {
+            if (cross) {  // corners: in the halo of two or more dimensions
+              const int64_t ix[3] = {x, y, z};
+              int nh = 0;
+              for (int d = 0; d < 3; ++d) {
+                const int64_t s = sz[d], h = hw[d], old = ol[d] + (s - n[d]);
+                if (!(s > 1 && old >= 2 * h && s >= old + h)) continue;
+                nh += (nb[d][0] >= 0 && ix[d] < h) || (nb[d][1] >= 0 && ix[d] >= s - h);
+              }
+              if (nh >= 2) continue;
+            }
             const double want = gval(f, gidx(r, f, 0, x), gidx(r, f, 1, y), gidx(r, f, 2, z));
             if (tiles[r].a[f][(z * sz[1] + y) * sz[0] + x] != want) {
               std::fprintf(stderr, "halo mismatch rank %d field %d at (%ld,%ld,%ld)\n", r, f,
@@ -424,6 +468,12 @@ int main() {
   EXPECT(halo_case({1, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, true) == 0);
   EXPECT(halo_case({2, 2, 1}, {1, 0, 0}, {6, 6, 1}, {2, 2, 2}, {1, 1, 1}, 1, true) == 0);  // minimal
   EXPECT(halo_case({2, 1, 2}, {0, 0, 1}, {8, 7, 6}, {2, 2, 2}, {1, 1, 1}, 0, false) == 0);  // 3D
+  // exchange_cross order (one group for all dimensions; corners not checked)
+  EXPECT(halo_case({2, 2, 1}, {0, 0, 0}, {12, 10, 1}, {2, 2, 2}, {1, 1, 1}, 1, false, true) == 0);
+  EXPECT(halo_case({2, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, false, true) == 0);
+  EXPECT(halo_case({1, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, true, true) == 0);
+  EXPECT(halo_case({2, 2, 1}, {1, 1, 0}, {6, 6, 1}, {2, 2, 2}, {1, 1, 1}, 1, true, true) == 0);
+  EXPECT(halo_case({4, 2, 1}, {1, 1, 0}, {9, 8, 1}, {2, 2, 2}, {1, 1, 1}, 0, false, true) == 0);
   {
     HaloField f;
     EXPECT(throws([&] { plan_exchange({f}, {{{1, 1}, {-1, -1}, {-1, -1}}}, 0, false, 7); }));
