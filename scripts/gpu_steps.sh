@@ -98,6 +98,12 @@ for s in "$@"; do
              NCCL_MIN_P2P_NCHANNELS=$c NCCL_MAX_P2P_NCHANNELS=$c step "$s" 300 python \
              bench/rccl_self_overhead.py --n 4096 --K 1 --variants perf_hide --steps 400 --pattern opop \
              --out "$OUT/$s.json" || exit 1 ;;
+    bench6000) step bench6000 400 python bench.py --steps 6000 --warmup 24 \
+             --json-out "$OUT/bench6000.json" || exit 1 ;;
+    pmc_bytes) prof pmc_bytes 300 --pmc FETCH_SIZE WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE \
+             --output-format csv -d "$R/$OUT/pmc_bytes" -o run -- python3 "$R/bench/pass_sweep.py" \
+             --n 101120 --rounds 1 --pipe 24 --kinds piper:24 --pipec "" \
+             --ldsdpp "" --old "" --alt "" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
