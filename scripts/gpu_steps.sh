@@ -100,8 +100,12 @@ for s in "$@"; do
              --out "$OUT/$s.json" || exit 1 ;;
     bench6000) step bench6000 400 python bench.py --steps 6000 --warmup 24 \
              --json-out "$OUT/bench6000.json" || exit 1 ;;
-    pmc_bytes) prof pmc_bytes 300 --pmc FETCH_SIZE WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE \
-             --output-format csv -d "$R/$OUT/pmc_bytes" -o run -- python3 "$R/bench/pass_sweep.py" \
+    pmc_bytes) prof pmc_fetch 300 --pmc FETCH_SIZE SQ_WAVES GRBM_GUI_ACTIVE \
+             --output-format csv -d "$R/$OUT/pmc_fetch" -o run -- python3 "$R/bench/pass_sweep.py" \
+             --n 101120 --rounds 1 --pipe 24 --kinds piper:24 --pipec "" \
+             --ldsdpp "" --old "" --alt "" && \
+             prof pmc_write 300 --pmc WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE \
+             --output-format csv -d "$R/$OUT/pmc_write" -o run -- python3 "$R/bench/pass_sweep.py" \
              --n 101120 --rounds 1 --pipe 24 --kinds piper:24 --pipec "" \
              --ldsdpp "" --old "" --alt "" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
