@@ -663,7 +663,7 @@ bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
 inline bool pipe_has_v5(int K, int S, int ar) {
   return ar == kArFast5 && S == 4 && K >= 16 && K <= 20;
 }
-// register-resident factors (stencil_pipe_r.hip): fast5, S = 4, K = 17..20
+// register-resident factors (stencil_pipe_r.hip): fast5, S = 4, K = 10..24
 bool dispatch_r(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe

@@ -1,12 +1,13 @@
 // Instantiations of the any-K pipelined kernel (stencil_pipe.h), unit r:
 // fast5 arithmetic with register-resident factor rows ("piper", arithmetic
 // kArFast5Reg): no LDS factor ring, one factor hand-off row per stage
-// boundary. Default stage split, K = 17..20 (5-level stages, 233 VGPRs at
-// K = 20): the executor's kernel for those depths (K=20 pass at 101120^2:
-// 68.07 vs 68.95 and 69.74 vs 71.21 ms, profiles/SUMMARY_r3.md). Where it does
-// not pay: K = 12 (equal), K = 16 (198 VGPRs: 2 waves per SIMD instead of 3,
-// 61.7 vs 56.4 ms), K = 21..24 (6-level stages need more than 256 VGPRs with
-// the two-row T prefetch; 89.3 vs 78.8 ms at K = 24 with 6 spilled).
+// boundary; stage 0 prefetches T and 1/Cp three rows ahead by LDS-DMA, which
+// keeps the prefetch out of the registers (K=24 234 VGPRs, K=20 201, K=16 161:
+// 3 waves per SIMD, K=12 123: 4). Default stage split, K = 10..24. The
+// executor's fast kernel from K = 14 (from K = 10 on tiles of >= 65536 rows):
+// per pass at 101120^2 K=10..24 -0.7..-7 % against the ring kernel (K=20
+// 68.69 vs 70.20 ms, K=24 79.03 vs 80.22); at 16384^2 K=10 / 12 slower
+// (+12 / +7 %). profiles/SUMMARY_r3.md section 8.
 #include "stencil_pipe.h"
 
 namespace rma {

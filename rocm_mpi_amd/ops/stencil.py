@@ -32,7 +32,8 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 #              csrc/kernels/stencil_pipe.h), "pipec" (10: the same pipeline with the
 #              canonical arithmetic, bitwise equal to K one-step updates), "piper"
 #              (12: "pipe" with the factor rows in registers instead of the LDS
-#              ring, K = 17..20, the executor's kernel at those depths).
+#              ring and an LDS-DMA prefetch, K = 10..24, the executor's fast
+#              kernel from K = 14; from K = 10 on tiles of >= 65536 rows).
 # LAB_KERNELS live in librma_lab.so (csrc/lab: superseded / experimental kernels kept as
 # test oracles and for sweeps), loaded on first use: K-step "march"/"lds"/"dpp" (0/1/2:
 # canonical variants of kernel 3), "fast" (4: reassociated, not bitwise), "fast5" (5: the
