@@ -108,6 +108,9 @@ for s in "$@"; do
              --output-format csv -d "$R/$OUT/pmc_write" -o run -- python3 "$R/bench/pass_sweep.py" \
              --n 101120 --rounds 1 --pipe 24 --kinds piper:24 --pipec "" \
              --ldsdpp "" --old "" --alt "" || exit 1 ;;
+    sweepc2) step sweepc2 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe "" \
+             --kinds piper:20:2560,piper:20:2816,piper:20,piper:20:3328,piper:20:3584,piper:24:2816,piper:24,piper:24:3328 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepc2.json" || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;
