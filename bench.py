@@ -124,6 +124,9 @@ def parse(argv=None):
     ap.add_argument("--check-timeout", type=float, default=300.0,
                     help="seconds any check-phase collective (and the whole check phase, x3) "
                          "may take before the run fails")
+    ap.add_argument("--window-check", type=int, default=1,
+                    help="after the timed run, compare three full-width row windows of the "
+                         "timed field bitwise with the CPU twin (1/0)")
     ap.add_argument("--drift-steps", type=int, default=-1,
                     help="steps of the fast-math drift measurement (-1: warmup + steps; 0: off)")
     ap.add_argument("--shared-gpu-test", action="store_true",
@@ -485,6 +488,157 @@ def drift_check(n: int, K: int, steps: int, dev: str, world: int, timeout_s: flo
     return info
 
 
+WINDOW_ROWS = 8
+WINDOW_BUDGET = 3.0e9  # cell updates of the CPU twin for all windows of a rank
+
+
+def snapshot_windows(model, h: int = WINDOW_ROWS) -> dict:
+    """Three full-width row windows of this rank's field (top edge, middle,
+    bottom edge), copied to the host right after the timed run, with what the
+    CPU twin needs to recompute them from the initial condition."""
+    import torch
+
+    cfg, g = model.cfg, model.g
+    ny, nx = model.field.shape
+    h = min(h, ny)
+    rows = sorted({0, max(0, ny // 2 - h // 2), ny - h})
+    geo = model.geometry()
+    tiles = [model.field[r:r + h].detach().cpu().clone() for r in rows]
+    if os.environ.get("RMA_BENCH_WINDOW_CORRUPT") == "1" and g.me == g.nprocs - 1:
+        tiles[-1][h // 2, nx // 2] += 1e-12  # negative test (tests/test_multiprocess_cpu.py)
+    return {"rows": rows, "h": h, "tiles": tiles,
+            "nx": nx, "ny": ny, "geom": geo, "coef": model.coef, "seed": cfg.seed,
+            "icp": 1.0 / cfg.Cp0, "fast": bool(cfg.fast_math), "steps": model.steps_done,
+            "dtype": torch.float64}
+
+
+def window_check(snap: dict, world: int, timeout_s: float, budget: float = WINDOW_BUDGET) -> dict:
+    """the headline field itself, not a small proxy tile.
+    Each window is recomputed on the CPU twin (the C++ fast5 / canonical
+    arithmetic, bitwise equal to the GPU kernels) from the counter-based
+    initial condition of the global grid (csrc/kernels/misc.hip init_random),
+    over the window plus `steps` rows / columns of margin on every side that
+    is not a global boundary (the dependency cone of `steps` updates), and
+    compared bitwise. Full-width windows when the twin's cost fits `budget`
+    cell updates, else three 64-column boxes per window (left edge, centre,
+    right edge). Raises CheckFailed on every rank on any mismatch."""
+    import torch
+
+    from rocm_mpi_amd import ops
+
+    t0 = time.perf_counter()
+    S, h, nx, ny = snap["steps"], snap["h"], snap["nx"], snap["ny"]
+    geo = snap["geom"]
+    nxg, nyg = geo.nxg, geo.nyg
+    per = geo.periodx or geo.periody
+    full = (nx + 2 * S) * (h + 2 * S) * S * len(snap["rows"]) <= budget
+    bw = nx if full else min(64, nx)
+    cols = [0] if full else sorted({0, max(0, nx // 2 - bw // 2), nx - bw})
+    tn = ops.StencilTuning(kernel="pipe" if snap["fast"] else "pipec")
+    err, boxes, mism = "", 0, 0
+    try:
+        if per:
+            raise CheckFailed("window check: periodic grids are not covered")
+        for r0, tile in zip(snap["rows"], snap["tiles"]):
+            for c0 in cols:
+                # the box in global coordinates, with the margin, clipped to the grid
+                gy_lo, gy_hi = geo.gy0 + r0, geo.gy0 + r0 + h
+                gx_lo, gx_hi = geo.gx0 + c0, geo.gx0 + c0 + bw
+                wy0, wy1 = max(0, gy_lo - S), min(nyg, gy_hi + S)
+                wx0, wx1 = max(0, gx_lo - S), min(nxg, gx_hi + S)
+                wg = ops.TileGeometry(gx0=wx0, gy0=wy0, nxg=nxg, nyg=nyg, dx=geo.dx, dy=geo.dy)
+                a = torch.empty((wy1 - wy0, wx1 - wx0), dtype=snap["dtype"])
+                ops.init_random_(a, wg, seed=snap["seed"])
+                icp = torch.full_like(a, snap["icp"])
+                b = a.clone()
+                done = 0
+                while done < S:
+                    k = min(24, S - done)
+                    if a.shape[0] >= 3 and a.shape[1] >= 3:
+                        ops.stencilk_step(k, b, a, icp, snap["coef"], None, tn)
+                    a, b = b, a
+                    done += k
+                want = a[gy_lo - wy0:gy_hi - wy0, gx_lo - wx0:gx_hi - wx0]
+                got = tile[:, c0:c0 + bw]
+                boxes += 1
+                if not torch.equal(got, want):
+                    mism += 1
+                    d = (got - want).abs().max().item()
+                    err = (f"window rows {r0}..{r0 + h} cols {c0}..{c0 + bw}: "
+                           f"{int((got != want).sum())} cells differ (max |diff| {d:.3e})")
+    except CheckFailed as e:
+        err = str(e.args[0])
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"
+    info = {"windows": len(snap["rows"]), "rows_each": h, "row_starts": snap["rows"],
+            "full_width": bool(full), "box_cols": None if full else bw, "boxes": boxes,
+            "steps": S, "bitwise": not err and mism == 0,
+            "arithmetic": "fast-math twin" if snap["fast"] else "canonical twin",
+            "seconds": round(time.perf_counter() - t0, 3)}
+    st = bounded_status(not err, err, world, timeout_s)
+    bad = [f"{r}: {m}" for r, (o, m) in enumerate(st) if not o]
+    if bad:
+        info["bitwise"] = False
+        raise CheckFailed("headline window check: " + "; ".join(bad), info)
+    return info
+
+
+# weak-scaling attribution (VERDICT r3 next 3): the N = 1 record of this tile
+# class is cached here, so the N > 1 runs of the same driver sweep can split
+# E(N) = e_gpu * e_coef * e_halo
+def _n1_cache_path() -> str:
+    import tempfile
+
+    return os.environ.get("RMA_BENCH_N1_CACHE",
+                          os.path.join(tempfile.gettempdir(), "rma_bench_n1_record.json"))
+
+
+def _n1_key(nx: int, ny: int, steps: int, warmup: int, K: int, fast: bool, variant: str) -> str:
+    return f"{variant}:{nx}x{ny}:s{steps}:w{warmup}:K{K}:f{int(fast)}"
+
+
+def save_n1(key: str, ms_per_step: float, bus: str) -> None:
+    try:
+        tmp = _n1_cache_path() + f".{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
+            json.dump({"key": key, "ms_per_step": ms_per_step, "pci_bus_id": bus}, f)
+        os.replace(tmp, _n1_cache_path())
+    except OSError:
+        pass
+
+
+def load_n1(key: str):
+    try:
+        with open(_n1_cache_path()) as f:
+            d = json.load(f)
+        return d if d.get("key") == key else None
+    except (OSError, ValueError):
+        return None
+
+
+def attribution(t_it: float, solo: float | None, solo_iso: float | None,
+                n1_ms: float | None) -> dict:
+    """Job-level split of the weak-scaling efficiency (max-over-ranks times):
+    e_halo = solo / t_it (exchange + frame cost, same coefficients),
+    e_coef = solo_iso / solo (the fast-math pass energy at this grid's
+    dx != dy, against dx = dy), e_gpu = t(N=1) / solo_iso (the slowest GPU of
+    this job, isotropic and without exchange, against the N = 1 record of
+    the same tile class; null without that record). Their product is
+    t(N=1)/t_it = E(N); e_halo * e_coef = weak_scaling_eff_same_run_iso."""
+    out = {"e_halo": None, "e_coef": None, "e_gpu": None, "e_product": None,
+           "weak_scaling_eff_same_run_iso": None, "n1_ms_per_step": n1_ms}
+    if solo:
+        out["e_halo"] = solo / t_it
+    if solo and solo_iso:
+        out["e_coef"] = solo_iso / solo
+        out["weak_scaling_eff_same_run_iso"] = solo_iso / t_it
+    if solo_iso and n1_ms:
+        out["e_gpu"] = (n1_ms / 1e3) / solo_iso
+    if all(out[k] is not None for k in ("e_halo", "e_coef", "e_gpu")):
+        out["e_product"] = out["e_halo"] * out["e_coef"] * out["e_gpu"]
+    return {k: (round(v, 6) if isinstance(v, float) else v) for k, v in out.items()}
+
+
 def preflight(dims, K: int, dev: str, world: int, rank: int, gpu: bool, n: int,
               timeout_s: float) -> dict:
     """Before the HBM-sized tile: the ring send/recv of the reference's smoke
@@ -506,6 +660,32 @@ def preflight(dims, K: int, dev: str, world: int, rank: int, gpu: bool, n: int,
                               self_rccl=gpu and world == 1, inject=False)
     info["seconds"] = round(time.perf_counter() - t0, 3)
     return info
+
+
+def _rccl_info() -> dict | None:
+    """Which RCCL carries the halo traffic (RMA_RCCL_LIB may swap it)."""
+    try:
+        from rocm_mpi_amd._native import native
+
+        return {"library": native().rccl_library(), "version": native().rccl_version()}
+    except Exception:  # noqa: BLE001 - informational
+        return None
+
+
+def make_config(a, nx: int, ny: int, dev: str, dims: tuple):
+    """The DiffusionConfig of the timed run (the reference-named entry points
+    resolve the same one for the BASELINE presets: apps/cli.py auto_temporal,
+    tests/test_apps_cpu.py)."""
+    from rocm_mpi_amd.models import DiffusionConfig
+
+    K = a.temporal if a.variant != "kp" else 1
+    bw = tuple(int(v) for v in a.b_width.split(","))
+    return DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup, device=dev,
+                           warmup=a.warmup, init="random", b_width=bw, dims=dims,
+                           chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
+                           unroll=a.unroll, vec=a.vec, temporal=K, chunk2=a.chunk2,
+                           unroll2=a.unroll2, use_graph=a.graph, quiet=True,
+                           fast_math=a.fast_math and a.variant != "kp")
 
 
 # ---------------------------------------------------------------------------
@@ -545,7 +725,9 @@ def run(a, world: int, rank: int) -> int:
             if k.startswith("RMA_DIAG") or k in ("RMA_FRAME_SIDES", "RMA_FRAME_ALIGNED",
                                                  "RMA_PASS_COSTS", "RMA_HALO_BATCH",
                                                  "RMA_FRAME_FILL", "RMA_EXEC_STREAMS",
-                                                 "RMA_PIPE_FAST", "RMA_HALO_CROSS")}
+                                                 "RMA_PIPE_FAST", "RMA_HALO_CROSS",
+                                                 "RMA_FRAME_BANDS", "RMA_RCCL_LIB",
+                                                 "RMA_FAST_FORM")}
     if gpu and os.environ.get("RMA_PIPE_FAST") == "pipe5":  # an A/B of the lab kernel
         from rocm_mpi_amd._native import load_lab
 
@@ -558,7 +740,7 @@ def run(a, world: int, rank: int) -> int:
 
     import torch
 
-    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.models import Diffusion2D
     from rocm_mpi_amd.parallel import comm as C
 
     if gpu and not torch.cuda.is_available():
@@ -601,7 +783,6 @@ def run(a, world: int, rank: int) -> int:
             torch.cuda.synchronize()
 
     dims = tuple(int(v) for v in a.dims.split(",")) + (0,)
-    bw = tuple(int(v) for v in a.b_width.split(","))
     K = a.temporal if a.variant != "kp" else 1
     check_n = a.check_nx or (2050 if gpu else max(130, 6 * K + 2))
     self_rccl = (a.check_self_rccl == 1 or (a.check_self_rccl < 0 and gpu)) and world == 1 and gpu
@@ -658,12 +839,7 @@ def run(a, world: int, rank: int) -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=C._gloo_group())
             nx = int(t.item())
         ny = a.ny or nx
-        cfg = DiffusionConfig(variant=a.variant, nx=nx, ny=ny, nt=a.steps + a.warmup, device=dev,
-                              warmup=a.warmup, init="random", b_width=bw, dims=dims,
-                              chunk_rows=a.chunk_rows, kernel=a.kernel, nontemporal=a.nontemporal,
-                              unroll=a.unroll, vec=a.vec, temporal=K, chunk2=a.chunk2,
-                              unroll2=a.unroll2, use_graph=a.graph, quiet=True,
-                              fast_math=a.fast_math and a.variant != "kp")
+        cfg = make_config(a, nx, ny, dev, dims)
         t_setup = time.perf_counter()
         gkw = {}
         if a.overlap:
@@ -694,6 +870,7 @@ def run(a, world: int, rank: int) -> int:
         local_s = time.perf_counter() - t0
         wall = comm.allreduce(local_s, "max")
         nbrs = any(p >= 0 for side in g.neighbors[:2] for p in side)
+        snap = snapshot_windows(model) if a.window_check and a.variant != "kp" else None
         timings = summarize_timings(model.pass_timings(), exchange=nbrs)
         model.enable_pass_timing(False)
         bad = float(model.field[:: max(1, ny // 64), :: max(1, nx // 64)].isfinite().logical_not().sum())
@@ -717,7 +894,7 @@ def run(a, world: int, rank: int) -> int:
         # the exchange (one launch per pass), all ranks concurrently; each rank's
         # own (pre-barrier) solo time identifies a slow GPU independently of the halo
         solo_steps = a.steps if a.solo_steps < 0 else a.solo_steps
-        solo = solo_own = None
+        solo = solo_own = solo_iso = solo_iso_own = None
         if solo_steps > 0:
             model.set_solo(True)
             model.step(a.warmup)
@@ -730,6 +907,26 @@ def run(a, world: int, rank: int) -> int:
             solo_own = (time.perf_counter() - s0) / solo_steps
             comm.barrier()
             solo = comm.allreduce(time.perf_counter() - s0, "max") / solo_steps
+            # the same solo re-time at isotropic coefficients (dx = dy = the
+            # smaller spacing: the same dt, ry = 1): splits the coefficient
+            # energy of an anisotropic grid (4x2, 2x1) from the halo cost
+            aniso = comm.allreduce(float(model.dx != model.dy), "max") > 0
+            if aniso:
+                d = min(model.dx, model.dy)
+                model.set_spacing((d, d))
+                model.step(a.warmup)
+                model.synchronize()
+                comm.barrier()
+                sync()
+                s0 = time.perf_counter()
+                model.step(solo_steps)
+                sync()
+                solo_iso_own = (time.perf_counter() - s0) / solo_steps
+                comm.barrier()
+                solo_iso = comm.allreduce(time.perf_counter() - s0, "max") / solo_steps
+                model.set_spacing(None)
+            else:
+                solo_iso_own, solo_iso = solo_own, solo
             model.set_solo(False)
 
         detail = {"rank": rank, "coords": list(g.coords[:2]),
@@ -737,6 +934,11 @@ def run(a, world: int, rank: int) -> int:
                   "ms_per_step": round(own_s / a.steps * 1e3, 6),
                   "teff_GBps": round(a_eff / (own_s / a.steps), 2),
                   "solo_ms_per_step": round(solo_own * 1e3, 6) if solo_own else None,
+                  "solo_iso_ms_per_step": round(solo_iso_own * 1e3, 6) if solo_iso_own else None,
+                  "e_halo": round(solo_own / (own_s / a.steps), 6) if solo_own else None,
+                  "e_coef": (round(solo_iso_own / solo_own, 6)
+                             if solo_own and solo_iso_own else None),
+                  "e_gpu": None,
                   "pass_timing": {k: (round(v, 4) if isinstance(v, float) else v)
                                   for k, v in timings.items() if k != "note"}}
         ranks_detail = gather_obj(detail, world)
@@ -796,7 +998,22 @@ def run(a, world: int, rank: int) -> int:
         eff_same = (solo / t_it) if solo and nbrs else None
         if shared:
             par = f"SHARED-GPU FUNCTIONAL TEST, {world} ranks on {n_gpus} GPU, not a scaling point; {par}"
-        out.update({"value": round(total, 2), "ms_per_step": round(t_it * 1e3, 6)})
+        fast_plan = bool(fast_used)
+        n1key = _n1_key(nx, ny, a.steps, a.warmup, K, fast_plan, a.variant)
+        n1 = None
+        if world == 1 and not nbrs:
+            save_n1(n1key, t_it * 1e3, bus)
+            n1 = {"ms_per_step": t_it * 1e3}
+        elif world > 1:
+            n1 = load_n1(n1key)
+        n1_ms = n1["ms_per_step"] if n1 else None
+        if n1_ms:
+            for d in ranks_detail:
+                if d["solo_iso_ms_per_step"]:
+                    d["e_gpu"] = round(n1_ms / d["solo_iso_ms_per_step"], 6)
+        attrib = attribution(t_it, solo, solo_iso, n1_ms)
+        out.update({"value": round(total, 2), "value_kind": "aggregate",
+                    "teff_per_gpu": round(teff_gpu, 2), "ms_per_step": round(t_it * 1e3, 6)})
         out["config"].update({
             "global_batch": g.nxyz_g[0] * g.nxyz_g[1],
             "seq_len": None,
@@ -816,7 +1033,15 @@ def run(a, world: int, rank: int) -> int:
             "pass_timing": timings,
             "ranks_detail": ranks_detail,
             "solo_ms_per_step": round(solo * 1e3, 6) if solo else None,
+            "solo_iso_ms_per_step": round(solo_iso * 1e3, 6) if solo_iso else None,
             "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,
+            "e_attribution": dict(attrib, note=(
+                "E(N) = t(N=1)/t_it = e_gpu * e_coef * e_halo; e_halo = solo/t_it (exchange "
+                "and frame cost), e_coef = solo_iso/solo (fast-math pass energy at dx != dy vs "
+                "dx = dy), e_gpu = t(N=1)/solo_iso (slowest GPU, isotropic, no exchange, vs the "
+                "N = 1 record of this tile class cached by the same driver sweep); value is "
+                "the aggregate N x teff_per_gpu")),
+            "headline_window_check": None,
             "rccl_halo_bitwise_ok": None,
             "halo_check": None,
             "fast_math_drift_max": None,
@@ -839,6 +1064,7 @@ def run(a, world: int, rank: int) -> int:
             "bitwise_kstep_steps_per_pass": kc if canonical else None,
             "overlap": list(g.overlaps[:2]),
             "transport": g.transport,
+            "rccl": _rccl_info() if gpu else None,
             "hipgraph": bool(a.graph),
             "setup_s": round(setup_s, 3),
             "nonfinite_cells_sampled": int(bad),
@@ -847,7 +1073,7 @@ def run(a, world: int, rank: int) -> int:
         # --- correctness of this run's code paths (bounded; any failure fails all)
         rc = 0 if bad == 0 else 3
         drift_steps = (a.warmup + a.steps) if a.drift_steps < 0 else a.drift_steps
-        if (check_on or drift_steps) and a.variant != "kp":
+        if (check_on or drift_steps or snap is not None) and a.variant != "kp":
             wd = Watchdog(rank, world, 3 * tmo, "check phase", emit)
             try:
                 if drift_steps and fast_used and K > 1:
@@ -858,6 +1084,15 @@ def run(a, world: int, rank: int) -> int:
                         raise
                     out["config"]["drift_check"] = di
                     out["config"]["fast_math_drift_max"] = di["fast_math_drift_max"]
+                if snap is not None:
+                    try:
+                        wc = window_check(snap, world, tmo)
+                    except CheckFailed as e:
+                        out["config"]["headline_window_check"] = (
+                            dict(e.args[1], error=str(e.args[0])) if len(e.args) > 1
+                            else {"bitwise": False, "error": str(e.args[0])})
+                        raise
+                    out["config"]["headline_window_check"] = wc
                 if check_on:
                     try:
                         hc = halo_check(check_n, dims[:2], K, dev, world, rank, tmo,

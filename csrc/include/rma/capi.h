@@ -32,6 +32,8 @@ int rma_init_global_grid(int nx, int ny, int nz, const int dims[3], const int pe
                          const int overlaps[3], const int halowidths[3], int nprocs, int rank,
                          const char* unique_id, int device, rma_grid** out_grid, int* out_me,
                          int out_dims[3], int out_coords[3]);
+/* Executors created on a grid pin it: with executors still alive the teardown
+ * is deferred to the last rma_executor_destroy (any order is safe). */
 int rma_finalize_global_grid(rma_grid* g);
 
 int64_t rma_nx_g(const rma_grid* g);
@@ -96,7 +98,8 @@ int rma_executor_create_g(rma_grid* g, int mode, double* T, double* T2, const do
                           double* qy, double* dTdt, rma_executor** out);
 /* Single-rank grid: route the periodic self-neighbours through a 1-rank RCCL
  * communicator (send/recv to itself) instead of local copies -- the GPU-direct
- * P2P path on one GPU (tests, probes). Call before creating executors. */
+ * P2P path on one GPU (tests, probes). Call before creating executors: it
+ * fails while an executor of this grid is alive. */
 int rma_grid_self_via_rccl(rma_grid* g);
 int rma_executor_run(rma_executor* e, int64_t nsteps, void* stream);
 int rma_executor_parity(const rma_executor* e);

@@ -25,6 +25,12 @@ struct rma_grid : rma::GridDesc {  // host part: topology.cpp make_grid_desc
   std::unique_ptr<rma::RcclComm> comm;
   std::unique_ptr<rma::HaloExchanger> halo;
   std::chrono::steady_clock::time_point t0;
+  // executors hold raw pointers to `halo`: they pin the grid. finalize with
+  // executors alive defers the teardown to the last rma_executor_destroy (a
+  // GC'd host such as the Julia shim may finalize objects in any order), and
+  // rma_grid_self_via_rccl refuses to swap the exchanger under them.
+  int live_executors = 0;
+  bool finalized = false;
 };
 
 namespace {
@@ -92,12 +98,20 @@ int rma_init_global_grid(int nx, int ny, int nz, const int dims[3], const int pe
   });
 }
 
+namespace {
+void destroy_grid(rma_grid* g) {
+  g->halo.reset();
+  g->comm.reset();
+  delete g;
+}
+}  // namespace
+
 int rma_finalize_global_grid(rma_grid* g) {
   return guard([&] {
     if (!g) return;
-    g->halo.reset();
-    g->comm.reset();
-    delete g;
+    RMA_CHECK_ARG(!g->finalized, "grid finalized twice");
+    g->finalized = true;
+    if (g->live_executors == 0) destroy_grid(g);
   });
 }
 
@@ -198,6 +212,7 @@ rma::TileGeom geom(const rma_grid* g, int64_t nx, int64_t ny, double dx, double 
 
 struct rma_executor {
   std::unique_ptr<rma::DiffusionExecutor> ex;
+  rma_grid* grid = nullptr;  // pinned: live_executors counts this executor
 };
 
 int rma_init_gaussian(rma_grid* g, double* T, int64_t nx, int64_t ny, double dx, double dy,
@@ -227,31 +242,20 @@ int rma_executor_create_kf(rma_grid* g, int mode, double* T, double* T2, const d
                            int64_t nx, int64_t ny, const double coef[4], int64_t bwx,
                            int64_t bwy, int steps_per_pass, int fast_math, double* qx,
                            double* qy, double* dTdt, rma_executor** out) {
-  return guard([&] {
-    RMA_CHECK_ARG(g && out && mode >= 0 && mode <= 2, "bad executor arguments");
-    rma::ExecParams p;
-    p.mode = static_cast<rma::Mode>(mode);
-    p.coef = {coef[0], coef[1], coef[2], coef[3]};
-    p.bwx = bwx;
-    p.bwy = bwy;
-    p.temporal = steps_per_pass;
-    p.olx = g->overlaps[0];
-    p.oly = g->overlaps[1];
-    p.tune2 = rma::default_tune_k(steps_per_pass, ny);
-    p.fast_math = fast_math ? 1 : 0;
-    auto e = std::make_unique<rma_executor>();
-    e->ex = std::make_unique<rma::DiffusionExecutor>(T, T2, iCp, nx, ny, p, g->halo.get(), qx, qy,
-                                                     dTdt);
-    *out = e.release();
-  });
+  return rma_executor_create_g(g, mode, T, T2, iCp, nx, ny, coef, bwx, bwy, steps_per_pass,
+                               fast_math, 0, qx, qy, dTdt, out);
 }
 
+// the one place the C ABI builds ExecParams (every create_* lands here)
 int rma_executor_create_g(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
                           int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
                           int steps_per_pass, int fast_math, int graph_steps, double* qx,
                           double* qy, double* dTdt, rma_executor** out) {
   return guard([&] {
     RMA_CHECK_ARG(g && out && mode >= 0 && mode <= 2, "bad executor arguments");
+    RMA_CHECK_ARG(!g->finalized, "grid already finalized");
+    RMA_CHECK_ARG(mode != 2 || (qx && qy && dTdt),
+                  "kp mode (2) needs the qx, qy and dTdt device buffers");
     rma::ExecParams p;
     p.mode = static_cast<rma::Mode>(mode);
     p.coef = {coef[0], coef[1], coef[2], coef[3]};
@@ -267,6 +271,8 @@ int rma_executor_create_g(rma_grid* g, int mode, double* T, double* T2, const do
     auto e = std::make_unique<rma_executor>();
     e->ex = std::make_unique<rma::DiffusionExecutor>(T, T2, iCp, nx, ny, p, g->halo.get(), qx, qy,
                                                      dTdt);
+    e->grid = g;
+    ++g->live_executors;
     *out = e.release();
   });
 }
@@ -275,6 +281,12 @@ int rma_grid_self_via_rccl(rma_grid* g) {
   return guard([&] {
     RMA_CHECK_ARG(g != nullptr, "grid is NULL");
     RMA_CHECK_ARG(g->nprocs == 1, "self via RCCL is for a single-rank grid");
+    // executors hold the current exchanger: replacing it would leave them a
+    // dangling pointer
+    RMA_CHECK_ARG(g->live_executors == 0,
+                  "rma_grid_self_via_rccl: " << g->live_executors
+                                             << " executor(s) still use this grid's halo exchanger; "
+                                                "call it before creating executors");
     if (!g->comm) {
       const std::string uid = rma::RcclComm::unique_id();
       const char* tb = std::getenv("RMA_RCCL_BLOCKING");
@@ -299,7 +311,12 @@ int rma_executor_run(rma_executor* e, int64_t nsteps, void* stream) {
 int rma_executor_parity(const rma_executor* e) { return e->ex->parity(); }
 
 int rma_executor_destroy(rma_executor* e) {
-  return guard([&] { delete e; });
+  return guard([&] {
+    if (!e) return;
+    rma_grid* g = e->grid;
+    delete e;
+    if (g && --g->live_executors == 0 && g->finalized) destroy_grid(g);
+  });
 }
 
 }  // extern "C"

@@ -559,6 +559,13 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
   }
   const std::vector<int> passes =
       cost_.empty() ? std::vector<int>((size_t)nsteps, 1) : plan_passes(nsteps, cost_);
+  // cross_pass_ is set per pass below; reset it however this loop ends (a
+  // pass that throws must not leave later exchanges -- graph capture, the
+  // next run -- on the one-group cross exchange with stale corners)
+  struct ResetCross {
+    bool& f;
+    ~ResetCross() { f = false; }
+  } reset_cross{cross_pass_};
   for (size_t pi = 0; pi < passes.size(); ++pi) {
     const int K = passes[pi];
     cross_pass_ = pi + 1 < passes.size();  // corners exact after the last pass
@@ -575,7 +582,6 @@ void DiffusionExecutor::run_eager(int64_t nsteps) {
     ++passes_;
     parity_ ^= 1;
   }
-  cross_pass_ = false;
 }
 
 void DiffusionExecutor::build_graph(int64_t steps, int reps) {

@@ -105,21 +105,41 @@ function toc(; stream::Ptr{Cvoid}=C_NULL)
 end
 
 # Native executor (mode 0 perf, 1 perf_hide, 2 kp; coef = (-lam, 1/dx, 1/dy, dt)).
+# The struct keeps every array the native executor reads or writes (T, T2,
+# 1/Cp and the kp buffers) referenced for as long as it lives, so the GC cannot
+# free one under a running executor (VERDICT r3: iCp was not kept).
 mutable struct DiffusionExecutor
     ptr::Ptr{Cvoid}
     T::Any
     T2::Any
+    iCp::Any
+    qx::Any
+    qy::Any
+    dTdt::Any
 end
+
+devptr(a) = a === nothing ? C_NULL : reinterpret(Ptr{Cvoid}, pointer(a))
 
 # steps_per_pass = K (1..24): at most K steps per kernel pass; run! plans the
 # passes (csrc/runtime/plan.cpp). fast_math=true: every pass uses the
 # 5-point-sum arithmetic (rounding-level difference from the canonical update,
 # bitwise equal to its C++ CPU twin). graph_steps > 0: replay steps from a
 # hipGraph of that many steps (rma_executor_create_g; needs a capturable halo
-# transport).
+# transport). mode=2 (kp, the three kernels of diffusion_2D_kp.jl:88-91) needs
+# qx, qy and dTdt: device arrays of size(T) (T-indexed flux / residual buffers,
+# csrc/kernels/kp.hip); T2 is unused there and may be `nothing`.
 function DiffusionExecutor(T, T2, iCp, coef::NTuple{4,Float64}; mode::Integer=1,
                            steps_per_pass::Integer=1, b_width=(1, 1), fast_math::Bool=false,
-                           graph_steps::Integer=0)
+                           graph_steps::Integer=0, qx=nothing, qy=nothing, dTdt=nothing)
+    if mode == 2
+        (qx === nothing || qy === nothing || dTdt === nothing) &&
+            error("DiffusionExecutor: kp mode (2) needs qx, qy and dTdt device arrays of size(T)")
+        for (name, a) in (("qx", qx), ("qy", qy), ("dTdt", dTdt))
+            size(a) == size(T) || error("DiffusionExecutor: $name must have size(T) = $(size(T)), got $(size(a))")
+        end
+    else
+        T2 === nothing && error("DiffusionExecutor: modes 0/1 need T2")
+    end
     out = Ref{Ptr{Cvoid}}(C_NULL)
     c = collect(coef)
     nx, ny = size(T, 1), size(T, 2)
@@ -127,10 +147,12 @@ function DiffusionExecutor(T, T2, iCp, coef::NTuple{4,Float64}; mode::Integer=1,
                 (Ptr{Cvoid}, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Ptr{Float64},
                  Int64, Int64, Cint, Cint, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid},
                  Ptr{Ptr{Cvoid}}),
-                GRID[], mode, pointer(T), pointer(T2), pointer(iCp), nx, ny, c, b_width[1],
-                b_width[2], steps_per_pass, Cint(fast_math), Cint(graph_steps), C_NULL, C_NULL,
-                C_NULL, out))
-    ex = DiffusionExecutor(out[], T, T2)
+                GRID[], mode, devptr(T), devptr(T2), devptr(iCp), nx, ny, c, b_width[1],
+                b_width[2], steps_per_pass, Cint(fast_math), Cint(graph_steps), devptr(qx),
+                devptr(qy), devptr(dTdt), out))
+    ex = DiffusionExecutor(out[], T, T2, iCp, qx, qy, dTdt)
+    # the native grid is pinned by its executors: finalize_global_grid before
+    # this finalizer runs is safe (the teardown waits for the last destroy)
     finalizer(e -> ccall(sym(:rma_executor_destroy), Cint, (Ptr{Cvoid},), e.ptr), ex)
     return ex
 end
@@ -139,6 +161,6 @@ run!(ex::DiffusionExecutor, n::Integer; stream::Ptr{Cvoid}=C_NULL) =
     check(ccall(sym(:rma_executor_run), Cint, (Ptr{Cvoid}, Int64, Ptr{Cvoid}), ex.ptr, n, stream))
 
 current_field(ex::DiffusionExecutor) =
-    ccall(sym(:rma_executor_parity), Cint, (Ptr{Cvoid},), ex.ptr) == 0 ? ex.T : ex.T2
+    ex.T2 === nothing || ccall(sym(:rma_executor_parity), Cint, (Ptr{Cvoid},), ex.ptr) == 0 ? ex.T : ex.T2
 
 end # module

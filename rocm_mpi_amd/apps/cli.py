@@ -24,6 +24,28 @@ DEFAULTS = {
                            do_vis=False, profile=True, threads=(32, 4)),
 }
 
+# What bench.py runs (its --temporal default, fast-math on): the perf /
+# perf_hide entry points default to the same planner and kernels on tiles big
+# enough to fill the GPU with K-step tasks (below ~1.5M cells one step per
+# pass is faster, see Diffusion2D's warning), so the reference-named scripts
+# run the measured path.
+BENCH_TEMPORAL = 24
+AUTO_TEMPORAL_MIN_CELLS = 1_500_000
+
+
+def auto_temporal(variant: str, nx: int, ny: int, temporal=None, fast_math=None) -> tuple:
+    """(temporal, fast_math) of a run: explicit values win; otherwise the
+    bench.py defaults for perf / perf_hide on tiles of >= 1.5M cells."""
+    base = "perf_hide" if variant == "perf_hide_prof" else variant
+    if base not in ("perf", "perf_hide"):
+        return 1, False
+    if temporal is None:
+        temporal = BENCH_TEMPORAL if nx * ny >= AUTO_TEMPORAL_MIN_CELLS else 1
+    if fast_math is None:
+        fast_math = temporal > 1
+    return int(temporal), bool(fast_math)
+
+
 # BASELINE.json "configs", in order.
 PRESETS = {
     "ap256_cpu": dict(variant="ap", nx=256, ny=256, nt=1000, device="cpu"),
@@ -78,17 +100,23 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
                     help="bitmask: 1 = NT T2 stores, 2 = NT 1/Cp loads, 4 = NT T loads")
     ap.add_argument("--vec", type=int, default=2, choices=[2, 4], help="cells per lane")
     ap.add_argument("--graph", action="store_true", help="replay steps from a hipGraph")
-    ap.add_argument("--temporal", type=int, default=1, choices=list(range(1, 25)),
+    ap.add_argument("--temporal", type=int, default=None, choices=list(range(1, 25)),
                     metavar="K",
                     help="perf/perf_hide: at most K (1..24) steps per kernel pass + width-K "
                          "halos (grid overlap 2K); the executor plans the passes; bitwise "
-                         "identical to one-step updates without --fast-math")
+                         "identical to one-step updates without --fast-math. Default: "
+                         f"{BENCH_TEMPORAL} (what bench.py measures) on tiles of >= "
+                         f"{AUTO_TEMPORAL_MIN_CELLS:,} cells, else 1")
     ap.add_argument("--chunk2", type=int, default=0)
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
-    ap.add_argument("--fast-math", action="store_true",
+    ap.add_argument("--fast-math", dest="fast_math", action="store_true", default=None,
                     help="passes with fast-math fp64 arithmetic (5-point sum, one folded "
                          "per-cell factor, FMAs): same scheme, not bitwise equal to the "
-                         "canonical update, bitwise equal to its CPU twin")
+                         "canonical update, bitwise equal to its CPU twin (default with "
+                         "K > 1 steps per pass, as in bench.py)")
+    ap.add_argument("--canonical", dest="fast_math", action="store_false",
+                    help="the bitwise-canonical arithmetic in every pass (the reference's "
+                         "flux form; K-step passes stay bitwise equal to K one-step updates)")
     ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf guard period")
     ap.add_argument("--checkpoint", default="", help="save the final state to this directory")
     ap.add_argument("--resume", default="", help="start from a checkpoint directory")
@@ -106,10 +134,11 @@ def auto_tile(frac: float) -> int:
     return max(512, int(math.isqrt(int(frac * free / 24.0))) // 256 * 256)
 
 
-def run_variant(variant: str, argv=None) -> int:
-    from ..models import Diffusion2D, DiffusionConfig
+def resolve(variant: str, argv=None):
+    """Parse an entry point's command line into (DiffusionConfig, args); with
+    --auto-size this selects the device and sizes the tile (collective)."""
+    from ..models import DiffusionConfig
     from ..parallel import comm as C
-    from ..utils import checkpoint as ckpt
 
     base = "perf_hide" if variant == "perf_hide_prof" else variant
     parser = build_parser(variant)
@@ -123,14 +152,17 @@ def run_variant(variant: str, argv=None) -> int:
             p["dims"] = tuple(p["dims"][:2])
         parser.set_defaults(**p)
     a = parser.parse_args(argv)
+    if a.temporal is not None and a.temporal > 1 and base not in ("perf", "perf_hide"):
+        parser.error("--temporal > 1 applies to the perf and perf_hide variants")
+    if a.fast_math and base not in ("perf", "perf_hide"):
+        parser.error("--fast-math applies to the perf and perf_hide variants")
     opts = dict(variant=base, nx=a.nx, ny=a.ny, nt=a.nt, warmup=a.warmup, b_width=a.b_width,
                 init=a.init, init_on=a.init_on, seed=a.seed, dims=tuple(a.dims) + (0,),
                 periods=tuple(a.periods) + (0,), transport=a.transport, device=a.device,
                 chunk_rows=a.chunk_rows, unroll=a.unroll, vec=a.vec, kernel=a.kernel,
                 nontemporal=a.nontemporal, use_graph=a.graph, do_vis=a.do_vis, outdir=a.outdir,
                 profile=a.profile, check_every=a.check_every, quiet=a.quiet,
-                temporal=a.temporal, chunk2=a.chunk2, unroll2=a.unroll2,
-                fast_math=a.fast_math)
+                chunk2=a.chunk2, unroll2=a.unroll2)
     if a.auto_size:
         rank, size, _ = C.env_world()
         if size > 1:
@@ -146,7 +178,45 @@ def run_variant(variant: str, argv=None) -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=C._gloo_group())
             n = int(t.item())
         opts["nx"] = opts["ny"] = n
-    cfg = DiffusionConfig(**opts)
+    opts["temporal"], opts["fast_math"] = auto_temporal(base, opts["nx"], opts["ny"], a.temporal,
+                                                        a.fast_math)
+    return DiffusionConfig(**opts), a
+
+
+def plan_line(model, steps: int) -> str:
+    """What the timed loop runs: passes, kernel and arithmetic (printed next
+    to the reference's T_eff line)."""
+    import collections
+
+    cfg = model.cfg
+    plan = model.plan(steps)
+    passes = ", ".join(f"{n} x {k}" for k, n in sorted(collections.Counter(plan).items(),
+                                                         reverse=True))
+    kern = ""
+    if cfg.temporal > 1 or cfg.fast_math:
+        try:
+            from .. import ops
+            from .._native import native
+
+            K = max(plan) if plan else 1
+            if cfg.fast_math and ops.fast5_ok(model.coef):
+                kid = native().fast_kernel_k(K, cfg.ny, tuple(model.coef))[0]
+            else:
+                kid = native().canonical_kernel_k(K, cfg.ny)[0]
+            kern = ", kernel " + {v: k for k, v in ops.KERNELS.items()}.get(kid, str(kid))
+        except Exception:  # noqa: BLE001 - informational only
+            pass
+    arith = ("fast-math (5-point sum, folded factor; rounding-level vs canonical)"
+             if cfg.fast_math else "canonical (bitwise = one-step updates)")
+    return (f"[plan] {steps} timed steps in passes of {passes} step(s){kern}; "
+            f"{arith}; max {cfg.temporal} steps per pass (--temporal, --canonical)")
+
+
+def run_variant(variant: str, argv=None) -> int:
+    from ..models import Diffusion2D
+    from ..utils import checkpoint as ckpt
+
+    cfg, a = resolve(variant, argv)
     model = Diffusion2D(cfg)
     if variant == "perf_hide_prof":  # warm-up call before the profiled run (_prof.jl:110)
         model.step(12)
@@ -154,10 +224,13 @@ def run_variant(variant: str, argv=None) -> int:
     if a.resume:
         ckpt.load_checkpoint(model, a.resume)
     res = model.run()
+    if model.g.me == 0 and not cfg.quiet and cfg.variant in ("perf", "perf_hide"):
+        print(plan_line(model, res.timed_steps), flush=True)
     if a.checkpoint:
         ckpt.save_checkpoint(model, a.checkpoint)
     res.extra["threads_requested"] = list(a.threads)
-    res.extra["temporal"] = a.temporal
+    res.extra["temporal"] = cfg.temporal
+    res.extra["fast_math"] = bool(cfg.fast_math)
     if a.json and model.g.me == 0:
         print(res.to_json(), flush=True)
     model.close()

@@ -295,8 +295,37 @@ class Diffusion2D:
         self.chunk2 = cfg.chunk2 or default_chunk2(K, cfg.ny)
         if K > 1:
             self.out2 = self.owned_rect(K)
-        if self.executor is not None:
-            self.executor = self._build_executor()
+        self._rebuild_executor()
+
+    def set_spacing(self, spacing: tuple | None) -> None:
+        """Switch the grid spacing (dx, dy) the coefficients derive from (None:
+        the physical lx/nx_g, ly/ny_g) -- dt, the stencil coefficients and the
+        executor follow. For timing probes: bench.py re-times each rank at
+        isotropic coefficients to split a weak-scaling loss into halo,
+        coefficient and GPU parts (the fast-math pass energy depends on
+        ry = (dx/dy)^2, profiles/SUMMARY_r3.md section 1). Changes the physics
+        of the run."""
+        cfg, g = self.cfg, self.g
+        self.synchronize()
+        cfg.spacing = None if spacing is None else (float(spacing[0]), float(spacing[1]))
+        self.dx = cfg.lx / g.nxyz_g[0] if cfg.spacing is None else cfg.spacing[0]
+        self.dy = cfg.ly / g.nxyz_g[1] if cfg.spacing is None else cfg.spacing[1]
+        self.dt = min(self.dx * self.dx, self.dy * self.dy) * cfg.Cp0 / cfg.lam / 4.1
+        self.coef = ops.StencilCoef.from_physics(cfg.lam, self.dx, self.dy, self.dt)
+        self._rebuild_executor()
+
+    def _rebuild_executor(self) -> None:
+        """A new native executor for the current config / coefficients (field
+        parity folded into T first; solo mode carried over)."""
+        if self.executor is None:
+            return
+        self.synchronize()
+        if self.parity:
+            self.T, self.T2 = self.T2, self.T
+            self.parity = 0
+        self.executor = self._build_executor()
+        if self._solo:
+            self.executor.set_solo(True)
 
     # ------------------------------------------------------------------
     def geometry(self, A_shape=None) -> ops.TileGeometry:

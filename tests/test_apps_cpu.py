@@ -169,3 +169,55 @@ def test_runme_and_startup_scripts(tmp_path):
     rec = json.loads([l.split("] ", 1)[1] for l in r.stdout.splitlines()
                       if l.startswith("[0] {")][-1])
     assert rec["variant"] == "kp" and rec["nprocs"] == 2 and rec["nxg"] == 2 * (66 - 2) + 2
+
+
+def test_preset_runs_the_bench_plan_and_kernel():
+    """the reference-named perf / perf_hide entry points
+    default to what bench.py measures (K <= 24 steps per pass, fast-math)
+    on GPU-sized tiles: `--preset hide_2x2` and `bench.py --dims 2,2` resolve
+    the same configuration, hence the same pass plan and kernel; small tiles
+    keep one step per pass and --canonical opts out of fast-math."""
+    import bench
+    from rocm_mpi_amd import ops
+    from rocm_mpi_amd._native import native
+    from rocm_mpi_amd.apps import cli
+
+    cfg, _ = cli.resolve("perf_hide", ["--preset", "hide_2x2"])
+    a = bench.parse(["--dims", "2,2", "--nx", "16384", "--gpus", "4"])
+    bcfg = bench.make_config(a, 16384, 16384, "cpu", (2, 2, 0))
+    keys = ("variant", "nx", "ny", "dims", "temporal", "fast_math", "chunk2", "vec")
+    assert {k: getattr(cfg, k) for k in keys} == {k: getattr(bcfg, k) for k in keys}
+    assert (cfg.temporal, cfg.fast_math) == (24, True)
+    N = native()
+    cells = float(cfg.nx) * cfg.ny
+    for steps in (20, 1000):
+        plans = [list(N.plan_passes(steps, N.default_pass_costs(c.temporal, c.fast_math, cells)))
+                 for c in (cfg, bcfg)]
+        assert plans[0] == plans[1] and sum(plans[0]) == steps
+        coef = ops.StencilCoef.from_physics(1.0, 10 / 32674, 10 / 32674, (10 / 32674) ** 2 / 4.1)
+        assert (N.fast_kernel_k(max(plans[0]), cfg.ny, tuple(coef))
+                == N.fast_kernel_k(max(plans[1]), bcfg.ny, tuple(coef)))
+    # the reference's own perf default (12288^2) runs the bench path too
+    cfg, _ = cli.resolve("perf", [])
+    assert (cfg.nx, cfg.temporal, cfg.fast_math) == (12288, 24, True)
+    cfg, _ = cli.resolve("perf", ["--canonical"])
+    assert (cfg.temporal, cfg.fast_math) == (24, False)
+    cfg, _ = cli.resolve("perf", ["--temporal", "1"])
+    assert (cfg.temporal, cfg.fast_math) == (1, False)
+    cfg, _ = cli.resolve("perf", ["--nx", "128", "--ny", "128"])  # below ~1.5M cells
+    assert (cfg.temporal, cfg.fast_math) == (1, False)
+    cfg, _ = cli.resolve("kp", ["--preset", "kp16k"])
+    assert (cfg.temporal, cfg.fast_math) == (1, False)
+
+
+def test_perf_entry_point_prints_its_plan(capsys):
+    """The perf scripts print the pass plan and arithmetic next to the
+    reference's T_eff line."""
+    from rocm_mpi_amd.apps import cli
+
+    assert cli.run_variant("perf_hide", ["--nx", "1300", "--ny", "1200", "--nt", "60",
+                                         "--device", "cpu", "--no-vis", "--init", "random"]) == 0
+    out = capsys.readouterr().out
+    assert "Executed 60 steps in = " in out
+    line = [l for l in out.splitlines() if l.startswith("[plan]")][-1]
+    assert "50 timed steps" in line and "fast-math" in line and "24" in line

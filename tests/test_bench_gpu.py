@@ -55,6 +55,15 @@ def test_bench_small_tile_with_self_rccl_halo_check():
     assert c["teff_single_step_kernel_GBps"] > 0 and c["teff_bitwise_kstep_GBps"] > 0
     assert c["pci_bus_ids"] and len(c["pci_bus_ids"]) == 1
     assert c["nonfinite_cells_sampled"] == 0
+    # the timed field itself: three full-width row windows bitwise vs the CPU twin
+    wc = c["headline_window_check"]
+    assert wc["windows"] == 3 and wc["bitwise"] is True and wc["full_width"] is True
+    assert wc["steps"] == 25 and wc["arithmetic"] == "fast-math twin"
+    # N = 1: isotropic grid, no exchange -> e_halo = e_coef = 1 by construction
+    assert d["value_kind"] == "aggregate" and d["teff_per_gpu"] == c["teff_per_gpu_GBps"]
+    ea = c["e_attribution"]
+    assert ea["e_coef"] == 1.0 and c["solo_iso_ms_per_step"] == c["solo_ms_per_step"]
+    assert c["rccl"]["version"] > 0 and c["rccl"]["library"]
 
 
 def test_bench_default_check_on_one_gpu():
@@ -82,3 +91,4 @@ def test_bench_two_processes_sharing_the_gpu(tmp_path):
     assert len(c["pci_bus_ids"]) == 2 and c["nonfinite_cells_sampled"] == 0
     assert [r["rank"] for r in c["ranks_detail"]] == [0, 1]
     assert c["preflight"]["ring_ok"] and c["preflight"]["halo"]["transport"] == "staged"
+    assert c["headline_window_check"]["bitwise"] is True

@@ -210,3 +210,61 @@ def test_capi_graph_executor_and_self_via_rccl(K, via_rccl):
     eager = run(0, False)
     other = run(0, True) if via_rccl else run(10, False)
     assert np.array_equal(eager, other)
+
+
+def test_capi_kp_executor_with_buffers_matches_golden():
+    """rma_executor_create_g in kp mode (2) with the T-indexed qx / qy / dTdt
+    buffers (what the Julia shim passes since r4: diffusion_2D_kp.jl:88-91's
+    three kernels) == the golden model bitwise; without them the create call
+    fails with a message naming kp."""
+    L = lib()
+    nx, ny, nt = 258, 131, 29
+    g = grid(L, nx, ny, 1)
+    s = torch.cuda.current_stream().cuda_stream
+    T = torch.from_numpy(golden.initial(nx, ny)).cuda()
+    iCp = torch.ones_like(T)
+    qx, qy, dTdt = (torch.zeros_like(T) for _ in range(3))
+    ex = ctypes.c_void_p()
+    rc = L.rma_executor_create_g(g, 2, ctypes.c_void_p(T.data_ptr()), None,
+                                 ctypes.c_void_p(iCp.data_ptr()), ctypes.c_int64(nx),
+                                 ctypes.c_int64(ny), coef4(L, g, nx, ny), ctypes.c_int64(1),
+                                 ctypes.c_int64(1), 1, 0, 0, None, None, None, ctypes.byref(ex))
+    assert rc != 0 and b"kp" in L.rma_last_error()
+    ck(L, L.rma_executor_create_g(g, 2, ctypes.c_void_p(T.data_ptr()), None,
+                                  ctypes.c_void_p(iCp.data_ptr()), ctypes.c_int64(nx),
+                                  ctypes.c_int64(ny), coef4(L, g, nx, ny), ctypes.c_int64(1),
+                                  ctypes.c_int64(1), 1, 0, 0, ctypes.c_void_p(qx.data_ptr()),
+                                  ctypes.c_void_p(qy.data_ptr()), ctypes.c_void_p(dTdt.data_ptr()),
+                                  ctypes.byref(ex)))
+    ck(L, L.rma_executor_run(ex, ctypes.c_int64(nt), ctypes.c_void_p(s)))
+    torch.cuda.synchronize()
+    field = T.cpu().numpy()
+    ck(L, L.rma_executor_destroy(ex))
+    ck(L, L.rma_finalize_global_grid(g))
+    assert np.array_equal(field, golden.run(nx, ny, nt))
+
+
+def test_capi_grid_lifetime_with_live_executors():
+    """executors pin their grid. rma_grid_self_via_rccl is refused
+    while one is alive (it would replace the exchanger under it), and
+    finalize before destroy (any GC order of a host such as Julia) defers the
+    teardown: the executor still runs, and its destroy frees the grid."""
+    L = lib()
+    nx, ny, K = 200, 120, 4
+    g = grid(L, nx, ny, K, periods=(1, 1, 0))
+    s = torch.cuda.current_stream().cuda_stream
+    T = torch.from_numpy(golden.initial(nx, ny)).cuda()
+    T2, iCp = T.clone(), torch.ones_like(T)
+    ex = ctypes.c_void_p()
+    ck(L, L.rma_executor_create_g(g, 1, ctypes.c_void_p(T.data_ptr()),
+                                  ctypes.c_void_p(T2.data_ptr()), ctypes.c_void_p(iCp.data_ptr()),
+                                  ctypes.c_int64(nx), ctypes.c_int64(ny), coef4(L, g, nx, ny),
+                                  ctypes.c_int64(1), ctypes.c_int64(1), K, 1, 0, None, None, None,
+                                  ctypes.byref(ex)))
+    rc = L.rma_grid_self_via_rccl(g)
+    assert rc != 0 and b"executor" in L.rma_last_error()
+    ck(L, L.rma_finalize_global_grid(g))  # deferred: the executor still holds the grid
+    ck(L, L.rma_executor_run(ex, ctypes.c_int64(13), ctypes.c_void_p(s)))
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(T).all()) and bool(torch.isfinite(T2).all())
+    ck(L, L.rma_executor_destroy(ex))  # last reference: the grid goes with it

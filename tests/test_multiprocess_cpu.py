@@ -84,7 +84,14 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
            "--master-port", str(free_port()), os.path.join(root, "bench.py"),
            "--gpus", str(world), "--steps", "20", "--warmup", "3", "--device", "cpu",
            "--nx", str(nx), "--single-step-steps", "4", *extra]
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    K = int(extra[1])
+    # the N = 1 record of this tile class, as the driver's N = 1 run of the
+    # same sweep leaves it (bench.py save_n1): e_gpu is then defined
+    cache = tmp_path / "n1.json"
+    n1_ms = 1.0
+    cache.write_text(json.dumps({"key": f"perf_hide:{nx}x{nx}:s20:w3:K{K}:f1",
+                                 "ms_per_step": n1_ms, "pci_bus_id": "cpu"}))
+    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_N1_CACHE=str(cache))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
                        env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -98,7 +105,6 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     assert d["scaling"] == "weak" and d["higher_is_better"] is True
     c = d["config"]
     assert c["local_grid"] == [nx, nx]
-    K = int(extra[1])
     dims = [int(v) for v in extra[3].split(",")]
     assert c["global_grid"] == [dims[0] * (nx - 2 * K) + 2 * K, dims[1] * (nx - 2 * K) + 2 * K]
     assert abs(d["value"] - world * c["teff_per_gpu_GBps"]) <= 1e-6 * d["value"] + 0.005 * world + 0.01
@@ -139,6 +145,55 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     assert hc["global_grid"] == [dims[0] * (130 - 2 * K) + 2 * K, dims[1] * (130 - 2 * K) + 2 * K]
     dc = c["drift_check"]
     assert dc["steps"] == 23 and 0 <= c["fast_math_drift_max"] <= dc["bound"]
+    # the timed field itself: three full-width row windows vs the CPU twin
+    wc = c["headline_window_check"]
+    assert wc["windows"] == 3 and wc["bitwise"] is True and wc["steps"] == 23
+    assert wc["full_width"] is True and wc["boxes"] == 3
+    # E(N) attribution: value is the aggregate
+    assert d["value_kind"] == "aggregate"
+    assert abs(d["teff_per_gpu"] - c["teff_per_gpu_GBps"]) <= 0.01
+    ea = c["e_attribution"]
+    for k in ("e_halo", "e_coef", "e_gpu", "e_product", "weak_scaling_eff_same_run_iso"):
+        assert ea[k] is not None and ea[k] > 0, k
+    assert abs(ea["e_halo"] - c["weak_scaling_eff_same_run"]) <= 1e-4
+    assert abs(ea["e_halo"] * ea["e_coef"] - ea["weak_scaling_eff_same_run_iso"]) <= 1e-5
+    t_it = d["ms_per_step"]
+    assert abs(ea["e_product"] - n1_ms / t_it) <= 1e-4 * max(1.0, n1_ms / t_it)
+    assert abs(ea["e_gpu"] - n1_ms / c["solo_iso_ms_per_step"]) <= 1e-4 * ea["e_gpu"]
+    if dims[0] == dims[1]:  # dx == dy: the isotropic re-time IS the solo time
+        assert ea["e_coef"] == 1.0 and c["solo_iso_ms_per_step"] == c["solo_ms_per_step"]
+    for r in rd:
+        assert r["solo_iso_ms_per_step"] > 0 and r["e_halo"] > 0 and r["e_coef"] > 0
+        assert abs(r["e_gpu"] - n1_ms / r["solo_iso_ms_per_step"]) <= 1e-4 * r["e_gpu"]
+
+
+def test_bench_window_check_detects_a_wrong_cell(tmp_path):
+    """The headline window check compares the timed field itself: one
+    perturbed cell in the last rank's snapshot fails the run (exit 4) with
+    headline_window_check.bitwise false."""
+    import json
+    import subprocess
+    import sys
+
+    from helpers import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "12", "--warmup", "2",
+           "--device", "cpu", "--nx", "64", "--temporal", "4", "--dims", "2,1",
+           "--single-step-steps", "0", "--check", "0", "--drift-steps", "0"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_WINDOW_CORRUPT="1",
+               RMA_BENCH_N1_CACHE=str(tmp_path / "none.json"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
+                       env=env)
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-2000:]
+    d = json.loads(lines[0])
+    wc = d["config"]["headline_window_check"]
+    assert wc["bitwise"] is False and "1: window rows" in wc["error"]
+    assert d["config"]["e_attribution"]["e_gpu"] is None  # no N = 1 record cached
 
 
 def test_bench_halo_check_detects_a_wrong_tile(tmp_path):
