@@ -48,10 +48,17 @@ def main(argv=None):
     ap.add_argument("--pipe2", default="", help="depths of the 2-column-wave pipe kernel")
     ap.add_argument("--chunks2", default="", help="pipe2 K:c1/c2/..., chunk-row variants")
     ap.add_argument("--pipe5", default="", help="depths of the pipe kernel at 5 cells per lane "
-                    "(needs n % 5 == 0)")
+                    "(needs n %% 5 == 0)")
     ap.add_argument("--chunks5", default="", help="pipe5 K:c1/c2/..., chunk-row variants")
     ap.add_argument("--kinds", default="", help="other K-step kernels by name, kernel:K[:chunk],"
                     "... (e.g. piper:24,piper:24:4096,pipe_diag1:24; 4 cells per lane)")
+    ap.add_argument("--coef-dims", default="1,1",
+                    help="coefficients of this process grid at overlap 48 (K = 24): dx = "
+                         "10/(dimx(n-48)+48), dy = 10/(dimy(n-48)+48); 1,1 = dx = dy (ry = 1), "
+                         "4,2 = the headline 8-GPU grid (ry ~ 0.25), 2,1 the 2-GPU grid")
+    ap.add_argument("--coef-alt", default="",
+                    help="a second coefficient grid (e.g. 1,1): every kernel is timed at both, "
+                         "interleaved in the same rounds (rows tagged with coef_dims)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -72,15 +79,21 @@ def main(argv=None):
     T2.copy_(T)
     iCp = torch.empty_like(T)
     ops.fill_(iCp, 1.0)
-    dx = 10.0 / n
-    coef = ops.StencilCoef.from_physics(1.0, dx, dx, dx * dx / 4.1)
+    def coef_of(spec):
+        dxm, dym = (int(v) for v in spec.split(","))
+        dx, dy = 10.0 / (dxm * (n - 48) + 48), 10.0 / (dym * (n - 48) + 48)
+        return ops.StencilCoef.from_physics(1.0, dx, dy, min(dx, dy) ** 2 / 4.1)
+
+    coefs = {a.coef_dims: coef_of(a.coef_dims)}
+    if a.coef_alt:
+        coefs[a.coef_alt] = coef_of(a.coef_alt)
     N = native()
 
     def chunk(K, c=0, kind="pipe"):
         # the executor's rows per task for this kernel and depth
         if c or a.chunk:
             return c or a.chunk
-        if kind in ("pipe", "pipe2", "pipeb", "pipe5", "piper", "pipe_diag1"):
+        if kind in ("pipe", "pipe2", "pipeb", "pipe5", "piper", "pipe_diag1", "piper6", "piper7"):
             return N.pipe_chunk_rows(K, n, False) or N.default_chunk_k(max(K, 3), n)
         if kind == "pipec":
             return N.pipe_chunk_rows(K, n, True) or N.default_chunk_k(max(K, 3), n)
@@ -120,8 +133,11 @@ def main(argv=None):
             cfgs.append(("pipe2", int(K), 0, int(c)))
 
     rect = [ops.interior_rect(n, n)]
+    # every configuration at every coefficient grid: (spec, kind, K, S[, chunk])
+    cfgs = [(cs,) + c for c in cfgs for cs in coefs]
 
-    def launch(kind, K, S, c=0):
+    def launch(cs, kind, K, S, c=0):
+        coef = coefs[cs]
         if kind == "march":
             ops.stencil_step(T2, T, iCp, coef, rect, ops.StencilTuning())
         elif kind == "two_step":
@@ -149,18 +165,20 @@ def main(argv=None):
         for i, c in enumerate(cfgs):
             times[c].append(ev[i][0].elapsed_time(ev[i][1]))
         print(f"[pass_sweep] round {r + 1}/{a.rounds} done", flush=True)
-    base = statistics.median(times[("march", 1, 0)])
+    base = statistics.median(times[(a.coef_dims, "march", 1, 0)])
     rows = []
     for c in cfgs:
+        cs, c = c[0], c[1:]
         kind, K, S = c[:3]
-        med = statistics.median(times[c])
-        rows.append({"kernel": kind, "K": K, "stages": S or (native().pipe_default_stages(K)
+        med = statistics.median(times[(cs,) + c])
+        rows.append({"coef_dims": cs, "ry": round(ops.fast5_constants(coefs[cs])[0], 6),
+                     "kernel": kind, "K": K, "stages": S or (native().pipe_default_stages(K)
                                                              if kind in ops.PIPE + ("pipe2", "pipe5")
                                                              else 0),
                      "chunk_rows": (chunk(K, c[3] if len(c) > 3 else 0, kind)
                                     if kind not in ("march", "two_step") else None),
                      "vec": (N.pipe_vec(K, S, 0, n, 5, True) if kind == "pipe5" else None),
-                     "ms_per_pass": round(med, 3), "ms_min": round(min(times[c]), 3),
+                     "ms_per_pass": round(med, 3), "ms_min": round(min(times[(cs,) + c]), 3),
                      "ms_per_step": round(med / K, 4), "rel": round(med / base, 4),
                      "teff_equiv_GBps": round(K * 24 * n * n / 1e9 / (med / 1e3), 1)})
     doc = {"tile": n, "rounds": a.rounds, "one_step_ms": round(base, 3), "rows": rows,

@@ -164,10 +164,15 @@ PYBIND11_MODULE(_C, m) {
           stencilk_rects_gpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx, ny,
                              r.data(), (int)r.size(), to_coef(coef), tn, S(stream));
         else {
-          // the CPU twin of the kernel's arithmetic: fast5 (kernels 5-9, 11) or canonical
-          const bool f5 = (kernel >= 5 && kernel <= 9) || kernel == 11;
+          // the CPU twin of the kernel's arithmetic: fast5 (kernels 5-9, 11, 12), the
+          // split fast-math form (14, 15) or canonical
+          const bool f5 = (kernel >= 5 && kernel <= 9) || kernel == 11 || kernel == 12;
+          const bool f6 = kernel == 14 || kernel == 15;
           py::gil_scoped_release nogil;
-          if (f5)
+          if (f6)
+            stencilk6_rects_cpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx,
+                                ny, r.data(), (int)r.size(), to_coef(coef));
+          else if (f5)
             stencilk5_rects_cpu(K, P<double>(T2), P<const double>(T), P<const double>(iCp), nx,
                                 ny, r.data(), (int)r.size(), to_coef(coef));
           else

@@ -100,6 +100,11 @@ void stencil5_rects_cpu(double* T2, const double* T, const double* iCp, int64_t 
                         const Rect* rects, int nrects, const StencilCoef& c);
 void stencilk5_rects_cpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
                          int64_t ny, const Rect* rects, int nrects, const StencilCoef& c);
+// the split fast-math form (kernels 14 / 15), see stencil_pipe.h kArFast6Reg
+void stencil6_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                        const Rect* rects, int nrects, const StencilCoef& c);
+void stencilk6_rects_cpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                         int64_t ny, const Rect* rects, int nrects, const StencilCoef& c);
 
 // Width (in cells) of one wave's x-strip in the march kernel; perf_hide rounds
 // its x-frame so the interior rect starts on a strip boundary.

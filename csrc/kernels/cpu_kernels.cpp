@@ -124,6 +124,51 @@ void stencilk5_rects_cpu(int K, double* T2, const double* T, const double* iCp, 
   stencil5_rects_cpu(T2, a.data(), iCp, nx, ny, rects, nrects, c);
 }
 
+// The split fast-math form (kernels 14 / 15, stencil_pipe.h kArFast6Reg /
+// kArFast7Reg): T2 = fma(g, fma(ry, fma(-2, c, U+D), fma(-2, c, L+R)), c).
+void stencil6_rects_cpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                        const Rect* rects, int nrects, const StencilCoef& c) {
+  RMA_CHECK_ARG(nrects >= 0 && nrects <= kMaxRects, "nrects=" << nrects);
+  RMA_CHECK_ARG(fast5_ok(c), "fast-math needs lam != 0 and finite coefficients");
+  const double ax = (-c.mlam) * c.rdx * c.rdx;
+  const double ay = (-c.mlam) * c.rdy * c.rdy;
+  const double ry = ay / ax;
+  const double gs = c.dt * ax;
+  for (int i = 0; i < nrects; ++i) {
+    const Rect r = rects[i];
+    if (r.empty()) continue;
+    RMA_CHECK_ARG(r.x0 >= 1 && r.x1 <= nx - 1 && r.y0 >= 1 && r.y1 <= ny - 1,
+                  "rect outside interior");
+    parallel_for(r.y0, r.y1, 64, [&](int64_t y) {
+      const double* up = T + (y - 1) * nx;
+      const double* cu = T + y * nx;
+      const double* dn = T + (y + 1) * nx;
+      const double* ic = iCp + y * nx;
+      double* out = T2 + y * nx;
+      for (int64_t x = r.x0; x < r.x1; ++x) {
+        const double g = gs * ic[x];
+        const double sx = cu[x + 1] + cu[x - 1];
+        const double sy = up[x] + dn[x];
+        const double t = std::fma(ry, std::fma(-2.0, cu[x], sy), std::fma(-2.0, cu[x], sx));
+        out[x] = std::fma(g, t, cu[x]);
+      }
+    });
+  }
+}
+
+void stencilk6_rects_cpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                         int64_t ny, const Rect* rects, int nrects, const StencilCoef& c) {
+  RMA_CHECK_ARG(K >= 1, "K=" << K);
+  RMA_CHECK_ARG(T2 != T, "multi-step update cannot run in place");
+  std::vector<double> a(T, T + nx * ny), b(a);
+  const Rect interior{1, nx - 1, 1, ny - 1};
+  for (int j = 1; j < K; ++j) {
+    stencil6_rects_cpu(b.data(), a.data(), iCp, nx, ny, &interior, 1, c);
+    a.swap(b);
+  }
+  stencil6_rects_cpu(T2, a.data(), iCp, nx, ny, rects, nrects, c);
+}
+
 void flux_cpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,
               double rdx, double rdy) {
   parallel_for(0, ny - 1, 64, [&](int64_t y) {

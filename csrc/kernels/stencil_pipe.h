@@ -99,6 +99,19 @@ constexpr int kArFast5 = 0, kArCanon = 1, kArFast5Perm = 2, kArFast5Reg = 3;
 // row of its level 1, i.e. one LDS ring row read per stage and iteration
 // instead of H; measures what the ring reads cost (energy / time)
 constexpr int kArDiagOneRow = 4;
+// register factors with the split form for anisotropic grids (dx != dy):
+//   T2 = fma(g, fma(ry, fma(-2, c, U+D), fma(-2, c, L+R)), c)
+// one full-mantissa constant multiplier (ry) instead of two (ry, -2(1+ry)):
+// the deep passes are power-capped and the multiplier toggling of the
+// constants costs ~2 % (profiles/SUMMARY_r3.md section 1). kArFast7Reg is
+// the same form with the -2c done as (c + c) and two subtractions (2c is
+// exact, so both round once: bitwise equal). A different rounding than the
+// 5-operation form; CPU twin stencil6_rects_cpu.
+constexpr int kArFast6Reg = 5, kArFast7Reg = 6;
+constexpr bool ar_reg(int Ar) {
+  return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg;
+}
+constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
 template <int K, int S, int V, bool Canon, int C = 1>
 constexpr int occupancy(int lds) {
@@ -152,7 +165,7 @@ constexpr int lds_bytes_reg() {  // T + factor hand-off rows, LDS-DMA staging (V
 }
 template <int K, int S, int V, int Ar, int C>
 constexpr int kernel_waves() {
-  if constexpr (Ar == kArFast5Reg) {
+  if constexpr (ar_reg(Ar)) {
     // + the H factor rows (measured 158 / 233 / 256 VGPRs at K = 12 / 20 / 24, V = 4)
     constexpr int H = Plan<K, S>::H;
     constexpr int vgpr = 8 * H * V + 8 * V + 40;
@@ -193,7 +206,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
                                           const RectList& L, const StencilCoef& k, int chunk_rows,
                                           int remap) {
   using P = Plan<K, S>;
-  constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = Ar == kArFast5Reg;
+  constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = ar_reg(Ar);
   static_assert(!kRegG || (C == 1 && V != 5), "register factors: V <= 4, one column wave");
   // register factors, 2 or 4 cells per lane: stage 0 prefetches T / 1/Cp three
   // rows ahead by LDS-DMA (global_load_lds_dwordx4 into three staging rows per
@@ -519,11 +532,32 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         }
         // the V cells' FMA chains interleaved (sched_barrier keeps them apart)
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (ar_split(Ar)) {
+          double u[V];
+          if constexpr (Ar == kArFast6Reg) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) t[v] = __builtin_fma(mkc, c[v], sx[v]);
-        __builtin_amdgcn_sched_barrier(0);
+            for (int v = 0; v < V; ++v) {
+              u[v] = __builtin_fma(-2.0, c[v], sx[v]);
+              t[v] = __builtin_fma(-2.0, c[v], sy[v]);
+            }
+          } else {
 #pragma unroll
-        for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, sy[v], t[v]);
+            for (int v = 0; v < V; ++v) {
+              const double d = c[v] + c[v];
+              u[v] = sx[v] - d;
+              t[v] = sy[v] - d;
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, t[v], u[v]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) t[v] = __builtin_fma(mkc, c[v], sx[v]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, sy[v], t[v]);
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int v = 0; v < V; ++v) res[v] = __builtin_fma(gl[v], t[v], c[v]);

@@ -11,7 +11,11 @@
 //     K=16 (profiles/pass_sweep_cols2_r2.json);
 //   * 5 cells per lane (fast5, K = 16..20, stencil_pipe5_lab.hip);
 //   * a diagnosis variant with one factor-ring read per stage and row (wrong
-//     results; what the ring reads cost: -5 % per K=24 pass, SUMMARY_r3).
+//     results; what the ring reads cost: -5 % per K=24 pass, SUMMARY_r3);
+//   * piper6 / piper7: register factors with the split 6-operation form for
+//     anisotropic grids (one full-mantissa constant multiplier instead of
+//     two; kernels 14 / 15, bitwise equal to each other and to
+//     stencil6_rects_cpu), K = 20, 24.
 #include "../kernels/lab_hooks.h"
 
 namespace rma {
@@ -29,6 +33,10 @@ bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(24, 4, kArFast5Perm)
   RMA_PIPE_CASE(20, 4, kArDiagOneRow)
   RMA_PIPE_CASE(24, 4, kArDiagOneRow)
+  RMA_PIPE_CASE(20, 4, kArFast6Reg)
+  RMA_PIPE_CASE(24, 4, kArFast6Reg)
+  RMA_PIPE_CASE(20, 4, kArFast7Reg)
+  RMA_PIPE_CASE(24, 4, kArFast7Reg)
   return false;
 }
 

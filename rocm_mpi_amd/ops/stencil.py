@@ -40,13 +40,16 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 # 5-point sum with one folded per-cell factor, the GPU oracle of "pipe"), "fast5p2/p4/p8"
 # (6/7/8: fixed-K pipelined fast5), "pipeb" (11: pipe with ds_bpermute lane moves), and
 # the pipelined kernels' non-default stage splits, two-column blocks and 5 cells per lane,
-# and "pipe_diag1" (13: a diagnosis, WRONG results: one factor-ring read per stage and row).
+# "pipe_diag1" (13: a diagnosis, WRONG results: one factor-ring read per stage and row),
+# and "piper6" / "piper7" (14 / 15: register factors with the split fast-math form for
+# dx != dy, T2 = fma(g, fma(ry, fma(-2,c,U+D), fma(-2,c,L+R)), c); CPU twin: FAST6).
 FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe", "pipeb", "piper")
-PIPE = ("pipe", "pipec", "pipeb", "piper", "pipe_diag1")
+FAST6 = ("piper6", "piper7")
+PIPE = ("pipe", "pipec", "pipeb", "piper", "pipe_diag1", "piper6", "piper7")
 PIPE_MAX_K = 24
 KERNELS = {"march": 0, "lds": 1, "lds_dpp": 3, "pipe": 9, "pipec": 10, "piper": 12}
 LAB_KERNELS = {"dpp": 2, "fast": 4, "fast5": 5, "fast5p2": 6, "fast5p4": 7, "fast5p8": 8,
-               "pipeb": 11, "pipe_diag1": 13}
+               "pipeb": 11, "pipe_diag1": 13, "piper6": 14, "piper7": 15}
 KSTEP_CORE = ("lds_dpp", "pipe", "pipec", "piper")
 
 
@@ -272,7 +275,7 @@ def stencilk_step(K: int, T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor,
         ch = native().default_chunk_k(K, ny) if has_native() else 16
         tuning = StencilTuning(chunk_rows=ch, kernel="lds_dpp", xcd_remap=1)
     tn = tuning
-    if tn.kernel in FAST5 and not fast5_ok(coef):
+    if tn.kernel in FAST5 + FAST6 and not fast5_ok(coef):
         raise ValueError("kernel 'fast5' folds dy^-2/dx^-2 into one factor: needs lam != 0 "
                          f"and finite coefficients, got {tuple(coef)}")
     if T.is_cuda:

@@ -111,6 +111,13 @@ for s in "$@"; do
     sweepc2) step sweepc2 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe "" \
              --kinds piper:20:2560,piper:20:2816,piper:20,piper:20:3328,piper:20:3584,piper:24:2816,piper:24,piper:24:3328 \
              --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/sweepc2.json" || exit 1 ;;
+    coef_ab) step coef_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
+             --pipec "" --ldsdpp "" --old "" --alt "" --coef-dims 4,2 --coef-alt 1,1 \
+             --kinds piper:20,piper:24,piper6:20,piper6:24,piper7:20,piper7:24 \
+             --out "$OUT/coef_ab.json" || exit 1 ;;
+    tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+             tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
+             -p no:cacheprovider || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
              --json-out "$OUT/bench20.json" || exit 1 ;;

@@ -311,3 +311,23 @@ def test_piper_register_factors_bitwise(nx, K):
     sub = [(K + 3, nx - K - 7, K + 2, ny - K - 5), (1, K + 3, 1, ny - 1)]
     assert torch.equal(gpu_run(K, T, iCp, sub, "piper", chunk=19, xcd=0),
                        cpu_ref(K, T, iCp, sub, "pipe"))
+
+
+@pytest.mark.parametrize("kernel", ["piper6", "piper7"])
+@pytest.mark.parametrize("nx", [515, 518, 1028])
+@pytest.mark.parametrize("K", [20, 24])
+def test_piper_split_form_bitwise(kernel, nx, K):
+    """piper6 / piper7 (register factors, the split fast-math form for dx != dy:
+    fma(g, fma(ry, fma(-2,c,U+D), fma(-2,c,L+R)), c), lab library): bitwise
+    equal to their CPU twin (stencil6_rects_cpu), to each other, and within
+    rounding of the 5-operation form."""
+    ny = 157
+    T, iCp = rand((ny, nx), 41 + K), rand((ny, nx), 42, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, kernel)
+    assert torch.equal(gpu_run(K, T, iCp, rects, kernel, chunk=43), ref)
+    sub = [(K + 3, nx - K - 7, K + 2, ny - K - 5), (1, K + 3, 1, ny - 1)]
+    assert torch.equal(gpu_run(K, T, iCp, sub, kernel, chunk=19, xcd=0),
+                       cpu_ref(K, T, iCp, sub, kernel))
+    f5 = cpu_ref(K, T, iCp, rects, "pipe")
+    assert float((ref - f5).abs().max()) < 1e-13
