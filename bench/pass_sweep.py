@@ -93,7 +93,8 @@ def main(argv=None):
         # the executor's rows per task for this kernel and depth
         if c or a.chunk:
             return c or a.chunk
-        if kind in ("pipe", "pipe2", "pipeb", "pipe5", "piper", "pipe_diag1", "piper6", "piper7"):
+        if kind in ("pipe", "pipe2", "pipeb", "pipe5", "piper", "pipe_diag1", "piper6", "piper7",
+                    "piper_u3"):
             return N.pipe_chunk_rows(K, n, False) or N.default_chunk_k(max(K, 3), n)
         if kind == "pipec":
             return N.pipe_chunk_rows(K, n, True) or N.default_chunk_k(max(K, 3), n)

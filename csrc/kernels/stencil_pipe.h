@@ -108,8 +108,11 @@ constexpr int kArDiagOneRow = 4;
 // exact, so both round once: bitwise equal). A different rounding than the
 // 5-operation form; CPU twin stencil6_rects_cpu.
 constexpr int kArFast6Reg = 5, kArFast7Reg = 6;
+// lab A/B: kArFast5Reg with the row loop unrolled by 3 in every stage (the
+// round-3 piper; see kU6 below), bitwise equal to piper
+constexpr int kArFast5RegU3 = 7;
 constexpr bool ar_reg(int Ar) {
-  return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg;
+  return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -176,6 +179,11 @@ constexpr int kernel_waves() {
     return waves_per_simd<K, S, V, Ar == kArCanon, C>();
   }
 }
+
+#ifndef RMA_PIPE_U6
+#define RMA_PIPE_U6 1
+#endif
+constexpr bool kPipeU6 = RMA_PIPE_U6;
 
 template <bool kDpp = true>
 __device__ __forceinline__ double from_next_lane(double v) {
@@ -621,7 +629,20 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   };
   // one row loop per stage role (stage is wave-uniform; every copy passes the
   // same barriers): stage 0 carries the HBM prefetch registers, the others not
+  // Register factors: a factor row lives H iterations and a new one starts
+  // every iteration, so with the loop unrolled by U < H the row started at
+  // phase p is still live when the next trip's phase-p row starts and the
+  // back edge has to move every row (20 v_mov_b64 per 3 rows at K=20: ~5 % of
+  // the VALU instructions). Unrolled by 6 >= H the rows keep their registers
+  // across the back edge (K=20: 2 moves per 6 rows). Stage 0 stays at 3: its LDS-DMA
+  // staging slot is the phase mod 3, and a read of a slot DMA'd earlier in the
+  // same trip would get a vmcnt(0) (see kGlds above).
+  // (H = 6, K >= 21: 39 VGPRs spill at K=24; H = 4, K = 13..16: 214 instead of
+  // 161 VGPRs at K=16, 2 instead of 3 waves per SIMD -> only H = 5, K = 17..20:
+  // 247 instead of 201 VGPRs, no spill, still 2 waves per SIMD)
+  constexpr bool kU6 = kRegG && P::H == 5 && kPipeU6 && Ar != kArFast5RegU3;
   auto run = [&](auto S0c, auto LASTc) {
+    constexpr bool U6 = kU6 && !decltype(S0c)::value;
     for (;;) {
       iter(std::integral_constant<int, 0>{}, S0c, LASTc);
       if (++i > iend) break;
@@ -629,6 +650,14 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       if (++i > iend) break;
       iter(std::integral_constant<int, 2>{}, S0c, LASTc);
       if (++i > iend) break;
+      if constexpr (U6) {
+        iter(std::integral_constant<int, 0>{}, S0c, LASTc);
+        if (++i > iend) break;
+        iter(std::integral_constant<int, 1>{}, S0c, LASTc);
+        if (++i > iend) break;
+        iter(std::integral_constant<int, 2>{}, S0c, LASTc);
+        if (++i > iend) break;
+      }
     }
   };
   if constexpr (S == 1) {

@@ -15,7 +15,9 @@
 //   * piper6 / piper7: register factors with the split 6-operation form for
 //     anisotropic grids (one full-mantissa constant multiplier instead of
 //     two; kernels 14 / 15, bitwise equal to each other and to
-//     stencil6_rects_cpu), K = 20, 24.
+//     stencil6_rects_cpu), K = 20, 24;
+//   * piper_u3 (kernel 16): piper with the row loop unrolled by 3 in every
+//     stage (the round-3 kernel; the core's K = 17..20 unroll by 6), A/B.
 #include "../kernels/lab_hooks.h"
 
 namespace rma {
@@ -37,6 +39,10 @@ bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(24, 4, kArFast6Reg)
   RMA_PIPE_CASE(20, 4, kArFast7Reg)
   RMA_PIPE_CASE(24, 4, kArFast7Reg)
+  RMA_PIPE_CASE(17, 4, kArFast5RegU3)
+  RMA_PIPE_CASE(18, 4, kArFast5RegU3)
+  RMA_PIPE_CASE(19, 4, kArFast5RegU3)
+  RMA_PIPE_CASE(20, 4, kArFast5RegU3)
   return false;
 }
 

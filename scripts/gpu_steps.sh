@@ -115,8 +115,14 @@ for s in "$@"; do
              --pipec "" --ldsdpp "" --old "" --alt "" --coef-dims 4,2 --coef-alt 1,1 \
              --kinds piper:20,piper:24,piper6:20,piper6:24,piper7:20,piper7:24 \
              --out "$OUT/coef_ab.json" || exit 1 ;;
+    u6_ab) step u6_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
+             --pipec "" --ldsdpp "" --old "" --alt "" \
+             --kinds piper:17,piper:18,piper:19,piper:20,piper_u3:17,piper_u3:18,piper_u3:19,piper_u3:20 \
+             --out "$OUT/u6_ab.json" || exit 1 ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
+             "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
+             "tests/test_pipe_gpu.py::test_piper_register_factors_bitwise" \
              -p no:cacheprovider || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \

@@ -331,3 +331,20 @@ def test_piper_split_form_bitwise(kernel, nx, K):
                        cpu_ref(K, T, iCp, sub, kernel))
     f5 = cpu_ref(K, T, iCp, rects, "pipe")
     assert float((ref - f5).abs().max()) < 1e-13
+
+
+@pytest.mark.parametrize("nx", [518, 1028])
+@pytest.mark.parametrize("K", [17, 18, 19, 20])
+def test_piper_unroll6_equals_unroll3(nx, K):
+    """The core piper unrolls the row loop of its non-first stages by 6 at
+    K = 17..20 (factor rows keep their registers across the back edge); the
+    lab's piper_u3 is the round-3 unroll by 3: bitwise equal, and both equal
+    the fast5 CPU twin."""
+    ny = 203
+    T, iCp = rand((ny, nx), 51 + K), rand((ny, nx), 52, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, "pipe")
+    for chunk in (7, 43):
+        a = gpu_run(K, T, iCp, rects, "piper", chunk=chunk)
+        b = gpu_run(K, T, iCp, rects, "piper_u3", chunk=chunk)
+        assert torch.equal(a, ref) and torch.equal(b, ref)
