@@ -130,6 +130,8 @@ class DiffusionExecutor {
   // kernel tuning of a K-step launch: part 0 = the interior / whole tile,
   // 1 = wide (y) frame strips, 2 = tall (x) frame strips
   StencilTuning pass_tuning(int K, int part = 0) const;
+  // rows per task of the aligned frame launch (interior_rows: the interior's)
+  int frame_chunk_rows(int K, int interior_rows) const;
   void multi_step(int K, double* Tin, double* Tout, const double* iCp, int64_t nx, int64_t ny,
                   const Rect* rects, int n, const StencilTuning& tn, void* stream) const;
   void exchange(double* A, stream_t s);

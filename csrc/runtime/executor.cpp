@@ -260,6 +260,18 @@ StencilTuning DiffusionExecutor::pass_tuning(int K, int part) const {
   return t;
 }
 
+int DiffusionExecutor::frame_chunk_rows(int K, int interior_rows) const {
+  // RMA_FRAME_CHUNK_DIV=d: the aligned frame's tasks take 1/d of the
+  // interior's rows (A/B knob; default 1)
+  static const int div = [] {
+    const char* e = std::getenv("RMA_FRAME_CHUNK_DIV");
+    const int d = e ? std::atoi(e) : 0;
+    return d >= 1 ? d : 1;
+  }();
+  (void)K;
+  return std::max(1, interior_rows / div);
+}
+
 void DiffusionExecutor::exchange(double* A, stream_t s) {
   if (!halo_ || solo_) return;
   // diagnosis only (profiles/SUMMARY_r2.md, x-neighbour pass cost): keep the
@@ -428,6 +440,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
       // with x and y neighbours; profiles/SUMMARY_r3.md)
       StencilTuning ft = tn;
       ft.xcd_remap = 0;
+      ft.chunk_rows = frame_chunk_rows(K, tn.chunk_rows);
       multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame.data(), (int)g.frame.size(), ft, s_hi_);
     } else {
       if (!g.frame_wide.empty())

@@ -147,10 +147,10 @@ for s in "$@"; do
     eq16k_x|eq16k_y|eq16k_xy) d=${s#eq16k_}
              step "$s" 300 python bench/rccl_self_overhead.py --n 16384 --K 24 --periodic "$d" \
              --steps 960 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
-    eqn*) # eqn<N>_<dims>[_strips]: N^2 tile, K=24, equal coefficients
-             t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""
-             case $t in *_strips) fa=0 ;; esac
-             RMA_FRAME_ALIGNED=$fa step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
+    eqn*) # eqn<N>_<dims>[_strips|_cd<D>]: N^2 tile, K=24, equal coefficients
+             t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""
+             case $t in *_strips) fa=0 ;; *_cd*) cd=${t##*_cd} ;; esac
+             RMA_FRAME_CHUNK_DIV=$cd RMA_FRAME_ALIGNED=$fa step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
              --periodic "$d" --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     chunk_sweep) step chunk_sweep 400 python bench/pass_sweep.py --pipe 20,24 --pipec "" \
              --ldsdpp "" --old "" --alt "" --rounds 3 \
