@@ -162,9 +162,36 @@ constexpr int waves_per_simd() {
 // row, like the T hand-off. LDS read bytes per cell update: the ring's one
 // factor row per level -> one factor row per stage (H levels); LDS per
 // block: 4 (S-1) rows.
-template <int K, int S, int V>
+#ifndef RMA_PIPE_U6
+#define RMA_PIPE_U6 1
+#endif
+constexpr bool kPipeU6 = RMA_PIPE_U6;
+// Register factors: a factor row lives H iterations and a new one starts
+// every iteration, so with the row loop unrolled by U < H the row started at
+// phase p is still live when the next trip's phase-p row starts and the back
+// edge has to move every row (20 v_mov_b64 per 3 rows at K=20: ~5 % of the
+// VALU instructions). Unrolled by 6 >= H the rows keep their registers across
+// the back edge (K=20: 2 moves per 6 rows in stages 1..3). Only H = 5 (K =
+// 17..20): H = 6 (K >= 21) spills 39 VGPRs at K=24, and H = 4 (K = 13..16)
+// takes 214 instead of 161 VGPRs at K=16 (2 instead of 3 waves per SIMD);
+// K=20: 247 instead of 201 VGPRs, no spill, still 2 waves per SIMD.
+template <int K, int S, int Ar>
+constexpr bool pipe_u6() {
+  return ar_reg(Ar) && Plan<K, S>::H == 5 && kPipeU6 && Ar != kArFast5RegU3;
+}
+// LDS-DMA staging rows per array: one per phase of the unrolled row loop, so
+// a row DMA'd at phase p is read at phase p of the next loop trip (across the
+// back edge: a read of a slot DMA'd earlier in the same trip gets a vmcnt(0)
+// from the compiler's LDS-DMA hazard check, which drains the prefetch)
+template <int K, int S, int Ar>
+constexpr int staging_rows() {
+  return pipe_u6<K, S, Ar>() ? 6 : 3;
+}
+template <int K, int S, int V, int Ar>
 constexpr int lds_bytes_reg() {  // T + factor hand-off rows, LDS-DMA staging (V = 2, 4)
-  return (4 * (S > 1 ? S - 1 : 1) + (V == 2 || V == 4 ? 6 : 0)) * Geo<K, S, V, 1>::WB * 8 + 8;
+  return (4 * (S > 1 ? S - 1 : 1) + (V == 2 || V == 4 ? 2 * staging_rows<K, S, Ar>() : 0)) *
+             Geo<K, S, V, 1>::WB * 8 +
+         8;
 }
 template <int K, int S, int V, int Ar, int C>
 constexpr int kernel_waves() {
@@ -173,17 +200,12 @@ constexpr int kernel_waves() {
     constexpr int H = Plan<K, S>::H;
     constexpr int vgpr = 8 * H * V + 8 * V + 40;
     constexpr int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
-    constexpr int w = occupancy<K, S, V, false, C>(lds_bytes_reg<K, S, V>());
+    constexpr int w = occupancy<K, S, V, false, C>(lds_bytes_reg<K, S, V, Ar>());
     return by_vgpr < 2 ? 2 : (by_vgpr < w ? by_vgpr : w);
   } else {
     return waves_per_simd<K, S, V, Ar == kArCanon, C>();
   }
 }
-
-#ifndef RMA_PIPE_U6
-#define RMA_PIPE_U6 1
-#endif
-constexpr bool kPipeU6 = RMA_PIPE_U6;
 
 template <bool kDpp = true>
 __device__ __forceinline__ double from_next_lane(double v) {
@@ -225,6 +247,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   // s_barrier after lgkmcnt(0): __syncthreads() would also wait vmcnt(0) and
   // drain the prefetch every row.
   constexpr bool kGlds = kRegG && (V == 2 || V == 4);
+  constexpr bool kU6 = pipe_u6<K, S, Ar>();
+  constexpr int NST = staging_rows<K, S, Ar>();  // staging rows per array
   using G = Geo<K, S, V, C>;
   constexpr int H = P::H, HL = P::HL, R = ring_rows<K, S, V>();
   constexpr int M = kRegG ? 0 : mirror_rows<K, S, V, Canon, C>();
@@ -316,7 +340,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   constexpr int kRing = kRegG ? 1 : (R + M) * WB, kHand = kRegG ? 4 : 2;
   __shared__ double ring[kRing];
   __shared__ double hand[kHand][NH][WB];
-  __shared__ double staging[kGlds ? 6 * WB : 1];
+  __shared__ double staging[kGlds ? 2 * NST * WB : 1];
   if constexpr (!kRegG)
     for (int t = threadIdx.x; t < kRing; t += S * C * kWave) ring[t] = 0.0;
   for (int t = threadIdx.x; t < kHand * NH * WB; t += S * C * kWave) (&hand[0][0][0])[t] = 0.0;
@@ -339,10 +363,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       for (int v = 0; v < V; ++v) gr[q][v] = gr[q - 1][v];
   };
   __syncthreads();
-  // LDS-DMA staging row of T (a = 0) / 1/Cp (a = 1) for relative row r (mod 3):
+  // LDS-DMA staging row of T (a = 0) / 1/Cp (a = 1) for relative row r (mod NST):
   // instruction h, lane l loads the cell pair 2l+h of the lane's window, which
   // lands at dbl2 slot h*64 + l: the pair-interleaved row layout rd2 reads
-  auto stg = [&](int a, int r) { return &staging[(3 * a + r) * WB]; };
+  auto stg = [&](int a, int r) { return &staging[(NST * a + r) * WB]; };
   auto glds_row = [&](int a, int y, int r) {
     const double* rb = (a ? iCp : T) + rowc(y) * nx;
 #pragma unroll
@@ -350,13 +374,12 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       __builtin_amdgcn_global_load_lds(at(rb, xob + 16u * h), stg(a, r) + h * 2 * kWave, 16, 0, 0);
   };
   if constexpr (kGlds) {
-    if (stage == 0) {  // rows i+1..i+3 of T and i..i+2 of 1/Cp, in the order they are waited for
-      glds_row(0, i + 1, 0);
-      glds_row(1, i, 0);
-      glds_row(0, i + 2, 1);
-      glds_row(1, i + 1, 1);
-      glds_row(0, i + 3, 2);
-      glds_row(1, i + 2, 2);
+    if (stage == 0) {  // rows i+1..i+NST of T and i..i+NST-1 of 1/Cp, in the order they are waited for
+#pragma unroll
+      for (int r = 0; r < NST; ++r) {
+        glds_row(0, i + 1 + r, r);
+        glds_row(1, i + r, r);
+      }
     }
   }
   // LDS rows hold cell pairs interleaved by parity (pair p at dbl2 slot
@@ -405,7 +428,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   const int lag = stage * (H + 1);  // rows behind stage 0
 
   auto iter = [&](auto Pc, auto S0c, auto LASTc) {
-    constexpr int Pr = decltype(Pc)::value;
+    constexpr int Ps = decltype(Pc)::value;  // phase of the unrolled loop (staging slot)
+    constexpr int Pr = Ps % 3;                // phase of the 3-row windows w
     constexpr bool S0 = decltype(S0c)::value;
     constexpr bool LAST = decltype(LASTc)::value;
     constexpr int NL = LAST ? HL : H;  // levels of this stage
@@ -417,20 +441,23 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       if constexpr (kRegG && !LAST) wr2(gh(par, 0), gr[H - 1]);
       const bool rin1 = i >= 1 && i <= ny32 - 2;
       if constexpr (kGlds) {
-        // three rows ahead: the staging slot of this iteration's rows (T i+1,
-        // 1/Cp i) is the unrolled phase (the loop starts at phase 0), and their
-        // DMA (issued three iterations ago, at this phase of the previous loop
-        // trip) has landed when at most the two later iterations' 2 x V
-        // instructions are outstanding. Same-phase slots keep every DMA -> read
-        // pair across the loop back-edge, where the compiler's LDS-DMA hazard
-        // check adds no vmcnt(0) (a read of a slot DMA'd earlier in the same
-        // trip got one, whatever the counted wait before it). The builtin
-        // (gfx9 encoding: vmcnt bits 3:0, expcnt 6:4 and lgkmcnt 11:8 at their
-        // maxima = no wait) plus an empty asm keeps the reads below the wait.
-        __builtin_amdgcn_s_waitcnt(0x0F70 | (V == 4 ? 8 : 4));
+        // NST (3, or 6 when unrolled by 6) rows ahead: the staging slot of this
+        // iteration's rows (T i+1, 1/Cp i) is the unrolled phase (the loop
+        // starts at phase 0), and their DMA (issued NST iterations ago, at this
+        // phase of the previous loop trip) has landed when at most the NST-1
+        // later iterations' 2 x V/2 instructions are outstanding. Same-phase
+        // slots keep every DMA -> read pair across the loop back-edge, where the
+        // compiler's LDS-DMA hazard check adds no vmcnt(0) (a read of a slot
+        // DMA'd earlier in the same trip got one, whatever the counted wait
+        // before it). The builtin (gfx9 encoding: vmcnt bits 3:0 and 15:14,
+        // expcnt 6:4 and lgkmcnt 11:8 at their maxima = no wait) plus an empty
+        // asm keeps the reads below the wait.
+        constexpr int kVm = (NST - 1) * V;
+        static_assert(kVm < 64, "vmcnt");
+        __builtin_amdgcn_s_waitcnt(0x0F70 | (kVm & 15) | ((kVm >> 4) << 14));
         asm volatile("" ::: "memory");
-        rd2(stg(0, Pr), pT);
-        rd2(stg(1, Pr), pC);
+        rd2(stg(0, Ps), pT);
+        rd2(stg(1, Ps), pC);
       }
 #pragma unroll
       for (int v = 0; v < V; ++v) w[0][Pr][v] = pT[v];
@@ -616,11 +643,11 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     if constexpr (kGlds) {  // no vmcnt(0): the staging DMA stays in flight across rows
       if constexpr (S0) {
         // the staging reads above are complete (lgkmcnt(0)) before the DMA of
-        // T row i+4 / 1/Cp row i+3 overwrites the same slots
+        // T row i+1+NST / 1/Cp row i+NST overwrites the same slots
         __builtin_amdgcn_s_waitcnt(0xC07F);
         asm volatile("" ::: "memory");
-        glds_row(0, i + 4, Pr);
-        glds_row(1, i + 3, Pr);
+        glds_row(0, i + 1 + NST, Ps);
+        glds_row(1, i + NST, Ps);
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     } else {
@@ -629,20 +656,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   };
   // one row loop per stage role (stage is wave-uniform; every copy passes the
   // same barriers): stage 0 carries the HBM prefetch registers, the others not
-  // Register factors: a factor row lives H iterations and a new one starts
-  // every iteration, so with the loop unrolled by U < H the row started at
-  // phase p is still live when the next trip's phase-p row starts and the
-  // back edge has to move every row (20 v_mov_b64 per 3 rows at K=20: ~5 % of
-  // the VALU instructions). Unrolled by 6 >= H the rows keep their registers
-  // across the back edge (K=20: 2 moves per 6 rows). Stage 0 stays at 3: its LDS-DMA
-  // staging slot is the phase mod 3, and a read of a slot DMA'd earlier in the
-  // same trip would get a vmcnt(0) (see kGlds above).
-  // (H = 6, K >= 21: 39 VGPRs spill at K=24; H = 4, K = 13..16: 214 instead of
-  // 161 VGPRs at K=16, 2 instead of 3 waves per SIMD -> only H = 5, K = 17..20:
-  // 247 instead of 201 VGPRs, no spill, still 2 waves per SIMD)
-  constexpr bool kU6 = kRegG && P::H == 5 && kPipeU6 && Ar != kArFast5RegU3;
+  // unrolled by 6 where the factor rows live 5 iterations (pipe_u6), else 3
   auto run = [&](auto S0c, auto LASTc) {
-    constexpr bool U6 = kU6 && !decltype(S0c)::value;
     for (;;) {
       iter(std::integral_constant<int, 0>{}, S0c, LASTc);
       if (++i > iend) break;
@@ -650,12 +665,12 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       if (++i > iend) break;
       iter(std::integral_constant<int, 2>{}, S0c, LASTc);
       if (++i > iend) break;
-      if constexpr (U6) {
-        iter(std::integral_constant<int, 0>{}, S0c, LASTc);
+      if constexpr (kU6) {
+        iter(std::integral_constant<int, 3>{}, S0c, LASTc);
         if (++i > iend) break;
-        iter(std::integral_constant<int, 1>{}, S0c, LASTc);
+        iter(std::integral_constant<int, 4>{}, S0c, LASTc);
         if (++i > iend) break;
-        iter(std::integral_constant<int, 2>{}, S0c, LASTc);
+        iter(std::integral_constant<int, 5>{}, S0c, LASTc);
         if (++i > iend) break;
       }
     }

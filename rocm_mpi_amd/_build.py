@@ -46,6 +46,9 @@ BUILD = ROOT / "build" / "native"
 PKG = ROOT / "rocm_mpi_amd"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RMA_OFFLOAD_ARCH", "gfx950")
+# gfx950 only: the core kernels use CDNA4 instructions (e.g. the 16-byte
+# global_load_lds of piper's stage-0 prefetch, csrc/kernels/stencil_pipe.h)
+SUPPORTED_ARCHS = ("gfx950",)
 
 # librma_core.so: every kernel the executor / ops run + the runtime + the C ABI
 # (usable without Python)
@@ -130,6 +133,10 @@ def _stale(src: Path, obj: Path, newest_header: float) -> bool:
 
 def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
     """Compile (incrementally) and link ``rocm_mpi_amd/_C*.so``; returns its path."""
+    if ARCH not in SUPPORTED_ARCHS:
+        raise SystemExit(f"rocm_mpi_amd builds for {', '.join(SUPPORTED_ARCHS)} (MI355X) only, "
+                         f"RMA_OFFLOAD_ARCH={ARCH!r}: the core kernels use CDNA4 instructions "
+                         "(16-byte LDS-DMA loads in the pipelined K-step kernel)")
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
     headers = _headers()

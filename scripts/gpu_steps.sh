@@ -123,6 +123,7 @@ for s in "$@"; do
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
              "tests/test_pipe_gpu.py::test_piper_register_factors_bitwise" \
+             "tests/test_temporal_gpu.py::test_headline_kernels_beyond_2e31_cells" \
              -p no:cacheprovider || exit 1 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench20) step bench20 300 python bench.py --gpus 1 --steps 20 --warmup 5 \

@@ -5,6 +5,7 @@ import pytest
 import torch
 
 from rocm_mpi_amd import ops
+from rocm_mpi_amd._native import native
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -256,6 +257,63 @@ def test_k_step_int64_indexing(K, kern, vec):
     ops.stencilk_step(K, small, Ts, Cs, coef(), [(1, nx - 1, h - rows, h - 1)], tn)
     assert torch.equal(got, small[h - rows:h - 1].cpu())
     torch.cuda.empty_cache()
+
+
+@pytest.fixture(scope="module")
+def headline_width_tile():
+    """A 101120-column tile (the headline's row width, nx % 4 == 0) of
+    2.15e9 cells > 2^31, random T and 1/Cp; freed after the module."""
+    free, _ = torch.cuda.mem_get_info()
+    ny, nx = 21300, 101120
+    if free < 3 * ny * nx * 8 * 1.1:
+        pytest.skip("not enough HBM")
+    T = torch.empty((ny, nx), dtype=torch.float64, device=DEV)
+    ops.init_random_(T, ops.TileGeometry(0, 0, nx, ny, 1.0, 1.0), seed=7)
+    iCp = torch.empty_like(T)
+    ops.init_random_(iCp, ops.TileGeometry(0, 0, nx, ny, 1.0, 1.0), seed=8)
+    iCp.mul_(0.5).add_(0.5)
+    out = torch.zeros_like(T)
+    yield T, iCp, out
+    del T, iCp, out
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kern,K", [("piper", 20), ("piper", 24), ("pipe", 20), ("pipe", 24),
+                                    ("pipec", 20), ("piper", 17)])
+def test_headline_kernels_beyond_2e31_cells(headline_width_tile, kern, K):
+    """the kernels the bench times (piper, kernel 12), the
+    ring kernel (pipe, 9) and the canonical side number (pipec, 10) on a tile
+    of > 2^31 cells with the headline's 101120-column rows: uniform 64-bit
+    row bases + 32-bit lane byte offsets (stencil_pipe.h). Rows at the top,
+    across the 2^31-cell boundary and at the bottom edge equal the C++ CPU
+    twin of the same arithmetic run on a copy of the rows they depend on."""
+    T, iCp, out = headline_width_tile
+    ny, nx = T.shape
+    rows = 24
+    twin = "pipec" if kern == "pipec" else "pipe"
+    if kern == "pipec":
+        tn = ops.StencilTuning(chunk_rows=native().pipe_chunk_rows(K, ny, True) or 1024,
+                               kernel="pipec", xcd_remap=1, vec=4)
+    else:
+        kid, vec, ch = native().fast_kernel_k(K, ny, tuple(coef()))
+        tn = ops.StencilTuning(chunk_rows=ch, kernel=kern, xcd_remap=1, vec=4)
+    cross = (2 ** 31) // nx  # the row holding cell 2^31
+    for y0 in (1, cross - rows // 2, ny - 1 - rows):
+        y1 = y0 + rows
+        out.fill_(-7.0)
+        ops.stencilk_step(K, out, T, iCp, coef(), [(1, nx - 1, y0, y1)], tn)
+        got = out[y0:y1].cpu()
+        # the CPU twin on the dependency rows [y0-K, y1+K) clipped to the tile
+        a0, a1 = max(0, y0 - K), min(ny, y1 + K)
+        Ts, Cs = T[a0:a1].cpu(), iCp[a0:a1].cpu()
+        ref = torch.full_like(Ts, -7.0)
+        ops.stencilk_step(K, ref, Ts, Cs, coef(), [(1, nx - 1, y0 - a0, y1 - a0)],
+                          ops.StencilTuning(kernel=twin))
+        want = ref[y0 - a0:y1 - a0]
+        # columns 0 and nx-1 are boundary cells (not written): compare inner ones
+        assert torch.equal(got[:, 1:nx - 1], want[:, 1:nx - 1]), (kern, K, y0)
+        assert bool((got[:, 0] == -7.0).all()) and bool((got[:, nx - 1] == -7.0).all())
 
 
 @pytest.mark.parametrize("kern", ["fast5p2", "fast5p4", "fast5p8"])
