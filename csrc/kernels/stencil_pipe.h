@@ -111,8 +111,14 @@ constexpr int kArFast6Reg = 5, kArFast7Reg = 6;
 // lab A/B: kArFast5Reg with the row loop unrolled by 3 in every stage (the
 // round-3 piper; see kU6 below), bitwise equal to piper
 constexpr int kArFast5RegU3 = 7;
+// isotropic grids (ry = (dx/dy)^2 == 1 exactly, e.g. N = 1, the 2x2 grid):
+// fma(ry, U+D, t) as the add (U+D) + t -- bitwise the same (1 * x is exact,
+// one rounding either way), one fp64 multiplier use fewer per update; the
+// host selects it only when ry == 1 (kernel 17 "piper_iso")
+constexpr int kArFast5RegIso = 8;
 constexpr bool ar_reg(int Ar) {
-  return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3;
+  return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
+         Ar == kArFast5RegIso;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -590,8 +596,13 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
 #pragma unroll
           for (int v = 0; v < V; ++v) t[v] = __builtin_fma(mkc, c[v], sx[v]);
           __builtin_amdgcn_sched_barrier(0);
+          if constexpr (Ar == kArFast5RegIso) {
 #pragma unroll
-          for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, sy[v], t[v]);
+            for (int v = 0; v < V; ++v) t[v] = sy[v] + t[v];
+          } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, sy[v], t[v]);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

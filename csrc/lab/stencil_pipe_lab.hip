@@ -17,7 +17,9 @@
 //     two; kernels 14 / 15, bitwise equal to each other and to
 //     stencil6_rects_cpu), K = 20, 24;
 //   * piper_u3 (kernel 16): piper with the row loop unrolled by 3 in every
-//     stage (the round-3 kernel; the core's K = 17..20 unroll by 6), A/B.
+//     stage (the round-3 kernel; the core's K = 17..20 unroll by 6), A/B;
+//   * piper_iso (kernel 17): piper with fma(1, U+D, t) as an add, for
+//     ry == 1 exactly (bitwise equal to piper there), K = 20, 24.
 #include "../kernels/lab_hooks.h"
 
 namespace rma {
@@ -43,6 +45,8 @@ bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(18, 4, kArFast5RegU3)
   RMA_PIPE_CASE(19, 4, kArFast5RegU3)
   RMA_PIPE_CASE(20, 4, kArFast5RegU3)
+  RMA_PIPE_CASE(20, 4, kArFast5RegIso)
+  RMA_PIPE_CASE(24, 4, kArFast5RegIso)
   return false;
 }
 

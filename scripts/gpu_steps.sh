@@ -119,9 +119,16 @@ for s in "$@"; do
              --pipec "" --ldsdpp "" --old "" --alt "" \
              --kinds piper:17,piper:18,piper:19,piper:20,piper_u3:17,piper_u3:18,piper_u3:19,piper_u3:20 \
              --out "$OUT/u6_ab.json" || exit 1 ;;
+    iso_ab) step iso_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
+             --pipec "" --ldsdpp "" --old "" --alt "" --coef-dims 1,1 \
+             --kinds piper:20,piper:24,piper_iso:20,piper_iso:24,piper_u3:20 \
+             --out "$OUT/iso_ab.json" || exit 1 ;;
+    eqsmall) for t in eqn4096_x eqn4096_x_cd2 eqn4096_xy eqn4096_xy_cd2 eqn4096_xy_strips \
+                      eqn8192_xy eqn8192_xy_cd2; do bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
+             "tests/test_pipe_gpu.py::test_piper_iso_bitwise_and_refused_when_anisotropic" \
              "tests/test_pipe_gpu.py::test_piper_register_factors_bitwise" \
              "tests/test_temporal_gpu.py::test_headline_kernels_beyond_2e31_cells" \
              -p no:cacheprovider || exit 1 ;;

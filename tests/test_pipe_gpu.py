@@ -348,3 +348,27 @@ def test_piper_unroll6_equals_unroll3(nx, K):
         a = gpu_run(K, T, iCp, rects, "piper", chunk=chunk)
         b = gpu_run(K, T, iCp, rects, "piper_u3", chunk=chunk)
         assert torch.equal(a, ref) and torch.equal(b, ref)
+
+
+@pytest.mark.parametrize("nx", [518, 1028])
+@pytest.mark.parametrize("K", [20, 24])
+def test_piper_iso_bitwise_and_refused_when_anisotropic(nx, K):
+    """piper_iso (lab, kernel 17: the y-sum FMA by ry = 1 as an add) on an
+    isotropic grid == piper == the fast5 CPU twin, bitwise; refused for
+    ry != 1."""
+    ny = 149
+    T, iCp = rand((ny, nx), 61 + K), rand((ny, nx), 62, 0.5, 1.0)
+    d = 0.039
+    iso = ops.StencilCoef(-1.3, 1 / d, 1 / d, 0.00028)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = torch.full_like(T, -5.0)
+    ops.stencilk_step(K, ref, T, iCp, iso, rects, ops.StencilTuning(kernel="pipe"))
+    for kern in ("piper", "piper_iso"):
+        out = torch.full(T.shape, -5.0, dtype=torch.float64, device=DEV)
+        ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), iso, rects,
+                          ops.StencilTuning(kernel=kern, xcd_remap=1, chunk_rows=37, vec=4))
+        assert torch.equal(out.cpu(), ref), kern
+    with pytest.raises(Exception, match="isotropic"):
+        out = torch.zeros(T.shape, dtype=torch.float64, device=DEV)
+        ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(), rects,
+                          ops.StencilTuning(kernel="piper_iso", xcd_remap=1, chunk_rows=37, vec=4))
