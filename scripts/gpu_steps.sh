@@ -125,6 +125,11 @@ for s in "$@"; do
              --out "$OUT/iso_ab.json" || exit 1 ;;
     eqsmall) for t in eqn4096_x eqn4096_x_cd2 eqn4096_xy eqn4096_xy_cd2 eqn4096_xy_strips \
                       eqn8192_xy eqn8192_xy_cd2; do bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    eqsmall2) for t in eqn4096_xy_cd2_bol eqn4096_xy_bol eqn4096_xy_cd4_bol eqn4096_x_cd4 \
+                      eqn4096_y eqn4096_y_cd2 eqn4096_y_bol eqn8192_xy_cd4 eqn8192_xy_cd2_bol \
+                      eqn8192_x eqn8192_x_cd2 eqn8192_y eqn8192_y_cd2 eqn16384_xy eqn16384_xy_cd2 \
+                      eqn2048_xy eqn2048_xy_cd2 eqn2048_xy_strips; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
@@ -155,10 +160,11 @@ for s in "$@"; do
     eq16k_x|eq16k_y|eq16k_xy) d=${s#eq16k_}
              step "$s" 300 python bench/rccl_self_overhead.py --n 16384 --K 24 --periodic "$d" \
              --steps 960 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
-    eqn*) # eqn<N>_<dims>[_strips|_cd<D>]: N^2 tile, K=24, equal coefficients
-             t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""
-             case $t in *_strips) fa=0 ;; *_cd*) cd=${t##*_cd} ;; esac
-             RMA_FRAME_CHUNK_DIV=$cd RMA_FRAME_ALIGNED=$fa step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
+    eqn*) # eqn<N>_<dims>[_strips][_cd<D>][_bol|_btask]: N^2 tile, K=24, equal coefficients
+             t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""; fb=""
+             for tok in ${t//_/ }; do case $tok in strips) fa=0 ;; cd*) cd=${tok#cd} ;;
+               bol) fb=ol ;; btask) fb=task ;; esac; done
+             RMA_FRAME_BANDS=$fb RMA_FRAME_CHUNK_DIV=$cd RMA_FRAME_ALIGNED=$fa step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
              --periodic "$d" --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     chunk_sweep) step chunk_sweep 400 python bench/pass_sweep.py --pipe 20,24 --pipec "" \
              --ldsdpp "" --old "" --alt "" --rounds 3 \
