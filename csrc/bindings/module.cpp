@@ -402,6 +402,13 @@ PYBIND11_MODULE(_C, m) {
       py::arg("nx"), py::arg("ny"), py::arg("K"), py::arg("neighbors"), py::arg("hide"),
       py::arg("bwx"), py::arg("bwy"), py::arg("olx"), py::arg("oly"));
   m.def(
+      "frame_layout",
+      [](int64_t ny, std::array<std::array<int, 2>, 3> nbr) {
+        const FrameLayout f = frame_layout(ny, nbr);
+        return std::make_tuple(f.chunk_div, f.bands);
+      },
+      py::arg("ny"), py::arg("neighbors"));
+  m.def(
       "canonical_kernel_k",
       [](int K, int64_t ny) {
         const StencilTuning t = canonical_tune_k(K, ny);

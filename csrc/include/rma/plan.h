@@ -59,9 +59,26 @@ struct PassGeom {
 // first / last strip column and chunk row (a few % of the tile) instead of
 // ol-wide strips, which a trapezoid kernel computes at several times the
 // interior's cost per cell.
+// bands: height of the aligned y-bands, -1 = the default / RMA_FRAME_BANDS,
+// 0 = the ol-K rows the exchange needs, 1 = whole task rows.
 PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool hide,
                        int64_t bwx, int64_t bwy, int64_t olx, int64_t oly, int64_t task_w = 0,
-                       int64_t task_h = 0, int vec = 1);
+                       int64_t task_h = 0, int vec = 1, int bands = -1);
+
+// Aligned frame layout per tile class and neighbour set (perf_hide K-step
+// passes, measured: RCCL-self overhead at K = 24, equal coefficients,
+// profiles/SUMMARY_r4.md section 3): the frame launch's rows per task as a
+// divisor of the interior's (chunk_div) and the y-band height (bands, as
+// above). Below ~1 wave of tasks per pass every task runs concurrently, so a
+// frame of whole interior tasks finishes with the interior and the exchange
+// is exposed; half-height frame tasks finish at ~60 % of the pass (4096^2:
+// x 10.5 -> 1.1 %, y 7.6 -> 3.1 %, x+y 17.6 -> 2.2 % with ol-K bands).
+// RMA_FRAME_CHUNK_DIV / RMA_FRAME_BANDS override.
+struct FrameLayout {
+  int chunk_div = 1;
+  int bands = -1;
+};
+FrameLayout frame_layout(int64_t ny, const Neighbors& nbr);
 
 // Relative cost of one pass of K steps (index K = 1..Kmax; index 0 unused;
 // +inf = no kernel), in units of one HBM sweep of the 3 arrays. Measured on

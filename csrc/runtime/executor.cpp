@@ -226,7 +226,7 @@ const PassGeom& DiffusionExecutor::geometry(int K) {
       th = t.chunk_rows;
     }
     geom_[K] = pass_geometry(nx_, ny_, K, nbr_, p_.mode == Mode::kHide, p_.bwx, p_.bwy, p_.olx,
-                             p_.oly, tw, th, vec);
+                             p_.oly, tw, th, vec, frame_layout(ny_, nbr_).bands);
     geom_ok_[K] = 1;
   }
   return geom_[K];
@@ -261,15 +261,10 @@ StencilTuning DiffusionExecutor::pass_tuning(int K, int part) const {
 }
 
 int DiffusionExecutor::frame_chunk_rows(int K, int interior_rows) const {
-  // RMA_FRAME_CHUNK_DIV=d: the aligned frame's tasks take 1/d of the
-  // interior's rows (A/B knob; default 1)
-  static const int div = [] {
-    const char* e = std::getenv("RMA_FRAME_CHUNK_DIV");
-    const int d = e ? std::atoi(e) : 0;
-    return d >= 1 ? d : 1;
-  }();
+  // the aligned frame's tasks: 1/chunk_div of the interior's rows (plan.cpp
+  // frame_layout: per tile class and neighbour set, measured)
   (void)K;
-  return std::max(1, interior_rows / div);
+  return std::max(1, interior_rows / frame_layout(ny_, nbr_).chunk_div);
 }
 
 void DiffusionExecutor::exchange(double* A, stream_t s) {

@@ -56,9 +56,29 @@ Rect owned_rect(int64_t nx, int64_t ny, int K, const Neighbors& nbr) {
   return r;
 }
 
+FrameLayout frame_layout(int64_t ny, const Neighbors& nbr) {
+  const bool x = nbr[0][0] >= 0 || nbr[0][1] >= 0, y = nbr[1][0] >= 0 || nbr[1][1] >= 0;
+  FrameLayout f;
+  // 4096^2 class (one wave of tasks per K=24 pass): half-height frame tasks,
+  // and with x AND y neighbours ol-K bands (whole-task-row bands at half
+  // height overflow the wave: x+y 29.6 %). 8192^2 class (~2.5 waves): half
+  // height helps the bands (y 8.2 -> 4.9 %, x+y 8.2 -> 5.7 %), not the tall
+  // x frames (0.8 -> 6.2 %). 2048^2 (47 -> 58 %) and >= 16384^2 (x+y 0.7 ->
+  // 5.8 %): whole tasks.
+  if (ny >= 3072 && ny < 6144) {
+    f.chunk_div = 2;
+    if (x && y) f.bands = 0;
+  } else if (ny >= 6144 && ny < 12288 && y) {
+    f.chunk_div = 2;
+  }
+  static const char* cd = std::getenv("RMA_FRAME_CHUNK_DIV");
+  if (cd && cd[0]) f.chunk_div = std::max(1, std::atoi(cd));
+  return f;
+}
+
 PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool hide,
                        int64_t bwx, int64_t bwy, int64_t olx, int64_t oly, int64_t task_w,
-                       int64_t task_h, int vec) {
+                       int64_t task_h, int vec, int bands) {
   PassGeom g;
   g.out = K == 1 ? Rect{1, nx - 1, 1, ny - 1} : owned_rect(nx, ny, K, nbr);
   const bool any_nbr = nbr[0][0] >= 0 || nbr[0][1] >= 0 || nbr[1][0] >= 0 || nbr[1][1] >= 0;
@@ -82,7 +102,7 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
   static const char* fa = std::getenv("RMA_FRAME_ALIGNED");
   static const char* fb = std::getenv("RMA_FRAME_BANDS");
   const bool want = fa && fa[0] ? fa[0] != '0' : true;
-  const bool task_bands = fb && fb[0] ? fb[0] == 't' : task_h <= 1024;
+  const bool task_bands = fb && fb[0] ? fb[0] == 't' : bands >= 0 ? bands == 1 : task_h <= 1024;
   const int64_t band = task_bands ? task_h : need_y;  // y-band height
   if (want && hide && any_nbr && task_w >= need_x && task_h >= 1 && band >= need_y &&
       o.x1 - o.x0 >= 3 * task_w && o.y1 - o.y0 >= (task_bands ? 3 * task_h : 2 * band + 1)) {

@@ -130,6 +130,10 @@ for s in "$@"; do
                       eqn8192_x eqn8192_x_cd2 eqn8192_y eqn8192_y_cd2 eqn16384_xy eqn16384_xy_cd2 \
                       eqn2048_xy eqn2048_xy_cd2 eqn2048_xy_strips; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    eqdefault) for t in eqn4096_x eqn4096_y eqn4096_xy eqn8192_x eqn8192_y eqn8192_xy eqn16384_xy; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    tests_frames) step tests_frames 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread \
+             "tests/test_multirank_gpu.py" -p no:cacheprovider || exit 1 ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \

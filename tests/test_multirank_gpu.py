@@ -463,3 +463,33 @@ def test_graph_replay_matches_eager_periodic(K, gs, nt, fast):
         gg.finalize_global_grid()
         return f
     assert torch.equal(run(True), run(False))
+
+
+@pytest.mark.parametrize("dims,ny", [((2, 2), 3500), ((1, 2), 3500), ((2, 1), 3500),
+                                     ((1, 2), 7000)])
+def test_small_tile_frame_layouts_bitwise(dims, ny):
+    """The per-tile frame layout (plan.cpp frame_layout):
+    4096-class tiles run half-height frame tasks (ol-K bands with x AND y
+    neighbours), 8192-class tiles with y neighbours half-height frame tasks;
+    every tile == its window of the 1-rank run, bitwise."""
+    from rocm_mpi_amd._native import native
+
+    K, nx, nt = 24, 1100, 53
+    P = dims[0] * dims[1]
+    res = run_loopback(P, spmd_bands, nx, ny, nt, dims, K, 0, timeout=240)
+    nxg, nyg, _ = res[0][2]
+    one = run_loopback(1, spmd_bands, nxg, nyg, nt, (1, 1), K, 0, timeout=240)[0][1]
+    for coords, T, _, geo in res:
+        nb = [[-1, -1], [-1, -1], [-1, -1]]
+        for d in (0, 1):
+            if dims[d] > 1:
+                nb[d] = [0 if coords[d] > 0 else -1, 0 if coords[d] < dims[d] - 1 else -1]
+        div, bands = native().frame_layout(ny, nb)
+        assert div == 2
+        assert bands == (0 if (dims[0] > 1 and dims[1] > 1 and ny < 6144) else -1)
+        assert geo["aligned"], (coords, geo)
+        if bands == 0:
+            for r in geo["frame_wide"]:
+                assert r[3] - r[2] < 2 * K
+        gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
+        assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
