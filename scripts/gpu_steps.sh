@@ -134,6 +134,14 @@ for s in "$@"; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     tests_frames) step tests_frames 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread \
              "tests/test_multirank_gpu.py" -p no:cacheprovider || exit 1 ;;
+    chunk20) step chunk20 600 python bench/pass_sweep.py --n 101120 --rounds 5 --pipe "" \
+             --kinds piper:20:2560,piper:20:2816,piper:20:2890,piper:20:2976,piper:20,piper:20:3160,piper:20:3328 \
+             --pipec "" --ldsdpp "" --old "" --alt "" --out "$OUT/chunk20.json" || exit 1 ;;
+    u6_small) for n in 16384 8192 4096; do
+               step u6_$n 600 python bench/pass_sweep.py --n $n --rounds 9 --pipe "" --pipec "" \
+               --ldsdpp "" --old "" --alt "" \
+               --kinds piper:17,piper:18,piper:19,piper:20,piper_u3:17,piper_u3:18,piper_u3:19,piper_u3:20 \
+               --out "$OUT/u6_$n.json" || exit 1; done ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
