@@ -59,6 +59,10 @@ def main(argv=None):
     ap.add_argument("--coef-alt", default="",
                     help="a second coefficient grid (e.g. 1,1): every kernel is timed at both, "
                          "interleaved in the same rounds (rows tagged with coef_dims)")
+    ap.add_argument("--exec", dest="exec_k", default="",
+                    help="depths timed with the executor's own fast-math kernel and tuning "
+                         "(native fast_kernel_k: ring kernel or piper, chunk rows); rows "
+                         "kernel='exec' (the planner's cost table input, scripts/fit_pass_costs.py)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -121,6 +125,7 @@ def main(argv=None):
             cfgs.append(("pipec", int(K), 0, int(c)))
     cfgs += [("pipe2", K, 0) for K in krange(a.pipe2)]
     cfgs += [("pipe5", K, 0) for K in krange(a.pipe5)]
+    cfgs += [("exec", K, 0) for K in krange(a.exec_k)]
     for item in filter(None, a.kinds.split(",")):
         k, K, *c = item.split(":")  # kernel:K[:chunk_rows]
         cfgs.append((k, int(K), 0, int(c[0])) if c else (k, int(K), 0))
@@ -134,6 +139,7 @@ def main(argv=None):
             cfgs.append(("pipe2", int(K), 0, int(c)))
 
     rect = [ops.interior_rect(n, n)]
+    names = {v: k for k, v in {**ops.KERNELS, **ops.LAB_KERNELS}.items()}
     # every configuration at every coefficient grid: (spec, kind, K, S[, chunk])
     cfgs = [(cs,) + c for c in cfgs for cs in coefs]
 
@@ -143,6 +149,10 @@ def main(argv=None):
             ops.stencil_step(T2, T, iCp, coef, rect, ops.StencilTuning())
         elif kind == "two_step":
             ops.stencil2_step(T2, T, iCp, coef, rect, ops.StencilTuning(chunk_rows=16, unroll=2))
+        elif kind == "exec":
+            kid, vec, ch = N.fast_kernel_k(K, n, tuple(coef))
+            tn = ops.StencilTuning(chunk_rows=ch, kernel=names[kid], vec=vec, xcd_remap=1)
+            ops.stencilk_step(K, T2, T, iCp, coef, rect, tn)
         else:
             vec = 2 if kind in ("lds_dpp", "fast5") else 5 if kind == "pipe5" else 4
             tn = ops.StencilTuning(chunk_rows=chunk(K, c, kind),
@@ -172,11 +182,13 @@ def main(argv=None):
         cs, c = c[0], c[1:]
         kind, K, S = c[:3]
         med = statistics.median(times[(cs,) + c])
+        ek = (names[N.fast_kernel_k(K, n, tuple(coefs[cs]))[0]] if kind == "exec" else None)
         rows.append({"coef_dims": cs, "ry": round(ops.fast5_constants(coefs[cs])[0], 6),
-                     "kernel": kind, "K": K, "stages": S or (native().pipe_default_stages(K)
+                     "kernel": kind, "exec_kernel": ek, "K": K, "stages": S or (native().pipe_default_stages(K)
                                                              if kind in ops.PIPE + ("pipe2", "pipe5")
                                                              else 0),
-                     "chunk_rows": (chunk(K, c[3] if len(c) > 3 else 0, kind)
+                     "chunk_rows": (N.fast_kernel_k(K, n, tuple(coefs[cs]))[2] if kind == "exec"
+                                    else chunk(K, c[3] if len(c) > 3 else 0, kind)
                                     if kind not in ("march", "two_step") else None),
                      "vec": (N.pipe_vec(K, S, 0, n, 5, True) if kind == "pipe5" else None),
                      "ms_per_pass": round(med, 3), "ms_min": round(min(times[(cs,) + c]), 3),

@@ -42,8 +42,11 @@ def tables(path: str):
         return None
 
     from_default = {}
-    for r in rows:  # first (default-chunk, default-stage) row per depth
-        if r["kernel"] == "pipe" and r["K"] not in from_default:
+    # the executor's own kernel per depth (pass_sweep.py --exec) when present,
+    # else the first (default-chunk, default-stage) ring-kernel row per depth
+    src = "exec" if any(r["kernel"] == "exec" for r in rows) else "pipe"
+    for r in rows:
+        if r["kernel"] == src and r["K"] not in from_default:
             from_default[r["K"]] = r["rel"]
     fast = fill(from_default)
     can = {1: 1.0}

@@ -142,6 +142,9 @@ for s in "$@"; do
                --ldsdpp "" --old "" --alt "" \
                --kinds piper:17,piper:18,piper:19,piper:20,piper_u3:17,piper_u3:18,piper_u3:19,piper_u3:20 \
                --out "$OUT/u6_$n.json" || exit 1; done ;;
+    exec_costs) for n in 101120 16384 8192 4096; do
+               step exec_$n 600 python bench/pass_sweep.py --n $n --rounds 7 --pipe "" --pipec "" \
+               --ldsdpp "" --old "" --alt "" --exec 1-24 --out "$OUT/exec_$n.json" || exit 1; done ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
