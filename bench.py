@@ -727,7 +727,7 @@ def run(a, world: int, rank: int) -> int:
                                                  "RMA_FRAME_FILL", "RMA_EXEC_STREAMS",
                                                  "RMA_PIPE_FAST", "RMA_HALO_CROSS",
                                                  "RMA_FRAME_BANDS", "RMA_RCCL_LIB",
-                                                 "RMA_FAST_FORM")}
+                                                 "RMA_FRAME_CHUNK_DIV")}
     if gpu and os.environ.get("RMA_PIPE_FAST") == "pipe5":  # an A/B of the lab kernel
         from rocm_mpi_amd._native import load_lab
 
