@@ -116,9 +116,13 @@ constexpr int kArFast5RegU3 = 7;
 // one rounding either way), one fp64 multiplier use fewer per update; the
 // host selects it only when ry == 1 (kernel 17 "piper_iso")
 constexpr int kArFast5RegIso = 8;
+// diagnosis only (lab, WRONG results): piper whose stage 0 runs H-1 levels
+// (stage 0 also streams T / 1/Cp and forms the factors: is it the block's
+// critical path at the per-row barrier?)
+constexpr int kArDiagS0 = 9;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
-         Ar == kArFast5RegIso;
+         Ar == kArFast5RegIso || Ar == kArDiagS0;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -438,7 +442,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     constexpr int Pr = Ps % 3;                // phase of the 3-row windows w
     constexpr bool S0 = decltype(S0c)::value;
     constexpr bool LAST = decltype(LASTc)::value;
-    constexpr int NL = LAST ? HL : H;  // levels of this stage
+    constexpr int NL = LAST ? HL : (S0 && Ar == kArDiagS0 ? H - 1 : H);  // levels of this stage
     constexpr int PC = (Pr + 2) % 3, PU = (Pr + 1) % 3;
     double g[V];
     if constexpr (S0) {

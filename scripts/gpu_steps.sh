@@ -145,6 +145,9 @@ for s in "$@"; do
     exec_costs) for n in 101120 16384 8192 4096; do
                step exec_$n 600 python bench/pass_sweep.py --n $n --rounds 7 --pipe "" --pipec "" \
                --ldsdpp "" --old "" --alt "" --exec 1-24 --out "$OUT/exec_$n.json" || exit 1; done ;;
+    diag_s0) step diag_s0 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
+             --pipec "" --ldsdpp "" --old "" --alt "" --kinds piper:20,piper_diag_s0:20 \
+             --out "$OUT/diag_s0.json" || exit 1 ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
