@@ -93,6 +93,28 @@ def apply_ratios(fast: list, ratios: dict, kmin: int) -> list:
 
 PIPER_SWEEPS_101376 = ["r3/pass_sweep_piper_lowK_101120.json", "r3/pass_sweep_piper_glds_boxE.json"]
 
+# round 4: piper's row loop unrolled by 6 at K = 17..20; same-box A/B against the
+# round-3 unroll by 3 (lab kernel piper_u3) per tile class
+U6_SWEEPS = {101376: "r4/u6_ab_all_stages.json", 16384: "r4/u6_16384.json",
+             8192: "r4/u6_8192.json", 4096: "r4/u6_4096.json"}
+
+
+def u6_ratios(path: str) -> dict:
+    """Per-depth piper / piper_u3 pass-time ratios of one same-run sweep."""
+    rows = json.load(open(path))["rows"]
+    u3 = {x["K"]: x["ms_per_pass"] for x in rows if x["kernel"] == "piper_u3"}
+    return {x["K"]: x["ms_per_pass"] / u3[x["K"]] for x in rows
+            if x["kernel"] == "piper" and x["K"] in u3}
+
+
+def apply_u6(fast: list, ratios: dict) -> list:
+    """Scale the measured depths (K = 17..20) by the unroll-by-6 ratios
+    (rounded to the table's 3 decimals after the round-3 scaling, as committed)."""
+    out = list(fast)
+    for K, f in ratios.items():
+        out[K - 1] = round(round(fast[K - 1], 3) * f, 3)
+    return out
+
 
 def fmt(name, vals):
     body = ", ".join(f"{v:.3f}" for v in vals)

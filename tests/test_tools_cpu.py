@@ -31,6 +31,8 @@ def test_planner_tables_come_from_the_committed_sweeps(tile):
     if tile == 101376:  # round 3: piper from K = 10, scaled by its measured ratios to pipe
         fast = fpc.apply_ratios(fast, fpc.piper_ratios(
             [os.path.join(P, q) for q in fpc.PIPER_SWEEPS_101376]), 10)
+    # round 4: K = 17..20 scaled by the unroll-by-6 / unroll-by-3 ratios
+    fast = fpc.apply_u6(fast, fpc.u6_ratios(os.path.join(P, fpc.U6_SWEEPS[tile])))
     cells = float(tile) * tile
     got_f = list(N.default_pass_costs(24, True, cells))[1:]
     got_c = list(N.default_pass_costs(24, False, cells))[1:]
