@@ -148,6 +148,9 @@ for s in "$@"; do
     diag_s0) step diag_s0 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
              --pipec "" --ldsdpp "" --old "" --alt "" --kinds piper:20,piper_diag_s0:20 \
              --out "$OUT/diag_s0.json" || exit 1 ;;
+    trace8192y) prof trace8192y 300 --kernel-trace --output-format csv -d "$R/$OUT/trace8192y" \
+             -o run -- python3 "$R/bench/rccl_self_overhead.py" --n 8192 --K 24 --variants perf_hide \
+             --periodic y --steps 480 --pattern op --spacing equal --out "$R/$OUT/trace8192y.json" || exit 1 ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
