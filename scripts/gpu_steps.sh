@@ -151,6 +151,9 @@ for s in "$@"; do
     trace8192y) prof trace8192y 300 --kernel-trace --output-format csv -d "$R/$OUT/trace8192y" \
              -o run -- python3 "$R/bench/rccl_self_overhead.py" --n 8192 --K 24 --variants perf_hide \
              --periodic y --steps 480 --pattern op --spacing equal --out "$R/$OUT/trace8192y.json" || exit 1 ;;
+    eqsmall3) for t in eqn8192_y_bol eqn8192_y_cd2_bol eqn8192_y_cd3 eqn8192_y_cd4_bol eqn8192_xy_bol \
+                      eqn8192_xy_cd3 eqn8192_xy_cd4_bol eqn8192_y eqn8192_y_cd2 eqn16384_x eqn16384_y; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
