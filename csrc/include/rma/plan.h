@@ -72,7 +72,8 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
 // above). Below ~1 wave of tasks per pass every task runs concurrently, so a
 // frame of whole interior tasks finishes with the interior and the exchange
 // is exposed; half-height frame tasks finish at ~60 % of the pass (4096^2:
-// x 10.5 -> 1.1 %, y 7.6 -> 3.1 %, x+y 17.6 -> 2.2 % with ol-K bands).
+// x 10.5 -> 1.1 %, y 7.6 -> 3.1 %, x+y 17.6 -> 2.2 % with ol-K bands; 8192^2
+// y 8.2 -> 3.1 % with ol-K bands).
 // RMA_FRAME_CHUNK_DIV / RMA_FRAME_BANDS override.
 struct FrameLayout {
   int chunk_div = 1;

@@ -61,15 +61,18 @@ FrameLayout frame_layout(int64_t ny, const Neighbors& nbr) {
   FrameLayout f;
   // 4096^2 class (one wave of tasks per K=24 pass): half-height frame tasks,
   // and with x AND y neighbours ol-K bands (whole-task-row bands at half
-  // height overflow the wave: x+y 29.6 %). 8192^2 class (~2.5 waves): half
-  // height helps the bands (y 8.2 -> 4.9 %, x+y 8.2 -> 5.7 %), not the tall
-  // x frames (0.8 -> 6.2 %). 2048^2 (47 -> 58 %) and >= 16384^2 (x+y 0.7 ->
-  // 5.8 %): whole tasks.
+  // height overflow the wave: x+y 29.6 %). 8192^2 class (~2.5 waves): y only:
+  // ol-K bands (8.2 -> 3.1 %); x and y: half-height frame tasks (8.2 -> 5.7-
+  // 6.1 %, ol bands 6.1 %); x only: whole tasks (half height: 0.8 -> 6.2 %).
+  // 2048^2 (47 -> 58 %) and >= 16384^2 (x+y 0.7 -> 5.8 %): whole tasks.
   if (ny >= 3072 && ny < 6144) {
     f.chunk_div = 2;
     if (x && y) f.bands = 0;
   } else if (ny >= 6144 && ny < 12288 && y) {
-    f.chunk_div = 2;
+    if (x)
+      f.chunk_div = 2;
+    else
+      f.bands = 0;
   }
   static const char* cd = std::getenv("RMA_FRAME_CHUNK_DIV");
   if (cd && cd[0]) f.chunk_div = std::max(1, std::atoi(cd));
