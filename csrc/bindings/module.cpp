@@ -285,7 +285,8 @@ PYBIND11_MODULE(_C, m) {
       .def("coords", &CartTopology::coords)
       .def("rank_of", &CartTopology::rank_of)
       .def("shift", &CartTopology::shift)
-      .def("neighbors", &CartTopology::neighbors);
+      .def("neighbors", &CartTopology::neighbors)
+      .def("diagonals", &CartTopology::diagonals);
 
   // ---------------- communication ----------------
   py::enum_<DType>(m, "DType")
@@ -366,6 +367,17 @@ PYBIND11_MODULE(_C, m) {
             h.prepare(to_fields(fields), mask);
           },
           py::arg("fields"), py::arg("dims_mask") = 7)
+      .def(
+          "exchange_merged",
+          [](HaloExchanger& h, const std::vector<FieldT>& fields, uintptr_t s) {
+            auto f = to_fields(fields);
+            py::gil_scoped_release nogil;
+            h.exchange_merged(f, S(s));
+          },
+          py::arg("fields"), py::arg("stream"))
+      .def("set_diagonals", &HaloExchanger::set_diagonals)
+      .def_property_readonly("has_diagonals", &HaloExchanger::has_diagonals)
+      .def_property_readonly("diagonals", &HaloExchanger::diagonals)
       .def("active", &HaloExchanger::active)
       .def("capturable", &HaloExchanger::capturable)
       .def("set_self_via_transport", &HaloExchanger::set_self_via_transport)

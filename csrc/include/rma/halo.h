@@ -46,8 +46,21 @@ class HaloExchanger {
   // update reads no corner halo cell (one-step passes): one group instead of
   // one per dimension, i.e. one RCCL enqueue and one RCCL kernel per exchange.
   void exchange_cross(const std::vector<HaloField>& fields, stream_t stream, int dims_mask = 7);
+  // x and y in ONE group with the corner blocks sent straight to the diagonal
+  // neighbours (halo_plan.h plan_exchange_merged): exact corners like
+  // exchange(), half the groups. Needs set_diagonals(); 2D fields.
+  void exchange_merged(const std::vector<HaloField>& fields, stream_t stream);
   // Pre-allocate the pack buffers for this field set (call before capture).
   void prepare(const std::vector<HaloField>& fields, int dims_mask = 7);
+  // ranks at (x-1,y-1), (x+1,y-1), (x-1,y+1), (x+1,y+1) (CartTopology::diagonals)
+  void set_diagonals(const std::array<int, 4>& d) {
+    diag_ = d;
+    has_diag_ = true;
+    cache_.clear();
+  }
+  bool has_diagonals() const { return has_diag_; }
+  // bit of dims_mask that selects the merged plan (planned() cache key)
+  static constexpr int kMerged = 8;
 
   bool active(int dim) const;  // any neighbour in this dim?
   // Graph capture is possible when no message goes through a non-capturable
@@ -70,6 +83,7 @@ class HaloExchanger {
   // exchanges served from the plan cache / planned afresh (tests, diagnosis)
   int64_t plan_hits() const { return hits_; }
   int64_t plan_misses() const { return misses_; }
+  const std::array<int, 4>& diagonals() const { return diag_; }
 
  private:
   // One planned exchange: the host plan plus its copy batches with every
@@ -90,6 +104,8 @@ class HaloExchanger {
   P2PTransport* comm_;
   int self_;
   bool self_via_comm_ = false;
+  std::array<int, 4> diag_{-1, -1, -1, -1};
+  bool has_diag_ = false;
   std::array<std::array<int, 2>, 3> nbr_;
   std::vector<void*> bufs_;
   std::vector<size_t> buf_bytes_;

@@ -77,6 +77,19 @@ HaloPlan plan_exchange(const std::vector<HaloField>& fields,
                        const std::array<std::array<int, 2>, 3>& nbr, int self,
                        bool self_via_comm, int dims_mask);
 
+// x and y in ONE group (2D fields, z flat): edge planes restricted to the
+// cells outside the other dimension's halo, plus the hw_x x hw_y corner blocks
+// sent straight to the diagonal neighbours, so the corners need no second,
+// dimension-ordered group. Every halo cell receives the value the
+// dimension-ordered exchange gives it (host self test: bitwise equal). diag:
+// the ranks at (x-1,y-1), (x+1,y-1), (x-1,y+1), (x+1,y+1) (-1: none). One
+// HaloDimPlan (dim = -1) whose sends are ordered by (field, direction) and
+// receives by (field, the sender's direction), so every pair of ranks matches
+// its messages in issue order.
+HaloPlan plan_exchange_merged(const std::vector<HaloField>& fields,
+                              const std::array<std::array<int, 2>, 3>& nbr,
+                              const std::array<int, 4>& diag, int self, bool self_via_comm);
+
 // The plane copies of one phase of a dimension, as (element bytes, copy) in
 // plan order: phase 0 = self copies + packs (before the group; independent:
 // halo planes [0,hw), [n-hw,n) vs send planes [ol-hw,ol), [n-ol,n-ol+hw) with

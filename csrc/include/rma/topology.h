@@ -35,6 +35,9 @@ class CartTopology {
   std::array<int, 2> shift(int rank, int dim) const;
   // neighbours[dim][0] = low side, [1] = high side (kProcNull at open edges)
   std::array<std::array<int, 2>, 3> neighbors(int rank) const;
+  // the x-y diagonal neighbours (x-1,y-1), (x+1,y-1), (x-1,y+1), (x+1,y+1)
+  // (kProcNull outside an open edge), for the merged halo exchange
+  std::array<int, 4> diagonals(int rank) const;
 
  private:
   int nprocs_;

@@ -89,6 +89,7 @@ int rma_init_global_grid(int nx, int ny, int nz, const int dims[3], const int pe
     }
     rma::set_rank_for_errors(rank);
     g->halo = std::make_unique<rma::HaloExchanger>(g->comm.get(), rank, g->topo->neighbors(rank));
+    g->halo->set_diagonals(g->topo->diagonals(rank));
     if (out_me) *out_me = rank;
     for (int d = 0; d < 3; ++d) {
       if (out_dims) out_dims[d] = g->dims[d];
@@ -294,6 +295,7 @@ int rma_grid_self_via_rccl(rma_grid* g) {
       g->comm = std::make_unique<rma::RcclComm>(1, 0, uid, g->device, init_timeout);
     }
     g->halo = std::make_unique<rma::HaloExchanger>(g->comm.get(), 0, g->topo->neighbors(0));
+    g->halo->set_diagonals(g->topo->diagonals(0));
     g->halo->set_self_via_transport(true);
   });
 }

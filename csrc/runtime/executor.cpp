@@ -296,10 +296,20 @@ void DiffusionExecutor::exchange(double* A, stream_t s) {
     const char* e = std::getenv("RMA_HALO_CROSS");
     return !(e && e[0] == '0');
   }();
-  // The last pass of a run() exchanges per dimension, so the arrays a run
-  // leaves behind have consistent corner halos (IGG update_halo! semantics).
+  // The last pass of a run() exchanges with exact corners, so the arrays a
+  // run leaves behind have consistent corner halos (IGG update_halo! semantics).
+  // With x AND y neighbours the exact exchange is ONE group with the corner
+  // blocks sent to the diagonal neighbours (halo_plan.h plan_exchange_merged)
+  // instead of one group per dimension (RMA_HALO_MERGED=0: per dimension).
+  static const bool merged_ok = [] {
+    const char* e = std::getenv("RMA_HALO_MERGED");
+    return !(e && e[0] == '0');
+  }();
+  const bool xy = (nbr_[0][0] >= 0 || nbr_[0][1] >= 0) && (nbr_[1][0] >= 0 || nbr_[1][1] >= 0);
   if (cross_ok && cross_pass_ && p_.temporal == 1 && p_.mode != Mode::kKp)
     halo_->exchange_cross({f}, s, 3);
+  else if (merged_ok && xy && halo_->has_diagonals())
+    halo_->exchange_merged({f}, s);
   else
     halo_->exchange({f}, s, 3);
 }
@@ -605,6 +615,8 @@ void DiffusionExecutor::build_graph(int64_t steps, int reps) {
     f.ol = {p_.olx, p_.oly, 2};
     f.hw = {hwx_, hwy_, 1};
     halo_->prepare({f}, 3);
+    if (halo_->has_diagonals()) halo_->prepare({f}, HaloExchanger::kMerged | 3);
+    halo_->prepare({f}, 3);  // (a larger merged slot may have reallocated: re-plan)
   }
   hipStream_t lo = S(s_lo_), hi = S(s_hi_);
   const int saved_parity = parity_;

@@ -70,7 +70,9 @@ const HaloExchanger::Planned& HaloExchanger::planned(const std::vector<HaloField
   c.dims_mask = dims_mask;
   // the order of operations is the host-only plan (halo_plan.cpp), which the
   // sanitizer self test also executes on host memory
-  c.plan = plan_exchange(fields, nbr_, self_, self_via_comm_, dims_mask);
+  c.plan = (dims_mask & kMerged)
+               ? plan_exchange_merged(fields, nbr_, diag_, self_, self_via_comm_)
+               : plan_exchange(fields, nbr_, self_, self_via_comm_, dims_mask);
   for (size_t s = 0; s < c.plan.slot_bytes.size(); ++s) buffer(s, c.plan.slot_bytes[s]);
   auto ptr = [&](const HaloMsg& m) -> void* {
     return m.slot >= 0 ? bufs_[m.slot]
@@ -134,6 +136,11 @@ void HaloExchanger::exchange(const std::vector<HaloField>& fields, stream_t stre
     launch_batches(c.batches[d][1], stream);
   }
   bytes_last_ = c.plan.bytes_sent;
+}
+
+void HaloExchanger::exchange_merged(const std::vector<HaloField>& fields, stream_t stream) {
+  RMA_CHECK_ARG(has_diag_, "merged halo exchange needs the diagonal neighbours (set_diagonals)");
+  exchange(fields, stream, kMerged | 3);
 }
 
 void HaloExchanger::exchange_cross(const std::vector<HaloField>& fields, stream_t stream,

@@ -1,5 +1,7 @@
 #include "rma/halo_plan.h"
 
+#include <algorithm>
+
 namespace rma {
 
 PlaneView plane_view(const HaloField& f, int dim, int64_t i0) {
@@ -72,6 +74,100 @@ HaloPlan plan_exchange(const std::vector<HaloField>& fields,
     }
     plan.dims.push_back(std::move(dp));
   }
+  return plan;
+}
+
+HaloPlan plan_exchange_merged(const std::vector<HaloField>& fields,
+                              const std::array<std::array<int, 2>, 3>& nbr,
+                              const std::array<int, 4>& diag, int self, bool self_via_comm) {
+  HaloPlan plan;
+  HaloDimPlan dp;
+  dp.dim = -1;
+  for (const auto& f : fields) {
+    validate_field(f);
+    RMA_CHECK_ARG(f.size[2] == 1, "merged x+y halo exchange: 2D fields only (nz = " << f.size[2]
+                                                                               << ")");
+  }
+  // direction k = (sy+1)*3 + (sx+1), k != 4; the message received from the
+  // neighbour at k was sent by it in direction 8 - k
+  auto peer_of = [&](int sx, int sy) {
+    if (sy == 0) return nbr[0][sx > 0];
+    if (sx == 0) return nbr[1][sy > 0];
+    return diag[(sy > 0 ? 2 : 0) + (sx > 0 ? 1 : 0)];
+  };
+  struct Msg {
+    int key;
+    HaloMsg m;
+  };
+  std::vector<Msg> sends, recvs;
+  for (int fi = 0; fi < (int)fields.size(); ++fi) {
+    const HaloField& f = fields[fi];
+    const int64_t nx = f.size[0], ny = f.size[1];
+    const int64_t olx = f.ol[0], oly = f.ol[1], hwx = f.hw[0], hwy = f.hw[1];
+    // sides with a halo exchange: a neighbour there and room for the planes
+    const bool hx = has_halo(f, 0), hy = has_halo(f, 1);
+    const bool on_x[2] = {hx && nbr[0][0] >= 0, hx && nbr[0][1] >= 0};
+    const bool on_y[2] = {hy && nbr[1][0] >= 0, hy && nbr[1][1] >= 0};
+    // the other dimension's extent of an edge plane: outside its halo
+    const int64_t x0 = on_x[0] ? hwx : 0, x1 = on_x[1] ? nx - hwx : nx;
+    const int64_t y0 = on_y[0] ? hwy : 0, y1 = on_y[1] ? ny - hwy : ny;
+    auto block = [&](int64_t c0, int64_t c1, int64_t r0, int64_t r1) {
+      return PlaneView{r0 * nx + c0, r1 - r0, c1 - c0, nx};
+    };
+    // the block sent toward direction (sx, sy) / received from it
+    auto send_block = [&](int sx, int sy) {
+      const int64_t c0 = sx == 0 ? x0 : sx < 0 ? olx - hwx : nx - olx;
+      const int64_t c1 = sx == 0 ? x1 : c0 + hwx;
+      const int64_t r0 = sy == 0 ? y0 : sy < 0 ? oly - hwy : ny - oly;
+      const int64_t r1 = sy == 0 ? y1 : r0 + hwy;
+      return block(c0, c1, r0, r1);
+    };
+    auto recv_block = [&](int sx, int sy) {
+      const int64_t c0 = sx == 0 ? x0 : sx < 0 ? 0 : nx - hwx;
+      const int64_t c1 = sx == 0 ? x1 : c0 + hwx;
+      const int64_t r0 = sy == 0 ? y0 : sy < 0 ? 0 : ny - hwy;
+      const int64_t r1 = sy == 0 ? y1 : r0 + hwy;
+      return block(c0, c1, r0, r1);
+    };
+    for (int k = 0; k < 9; ++k) {
+      if (k == 4) continue;
+      const int sx = k % 3 - 1, sy = k / 3 - 1;
+      if ((sx != 0 && !on_x[sx > 0]) || (sy != 0 && !on_y[sy > 0])) continue;
+      const int p = peer_of(sx, sy);
+      RMA_CHECK_ARG(p >= 0, "merged halo exchange: no rank at diagonal (" << sx << "," << sy
+                                                                         << ")");
+      const PlaneView sv = send_block(sx, sy), rv = recv_block(sx, sy);
+      if (sv.elems() == 0) continue;
+      if (p == self && !self_via_comm) {
+        // periodic self neighbour: my halo toward k <- my own block toward 8 - k
+        dp.copies.push_back({fi, rv, send_block(-sx, -sy)});
+        continue;
+      }
+      const size_t bytes = (size_t)sv.elems() * f.elem_bytes;
+      RMA_CHECK_ARG(rv.elems() == sv.elems(), "merged halo blocks differ in size");
+      HaloMsg sm{p, fi, sv, -1, bytes}, rm{p, fi, rv, -1, bytes};
+      if (!sv.contiguous()) {
+        sm.slot = (int)plan.slot_bytes.size();
+        plan.slot_bytes.push_back(bytes);
+        dp.packs.push_back({fi, sv, sm.slot});
+      }
+      if (!rv.contiguous()) {
+        rm.slot = (int)plan.slot_bytes.size();
+        plan.slot_bytes.push_back(bytes);
+        dp.unpacks.push_back({fi, rv, rm.slot});
+      }
+      sends.push_back({fi * 9 + k, sm});
+      recvs.push_back({fi * 9 + (8 - k), rm});
+      plan.bytes_sent += (int64_t)bytes;
+    }
+  }
+  auto by_key = [](const Msg& a, const Msg& b) { return a.key < b.key; };
+  std::stable_sort(sends.begin(), sends.end(), by_key);
+  std::stable_sort(recvs.begin(), recvs.end(), by_key);
+  for (const Msg& m : sends) dp.sends.push_back(m.m);
+  for (const Msg& m : recvs) dp.recvs.push_back(m.m);
+  if (!dp.copies.empty() || !dp.sends.empty() || !dp.recvs.empty())
+    plan.dims.push_back(std::move(dp));
   return plan;
 }
 

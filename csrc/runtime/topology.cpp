@@ -81,6 +81,18 @@ std::array<std::array<int, 2>, 3> CartTopology::neighbors(int rank) const {
   return {shift(rank, 0), shift(rank, 1), shift(rank, 2)};
 }
 
+std::array<int, 4> CartTopology::diagonals(int rank) const {
+  std::array<int, 4> out{};
+  const auto c = coords(rank);
+  for (int k = 0; k < 4; ++k) {
+    auto d = c;
+    d[0] += (k & 1) ? 1 : -1;
+    d[1] += (k & 2) ? 1 : -1;
+    out[k] = rank_of(d);
+  }
+  return out;
+}
+
 GridDesc make_grid_desc(int nx, int ny, int nz, const int dims[3], const int periods[3],
                         const int overlaps[3], const int halowidths[3], int nprocs, int rank) {
   RMA_CHECK_ARG(nprocs >= 1 && rank >= 0 && rank < nprocs, "rank " << rank << " of " << nprocs);

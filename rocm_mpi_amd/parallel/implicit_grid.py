@@ -240,6 +240,9 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
         halo = native().HaloExchanger(ncomm, me, [list(p) for p in neighbors])
         if self_via_transport:
             halo.set_self_via_transport(True)
+        # diagonal ranks: the executor's exact exchange with x AND y
+        # neighbours is then one group (corner blocks to the diagonals)
+        halo.set_diagonals(list(topo.diagonals(me)))
 
     g = GlobalGrid(nxyz=nxyz, nxyz_g=nxyz_g, dims=dims, overlaps=overlaps, halowidths=halowidths,
                    periods=periods, nprocs=comm_size, me=me, coords=coords, neighbors=neighbors,

@@ -90,6 +90,17 @@ class PyCartTopology:
     def neighbors(self, rank: int) -> list[list[int]]:
         return [self.shift(rank, d) for d in range(3)]
 
+    def diagonals(self, rank: int) -> list[int]:
+        """Ranks at (x-1,y-1), (x+1,y-1), (x-1,y+1), (x+1,y+1) (-1 outside)."""
+        c = self.coords(rank)
+        out = []
+        for k in range(4):
+            d = list(c)
+            d[0] += 1 if k & 1 else -1
+            d[1] += 1 if k & 2 else -1
+            out.append(self.rank_of(d))
+        return out
+
 
 def CartTopology(nprocs: int, dims: Sequence[int], periods: Sequence[int]):
     if has_native():

@@ -154,6 +154,15 @@ for s in "$@"; do
     eqsmall3) for t in eqn8192_y_bol eqn8192_y_cd2_bol eqn8192_y_cd3 eqn8192_y_cd4_bol eqn8192_xy_bol \
                       eqn8192_xy_cd3 eqn8192_xy_cd4_bol eqn8192_y eqn8192_y_cd2 eqn16384_x eqn16384_y; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    eqmerge) for t in eqn2048_xy eqn2048_xy_nomerge eqn4096_xy eqn4096_xy_nomerge eqn8192_xy \
+                      eqn8192_xy_nomerge eqn16384_xy eqn16384_xy_nomerge; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    eq_xy_nomerge) RMA_HALO_MERGED=0 step eq_xy_nomerge 400 python bench/rccl_self_overhead.py \
+             --K 24 --periodic xy --steps 320 --pattern opop --spacing equal \
+             --out "$OUT/eq_xy_nomerge.json" || exit 1 ;;
+    tests_merge) step tests_merge 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread \
+             tests/test_multirank_gpu.py tests/test_capi_gpu.py tests/test_bench_gpu.py \
+             -p no:cacheprovider || exit 1 ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
@@ -185,10 +194,11 @@ for s in "$@"; do
              step "$s" 300 python bench/rccl_self_overhead.py --n 16384 --K 24 --periodic "$d" \
              --steps 960 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     eqn*) # eqn<N>_<dims>[_strips][_cd<D>][_bol|_btask]: N^2 tile, K=24, equal coefficients
-             t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""; fb=""
+             t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""; fb=""; hm=""
              for tok in ${t//_/ }; do case $tok in strips) fa=0 ;; cd*) cd=${tok#cd} ;;
-               bol) fb=ol ;; btask) fb=task ;; esac; done
-             RMA_FRAME_BANDS=$fb RMA_FRAME_CHUNK_DIV=$cd RMA_FRAME_ALIGNED=$fa step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
+               bol) fb=ol ;; btask) fb=task ;; nomerge) hm=0 ;; esac; done
+             RMA_HALO_MERGED=$hm RMA_FRAME_BANDS=$fb RMA_FRAME_CHUNK_DIV=$cd RMA_FRAME_ALIGNED=$fa \
+             step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
              --periodic "$d" --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     chunk_sweep) step chunk_sweep 400 python bench/pass_sweep.py --pipe 20,24 --pipec "" \
              --ldsdpp "" --old "" --alt "" --rounds 3 \

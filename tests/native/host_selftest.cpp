@@ -51,9 +51,12 @@ bool throws(F&& f) {
 // of the global field. cross: the order of HaloExchanger::exchange_cross
 // (packs of every dimension, ONE group with all sends and receives, unpacks):
 // every cell must match except corners (cells in two dimensions' halos).
+// merged: plan_exchange_merged (x and y in one group, corner blocks to the
+// diagonal ranks), executed like cross; every cell, corners included, must match.
 int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<int, 3> n,
               std::array<int, 3> ol, std::array<int, 3> hw, int stagger_x, bool via_comm,
-              bool cross = false) {
+              bool cross = false, bool merged = false) {
+  const bool one_group = cross || merged;
   const int P = dims[0] * dims[1] * dims[2];
   CartTopology topo(P, dims, periods);
   std::array<int64_t, 3> ng;
@@ -116,7 +119,9 @@ int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<in
   std::vector<HaloPlan> plans(P);
   std::vector<std::vector<std::vector<double>>> bufs(P);
   for (int r = 0; r < P; ++r) {
-    plans[r] = plan_exchange(fields[r], topo.neighbors(r), r, via_comm, 7);
+    plans[r] = merged ? plan_exchange_merged(fields[r], topo.neighbors(r), topo.diagonals(r), r,
+                                             via_comm)
+                      : plan_exchange(fields[r], topo.neighbors(r), r, via_comm, 7);
     for (size_t b : plans[r].slot_bytes) bufs[r].push_back(std::vector<double>(b / 8, -9.0));
   }
   std::vector<std::vector<void*>> slots(P);
@@ -127,9 +132,10 @@ int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<in
   };
   // dimension by dimension on every rank (the plans list the same dims)
   std::map<std::pair<int, int>, std::deque<std::vector<char>>> wire;
-  if (cross) {
+  if (one_group) {
     for (int r = 0; r < P; ++r) {
-      if (plans[r].dims.size() != plans[0].dims.size()) return 101;
+      if (!merged && plans[r].dims.size() != plans[0].dims.size()) return 101;
+      if (merged && plans[r].dims.size() > 1) return 106;
       for (const HaloDimPlan& dp : plans[r].dims)
         for (const CopyBatch& b : batch_copies(dim_copies(dp, fields[r], slots[r], 0)))
           copy2d_batch_cpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes);
@@ -157,7 +163,7 @@ int halo_case(std::array<int, 3> dims, std::array<int, 3> periods, std::array<in
         for (const CopyBatch& b : batch_copies(dim_copies(dp, fields[r], slots[r], 1)))
           copy2d_batch_cpu(b.copies.data(), (int)b.copies.size(), b.elem_bytes);
   }
-  for (size_t k = 0; !cross && k < plans[0].dims.size(); ++k) {
+  for (size_t k = 0; !one_group && k < plans[0].dims.size(); ++k) {
     for (int r = 0; r < P; ++r) {
       if (plans[r].dims.size() != plans[0].dims.size()) return 101;
       const HaloDimPlan& dp = plans[r].dims[k];
@@ -474,6 +480,29 @@ int main() {
   EXPECT(halo_case({1, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, true, true) == 0);
   EXPECT(halo_case({2, 2, 1}, {1, 1, 0}, {6, 6, 1}, {2, 2, 2}, {1, 1, 1}, 1, true, true) == 0);
   EXPECT(halo_case({4, 2, 1}, {1, 1, 0}, {9, 8, 1}, {2, 2, 2}, {1, 1, 1}, 0, false, true) == 0);
+  // merged x+y exchange (one group, corner blocks to the diagonals): every
+  // cell incl. corners == the global field, open / periodic / mixed grids,
+  // self neighbours by copy and through the transport, staggered fields,
+  // width-K halos (2K overlaps) and a 4x2 grid of width-16 halos
+  EXPECT(halo_case({2, 2, 1}, {0, 0, 0}, {12, 10, 1}, {2, 2, 2}, {1, 1, 1}, 1, false, false, true) == 0);
+  EXPECT(halo_case({4, 2, 1}, {0, 0, 0}, {40, 36, 1}, {32, 32, 2}, {16, 16, 1}, 1, false, false, true) == 0);
+  EXPECT(halo_case({4, 2, 1}, {1, 1, 0}, {9, 8, 1}, {2, 2, 2}, {1, 1, 1}, 0, false, false, true) == 0);
+  EXPECT(halo_case({2, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, false, false, true) == 0);
+  EXPECT(halo_case({1, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, false, false, true) == 0);
+  EXPECT(halo_case({1, 1, 1}, {1, 1, 0}, {10, 9, 1}, {4, 4, 2}, {2, 2, 1}, 0, true, false, true) == 0);
+  EXPECT(halo_case({2, 2, 1}, {1, 1, 0}, {6, 6, 1}, {2, 2, 2}, {1, 1, 1}, 1, true, false, true) == 0);
+  EXPECT(halo_case({2, 2, 1}, {1, 0, 0}, {6, 6, 1}, {2, 2, 2}, {1, 1, 1}, 1, false, false, true) == 0);
+  EXPECT(halo_case({3, 2, 1}, {0, 1, 0}, {20, 18, 1}, {8, 8, 2}, {4, 4, 1}, 1, false, false, true) == 0);
+  EXPECT(halo_case({1, 3, 1}, {0, 0, 0}, {12, 14, 1}, {4, 4, 2}, {2, 2, 1}, 0, false, false, true) == 0);
+  EXPECT(halo_case({3, 1, 1}, {0, 0, 0}, {12, 14, 1}, {4, 4, 2}, {2, 2, 1}, 0, false, false, true) == 0);
+  {  // 3D fields are refused
+    HaloField f3;
+    f3.ptr = &f3;
+    f3.size = {8, 8, 4};
+    EXPECT(throws([&] {
+      plan_exchange_merged({f3}, {{{1, 1}, {1, 1}, {-1, -1}}}, {1, 1, 1, 1}, 0, false);
+    }));
+  }
   {
     HaloField f;
     EXPECT(throws([&] { plan_exchange({f}, {{{1, 1}, {-1, -1}, {-1, -1}}}, 0, false, 7); }));

@@ -496,3 +496,38 @@ def test_small_tile_frame_layouts_bitwise(dims, ny):
                 assert r[3] - r[2] < 2 * K
         gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
+
+
+@pytest.mark.parametrize("via_rccl", [False, True])
+@pytest.mark.parametrize("hw,ol", [(1, 2), (8, 16), (24, 48)])
+def test_merged_exchange_equals_dimension_ordered(via_rccl, hw, ol):
+    """HaloExchanger.exchange_merged (x and y in ONE group, the corner blocks
+    sent to the diagonal neighbours -- all of them this rank on a periodic
+    single-rank tile; through RCCL send/recv to itself or local copies) leaves
+    the field bitwise equal to the dimension-ordered exchange, corners
+    included."""
+    from rocm_mpi_amd._native import native
+    from rocm_mpi_amd.parallel import comm as C
+
+    n = native()
+    rc = C.RcclComm(torch.device("cuda", torch.cuda.current_device())) if via_rccl else None
+    nb = [[0, 0], [0, 0], [-1, -1]]
+    s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cpu").manual_seed(hw)
+    A = torch.rand(203, 331, generator=g, dtype=torch.float64).cuda()
+    B = A.clone()
+    f = lambda T: [(T.data_ptr(), [331, 203, 1], 8, [ol, ol, 2], [hw, hw, 1])]  # noqa: E731
+    h1 = n.HaloExchanger(rc.native if rc else None, 0, nb)
+    h2 = n.HaloExchanger(rc.native if rc else None, 0, nb)
+    for h in (h1, h2):
+        if via_rccl:
+            h.set_self_via_transport(True)
+        h.set_diagonals([0, 0, 0, 0])
+    h1.exchange(f(A), s, 3)
+    h2.exchange_merged(f(B), s)
+    torch.cuda.synchronize()
+    assert torch.equal(A, B)
+    assert not torch.equal(A, torch.rand(203, 331, generator=torch.Generator().manual_seed(hw),
+                                         dtype=torch.float64).cuda())  # the halos did change
+    if rc:
+        rc.finalize()
