@@ -77,10 +77,12 @@ HaloPlan plan_exchange(const std::vector<HaloField>& fields,
                        const std::array<std::array<int, 2>, 3>& nbr, int self,
                        bool self_via_comm, int dims_mask);
 
-// x and y in ONE group (2D fields, z flat): edge planes restricted to the
-// cells outside the other dimension's halo, plus the hw_x x hw_y corner blocks
-// sent straight to the diagonal neighbours, so the corners need no second,
-// dimension-ordered group. Every halo cell receives the value the
+// x and y in ONE group (2D fields, z flat): x planes restricted to the rows
+// outside the y halo, y planes as full contiguous rows (zero-copy; their
+// corner cells are rewritten after the group), plus the hw_x x hw_y corner
+// blocks sent straight to the diagonal neighbours and unpacked after the
+// group, so the corners need no second, dimension-ordered group (local
+// periodic copies: disjoint blocks, y planes restricted too). Every halo cell receives the value the
 // dimension-ordered exchange gives it (host self test: bitwise equal). diag:
 // the ranks at (x-1,y-1), (x+1,y-1), (x-1,y+1), (x+1,y+1) (-1: none). One
 // HaloDimPlan (dim = -1) whose sends are ordered by (field, direction) and

@@ -136,12 +136,21 @@ HaloPlan plan_exchange_merged(const std::vector<HaloField>& fields,
       const int p = peer_of(sx, sy);
       RMA_CHECK_ARG(p >= 0, "merged halo exchange: no rank at diagonal (" << sx << "," << sy
                                                                          << ")");
-      const PlaneView sv = send_block(sx, sy), rv = recv_block(sx, sy);
+      PlaneView sv = send_block(sx, sy), rv = recv_block(sx, sy);
       if (sv.elems() == 0) continue;
       if (p == self && !self_via_comm) {
         // periodic self neighbour: my halo toward k <- my own block toward 8 - k
+        // (disjoint blocks: the batched copies may run concurrently)
         dp.copies.push_back({fi, rv, send_block(-sx, -sy)});
         continue;
+      }
+      // a y message (sx = 0) through the transport takes the full rows: one
+      // contiguous zero-copy plane; the x-halo cells it carries (the sender's
+      // stale ones) are corners, rewritten by the corner unpacks after the group
+      const bool corner = sx != 0 && sy != 0;
+      if (sx == 0 && (on_x[0] || on_x[1])) {
+        sv = block(0, nx, sv.offset / nx, sv.offset / nx + sv.n_o);
+        rv = block(0, nx, rv.offset / nx, rv.offset / nx + rv.n_o);
       }
       const size_t bytes = (size_t)sv.elems() * f.elem_bytes;
       RMA_CHECK_ARG(rv.elems() == sv.elems(), "merged halo blocks differ in size");
@@ -151,7 +160,9 @@ HaloPlan plan_exchange_merged(const std::vector<HaloField>& fields,
         plan.slot_bytes.push_back(bytes);
         dp.packs.push_back({fi, sv, sm.slot});
       }
-      if (!rv.contiguous()) {
+      // corners and x planes always land after the group (never during it:
+      // a sender's full y rows include those cells)
+      if (corner || sx != 0 || !rv.contiguous()) {
         rm.slot = (int)plan.slot_bytes.size();
         plan.slot_bytes.push_back(bytes);
         dp.unpacks.push_back({fi, rv, rm.slot});
