@@ -159,6 +159,10 @@ class DiffusionExecutor {
   void* e_hi_ = nullptr;  // hipEvent_t
   void* e_lo_ = nullptr;
   void* e_in_ = nullptr;
+  // frame of the last overlapped pass done (s_hi, before its exchange): the
+  // next pass's interior waits for this instead of the exchange (lag_)
+  void* e_fr_ = nullptr;
+  bool lag_ = true;
   void* graph_exec_ = nullptr;  // hipGraphExec_t
   int64_t graph_len_ = 0;
   int parity_ = 0;

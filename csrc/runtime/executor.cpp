@@ -180,13 +180,23 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
             greatest, mode.c_str(), (void*)hi, (void*)lo);
   s_hi_ = hi;
   s_lo_ = lo;
-  hipEvent_t a, b, c;
+  hipEvent_t a, b, c, d;
   RMA_HIP_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
   RMA_HIP_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
   RMA_HIP_CHECK(hipEventCreateWithFlags(&c, hipEventDisableTiming));
+  RMA_HIP_CHECK(hipEventCreateWithFlags(&d, hipEventDisableTiming));
   e_hi_ = a;
   e_lo_ = b;
   e_in_ = c;
+  e_fr_ = d;
+  // The interior of pass n+1 reads cells >= K away from the halo (its rect is
+  // inset by the frame, >= ol - K = K cells) and writes the other buffer, so
+  // it depends on pass n's frame and interior, not on pass n's exchange: with
+  // the lag the exchange of pass n overlaps the interior of pass n+1 and only
+  // pass n+1's frame (same stream as the exchange) waits for it.
+  // RMA_EXEC_LAG=0: every pass waits for the previous exchange.
+  const char* lg = std::getenv("RMA_EXEC_LAG");
+  lag_ = !(lg && lg[0] == '0');
   const char* pr = std::getenv("RMA_EXEC_PRIME");
   if (!(pr && pr[0] == '0')) prime();
 }
@@ -197,6 +207,7 @@ DiffusionExecutor::~DiffusionExecutor() {
   if (e_hi_) (void)hipEventDestroy(E(e_hi_));
   if (e_lo_) (void)hipEventDestroy(E(e_lo_));
   if (e_in_) (void)hipEventDestroy(E(e_in_));
+  if (e_fr_) (void)hipEventDestroy(E(e_fr_));
   if (pooled_) {  // back to the pool, drained
     (void)hipStreamSynchronize(S(s_hi_));
     (void)hipStreamSynchronize(S(s_lo_));
@@ -351,9 +362,10 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
     return;
   }
   TraceRange tr("rma.step.hide");
-  // previous step fully done on both streams before this one touches T/T2
+  // the frame waits for the previous step on both streams; the interior for
+  // the previous frame and interior (lag_: not the previous exchange)
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
-  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(lag_ ? e_fr_ : e_hi_), 0));
   rec(0, s_hi_);
   StencilTuning ft = p_.tune;
   ft.chunk_rows = std::min(ft.chunk_rows, 16);
@@ -361,6 +373,7 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
     TraceRange tb("rma.boundary");
     stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, frame_.data(), (int)frame_.size(), c, ft, s_hi_);
   }
+  RMA_HIP_CHECK(hipEventRecord(E(e_fr_), S(s_hi_)));
   rec(1, s_hi_);
   {
     TraceRange th("rma.halo");
@@ -432,7 +445,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   }
   TraceRange tr("rma.pass.hide");
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
-  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(lag_ ? e_fr_ : e_hi_), 0));
   rec(0, s_hi_);
   if (!g.frame.empty()) {
     TraceRange tb("rma.boundary");
@@ -456,6 +469,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
                    pass_tuning(K, 2), s_hi_);
     }
   }
+  RMA_HIP_CHECK(hipEventRecord(E(e_fr_), S(s_hi_)));
   rec(1, s_hi_);
   {
     TraceRange th("rma.halo");
@@ -628,6 +642,7 @@ void DiffusionExecutor::build_graph(int64_t steps, int reps) {
     RMA_HIP_CHECK(hipEventRecord(E(e_in_), lo));
     RMA_HIP_CHECK(hipStreamWaitEvent(hi, E(e_in_), 0));
     RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
+    RMA_HIP_CHECK(hipEventRecord(E(e_fr_), hi));
     RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
     for (int r = 0; r < reps; ++r) run_eager(steps);
     // join hi back
@@ -665,6 +680,7 @@ void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
   RMA_HIP_CHECK(hipStreamWaitEvent(hi, E(e_in_), 0));
   // make the per-step cross-stream waits of kHide start from "caller done"
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
+  RMA_HIP_CHECK(hipEventRecord(E(e_fr_), hi));
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
   int64_t left = nsteps;
   if (p_.use_graph) {
@@ -685,6 +701,7 @@ void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
       RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
       RMA_HIP_CHECK(hipStreamWaitEvent(hi, E(e_lo_), 0));
       RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
+      RMA_HIP_CHECK(hipEventRecord(E(e_fr_), hi));
     }
   }
   run_eager(left);
