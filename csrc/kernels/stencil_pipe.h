@@ -120,9 +120,14 @@ constexpr int kArFast5RegIso = 8;
 // (stage 0 also streams T / 1/Cp and forms the factors: is it the block's
 // critical path at the per-row barrier?)
 constexpr int kArDiagS0 = 9;
+// lab: piper at ONE wave per SIMD (one 4-wave block per CU, up to 512
+// registers incl. AGPRs) with the row loop unrolled by 6 also at H = 6 (K =
+// 21..24, which spill 39 VGPRs at 2 waves per SIMD): no factor-row moves
+// against no second block to hide the per-row barrier
+constexpr int kArFast5RegW1 = 10;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
-         Ar == kArFast5RegIso || Ar == kArDiagS0;
+         Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -187,7 +192,8 @@ constexpr bool kPipeU6 = RMA_PIPE_U6;
 // K=20: 247 instead of 201 VGPRs, no spill, still 2 waves per SIMD.
 template <int K, int S, int Ar>
 constexpr bool pipe_u6() {
-  return ar_reg(Ar) && Plan<K, S>::H == 5 && kPipeU6 && Ar != kArFast5RegU3;
+  return ar_reg(Ar) && kPipeU6 && Ar != kArFast5RegU3 &&
+         (Plan<K, S>::H == 5 || (Ar == kArFast5RegW1 && Plan<K, S>::H == 6));
 }
 // LDS-DMA staging rows per array: one per phase of the unrolled row loop, so
 // a row DMA'd at phase p is read at phase p of the next loop trip (across the
@@ -211,6 +217,7 @@ constexpr int kernel_waves() {
     constexpr int vgpr = 8 * H * V + 8 * V + 40;
     constexpr int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
     constexpr int w = occupancy<K, S, V, false, C>(lds_bytes_reg<K, S, V, Ar>());
+    if constexpr (Ar == kArFast5RegW1) return 1;
     return by_vgpr < 2 ? 2 : (by_vgpr < w ? by_vgpr : w);
   } else {
     return waves_per_simd<K, S, V, Ar == kArCanon, C>();

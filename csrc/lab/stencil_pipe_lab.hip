@@ -48,6 +48,8 @@ bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(20, 4, kArFast5RegIso)
   RMA_PIPE_CASE(24, 4, kArFast5RegIso)
   RMA_PIPE_CASE(20, 4, kArDiagS0)
+  RMA_PIPE_CASE(20, 4, kArFast5RegW1)
+  RMA_PIPE_CASE(24, 4, kArFast5RegW1)
   return false;
 }
 

@@ -372,3 +372,16 @@ def test_piper_iso_bitwise_and_refused_when_anisotropic(nx, K):
         out = torch.zeros(T.shape, dtype=torch.float64, device=DEV)
         ops.stencilk_step(K, out, T.to(DEV), iCp.to(DEV), coef(), rects,
                           ops.StencilTuning(kernel="piper_iso", xcd_remap=1, chunk_rows=37, vec=4))
+
+
+@pytest.mark.parametrize("nx", [518, 1028])
+@pytest.mark.parametrize("K", [20, 24])
+def test_piper_one_wave_per_simd_bitwise(nx, K):
+    """piper_w1 (lab: one wave per SIMD, row loop unrolled by 6 at K = 20 and
+    24) == the fast5 CPU twin, bitwise."""
+    ny = 181
+    T, iCp = rand((ny, nx), 71 + K), rand((ny, nx), 72, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, "pipe")
+    for chunk in (7, 43):
+        assert torch.equal(gpu_run(K, T, iCp, rects, "piper_w1", chunk=chunk), ref)
