@@ -168,7 +168,7 @@ for s in "$@"; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     w1_ab) step w1_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
              --pipec "" --ldsdpp "" --old "" --alt "" \
-             --kinds piper:20,piper_w1:20,piper:24,piper_w1:24,piper_u3:24 --out "$OUT/w1_ab.json" || exit 1 ;;
+             --kinds piper:20,piper_w1:20,piper:24,piper_w1:24 --out "$OUT/w1_ab.json" || exit 1 ;;
     tests_w1) step tests_w1 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_one_wave_per_simd_bitwise" -p no:cacheprovider || exit 1 ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
