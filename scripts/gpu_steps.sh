@@ -171,6 +171,15 @@ for s in "$@"; do
              --kinds piper:20,piper_w1:20,piper:24,piper_w1:24 --out "$OUT/w1_ab.json" || exit 1 ;;
     tests_w1) step tests_w1 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_one_wave_per_simd_bitwise" -p no:cacheprovider || exit 1 ;;
+    apps_r4) step app_hide16k 300 python -m rocm_mpi_amd.apps.diffusion_2D_perf_hide --nx 16384 \
+               --ny 16384 --nt 1000 --json && \
+             step app_perf12k 300 python -m rocm_mpi_amd.apps.diffusion_2D_perf --nt 1000 --json && \
+             step app_perf12k_canonical 300 python -m rocm_mpi_amd.apps.diffusion_2D_perf --nt 1000 \
+               --canonical --json && \
+             step app_perf12k_k1 300 python -m rocm_mpi_amd.apps.diffusion_2D_perf --nt 1000 \
+               --temporal 1 --json && \
+             step baseline_presets 600 python bench/baseline_configs.py --max-gpus 1 \
+               --out "$OUT/baseline_configs.json" || exit 1 ;;
     tests_r4) step tests_r4 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              tests/test_capi_gpu.py tests/test_bench_gpu.py "tests/test_pipe_gpu.py::test_piper_split_form_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_unroll6_equals_unroll3" \
