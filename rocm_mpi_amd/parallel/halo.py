@@ -15,6 +15,8 @@ the reference does with ``T_nh .= Array(T[2:end-1,2:end-1])``).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import comm as C
@@ -86,7 +88,17 @@ def update_halo_(*arrays: torch.Tensor, dims=(0, 1, 2)) -> None:
             ol = field_overlaps(g, A)
             fields.append((A.data_ptr(), list(sz), A.element_size(), list(ol),
                            list(g.halowidths)))
-        g.halo.exchange(fields, torch.cuda.current_stream(dev).cuda_stream, mask)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        # x AND y neighbours, 2D fields: one group with the corner blocks sent to
+        # the diagonal ranks (bitwise the same halos as the per-dimension groups;
+        # csrc/runtime/halo_plan.cpp plan_exchange_merged, RMA_HALO_MERGED=0: off)
+        nb = g.neighbors
+        if (mask & 3) == 3 and all(f[1][2] == 1 for f in fields) and g.halo.has_diagonals \
+                and max(nb[0]) >= 0 and max(nb[1]) >= 0 \
+                and os.environ.get("RMA_HALO_MERGED", "1") != "0":
+            g.halo.exchange_merged(fields, stream)
+        else:
+            g.halo.exchange(fields, stream, mask)
         return
     _update_halo_python(g, arrays, mask)
 
