@@ -125,9 +125,19 @@ constexpr int kArDiagS0 = 9;
 // 21..24, which spill 39 VGPRs at 2 waves per SIMD): no factor-row moves
 // against no second block to hide the per-row barrier
 constexpr int kArFast5RegW1 = 10;
+// lab: piper with the lanes outside the level's valid cone masked off. Level l
+// of a strip window is valid on columns [l, W - l) only (each level loses one
+// column per side); a lane whose V cells all lie outside skips that level's
+// arithmetic under EXEC (its registers keep stale values no valid output reads).
+// ~7 % of the lane-updates of a K=20 pass: does an EXEC-masked lane save the
+// power-capped pass its energy? Bitwise equal to piper.
+constexpr int kArFast5RegMask = 11;
+// its control: the same asm statement under the full EXEC (the schedule's cost alone)
+constexpr int kArFast5RegMaskCtl = 12;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
-         Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1;
+         Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1 || Ar == kArFast5RegMask ||
+         Ar == kArFast5RegMaskCtl;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -443,6 +453,15 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   for (int v = 0; v < V; ++v) gp[v] = 0.0;
   int par = 0;
   const int lag = stage * (H + 1);  // rows behind stage 0
+  // kArFast5RegMask: per local level, is any of this lane's cells inside the
+  // level's valid cone (loop-invariant lane masks, kept in SGPR pairs)
+  constexpr bool kMask = (Ar == kArFast5RegMask || Ar == kArFast5RegMaskCtl) && V == 4;  // other V: plain piper
+  uint64_t amask[kMask ? H : 1];
+#pragma unroll
+  for (int j = 1; j <= (kMask ? H : 1); ++j) {
+    const int l = stage * H + j;
+    amask[j - 1] = __ballot(Ar == kArFast5RegMaskCtl || (lane * V + V > l && lane * V < W - l));
+  }
 
   auto iter = [&](auto Pc, auto S0c, auto LASTc) {
     constexpr int Ps = decltype(Pc)::value;  // phase of the unrolled loop (staging slot)
@@ -570,10 +589,57 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       const double(&c)[V] = w[j - 1][PC];
       const double(&dn)[V] = w[j - 1][Pr];
       double res[V];
+      uint64_t saved_exec = 0;
       if constexpr (!Canon) {
         const double(&up)[V] = w[j - 1][PU];
         const double rn = from_next_lane<kDpp>(c[0]);
         const double ln = from_prev_lane<kDpp>(c[V - 1]);
+        if constexpr (kMask) {
+          // the level's arithmetic in ONE asm statement under the cone's lane
+          // mask (the compiler can place nothing of its own under the narrowed
+          // EXEC); the lane moves above ran under the full EXEC (a neighbour
+          // may skip the level). Same operations and order as below, per cell:
+          // sx = L + R; t = fma(mkc, c, sx); t = fma(ry, U + D, t);
+          // res = fma(g, t, c). Inactive lanes keep stale registers that no
+          // valid output reads. s_nop 1: VALU write -> DPP read wait states.
+          // In place where the input dies here: L + R of cell 0 / 3 into the lane
+          // moves' registers, U + D into the oldest row `up` (dead after this level).
+          double(&um)[V] = w[j - 1][PU];
+          res[0] = ln;
+          res[3] = rn;
+          asm volatile(
+              "s_and_saveexec_b64 %[sv], %[m]\n\t"
+              "v_add_f64 %[r0], %[c1], %[r0]\n\t"
+              "v_add_f64 %[r1], %[c2], %[c0]\n\t"
+              "v_add_f64 %[r2], %[c3], %[c1]\n\t"
+              "v_add_f64 %[r3], %[r3], %[c2]\n\t"
+              "v_add_f64 %[u0], %[u0], %[d0]\n\t"
+              "v_add_f64 %[u1], %[u1], %[d1]\n\t"
+              "v_add_f64 %[u2], %[u2], %[d2]\n\t"
+              "v_add_f64 %[u3], %[u3], %[d3]\n\t"
+              "v_fma_f64 %[r0], %[mk], %[c0], %[r0]\n\t"
+              "v_fma_f64 %[r1], %[mk], %[c1], %[r1]\n\t"
+              "v_fma_f64 %[r2], %[mk], %[c2], %[r2]\n\t"
+              "v_fma_f64 %[r3], %[mk], %[c3], %[r3]\n\t"
+              "v_fma_f64 %[r0], %[ry], %[u0], %[r0]\n\t"
+              "v_fma_f64 %[r1], %[ry], %[u1], %[r1]\n\t"
+              "v_fma_f64 %[r2], %[ry], %[u2], %[r2]\n\t"
+              "v_fma_f64 %[r3], %[ry], %[u3], %[r3]\n\t"
+              "v_fma_f64 %[r0], %[g0], %[r0], %[c0]\n\t"
+              "v_fma_f64 %[r1], %[g1], %[r1], %[c1]\n\t"
+              "v_fma_f64 %[r2], %[g2], %[r2], %[c2]\n\t"
+              "v_fma_f64 %[r3], %[g3], %[r3], %[c3]\n\t"
+              "s_or_b64 exec, exec, %[sv]\n\t"
+              "s_nop 1"
+              : [r0] "+v"(res[0]), [r1] "=&v"(res[1]), [r2] "=&v"(res[2]), [r3] "+v"(res[3]),
+                [u0] "+v"(um[0]), [u1] "+v"(um[1]), [u2] "+v"(um[2]), [u3] "+v"(um[3]),
+                [sv] "=&s"(saved_exec)
+              : [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]),
+                [d0] "v"(dn[0]), [d1] "v"(dn[1]), [d2] "v"(dn[2]), [d3] "v"(dn[3]),
+                [g0] "v"(gl[0]), [g1] "v"(gl[1]), [g2] "v"(gl[2]), [g3] "v"(gl[3]),
+                [ry] "v"(ry), [mk] "v"(mkc), [m] "s"(amask[j - 1])
+              : "scc");
+        } else {
         double sx[V], sy[V], t[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -618,6 +684,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int v = 0; v < V; ++v) res[v] = __builtin_fma(gl[v], t[v], c[v]);
+        }  // !kMask
       } else {
         // canonical: same expressions and rounding as rma/common.h
         const double rn = from_next_lane(c[0]);
@@ -637,6 +704,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
           res[v] = c[v] + k.dt * (gl[v] * ((-(qr[v] - qL)) * k.rdx - (qU - qD) * k.rdy));
         }
       }
+      (void)saved_exec;
       if (j < NL) {
         const int jj = j < NL ? j : NL - 1;
 #pragma unroll

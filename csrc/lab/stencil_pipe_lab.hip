@@ -19,7 +19,9 @@
 //   * piper_u3 (kernel 16): piper with the row loop unrolled by 3 in every
 //     stage (the round-3 kernel; the core's K = 17..20 unroll by 6), A/B;
 //   * piper_iso (kernel 17): piper with fma(1, U+D, t) as an add, for
-//     ry == 1 exactly (bitwise equal to piper there), K = 20, 24.
+//     ry == 1 exactly (bitwise equal to piper there), K = 20, 24;
+//   * piper_mask (kernel 20): piper whose lanes outside a level's valid cone
+//     skip the level under EXEC (bitwise equal to piper), K = 20, 24.
 #include "../kernels/lab_hooks.h"
 
 namespace rma {
@@ -50,6 +52,10 @@ bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(20, 4, kArDiagS0)
   RMA_PIPE_CASE(20, 4, kArFast5RegW1)
   RMA_PIPE_CASE(24, 4, kArFast5RegW1)
+  RMA_PIPE_CASE(20, 4, kArFast5RegMask)
+  RMA_PIPE_CASE(24, 4, kArFast5RegMask)
+  RMA_PIPE_CASE(20, 4, kArFast5RegMaskCtl)
+  RMA_PIPE_CASE(24, 4, kArFast5RegMaskCtl)
   return false;
 }
 

@@ -385,3 +385,18 @@ def test_piper_one_wave_per_simd_bitwise(nx, K):
     ref = cpu_ref(K, T, iCp, rects, "pipe")
     for chunk in (7, 43):
         assert torch.equal(gpu_run(K, T, iCp, rects, "piper_w1", chunk=chunk), ref)
+
+
+@pytest.mark.parametrize("nx", [516, 1028])
+@pytest.mark.parametrize("K", [20, 24])
+def test_piper_masked_cone_bitwise(nx, K):
+    """piper_mask (lab: lanes outside a level's valid cone skip the level under
+    EXEC, the level's arithmetic in one asm statement) == the fast5 CPU twin,
+    bitwise, on several rects (strip windows at both x edges of the array)."""
+    ny = 167
+    T, iCp = rand((ny, nx), 81 + K), rand((ny, nx), 82, 0.5, 1.0)
+    for rects in ([ops.interior_rect(nx, ny)], [(1, nx // 2, 1, 100), (37, nx - 3, 100, ny - 1)]):
+        ref = cpu_ref(K, T, iCp, rects, "pipe")
+        for chunk in (7, 43):
+            for kern in ("piper_mask", "piper_mask_ctl"):
+                assert torch.equal(gpu_run(K, T, iCp, rects, kern, chunk=chunk), ref), kern
