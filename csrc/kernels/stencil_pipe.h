@@ -134,10 +134,13 @@ constexpr int kArFast5RegW1 = 10;
 constexpr int kArFast5RegMask = 11;
 // its control: the same asm statement under the full EXEC (the schedule's cost alone)
 constexpr int kArFast5RegMaskCtl = 12;
+// lab: piper without the sched_barriers between the phases of a level's
+// arithmetic (the scheduler free to overlap levels), A/B of the schedule
+constexpr int kArFast5RegNoSB = 13;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
          Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1 || Ar == kArFast5RegMask ||
-         Ar == kArFast5RegMaskCtl;
+         Ar == kArFast5RegMaskCtl || Ar == kArFast5RegNoSB;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -649,7 +652,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
           sy[v] = up[v] + dn[v];
         }
         // the V cells' FMA chains interleaved (sched_barrier keeps them apart)
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (Ar != kArFast5RegNoSB) __builtin_amdgcn_sched_barrier(0);
         if constexpr (ar_split(Ar)) {
           double u[V];
           if constexpr (Ar == kArFast6Reg) {
@@ -666,13 +669,13 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
               t[v] = sy[v] - d;
             }
           }
-          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (Ar != kArFast5RegNoSB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, t[v], u[v]);
         } else {
 #pragma unroll
           for (int v = 0; v < V; ++v) t[v] = __builtin_fma(mkc, c[v], sx[v]);
-          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (Ar != kArFast5RegNoSB) __builtin_amdgcn_sched_barrier(0);
           if constexpr (Ar == kArFast5RegIso) {
 #pragma unroll
             for (int v = 0; v < V; ++v) t[v] = sy[v] + t[v];
@@ -681,7 +684,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
             for (int v = 0; v < V; ++v) t[v] = __builtin_fma(ry, sy[v], t[v]);
           }
         }
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (Ar != kArFast5RegNoSB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int v = 0; v < V; ++v) res[v] = __builtin_fma(gl[v], t[v], c[v]);
         }  // !kMask

@@ -400,3 +400,14 @@ def test_piper_masked_cone_bitwise(nx, K):
         for chunk in (7, 43):
             for kern in ("piper_mask", "piper_mask_ctl"):
                 assert torch.equal(gpu_run(K, T, iCp, rects, kern, chunk=chunk), ref), kern
+
+
+@pytest.mark.parametrize("K", [20, 24])
+def test_piper_schedule_variants_bitwise(K):
+    """piper_nosb (lab: no sched_barriers inside a level) == the fast5 CPU twin."""
+    nx, ny = 1028, 149
+    T, iCp = rand((ny, nx), 91 + K), rand((ny, nx), 92, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, "pipe")
+    for chunk in (11, 64):
+        assert torch.equal(gpu_run(K, T, iCp, rects, "piper_nosb", chunk=chunk), ref)
