@@ -175,6 +175,11 @@ for s in "$@"; do
     nosb_ab) step nosb_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
              --pipec "" --ldsdpp "" --old "" --alt "" \
              --kinds piper:20,piper_nosb:20,piper:24,piper_nosb:24 --out "$OUT/nosb_ab.json" || exit 1 ;;
+    tests_user) step tests_user 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+             "tests/test_multirank_gpu.py::test_user_example_gpu_equals_golden" -p no:cacheprovider && \
+             step user_example 120 python examples/diffusion_2D_user.py --nx 8192 --ny 8192 --nt 200 && \
+             step user_example_hide 120 python examples/diffusion_2D_user.py --nx 8192 --ny 8192 \
+               --nt 200 --hide || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" -p no:cacheprovider || exit 1 ;;

@@ -119,3 +119,18 @@ def slurm_env(rank, world, outdir):
     np.save(os.path.join(outdir, f"slurm{rank}.npy"),
             np.array([me, nprocs, g.local_rank, g.local_size, s]))
     gg.finalize_global_grid()
+
+
+def user_example(rank, world, outdir, nx, ny, nt, dims):
+    """examples/diffusion_2D_user.py on gloo ranks (CPU twins)."""
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        "diffusion_2D_user", os.path.join(root, "examples", "diffusion_2D_user.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    T0, T, _ = mod.diffusion2D(nx, ny, nt, device="cpu", dims=dims, quiet=True)
+    if rank == 0:
+        np.save(os.path.join(outdir, "T0.npy"), T0.numpy())
+        np.save(os.path.join(outdir, "T.npy"), T.numpy())

@@ -25,6 +25,17 @@ def test_gloo_decomposition_invariance(tmp_path, variant, world, dims):
     assert np.array_equal(Tv, G[1:-1, 1:-1])
 
 
+@pytest.mark.parametrize("world,dims", [(2, (2, 1)), (4, (2, 2))])
+def test_user_example_matches_golden(tmp_path, world, dims):
+    """examples/diffusion_2D_user.py (the user's own loop over the IGG API,
+    stencil_step + update_halo_ per step) on gloo ranks == the golden model."""
+    nx, ny, nt = 40, 36, 30
+    run_procs(world, "mp_targets:user_example", str(tmp_path), nx, ny, nt, dims)
+    nxg, nyg = dims[0] * (nx - 2) + 2, dims[1] * (ny - 2) + 2
+    assert np.array_equal(np.load(tmp_path / "T0.npy"), golden.initial(nxg, nyg)[1:-1, 1:-1])
+    assert np.array_equal(np.load(tmp_path / "T.npy"), golden.run(nxg, nyg, nt)[1:-1, 1:-1])
+
+
 def test_ring_sendrecv(tmp_path):
     run_procs(3, "mp_targets:ring", str(tmp_path))
     for r in range(3):

@@ -531,3 +531,34 @@ def test_merged_exchange_equals_dimension_ordered(via_rccl, hw, ol):
                                          dtype=torch.float64).cuda())  # the halos did change
     if rc:
         rc.finalize()
+
+
+def _user_example():
+    import importlib.util
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        "diffusion_2D_user", os.path.join(root, "examples", "diffusion_2D_user.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def spmd_user_example(rank, hub, nx, ny, nt, dims, hide):
+    T0, T, _ = _user_example().diffusion2D(nx, ny, nt, device="cuda", dims=dims, hide=hide,
+                                           quiet=True, b_width=(8, 4),
+                                           grid_kw=dict(loopback=(hub, rank)))
+    return None if T is None else T.numpy()
+
+
+@pytest.mark.parametrize("hide", [False, True])
+@pytest.mark.parametrize("P,dims", [(1, (1, 1)), (4, (2, 2))])
+def test_user_example_gpu_equals_golden(hide, P, dims):
+    """examples/diffusion_2D_user.py on cuda:0 (--hide: frame and update_halo_
+    on a high-priority stream, interior on a low-priority one; 2x2 loopback
+    ranks: the merged x+y exchange) == the golden model, bitwise."""
+    nx, ny, nt = 300, 134, 23
+    T = run_loopback(P, spmd_user_example, nx, ny, nt, dims, hide, timeout=120)[0]
+    nxg, nyg = dims[0] * (nx - 2) + 2, dims[1] * (ny - 2) + 2
+    assert np.array_equal(T, golden.run(nxg, nyg, nt)[1:-1, 1:-1])
