@@ -23,6 +23,21 @@ def initial(nxg, nyg, lx=10.0, ly=10.0):
     return np.exp(-(a * a)[None, :] - (b * b)[:, None])  # shape (nyg, nxg)
 
 
+def initial_torch(nxg, nyg, lx=10.0, ly=10.0):
+    """initial() with torch's exp: the same doubles up to exp's last-ulp rounding,
+    which differs between exp implementations (NumPy's and torch's vector paths
+    differ on some CPUs): the oracle for code that evaluates the initial
+    condition with torch."""
+    import torch
+
+    dx, dy, _ = params(nxg, nyg, lx, ly)
+    x = torch.arange(nxg, dtype=torch.float64) * dx
+    y = torch.arange(nyg, dtype=torch.float64) * dy
+    a = (x + dx / 2) - lx / 2
+    b = (y + dy / 2) - ly / 2
+    return torch.exp(-(a * a)[None, :] - (b * b)[:, None]).numpy()
+
+
 def step(T, iCp, mlam, rdx, rdy, dt):
     cu = T[1:-1, 1:-1]
     qxR = (mlam * (T[1:-1, 2:] - cu)) * rdx
