@@ -180,6 +180,11 @@ for s in "$@"; do
              step user_example 120 python examples/diffusion_2D_user.py --nx 8192 --ny 8192 --nt 200 && \
              step user_example_hide 120 python examples/diffusion_2D_user.py --nx 8192 --ny 8192 \
                --nt 200 --hide || exit 1 ;;
+    pmc_u6) prof pmc_u6 240 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+             SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE \
+             --output-format csv -d "$R/$OUT/pmc_u6" -o run -- python3 "$R/bench/pass_sweep.py" \
+             --n 101120 --rounds 1 --pipe "" --pipec "" --ldsdpp "" --old "" --alt "" \
+             --kinds piper:20,piper_u3:20,piper:24 || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" -p no:cacheprovider || exit 1 ;;
