@@ -137,10 +137,14 @@ constexpr int kArFast5RegMaskCtl = 12;
 // lab: piper without the sched_barriers between the phases of a level's
 // arithmetic (the scheduler free to overlap levels), A/B of the schedule
 constexpr int kArFast5RegNoSB = 13;
+// lab: piper with the stage -> wave map rotated by 2 in odd blocks (waves are
+// dealt to SIMDs in order, so two co-resident blocks of the same parity put
+// both stage-0 waves, the heaviest, on one SIMD): A/B of the SIMD balance
+constexpr int kArFast5RegRot = 14;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
          Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1 || Ar == kArFast5RegMask ||
-         Ar == kArFast5RegMaskCtl || Ar == kArFast5RegNoSB;
+         Ar == kArFast5RegMaskCtl || Ar == kArFast5RegNoSB || Ar == kArFast5RegRot;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -288,7 +292,9 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   constexpr int kStep = G::kStep;  // output columns per strip (plan_strip_tasks, sw = WB)
   constexpr int NH = S > 1 ? S - 1 : 1;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int stage = C > 1 ? wv % S : wv;  // waves c*S .. c*S+S-1: column c, one per SIMD
+  const int stage = Ar == kArFast5RegRot ? (wv + 2 * (int)(blockIdx.x & 1)) % S
+                    : C > 1              ? wv % S
+                                         : wv;  // waves c*S .. c*S+S-1: column c, one per SIMD
   const int col = C > 1 ? wv / S : 0;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;

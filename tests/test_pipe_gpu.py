@@ -410,4 +410,5 @@ def test_piper_schedule_variants_bitwise(K):
     rects = [ops.interior_rect(nx, ny)]
     ref = cpu_ref(K, T, iCp, rects, "pipe")
     for chunk in (11, 64):
-        assert torch.equal(gpu_run(K, T, iCp, rects, "piper_nosb", chunk=chunk), ref)
+        for kern in ("piper_nosb", "piper_rot"):
+            assert torch.equal(gpu_run(K, T, iCp, rects, kern, chunk=chunk), ref), kern
