@@ -141,10 +141,14 @@ constexpr int kArFast5RegNoSB = 13;
 // dealt to SIMDs in order, so two co-resident blocks of the same parity put
 // both stage-0 waves, the heaviest, on one SIMD): A/B of the SIMD balance
 constexpr int kArFast5RegRot = 14;
+// diagnosis only (lab, WRONG results: the hand-off rows race): piper with the
+// row barrier on every other row only -- the most that fewer barriers could buy
+constexpr int kArDiagHalfBarrier = 15;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
          Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1 || Ar == kArFast5RegMask ||
-         Ar == kArFast5RegMaskCtl || Ar == kArFast5RegNoSB || Ar == kArFast5RegRot;
+         Ar == kArFast5RegMaskCtl || Ar == kArFast5RegNoSB || Ar == kArFast5RegRot ||
+         Ar == kArDiagHalfBarrier;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -748,7 +752,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         glds_row(0, i + 1 + NST, Ps);
         glds_row(1, i + NST, Ps);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (Ar != kArDiagHalfBarrier || (Ps & 1))
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
       __syncthreads();  // hand-off and ring rows visible; this iteration's reads done
     }

@@ -60,6 +60,7 @@ bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(24, 4, kArFast5RegNoSB)
   RMA_PIPE_CASE(20, 4, kArFast5RegRot)
   RMA_PIPE_CASE(24, 4, kArFast5RegRot)
+  RMA_PIPE_CASE(20, 4, kArDiagHalfBarrier)
   return false;
 }
 

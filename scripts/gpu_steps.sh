@@ -188,6 +188,9 @@ for s in "$@"; do
     rot_ab) step rot_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
              --pipec "" --ldsdpp "" --old "" --alt "" \
              --kinds piper:20,piper_rot:20,piper:24,piper_rot:24 --out "$OUT/rot_ab.json" || exit 1 ;;
+    hb_ab) step hb_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
+             --pipec "" --ldsdpp "" --old "" --alt "" \
+             --kinds piper:20,piper_diag_hb:20 --out "$OUT/hb_ab.json" || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" -p no:cacheprovider || exit 1 ;;
