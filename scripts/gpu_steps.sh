@@ -163,6 +163,9 @@ for s in "$@"; do
     tests_merge) step tests_merge 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread \
              tests/test_multirank_gpu.py tests/test_capi_gpu.py tests/test_bench_gpu.py \
              -p no:cacheprovider || exit 1 ;;
+    eqchan) for t in eqn8192_xy eqn8192_xy_ch1 eqn8192_xy_ch2 eqn8192_xy_pp1 eqn4096_xy \
+                     eqn4096_xy_ch1 eqn16384_xy eqn16384_xy_ch1; do
+             bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     eqlag) for t in eqn2048_xy eqn2048_xy_nolag eqn4096_xy eqn4096_xy_nolag eqn4096_x eqn4096_x_nolag \
                     eqn8192_xy eqn8192_xy_nolag eqn16384_xy eqn16384_xy_nolag; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
@@ -237,10 +240,13 @@ for s in "$@"; do
              --steps 960 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     eqn*) # eqn<N>_<dims>[_strips][_cd<D>][_bol|_btask]: N^2 tile, K=24, equal coefficients
              t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""; fb=""; hm=""; lg=""
+             mc=""; pp=""
              for tok in ${t//_/ }; do case $tok in strips) fa=0 ;; cd*) cd=${tok#cd} ;;
-               bol) fb=ol ;; btask) fb=task ;; nomerge) hm=0 ;; nolag) lg=0 ;; esac; done
+               bol) fb=ol ;; btask) fb=task ;; nomerge) hm=0 ;; nolag) lg=0 ;;
+               ch*) mc=${tok#ch} ;; pp*) pp=${tok#pp} ;; esac; done
              RMA_EXEC_LAG=$lg RMA_HALO_MERGED=$hm RMA_FRAME_BANDS=$fb RMA_FRAME_CHUNK_DIV=$cd \
-             RMA_FRAME_ALIGNED=$fa step "$s" 300 python bench/rccl_self_overhead.py --n "$n" --K 24 \
+             RMA_FRAME_ALIGNED=$fa step "$s" 300 env ${mc:+NCCL_MAX_P2P_NCHANNELS=$mc} \
+             ${pp:+NCCL_NCHANNELS_PER_PEER=$pp} python bench/rccl_self_overhead.py --n "$n" --K 24 \
              --periodic "$d" --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     chunk_sweep) step chunk_sweep 400 python bench/pass_sweep.py --pipe 20,24 --pipec "" \
              --ldsdpp "" --old "" --alt "" --rounds 3 \
