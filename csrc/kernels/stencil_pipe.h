@@ -144,11 +144,14 @@ constexpr int kArFast5RegRot = 14;
 // diagnosis only (lab, WRONG results: the hand-off rows race): piper with the
 // row barrier on every other row only -- the most that fewer barriers could buy
 constexpr int kArDiagHalfBarrier = 15;
+// lab: piper unrolled by 6 also at H = 6 (K = 21..24), accepting the spills
+// (~10-17 scratch accesses per 6 rows and stage instead of ~44-64 row moves)
+constexpr int kArFast5RegU6S = 16;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
          Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1 || Ar == kArFast5RegMask ||
          Ar == kArFast5RegMaskCtl || Ar == kArFast5RegNoSB || Ar == kArFast5RegRot ||
-         Ar == kArDiagHalfBarrier;
+         Ar == kArDiagHalfBarrier || Ar == kArFast5RegU6S;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -202,6 +205,9 @@ constexpr int waves_per_simd() {
 #define RMA_PIPE_U6 1
 #endif
 constexpr bool kPipeU6 = RMA_PIPE_U6;
+#ifndef RMA_PIPE_U6_H6  // experiments only: unroll by 6 also at H = 6 (spills, see below)
+#define RMA_PIPE_U6_H6 0
+#endif
 // Register factors: a factor row lives H iterations and a new one starts
 // every iteration, so with the row loop unrolled by U < H the row started at
 // phase p is still live when the next trip's phase-p row starts and the back
@@ -214,7 +220,9 @@ constexpr bool kPipeU6 = RMA_PIPE_U6;
 template <int K, int S, int Ar>
 constexpr bool pipe_u6() {
   return ar_reg(Ar) && kPipeU6 && Ar != kArFast5RegU3 &&
-         (Plan<K, S>::H == 5 || (Ar == kArFast5RegW1 && Plan<K, S>::H == 6));
+         (Plan<K, S>::H == 5 ||
+          ((Ar == kArFast5RegW1 || Ar == kArFast5RegU6S || (RMA_PIPE_U6_H6 && Ar == kArFast5Reg)) &&
+           Plan<K, S>::H == 6));
 }
 // LDS-DMA staging rows per array: one per phase of the unrolled row loop, so
 // a row DMA'd at phase p is read at phase p of the next loop trip (across the

@@ -194,9 +194,13 @@ for s in "$@"; do
     hb_ab) step hb_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
              --pipec "" --ldsdpp "" --old "" --alt "" \
              --kinds piper:20,piper_diag_hb:20 --out "$OUT/hb_ab.json" || exit 1 ;;
+    u6s_ab) step u6s_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
+             --pipec "" --ldsdpp "" --old "" --alt "" \
+             --kinds piper:21,piper_u6s:21,piper:24,piper_u6s:24 --out "$OUT/u6s_ab.json" || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
-             "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" -p no:cacheprovider || exit 1 ;;
+             "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
+             "tests/test_pipe_gpu.py::test_piper_u6_spilling_bitwise" -p no:cacheprovider || exit 1 ;;
     tests_w1) step tests_w1 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_one_wave_per_simd_bitwise" -p no:cacheprovider || exit 1 ;;
     apps_r4) step app_hide16k 300 python -m rocm_mpi_amd.apps.diffusion_2D_perf_hide --nx 16384 \

@@ -412,3 +412,15 @@ def test_piper_schedule_variants_bitwise(K):
     for chunk in (11, 64):
         for kern in ("piper_nosb", "piper_rot"):
             assert torch.equal(gpu_run(K, T, iCp, rects, kern, chunk=chunk), ref), kern
+
+
+@pytest.mark.parametrize("K", [21, 24])
+def test_piper_u6_spilling_bitwise(K):
+    """piper_u6s (lab: unrolled by 6 at H = 6, with register spills) == the
+    fast5 CPU twin."""
+    nx, ny = 1028, 151
+    T, iCp = rand((ny, nx), 95 + K, ), rand((ny, nx), 96, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, "pipe")
+    for chunk in (13, 64):
+        assert torch.equal(gpu_run(K, T, iCp, rects, "piper_u6s", chunk=chunk), ref)
