@@ -169,7 +169,7 @@ PYBIND11_MODULE(_C, m) {
           const bool f5 = (kernel >= 5 && kernel <= 9) || kernel == 11 || kernel == 12 ||
                           kernel == 16 || kernel == 17 || kernel == 19 ||
                           kernel == 20 || kernel == 21 || kernel == 22 || kernel == 23 ||
-                          kernel == 25;
+                          kernel == 25 || kernel == 26 || kernel == 27;
           const bool f6 = kernel == 14 || kernel == 15;
           py::gil_scoped_release nogil;
           if (f6)

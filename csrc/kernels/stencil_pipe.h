@@ -147,11 +147,19 @@ constexpr int kArDiagHalfBarrier = 15;
 // lab: piper unrolled by 6 also at H = 6 (K = 21..24), accepting the spills
 // (~10-17 scratch accesses per 6 rows and stage instead of ~44-64 row moves)
 constexpr int kArFast5RegU6S = 16;
+// lab: piper with the levels software-pipelined: level j+1's lane moves, L+R
+// and fma(mkc, c, L+R) (which read only the previous row iteration's values)
+// are issued while level j's chain U+D -> fma(ry) -> fma(g) runs, so the chain
+// after a new row lands is 3 dependent operations instead of 5 plus the lane
+// moves. Same operations and rounding as piper (bitwise). kArFast5RegSP: one
+// sched_barrier per level; kArFast5RegSP2: none.
+constexpr int kArFast5RegSP = 17, kArFast5RegSP2 = 18;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
          Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1 || Ar == kArFast5RegMask ||
          Ar == kArFast5RegMaskCtl || Ar == kArFast5RegNoSB || Ar == kArFast5RegRot ||
-         Ar == kArDiagHalfBarrier || Ar == kArFast5RegU6S;
+         Ar == kArDiagHalfBarrier || Ar == kArFast5RegU6S || Ar == kArFast5RegSP ||
+         Ar == kArFast5RegSP2;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -595,6 +603,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     } else {
       rd2(ring_row(1), gn);
     }
+    constexpr bool kSP = Ar == kArFast5RegSP || Ar == kArFast5RegSP2;
+    double tq[kSP ? V : 1];  // software pipelining: the next level's fma(mkc, c, L+R)
 #pragma unroll
     for (int j = 1; j <= NL; ++j) {
       const int row = i - (S0 ? 0 : lag) - (j - 1);
@@ -660,6 +670,29 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
                 [g0] "v"(gl[0]), [g1] "v"(gl[1]), [g2] "v"(gl[2]), [g3] "v"(gl[3]),
                 [ry] "v"(ry), [mk] "v"(mkc), [m] "s"(amask[j - 1])
               : "scc");
+        } else if constexpr (kSP) {
+          auto partial = [&](const double(&cc)[V], double r_n, double l_n, double(&out)[V]) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+              const double rv = v + 1 < V ? cc[v + 1] : r_n;
+              const double lv = v > 0 ? cc[v - 1] : l_n;
+              out[v] = __builtin_fma(mkc, cc[v], rv + lv);
+            }
+          };
+          if (j == 1) partial(c, rn, ln, tq);
+          double t[V];
+#pragma unroll
+          for (int v = 0; v < V; ++v) t[v] = tq[v];
+          if (j < NL) {  // the next level's centre row: the previous row iteration's
+            const double(&cn)[V] = w[j][PC];
+            partial(cn, from_next_lane<kDpp>(cn[0]), from_prev_lane<kDpp>(cn[V - 1]), tq);
+          }
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            t[v] = __builtin_fma(ry, up[v] + dn[v], t[v]);
+            res[v] = __builtin_fma(gl[v], t[v], c[v]);
+          }
+          if constexpr (Ar == kArFast5RegSP) __builtin_amdgcn_sched_barrier(0);
         } else {
         double sx[V], sy[V], t[V];
 #pragma unroll

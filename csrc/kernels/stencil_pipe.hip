@@ -41,6 +41,8 @@ bool pipe_has(int K, int S, int arith) {
     return S == 4 && (K == 20 || K == 24);
   if (arith == pipe::kArDiagHalfBarrier) return S == 4 && K == 20;
   if (arith == pipe::kArFast5RegU6S) return S == 4 && (K == 21 || K == 24);
+  if (arith == pipe::kArFast5RegSP || arith == pipe::kArFast5RegSP2)
+    return S == 4 && (K == 20 || K == 24);
   if (S == pipe_default_stages(K)) return true;
   // alternative stage splits instantiated for sweeps (csrc/lab/stencil_pipe_lab.hip)
   return (K == 12 && S == 3) || (K == 16 && S == 8) || (K == 24 && S == 8) ||
@@ -78,7 +80,7 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
                 "pipelined K-step kernel: 1 <= K <= " << kPipeMaxK << ", got " << K);
   RMA_CHECK_ARG(pipe_has(K, S, arith), "no pipelined kernel instantiated for K=" << K << " S=" << S
                                                                              << " arithmetic " << arith);
-  RMA_CHECK_ARG(arith >= 0 && arith <= 16, "pipelined kernel arithmetic " << arith);
+  RMA_CHECK_ARG(arith >= 0 && arith <= 18, "pipelined kernel arithmetic " << arith);
   if (arith == pipe::kArFast5RegIso) {
     const double ax = (-c.mlam) * c.rdx * c.rdx, ay = (-c.mlam) * c.rdy * c.rdy;
     RMA_CHECK_ARG(ay / ax == 1.0, "the isotropic fast-math kernel needs ry = (dx/dy)^2 == 1");

@@ -197,6 +197,10 @@ for s in "$@"; do
     u6s_ab) step u6s_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
              --pipec "" --ldsdpp "" --old "" --alt "" \
              --kinds piper:21,piper_u6s:21,piper:24,piper_u6s:24 --out "$OUT/u6s_ab.json" || exit 1 ;;
+    sp_ab) step sp_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
+             --pipec "" --ldsdpp "" --old "" --alt "" \
+             --kinds piper:20,piper_sp:20,piper_sp2:20,piper:24,piper_sp:24,piper_sp2:24 \
+             --out "$OUT/sp_ab.json" || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
