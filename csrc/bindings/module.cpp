@@ -15,6 +15,7 @@
 #include "rma/common.h"
 #include "rma/executor.h"
 #include "rma/halo.h"
+#include "rma/ipc.h"
 #include "rma/kernels.h"
 #include "rma/loopback.h"
 #include "rma/p2p.h"
@@ -318,6 +319,14 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("size", &LoopbackHub::size);
   py::class_<LoopbackEndpoint, P2PTransport>(m, "LoopbackEndpoint")
       .def(py::init<std::shared_ptr<LoopbackHub>, int>(), py::arg("hub"), py::arg("rank"));
+  py::class_<IpcTransport, P2PTransport>(m, "IpcTransport")
+      .def(py::init<int, int, int, const std::vector<int>&, size_t, const std::string&, double>(),
+           py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("peers"),
+           py::arg("mailbox_bytes"), py::arg("token"), py::arg("timeout_s") = 300.0)
+      .def("export_for", [](const IpcTransport& t, int p) { return py::bytes(t.export_for(p)); })
+      .def("connect", [](IpcTransport& t, int p, py::bytes blob) { t.connect(p, blob); })
+      .def_property_readonly("connected", &IpcTransport::connected)
+      .def_property_readonly("mailbox_bytes", &IpcTransport::mailbox_bytes);
   py::class_<RcclComm, P2PTransport>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def(py::init([](int nranks, int rank, py::bytes uid, int device, double init_timeout_s) {

@@ -329,6 +329,63 @@ class RcclComm(Communicator):
                 self._c = None
 
 
+_ipc_generation = 0
+
+
+class IpcComm(TorchDistComm):
+    """Device-direct halo transport between the processes of ONE node over HIP
+    IPC (``csrc/include/rma/ipc.h``): every receiver owns a double-buffered
+    device mailbox per sender, which the sender maps and fills with one
+    device-to-device copy per message (over xGMI between GPUs, on-device when
+    ranks share a GPU); host handshake through POSIX shared memory, GPU
+    ordering through interprocess events. The reference's intra-node
+    ROCm-aware MPI path (``scripts/rocmaware_test_selectdevice.jl:16-22``) without
+    MPI or RCCL. Collectives and gather stay on gloo (host-staged), as in
+    ``staged``. ``peers``: the halo peers (Cartesian neighbours and diagonals).
+    Mailbox size per slot: ``RMA_IPC_MAILBOX_MB`` (default 64 MiB).
+    """
+
+    def __init__(self, device: torch.device, peers, timeout_s: float = DEFAULT_TIMEOUT_S,
+                 mailbox_mb: float | None = None, store=None):
+        super().__init__(staged=True)
+        self.name = "ipc"
+        from .._native import native
+
+        global _ipc_generation
+        key = f"rma/ipc/{_ipc_generation}"
+        _ipc_generation += 1
+        store = store if store is not None else dist.distributed_c10d._get_default_store()
+        if self.rank == 0:
+            import secrets
+
+            store.set(f"{key}/token", f"{os.getpid():x}{secrets.token_hex(4)}")
+        token = store.get(f"{key}/token").decode()
+        mb = float(mailbox_mb if mailbox_mb is not None
+                   else os.environ.get("RMA_IPC_MAILBOX_MB", "64"))
+        cap = max(8, int(mb * (1 << 20)))
+        self.device = torch.device(device)
+        self.peers = sorted({int(p) for p in peers if int(p) >= 0})
+        self._c = native().IpcTransport(self.rank, self.size, self.device.index or 0, self.peers,
+                                        cap, token, timeout_s)
+        others = [p for p in self.peers if p != self.rank]
+        for p in others:  # what p needs from me (my mailbox, my events)
+            store.set(f"{key}/{self.rank}/{p}", self._c.export_for(p))
+        for p in others:  # p's shared-memory block exists: it published after creating it
+            self._c.connect(p, store.get(f"{key}/{p}/{self.rank}"))
+
+    @property
+    def native(self):
+        return self._c
+
+    def finalize(self) -> None:
+        if self._c is not None:
+            if torch.cuda.is_available() and torch.cuda.is_initialized():
+                torch.cuda.synchronize(self.device)
+            # every rank is done with every mailbox before any rank unmaps its own
+            dist.barrier(group=self._pg)
+            self._c = None
+
+
 # ---------------------------------------------------------------------------
 # loopback: N logical ranks = N threads of one process
 # ---------------------------------------------------------------------------

@@ -107,10 +107,12 @@ def _choose_transport(transport: str, size: int, device: torch.device) -> str:
         if size == 1:
             return "self"
         return "rccl" if device.type == "cuda" else "gloo"
-    if t not in ("rccl", "staged", "gloo", "loopback", "self"):
+    if t not in ("rccl", "ipc", "staged", "gloo", "loopback", "self"):
         raise ValueError(f"unknown transport {t!r}")
-    if t == "rccl" and device.type != "cuda":
-        raise ValueError("transport 'rccl' needs a GPU device")
+    if t in ("rccl", "ipc") and device.type != "cuda":
+        raise ValueError(f"transport {t!r} needs a GPU device")
+    if t == "ipc" and size == 1:
+        return "self"
     return t
 
 
@@ -212,6 +214,8 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
                           "transport (RMA_RCCL_FALLBACK=1)", RuntimeWarning, stacklevel=2)
             tname = "staged"
             comm = C.TorchDistComm(staged=True)
+    elif tname == "ipc":
+        comm = None  # needs the topology's peers: built below
     else:
         comm = C.TorchDistComm(staged=(tname == "staged"))
 
@@ -220,12 +224,15 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
     me = comm_rank
     coords = tuple(topo.coords(me))
     neighbors = tuple(tuple(p) for p in topo.neighbors(me))
+    if tname == "ipc":
+        peers = [p for nb in neighbors for p in nb] + list(topo.diagonals(me))
+        comm = C.IpcComm(dev, peers, timeout_s=timeout_s)
     nxyz_g = tuple(geo.n_global(nxyz[d], dims[d], overlaps[d], periods[d]) if nxyz[d] > 1 else 1
                    for d in range(3))
 
     halo = None
     extra = {}
-    if dev.type == "cuda" and tname in ("rccl", "self", "loopback"):
+    if dev.type == "cuda" and tname in ("rccl", "ipc", "self", "loopback"):
         from .._native import native
 
         if tname == "loopback":
@@ -236,7 +243,7 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
             extra["stream"] = stream
             torch.cuda.set_stream(stream)
         else:
-            ncomm = comm.native if isinstance(comm, C.RcclComm) else None
+            ncomm = comm.native if isinstance(comm, (C.RcclComm, C.IpcComm)) else None
         halo = native().HaloExchanger(ncomm, me, [list(p) for p in neighbors])
         if self_via_transport:
             halo.set_self_via_transport(True)

@@ -201,6 +201,12 @@ for s in "$@"; do
              --pipec "" --ldsdpp "" --old "" --alt "" \
              --kinds piper:20,piper_sp:20,piper_sp2:20,piper:24,piper_sp:24,piper_sp2:24 \
              --out "$OUT/sp_ab.json" || exit 1 ;;
+    tests_ipc) step tests_ipc 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+             "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
+             "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" -p no:cacheprovider || exit 1 ;;
+    tests_ipc_hs) RMA_IPC_HOST_SYNC=1 step tests_ipc_hs 400 python -u -m pytest -x -v --timeout 120 \
+             --timeout-method thread "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
+             "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" -p no:cacheprovider || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \

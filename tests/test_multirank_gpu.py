@@ -563,3 +563,41 @@ def test_user_example_gpu_equals_golden(hide, P, dims):
     nxg, nyg = dims[0] * (nx - 2) + 2, dims[1] * (ny - 2) + 2
     G0 = golden.initial_torch(nxg, nyg)
     assert np.array_equal(T, golden.run(nxg, nyg, nt, T0=G0)[1:-1, 1:-1])
+
+
+@pytest.mark.parametrize("variant,world,dims", [("perf_hide", 2, (2, 1)), ("perf", 4, (2, 2)),
+                                                ("kp", 2, (1, 2)), ("perf_hide", 4, (4, 1))])
+def test_ipc_transport_processes(tmp_path, variant, world, dims):
+    """transport="ipc": separate processes sharing cuda:0 move every halo
+    device-to-device through HIP IPC mailboxes (no RCCL, no host staging);
+    the gathered field == the golden model, bitwise (2x2: the merged x+y group
+    with corner blocks to the diagonal ranks)."""
+    run_procs(world, "mp_targets:diffusion_gpu", str(tmp_path), variant, 130, 66, 25, dims,
+              env={"RMA_TRANSPORT": "ipc", "RMA_IPC_MAILBOX_MB": "1"})
+    Tv = np.load(tmp_path / "Tv.npy")
+    nxg, nyg, transport = open(tmp_path / "meta.txt").read().split()[:3]
+    assert transport == "ipc"
+    assert np.array_equal(Tv, golden.run(int(nxg), int(nyg), 25)[1:-1, 1:-1])
+
+
+@pytest.mark.parametrize("K", [4, 8])
+def test_ipc_transport_temporal_tiles(tmp_path, K):
+    """K-step passes (width-K halos, one exchange per pass, frame on the
+    high-priority stream) over the IPC transport, 2x2 processes: every tile ==
+    the golden model's window, bitwise."""
+    from rocm_mpi_amd import ops
+
+    nx, ny, nt = 120, 90, 3 * K + 1
+    run_procs(4, "mp_targets:diffusion_tiles", str(tmp_path), "perf_hide", nx, ny, nt, (2, 2), K,
+              "cuda:0", env={"RMA_TRANSPORT": "ipc"})
+    metas = [open(tmp_path / f"meta{r}.txt").read().split() for r in range(4)]
+    nxg, nyg = int(metas[0][2]), int(metas[0][3])
+    assert metas[0][6] == "ipc"
+    T0 = torch.empty((nyg, nxg), dtype=torch.float64)
+    ops.init_random_(T0, ops.TileGeometry(0, 0, nxg, nyg, 1.0, 1.0), seed=1234)
+    G = golden.run(nxg, nyg, nt, T0=T0.numpy())
+    for r in range(4):
+        cx, cy, ol = int(metas[r][0]), int(metas[r][1]), int(metas[r][4])
+        T = np.load(tmp_path / f"tile{r}.npy")
+        gx0, gy0 = cx * (nx - ol), cy * (ny - ol)
+        assert np.array_equal(T, G[gy0:gy0 + ny, gx0:gx0 + nx])
