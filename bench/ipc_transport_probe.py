@@ -1,0 +1,76 @@
+#!/usr/bin/env python
+"""Multi-process halo transports on ONE node: HIP IPC (device-direct) vs the
+host-staged gloo path, with every process on cuda:0 (RCCL refuses ranks that
+share a GPU) -- run under the package launcher:
+
+    python -m rocm_mpi_amd.launch -n 4 -- bench/ipc_transport_probe.py \\
+        --transport ipc --n 2048 --K 1 --steps 400 --check
+
+Rank 0 prints one JSON line: ms per step (max over ranks), the transport, and
+with --check (canonical arithmetic) whether the gathered field equals the
+NumPy golden model bitwise. perf_hide with K = 1 exchanges every step, the
+hardest ordering test for a transport (tests/golden.py is the oracle).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--transport", default="ipc", choices=["ipc", "staged"])
+    ap.add_argument("--n", type=int, default=2048, help="local tile edge")
+    ap.add_argument("--K", type=int, default=1, help="steps per pass")
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--variant", default="perf_hide")
+    ap.add_argument("--dims", default="0,0")
+    ap.add_argument("--check", action="store_true", help="canonical arithmetic, golden compare")
+    a = ap.parse_args(argv)
+    os.environ["RMA_TRANSPORT"] = a.transport
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    dims = tuple(int(v) for v in a.dims.split(",")) + (0,)
+    m = Diffusion2D(DiffusionConfig(variant=a.variant, nx=a.n, ny=a.n, nt=a.steps, dims=dims,
+                                    quiet=True, init="gaussian", init_on="host", temporal=a.K,
+                                    fast_math=a.K > 1 and not a.check, device="cuda:0"))
+    g = gg.global_grid()
+    m.step(2 * a.K)
+    m.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    m.step(a.steps)
+    m.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = {"transport": g.transport, "ranks": g.nprocs, "dims": list(g.dims[:2]), "tile": a.n,
+           "K": a.K, "steps": a.steps, "variant": a.variant,
+           "ms_per_step_max": float(t.item()) * 1e3}
+    if a.check:
+        Tv = m.gather_interior()
+        if g.me == 0:
+            import golden
+
+            G = golden.run(g.nxyz_g[0], g.nxyz_g[1], a.steps + 2 * a.K)
+            out["bitwise_golden"] = bool(np.array_equal(Tv.numpy(), G[1:-1, 1:-1]))
+    m.close()  # finalizes the grid it created
+    if g.me == 0:
+        print(json.dumps(out), flush=True)
+    return 0 if out.get("bitwise_golden", True) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -10,13 +10,15 @@
 // ranks drive different GPUs, on-device when they share one). Ordering is
 // stream-ordered on the GPU and handshaked on the host:
 //   * sender, generation g of a (sender, receiver) pair: waits (host) until the
-//     receiver has ENQUEUED its "done with g-2" event record, makes its stream
-//     wait on that interprocess event, copies into slot g%2, records its own
-//     interprocess "sent" event, publishes g in the receiver's shared-memory
-//     flag block;
-//   * receiver: waits (host) until the sender published g, makes its stream
-//     wait on the sender's "sent" event, copies the slot out, records its
-//     "done" event, publishes g.
+//     receiver has published "done with g-2", copies into slot g%2, records
+//     its "sent" event, waits for it on the host, publishes g in the
+//     receiver's shared-memory flag block;
+//   * receiver: waits (host) until the sender published g, copies the slot
+//     out, records its "done" event, waits for it, publishes g.
+// (RMA_IPC_GPU_EVENTS=1: the flags mean "record enqueued" and the streams wait
+// on the peer's interprocess events instead of the host; see ipc.cpp.) The
+// executor enqueues the interior before the frame and the exchange for such a
+// host-synchronising transport, so the blocking costs no overlap.
 // Host waits are bounded (timeout -> rma::Error naming the peer); the GPU only
 // ever waits on event records the host has seen enqueued, so a dead peer ends
 // in an exception, not a hang. Flags live in one POSIX shared-memory block per
@@ -76,6 +78,10 @@ class IpcTransport : public P2PTransport {
     void* done_ev = nullptr;
     // mine (sender side): sent event for my messages to this peer
     void* sent_ev = nullptr;
+    // host-synchronised mode: plain events (a host wait on an interprocess
+    // event costs ~1 ms on this runtime)
+    void* sent_local = nullptr;
+    void* done_local = nullptr;
     // the peer's, opened: its mailbox for my messages, its done / sent events
     void* r_mailbox = nullptr;
     void* r_done_ev = nullptr;

@@ -366,6 +366,21 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
   // the previous frame and interior (lag_: not the previous exchange)
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(lag_ ? e_fr_ : e_hi_), 0));
+  // a transport that synchronises on the host (loopback, IPC) blocks in
+  // exchange() until the frame is done: enqueue the interior first, so it
+  // overlaps the frame and the exchange all the same (its dependencies were set
+  // just above; the order of the two streams' launches changes nothing else)
+  const bool interior_first = halo_ && !halo_->capturable();
+  auto interior = [&]() {
+    rec(3, s_lo_);
+    if (!interior_.empty()) {
+      TraceRange ti("rma.interior");
+      stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &interior_, 1, c, p_.tune, s_lo_);
+    }
+    rec(4, s_lo_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+  };
+  if (interior_first) interior();
   rec(0, s_hi_);
   StencilTuning ft = p_.tune;
   ft.chunk_rows = std::min(ft.chunk_rows, 16);
@@ -381,13 +396,7 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
   }
   rec(2, s_hi_);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
-  rec(3, s_lo_);
-  if (!interior_.empty()) {
-    TraceRange ti("rma.interior");
-    stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, &interior_, 1, c, p_.tune, s_lo_);
-  }
-  rec(4, s_lo_);
-  RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+  if (!interior_first) interior();
   if (ev[4]) tseq_.push_back(0);
 }
 
@@ -446,6 +455,18 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   TraceRange tr("rma.pass.hide");
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(lag_ ? e_fr_ : e_hi_), 0));
+  // host-synchronising transport (loopback, IPC): interior first, see enqueue_step
+  const bool interior_first = halo_ && !halo_->capturable();
+  auto interior = [&]() {
+    rec(3, s_lo_);
+    if (!g.interior.empty()) {
+      TraceRange ti("rma.interior");
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.interior, 1, tn, s_lo_);
+    }
+    rec(4, s_lo_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+  };
+  if (interior_first) interior();
   rec(0, s_hi_);
   if (!g.frame.empty()) {
     TraceRange tb("rma.boundary");
@@ -477,13 +498,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   }
   rec(2, s_hi_);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
-  rec(3, s_lo_);
-  if (!g.interior.empty()) {
-    TraceRange ti("rma.interior");
-    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.interior, 1, tn, s_lo_);
-  }
-  rec(4, s_lo_);
-  RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+  if (!interior_first) interior();
   if (ev[4]) tseq_.push_back(0);
 }
 

@@ -25,13 +25,17 @@ std::atomic<uint64_t>* slot_flag(void* block, int sender, int which) {
   return reinterpret_cast<std::atomic<uint64_t>*>(block) + 2 * sender + which;
 }
 constexpr int kSent = 0, kDone = 1;
-// RMA_IPC_HOST_SYNC=1: the sender waits on the host for its copies before it
-// publishes a generation, the receiver for its copies before it frees the slot
-// (no interprocess event waits on the GPU)
+// Default: the sender waits on the host for its own copies (its own event)
+// before it publishes a generation, the receiver for its own copies before it
+// frees the slot, so no process ever waits on an event it opened from another
+// one. RMA_IPC_GPU_EVENTS=1 instead makes the streams wait on the peers'
+// interprocess events (no host blocking); on the HIP 7.0 runtime in torch that
+// hipStreamWaitEvent on an opened event fails intermittently with "invalid
+// argument" (bench/ipc_transport_probe.py, profiles/SUMMARY_r4.md §9).
 bool host_sync() {
   static const bool v = [] {
-    const char* e = std::getenv("RMA_IPC_HOST_SYNC");
-    return e && e[0] == '1';
+    const char* e = std::getenv("RMA_IPC_GPU_EVENTS");
+    return !(e && e[0] == '1');
   }();
   return v;
 }
@@ -85,6 +89,10 @@ IpcTransport::IpcTransport(int rank, int size, int device, const std::vector<int
     P.done_ev = e;
     RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventInterprocess | hipEventDisableTiming));
     P.sent_ev = e;
+    RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    P.sent_local = e;
+    RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    P.done_local = e;
     if (p == rank) {  // periodic self neighbour through the transport: no IPC
       P.r_mailbox = P.mailbox;
       P.r_done_ev = P.done_ev;
@@ -109,6 +117,8 @@ IpcTransport::~IpcTransport() {
     if (P.mailbox) (void)hipFree(P.mailbox);
     if (P.done_ev) (void)hipEventDestroy(E(P.done_ev));
     if (P.sent_ev) (void)hipEventDestroy(E(P.sent_ev));
+    if (P.sent_local) (void)hipEventDestroy(E(P.sent_local));
+    if (P.done_local) (void)hipEventDestroy(E(P.done_local));
   }
   if (flags_) {
     munmap(flags_, flags_bytes_);
@@ -253,8 +263,12 @@ void IpcTransport::group_end() {
         RMA_HIP_CHECK(hipMemcpyAsync(dst + off, o->buf, o->bytes, hipMemcpyDeviceToDevice, s));
       off += o->bytes;
     }
-    RMA_HIP_CHECK(hipEventRecord(E(P.sent_ev), s));
-    if (hs) RMA_HIP_CHECK(hipEventSynchronize(E(P.sent_ev)));
+    if (hs) {
+      RMA_HIP_CHECK(hipEventRecord(E(P.sent_local), s));
+      RMA_HIP_CHECK(hipEventSynchronize(E(P.sent_local)));
+    } else {
+      RMA_HIP_CHECK(hipEventRecord(E(P.sent_ev), s));
+    }
     slot_flag(P.r_flags, rank_, kSent)->store(g, std::memory_order_release);
   }
   for (auto& [p, ops] : in) {
@@ -278,8 +292,12 @@ void IpcTransport::group_end() {
         RMA_HIP_CHECK(hipMemcpyAsync(o->buf, src + off, o->bytes, hipMemcpyDeviceToDevice, s));
       off += o->bytes;
     }
-    RMA_HIP_CHECK(hipEventRecord(E(P.done_ev), s));
-    if (hs) RMA_HIP_CHECK(hipEventSynchronize(E(P.done_ev)));
+    if (hs) {
+      RMA_HIP_CHECK(hipEventRecord(E(P.done_local), s));
+      RMA_HIP_CHECK(hipEventSynchronize(E(P.done_local)));
+    } else {
+      RMA_HIP_CHECK(hipEventRecord(E(P.done_ev), s));
+    }
     slot_flag(flags_, p, kDone)->store(g, std::memory_order_release);
   }
   sends_.clear();

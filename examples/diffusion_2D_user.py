@@ -6,7 +6,7 @@ loop, the package supplies the implicit global grid, the halo update and the
 HIP stencil kernel.
 
     python examples/diffusion_2D_user.py --nx 4096 --ny 4096 --nt 200
-    python -m rocm_mpi_amd.launch -n 4 examples/diffusion_2D_user.py -- --hide
+    python -m rocm_mpi_amd.launch -n 4 -- examples/diffusion_2D_user.py --hide
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
         examples/diffusion_2D_user.py --device cpu           # gloo, CPU twins
 

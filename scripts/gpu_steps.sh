@@ -204,9 +204,18 @@ for s in "$@"; do
     tests_ipc) step tests_ipc 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
              "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
              "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" -p no:cacheprovider || exit 1 ;;
-    tests_ipc_hs) RMA_IPC_HOST_SYNC=1 step tests_ipc_hs 400 python -u -m pytest -x -v --timeout 120 \
+    tests_ipc_ev) RMA_IPC_GPU_EVENTS=1 step tests_ipc_ev 400 python -u -m pytest -x -v --timeout 120 \
              --timeout-method thread "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
              "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" -p no:cacheprovider || exit 1 ;;
+    ipc_probe) for cfg in "ipc 258 1 2000 --check" "staged 258 1 2000 --check" "ipc 1026 1 400 --check" \
+                          "ipc 2048 1 400" "staged 2048 1 400" "ipc 4096 24 480" "staged 4096 24 480"; do
+               set -- $cfg; tag="ipc_probe_$1_$2_$3"
+               step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- bench/ipc_transport_probe.py \
+                 --transport $1 --n $2 --K $3 --steps $4 $5 || exit 1
+             done ;;
+    tests_multirank) step tests_multirank 600 python -u -m pytest -x -q --timeout 120 \
+             --timeout-method thread tests/test_multirank_gpu.py tests/test_executor_gpu.py \
+             -p no:cacheprovider || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
