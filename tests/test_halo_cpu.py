@@ -180,3 +180,15 @@ def test_copy_planes_cpu_twin():
     assert torch.equal(B, ref)
     with pytest.raises(ValueError):
         ops.copy_planes([(B[:, :1], A[:, :1])] * 9)
+
+
+def test_ipc_transport_selection():
+    """transport="ipc" needs GPU fields; one rank needs no transport."""
+    import torch
+
+    from rocm_mpi_amd.parallel.implicit_grid import _choose_transport
+
+    with pytest.raises(ValueError, match="needs a GPU"):
+        _choose_transport("ipc", 2, torch.device("cpu"))
+    assert _choose_transport("ipc", 1, torch.device("cuda", 0)) == "self"
+    assert _choose_transport("ipc", 4, torch.device("cuda", 0)) == "ipc"
