@@ -133,6 +133,9 @@ def parse(argv=None):
                     help="functional test of the multi-process path on ONE GPU: ranks share "
                          "the card over the host-staged transport; the record says so and is "
                          "never a scaling point")
+    ap.add_argument("--shared-gpu-transport", default="staged", choices=["staged", "ipc"],
+                    help="halo transport of --shared-gpu-test: host-staged gloo, or HIP IPC "
+                         "device-to-device copies between the processes")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the same driver on the C++ CPU twins over gloo (tests of the "
@@ -716,7 +719,7 @@ def run(a, world: int, rank: int) -> int:
     gpu = a.device == "cuda"
     shared = a.shared_gpu_test and gpu and world > 1
     if shared:
-        os.environ["RMA_TRANSPORT"] = "staged"
+        os.environ["RMA_TRANSPORT"] = a.shared_gpu_transport
     elif gpu and world > 1:
         # a scaling point must never silently run on the host-staged transport
         os.environ["RMA_RCCL_STRICT"] = "1"

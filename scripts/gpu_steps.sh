@@ -216,6 +216,8 @@ for s in "$@"; do
     tests_multirank) step tests_multirank 600 python -u -m pytest -x -q --timeout 120 \
              --timeout-method thread tests/test_multirank_gpu.py tests/test_executor_gpu.py \
              -p no:cacheprovider || exit 1 ;;
+    tests_shared) step tests_shared 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+             "tests/test_bench_gpu.py::test_bench_two_processes_sharing_the_gpu" -p no:cacheprovider || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \

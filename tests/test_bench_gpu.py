@@ -77,18 +77,20 @@ def test_bench_default_check_on_one_gpu():
     assert c["drift_check"]["steps"] == 52 and c["fast_math_drift_max"] <= 1e-14
 
 
-def test_bench_two_processes_sharing_the_gpu(tmp_path):
-    """The multi-process bench flow on one GPU (torchrun-style ranks, staged
-    halo transport, per-rank timings, solo re-time, in-run halo check): a
-    functional test, labelled so it can never pass for a scaling point."""
-    d = bench("--gpus", "2", "--shared-gpu-test", "--nx", "4096", "--steps", "24", "--warmup", "5",
-              "--single-step-steps", "4", "--check-nx", "530", timeout=600)
+@pytest.mark.parametrize("transport", ["staged", "ipc"])
+def test_bench_two_processes_sharing_the_gpu(tmp_path, transport):
+    """The multi-process bench flow on one GPU (torchrun-style ranks, staged or
+    HIP-IPC halo transport, per-rank timings, solo re-time, in-run halo check):
+    a functional test, labelled so it can never pass for a scaling point."""
+    d = bench("--gpus", "2", "--shared-gpu-test", "--shared-gpu-transport", transport, "--nx",
+              "4096", "--steps", "24", "--warmup", "5", "--single-step-steps", "4", "--check-nx",
+              "530", timeout=600)
     c = d["config"]
     assert c["shared_gpu_test"] is True and "shared-GPU" in d["metric"]
-    assert c["ranks"] == 2 and d["n_gpus"] == 1 and c["transport"] == "staged"
+    assert c["ranks"] == 2 and d["n_gpus"] == 1 and c["transport"] == transport
     assert c["rccl_halo_bitwise_ok"] is True and c["halo_check"]["tiles_mismatched"] == 0
     assert c["pass_timing"]["passes"] == len(c["passes_timed"]) and sum(c["passes_timed"]) == 24
     assert len(c["pci_bus_ids"]) == 2 and c["nonfinite_cells_sampled"] == 0
     assert [r["rank"] for r in c["ranks_detail"]] == [0, 1]
-    assert c["preflight"]["ring_ok"] and c["preflight"]["halo"]["transport"] == "staged"
+    assert c["preflight"]["ring_ok"] and c["preflight"]["halo"]["transport"] == transport
     assert c["headline_window_check"]["bitwise"] is True
