@@ -4,7 +4,9 @@ Reference: scripts/rocmaware_test_selectdevice.jl:1-25 — MPI.Init, node-local
 rank via Comm_split_type(COMM_TYPE_SHARED), AMDGPU.device!(rank_l+1), a
 4-element Float64 device buffer filled with the rank, ring Sendrecv! on the
 DEVICE buffers between barriers. Here: torch.distributed bootstrap, RCCL
-send/recv on device tensors over xGMI (gloo on CPU-only hosts).
+send/recv on device tensors over xGMI (gloo on CPU-only hosts); ``--transport
+ipc``: HIP IPC device-to-device copies between the processes of one node
+(which also runs with every rank on one GPU, where RCCL refuses).
 
 Fixes the reference quirk (:12-13) of computing ring neighbours from the
 node-local rank modulo the GLOBAL size (only correct on one node): the ring
@@ -35,13 +37,15 @@ def run(n: int = 4, transport: str = "auto", verbose: bool = True,
     local, lsize = C.node_local_rank(rank, size)
     dev = C.select_device(local)
     t = _choose_transport(transport, size, dev)
+    dst, src = (rank + 1) % size, (rank - 1) % size
     if t == "rccl":
         comm = C.RcclComm(dev)
+    elif t == "ipc":  # device-to-device between processes of one node, no RCCL
+        comm = C.IpcComm(dev, [dst, src])
     elif t == "self":
         comm = C.SelfComm()
     else:
         comm = C.TorchDistComm(staged=(t == "staged"))
-    dst, src = (rank + 1) % size, (rank - 1) % size
     if verbose:
         name = torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"
         print(f"rank={rank} local_rank={local}/{lsize} (device={dev} {name}), size={size}, "

@@ -377,6 +377,28 @@ class IpcComm(TorchDistComm):
     def native(self):
         return self._c
 
+    def exchange(self, ops):
+        """Device tensors to / from connected peers: device-to-device through
+        the mailboxes, stream-ordered on the current stream; anything else
+        host-staged over gloo."""
+        if not ops:
+            return
+        if not all(o.tensor.is_cuda and o.tensor.is_contiguous() and o.peer in self.peers
+                   for o in ops):
+            return super().exchange(ops)
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        self._c.group_start()
+        try:
+            for o in ops:
+                t = o.tensor
+                nb = t.numel() * t.element_size()
+                if o.kind == "send":
+                    self._c.send(t.data_ptr(), nb, o.peer, s)
+                else:
+                    self._c.recv(t.data_ptr(), nb, o.peer, s)
+        finally:
+            self._c.group_end()
+
     def finalize(self) -> None:
         if self._c is not None:
             if torch.cuda.is_available() and torch.cuda.is_initialized():

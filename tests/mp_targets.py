@@ -134,3 +134,15 @@ def user_example(rank, world, outdir, nx, ny, nt, dims):
     if rank == 0:
         np.save(os.path.join(outdir, "T0.npy"), T0.numpy())
         np.save(os.path.join(outdir, "T.npy"), T.numpy())
+
+
+def ring_gpu(rank, world, outdir, transport):
+    """The reference smoke test's device-buffer ring on cuda (every rank on the
+    one visible GPU)."""
+    from rocm_mpi_amd.apps import rocmaware_test_selectdevice as app
+
+    vals = app.run(4, transport=transport, verbose=False)
+    np.save(os.path.join(outdir, f"ring{rank}.npy"), np.array(vals))
+    from rocm_mpi_amd.parallel import comm as C
+
+    C.shutdown_distributed()

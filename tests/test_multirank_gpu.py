@@ -601,3 +601,12 @@ def test_ipc_transport_temporal_tiles(tmp_path, K):
         T = np.load(tmp_path / f"tile{r}.npy")
         gx0, gy0 = cx * (nx - ol), cy * (ny - ol)
         assert np.array_equal(T, G[gy0:gy0 + ny, gx0:gx0 + nx])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_ring_smoke_test(tmp_path, world):
+    """The reference's rocmaware_test_selectdevice ring (4 doubles per rank on
+    the device, sent to rank+1) over HIP IPC between processes on cuda:0."""
+    run_procs(world, "mp_targets:ring_gpu", str(tmp_path), "ipc")
+    for r in range(world):
+        assert np.load(tmp_path / f"ring{r}.npy").tolist() == [float((r - 1) % world)] * 4
