@@ -219,6 +219,11 @@ for s in "$@"; do
              -p no:cacheprovider || exit 1 ;;
     tests_shared) step tests_shared 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
              "tests/test_bench_gpu.py::test_bench_two_processes_sharing_the_gpu" -p no:cacheprovider || exit 1 ;;
+    chunk8192) for c in 128 192 256 384 512; do
+               step "chunk8192_xy_$c" 300 python bench/rccl_self_overhead.py --n 8192 --K 24 \
+                 --periodic xy --steps 2400 --pattern opop --spacing equal --chunk2 $c \
+                 --out "$OUT/chunk8192_xy_$c.json" || exit 1
+             done ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
