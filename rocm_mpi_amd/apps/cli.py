@@ -83,7 +83,7 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--init-on", choices=["auto", "device", "host"], default="auto")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--transport", default=os.environ.get("RMA_TRANSPORT", "auto"),
-                    choices=["auto", "rccl", "staged", "gloo", "self"])
+                    choices=["auto", "rccl", "ipc", "staged", "gloo", "self"])
     ap.add_argument("--device", default=None, help="cpu, cuda, cuda:N (default: one GPU per rank)")
     ap.add_argument("--vis", dest="do_vis", action="store_true", default=d["do_vis"])
     ap.add_argument("--no-vis", dest="do_vis", action="store_false")
