@@ -82,6 +82,7 @@ def main(argv=None) -> int:
     rank, size, _ = C.env_world()
     vals = run(a.n, a.transport, self_ring=a.self_ring)
     ok = all(v == float((rank - 1) % size) for v in vals)
+    C.shutdown_distributed()
     return 0 if ok else 1
 
 

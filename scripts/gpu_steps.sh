@@ -224,6 +224,11 @@ for s in "$@"; do
                  --periodic xy --steps 2400 --pattern opop --spacing equal --chunk2 $c \
                  --out "$OUT/chunk8192_xy_$c.json" || exit 1
              done ;;
+    apps_ipc) step ring_ipc 120 python -m rocm_mpi_amd.launch -n 4 -m \
+               rocm_mpi_amd.apps.rocmaware_test_selectdevice -- --transport ipc && \
+             step hide_ipc_2x2 300 python -m rocm_mpi_amd.launch -n 4 -m \
+               rocm_mpi_amd.apps.diffusion_2D_perf_hide -- --transport ipc --nx 4096 --ny 4096 \
+               --nt 1000 --dims 2,2 --device cuda:0 || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
