@@ -146,3 +146,25 @@ def ring_gpu(rank, world, outdir, transport):
     from rocm_mpi_amd.parallel import comm as C
 
     C.shutdown_distributed()
+
+
+def ipc_overflow(rank, world, outdir):
+    """A halo message larger than the IPC mailbox fails loudly on every rank
+    (before any rank waits for another), then the grid still finalizes."""
+    import torch
+
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+    from rocm_mpi_amd.parallel.halo import update_halo_
+
+    gg.init_global_grid(130, 66, 1, dimx=world, quiet=True, device="cuda:0")
+    assert gg.global_grid().transport == "ipc"
+    A = torch.zeros((66, 130), dtype=torch.float64, device="cuda:0")
+    msg = ""
+    try:
+        update_halo_(A)
+    except RuntimeError as e:
+        msg = str(e)
+    torch.cuda.synchronize()
+    gg.finalize_global_grid()
+    with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+        f.write(msg)

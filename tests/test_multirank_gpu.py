@@ -610,3 +610,12 @@ def test_ipc_ring_smoke_test(tmp_path, world):
     run_procs(world, "mp_targets:ring_gpu", str(tmp_path), "ipc")
     for r in range(world):
         assert np.load(tmp_path / f"ring{r}.npy").tolist() == [float((r - 1) % world)] * 4
+
+
+def test_ipc_mailbox_overflow_fails_on_every_rank(tmp_path):
+    """RMA_IPC_MAILBOX_MB too small for a halo plane: every rank raises an
+    error naming the setting (no rank waits for a peer that gave up)."""
+    run_procs(2, "mp_targets:ipc_overflow", str(tmp_path),
+              env={"RMA_TRANSPORT": "ipc", "RMA_IPC_MAILBOX_MB": "0.0001"})
+    for r in range(2):
+        assert "RMA_IPC_MAILBOX_MB" in open(tmp_path / f"err{r}.txt").read()
