@@ -231,6 +231,11 @@ for s in "$@"; do
              step hide_ipc_2x2 300 python -m rocm_mpi_amd.launch -n 4 -m \
                rocm_mpi_amd.apps.diffusion_2D_perf_hide -- --transport ipc --nx 4096 --ny 4096 \
                --nt 1000 --dims 2,2 --device cuda:0 || exit 1 ;;
+    ipc_trace) for t in ipc staged; do
+               PYTHONPATH="$R" prof "ipc_trace_$t" 240 --memory-copy-trace --kernel-trace --stats --output-format csv \
+                 -d "$R/$OUT/ipc_trace_$t" -o run -- python3 -m rocm_mpi_amd.launch -n 4 -- \
+                 "$R/bench/ipc_transport_probe.py" --transport $t --n 258 --K 1 --steps 200 || exit 1
+             done ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
