@@ -16,7 +16,8 @@
 //   * receiver: waits (host) until the sender published g, copies the slot
 //     out, records its "done" event, waits for it, publishes g.
 // (RMA_IPC_GPU_EVENTS=1: the flags mean "record enqueued" and the streams wait
-// on the peer's interprocess events instead of the host; see ipc.cpp.) The
+// on the peer's interprocess events instead of the host; RMA_IPC_STREAM_FLAGS=1:
+// the GPU writes the flags after the copies; see ipc.cpp.) The
 // executor enqueues the interior before the frame and the exchange for such a
 // host-synchronising transport, so the blocking costs no overlap.
 // Host waits are bounded (timeout -> rma::Error naming the peer); the GPU only
@@ -87,6 +88,7 @@ class IpcTransport : public P2PTransport {
     void* r_done_ev = nullptr;
     void* r_sent_ev = nullptr;
     void* r_flags = nullptr;  // the peer's shared-memory flag block (mapped)
+    void* r_flags_dev = nullptr;  // ... registered for GPU writes (stream flags)
     uint64_t send_gen = 0, recv_gen = 0;
     bool connected = false;
   };
@@ -99,6 +101,7 @@ class IpcTransport : public P2PTransport {
   std::string token_;
   std::vector<Peer> peers_;
   void* flags_ = nullptr;  // my flag block: [sender][2] = {sent, done}
+  void* flags_dev_ = nullptr;  // its device address (RMA_IPC_STREAM_FLAGS=1)
   size_t flags_bytes_ = 0;
   std::string shm_name_;
   int depth_ = 0;

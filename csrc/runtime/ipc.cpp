@@ -39,6 +39,25 @@ bool host_sync() {
   }();
   return v;
 }
+// RMA_IPC_STREAM_FLAGS=1: the flags are written by the GPU, in stream order
+// after the copies (hipStreamWriteValue64 into the shared-memory block,
+// registered with hipHostRegister in every process that writes it), so the
+// sender's host never waits for its copies; the receiver's host still polls
+// for the sender's flag before it enqueues its copies
+bool stream_flags() {
+  static const bool v = [] {
+    const char* e = std::getenv("RMA_IPC_STREAM_FLAGS");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+size_t page_round(size_t b) { return (b + 4095) / 4096 * 4096; }
+void* register_block(void* host, size_t bytes) {
+  RMA_HIP_CHECK(hipHostRegister(host, bytes, hipHostRegisterMapped));
+  void* d = nullptr;
+  RMA_HIP_CHECK(hipHostGetDevicePointer(&d, host, 0));
+  return d;
+}
 }  // namespace
 
 std::string ipc_shm_name(const std::string& token, int rank) {
@@ -57,7 +76,7 @@ IpcTransport::IpcTransport(int rank, int size, int device, const std::vector<int
   RMA_HIP_CHECK(hipSetDevice(device));
   // my flag block: per sender {sent generation, done generation}
   shm_name_ = ipc_shm_name(token, rank);
-  flags_bytes_ = sizeof(uint64_t) * 2 * (size_t)size;
+  flags_bytes_ = page_round(sizeof(uint64_t) * 2 * (size_t)size);
   const int fd = shm_open(shm_name_.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0600);
   if (fd < 0) throw_error("shm_open failed", __FILE__, __LINE__, shm_name_);
   if (ftruncate(fd, (off_t)flags_bytes_) != 0) {
@@ -74,6 +93,7 @@ IpcTransport::IpcTransport(int rank, int size, int device, const std::vector<int
     slot_flag(flags_, s, kSent)->store(0);
     slot_flag(flags_, s, kDone)->store(0);
   }
+  if (stream_flags()) flags_dev_ = register_block(flags_, flags_bytes_);
   peers_.resize(size);
   std::vector<int> ps(peers);
   std::sort(ps.begin(), ps.end());
@@ -98,6 +118,7 @@ IpcTransport::IpcTransport(int rank, int size, int device, const std::vector<int
       P.r_done_ev = P.done_ev;
       P.r_sent_ev = P.sent_ev;
       P.r_flags = flags_;
+      P.r_flags_dev = flags_dev_;
       P.connected = true;
     }
   }
@@ -112,6 +133,7 @@ IpcTransport::~IpcTransport() {
       if (P.r_mailbox) (void)hipIpcCloseMemHandle(P.r_mailbox);
       if (P.r_done_ev) (void)hipEventDestroy(E(P.r_done_ev));
       if (P.r_sent_ev) (void)hipEventDestroy(E(P.r_sent_ev));
+      if (P.r_flags_dev) (void)hipHostUnregister(P.r_flags);
       if (P.r_flags) munmap(P.r_flags, flags_bytes_);
     }
     if (P.mailbox) (void)hipFree(P.mailbox);
@@ -121,6 +143,7 @@ IpcTransport::~IpcTransport() {
     if (P.done_local) (void)hipEventDestroy(E(P.done_local));
   }
   if (flags_) {
+    if (flags_dev_) (void)hipHostUnregister(flags_);
     munmap(flags_, flags_bytes_);
     shm_unlink(shm_name_.c_str());
   }
@@ -181,6 +204,7 @@ void IpcTransport::connect(int p, const std::string& blob) {
   close(fd);
   if (m == MAP_FAILED) throw_error("mmap of a peer's IPC flag block failed", __FILE__, __LINE__, name);
   P.r_flags = m;
+  if (stream_flags()) P.r_flags_dev = register_block(m, flags_bytes_);
   P.connected = true;
 }
 
@@ -254,7 +278,7 @@ void IpcTransport::group_end() {
     const uint64_t g = ++P.send_gen;
     if (g > 2) {  // slot g % 2 was last read by the peer's receive of g - 2
       wait_flag(slot_flag(P.r_flags, rank_, kDone), g - 2, p, "receive done");
-      if (!hs) RMA_HIP_CHECK(hipStreamWaitEvent(s, E(P.r_done_ev), 0));
+      if (!hs && !P.r_flags_dev) RMA_HIP_CHECK(hipStreamWaitEvent(s, E(P.r_done_ev), 0));
     }
     char* dst = static_cast<char*>(P.r_mailbox) + (g & 1) * cap_;
     size_t off = 0;
@@ -262,6 +286,11 @@ void IpcTransport::group_end() {
       if (o->bytes)
         RMA_HIP_CHECK(hipMemcpyAsync(dst + off, o->buf, o->bytes, hipMemcpyDeviceToDevice, s));
       off += o->bytes;
+    }
+    if (P.r_flags_dev) {  // the GPU publishes g once the copies are done
+      RMA_HIP_CHECK(hipStreamWriteValue64(
+          s, slot_flag(P.r_flags_dev, rank_, kSent), g, 0));
+      continue;
     }
     if (hs) {
       RMA_HIP_CHECK(hipEventRecord(E(P.sent_local), s));
@@ -284,13 +313,17 @@ void IpcTransport::group_end() {
                                                    << cap_ << " (RMA_IPC_MAILBOX_MB)");
     const uint64_t g = ++P.recv_gen;
     wait_flag(slot_flag(flags_, p, kSent), g, p, "send");
-    if (!hs) RMA_HIP_CHECK(hipStreamWaitEvent(s, E(P.r_sent_ev), 0));
+    if (!hs && !flags_dev_) RMA_HIP_CHECK(hipStreamWaitEvent(s, E(P.r_sent_ev), 0));
     const char* src = static_cast<const char*>(P.mailbox) + (g & 1) * cap_;
     size_t off = 0;
     for (const Op* o : ops) {
       if (o->bytes)
         RMA_HIP_CHECK(hipMemcpyAsync(o->buf, src + off, o->bytes, hipMemcpyDeviceToDevice, s));
       off += o->bytes;
+    }
+    if (flags_dev_) {  // the GPU frees the slot once the copies are done
+      RMA_HIP_CHECK(hipStreamWriteValue64(s, slot_flag(flags_dev_, p, kDone), g, 0));
+      continue;
     }
     if (hs) {
       RMA_HIP_CHECK(hipEventRecord(E(P.done_local), s));

@@ -236,6 +236,15 @@ for s in "$@"; do
                  -d "$R/$OUT/ipc_trace_$t" -o run -- python3 -m rocm_mpi_amd.launch -n 4 -- \
                  "$R/bench/ipc_transport_probe.py" --transport $t --n 258 --K 1 --steps 200 || exit 1
              done ;;
+    tests_ipc_sf) RMA_IPC_STREAM_FLAGS=1 step tests_ipc_sf 400 python -u -m pytest -x -v --timeout 120 \
+             --timeout-method thread "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
+             "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" \
+             "tests/test_multirank_gpu.py::test_ipc_ring_smoke_test" -p no:cacheprovider || exit 1 ;;
+    ipc_probe_sf) for cfg in "ipc 258 1 2000 --check" "ipc 2048 1 400" "ipc 4096 24 480"; do
+               set -- $cfg; tag="ipc_probe_sf_$1_$2_$3"
+               RMA_IPC_STREAM_FLAGS=1 step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
+                 bench/ipc_transport_probe.py --transport $1 --n $2 --K $3 --steps $4 $5 || exit 1
+             done ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
