@@ -245,6 +245,9 @@ for s in "$@"; do
                RMA_IPC_STREAM_FLAGS=1 step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
                  bench/ipc_transport_probe.py --transport $1 --n $2 --K $3 --steps $4 $5 || exit 1
              done ;;
+    bench_small) for n in 16384 8192 4096; do
+               step "bench1000_$n" 300 python bench.py --nx $n --steps 1000 --json-out "$OUT/bench1000_$n.json" || exit 1
+             done ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
