@@ -248,6 +248,8 @@ for s in "$@"; do
     bench_small) for n in 16384 8192 4096; do
                step "bench1000_$n" 300 python bench.py --nx $n --steps 1000 --json-out "$OUT/bench1000_$n.json" || exit 1
              done ;;
+    tests_halo) step tests_halo 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+             tests/test_halo_gpu.py -p no:cacheprovider || exit 1 ;;
     tests_mask) step tests_mask 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
              "tests/test_pipe_gpu.py::test_piper_masked_cone_bitwise" \
              "tests/test_pipe_gpu.py::test_piper_schedule_variants_bitwise" \
