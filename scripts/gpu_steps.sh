@@ -206,6 +206,7 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" \
              "tests/test_multirank_gpu.py::test_ipc_ring_smoke_test" \
              "tests/test_multirank_gpu.py::test_ipc_mailbox_overflow_fails_on_every_rank" \
+             "tests/test_multirank_gpu.py::test_ipc_update_halo_device_fields" \
              -p no:cacheprovider || exit 1 ;;
     tests_ipc_ev) RMA_IPC_GPU_EVENTS=1 step tests_ipc_ev 400 python -u -m pytest -x -v --timeout 120 \
              --timeout-method thread "tests/test_multirank_gpu.py::test_ipc_transport_processes" \

@@ -168,3 +168,42 @@ def ipc_overflow(rank, world, outdir):
     gg.finalize_global_grid()
     with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
         f.write(msg)
+
+
+def halo_device(rank, world, outdir, nxyz, dims, periods, overlaps, staggers, nfields):
+    """update_halo_ of device fields (the native engine over RMA_TRANSPORT's
+    transport, every process on cuda:0) against the global truth."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_halo_cpu import corrupt
+    from test_halo_gpu import local_block
+
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+    from rocm_mpi_amd.parallel.halo import update_halo_
+
+    gg.init_global_grid(*nxyz, dimx=dims[0], dimy=dims[1], dimz=dims[2], periodx=periods[0],
+                        periody=periods[1], periodz=periods[2], overlaps=overlaps, quiet=True,
+                        device="cuda:0")
+    g = gg.global_grid()
+    nd = 3 if nxyz[2] > 1 else (2 if nxyz[1] > 1 else 1)
+    fields, expect = [], []
+    for f in range(nfields):
+        st = staggers[f % len(staggers)]
+        shp_l = tuple(nxyz[d] + st[d] for d in reversed(range(nd)))
+        shp_g = tuple(g.nxyz_g[d] + st[d] for d in reversed(range(nd)))
+        G = torch.rand(shp_g, generator=torch.Generator().manual_seed(100 + f),
+                       dtype=torch.float64)
+        A = local_block(G, g, shp_l)
+        expect.append(A.clone())
+        corrupt(A, g)
+        fields.append(A.to("cuda:0"))
+    update_halo_(*fields)
+    torch.cuda.synchronize()
+    ok = all(torch.equal(a.cpu(), e) for a, e in zip(fields, expect))
+    transport = g.transport
+    gg.finalize_global_grid()
+    with open(os.path.join(outdir, f"ok{rank}.txt"), "w") as fh:
+        fh.write(f"{int(ok)} {transport}")

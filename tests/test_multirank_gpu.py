@@ -619,3 +619,19 @@ def test_ipc_mailbox_overflow_fails_on_every_rank(tmp_path):
               env={"RMA_TRANSPORT": "ipc", "RMA_IPC_MAILBOX_MB": "0.0001"})
     for r in range(2):
         assert "RMA_IPC_MAILBOX_MB" in open(tmp_path / f"err{r}.txt").read()
+
+
+@pytest.mark.parametrize("case", [
+    ((9, 7, 1), (2, 2, 1), (0, 0, 0), (2, 2, 2), [(0, 0, 0), (1, 0, 0), (0, 1, 0), (-1, 0, 0)], 4),
+    ((12, 10, 1), (2, 2, 1), (1, 1, 0), (4, 4, 2), [(0, 0, 0)], 2),
+    ((6, 5, 7), (2, 2, 2), (0, 0, 0), (2, 2, 2), [(0, 0, 0), (0, 0, 1)], 2),
+], ids=["2d-staggered", "2d-periodic-hw2", "3d"])
+def test_ipc_update_halo_device_fields(tmp_path, case):
+    """update_halo_ of device fields between PROCESSES over the IPC transport
+    (merged x+y group for the 2-D fields, per-dimension groups in 3-D)."""
+    nxyz, dims, periods, overlaps, staggers, nf = case
+    world = dims[0] * dims[1] * dims[2]
+    run_procs(world, "mp_targets:halo_device", str(tmp_path), nxyz, dims, periods, overlaps,
+              staggers, nf, env={"RMA_TRANSPORT": "ipc", "RMA_IPC_MAILBOX_MB": "1"})
+    for r in range(world):
+        assert open(tmp_path / f"ok{r}.txt").read() == "1 ipc"
