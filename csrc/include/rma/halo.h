@@ -109,6 +109,7 @@ class HaloExchanger {
   std::array<std::array<int, 2>, 3> nbr_;
   std::vector<void*> bufs_;
   std::vector<size_t> buf_bytes_;
+  std::vector<void*> retired_;  // outgrown pack buffers, freed in the destructor
   int64_t bytes_last_ = 0;
   std::vector<Planned> cache_;
   uint64_t tick_ = 0;

@@ -40,8 +40,19 @@ class LoopbackHub {
   void wait_consumed(const Msg& m);               // blocks until receiver enqueued the copy
   std::mutex& mu_ref() { return mu_; }
   void notify() { cv_.notify_all(); }
+  // next event of `rank`'s pool (created on first use, recycled round-robin
+  // after kEventPool; owned by the hub). Only rank's own thread calls this.
+  void* event(int rank);
+  ~LoopbackHub();
+  LoopbackHub(const LoopbackHub&) = delete;
+  LoopbackHub& operator=(const LoopbackHub&) = delete;
 
  private:
+  struct Pool {
+    std::vector<void*> ev;
+    size_t next = 0;
+  };
+  std::vector<Pool> pools_;  // per rank
   int n_;
   double timeout_s_;
   std::mutex mu_;
@@ -68,13 +79,10 @@ class LoopbackEndpoint : public P2PTransport {
     int peer;
     stream_t stream;
   };
-  void* event();  // from a pool
   std::shared_ptr<LoopbackHub> hub_;
   int rank_;
   int depth_ = 0;
   std::vector<Op> sends_, recvs_;
-  std::vector<void*> pool_;
-  size_t next_ = 0;
 };
 
 }  // namespace rma

@@ -25,6 +25,7 @@ HaloExchanger::HaloExchanger(P2PTransport* comm, int self_rank,
 HaloExchanger::~HaloExchanger() {
   for (void* p : bufs_)
     if (p) (void)hipFree(p);
+  for (void* p : retired_) (void)hipFree(p);
 }
 
 bool HaloExchanger::active(int dim) const { return nbr_[dim][0] >= 0 || nbr_[dim][1] >= 0; }
@@ -35,7 +36,10 @@ void* HaloExchanger::buffer(size_t slot, size_t bytes) {
     buf_bytes_.resize(slot + 1, 0);
   }
   if (buf_bytes_[slot] < bytes) {
-    if (bufs_[slot]) RMA_HIP_CHECK(hipFree(bufs_[slot]));
+    // a peer's copy out of the old buffer may still be queued on the peer's
+    // stream (a send completes when the receiver ENQUEUED its copy): retire
+    // it until this exchanger goes away instead of freeing it under the copy
+    if (bufs_[slot]) retired_.push_back(bufs_[slot]);
     bufs_[slot] = nullptr;
     RMA_HIP_CHECK(hipMalloc(&bufs_[slot], bytes));
     buf_bytes_[slot] = bytes;

@@ -13,8 +13,27 @@ constexpr size_t kPool = 4096;
 hipEvent_t E(void* p) { return reinterpret_cast<hipEvent_t>(p); }
 }  // namespace
 
-LoopbackHub::LoopbackHub(int nranks, double timeout_s) : n_(nranks), timeout_s_(timeout_s) {
+LoopbackHub::LoopbackHub(int nranks, double timeout_s)
+    : pools_(nranks > 0 ? (size_t)nranks : 0), n_(nranks), timeout_s_(timeout_s) {
   RMA_CHECK_ARG(nranks >= 1, "nranks=" << nranks);
+}
+
+LoopbackHub::~LoopbackHub() {
+  for (Pool& p : pools_)
+    for (void* e : p.ev) (void)hipEventDestroy(E(e));
+}
+
+void* LoopbackHub::event(int rank) {
+  Pool& p = pools_[(size_t)rank];
+  if (p.ev.size() < kPool) {
+    hipEvent_t e;
+    RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    p.ev.push_back(e);
+    return e;
+  }
+  void* e = p.ev[p.next];
+  p.next = (p.next + 1) % kPool;
+  return e;
 }
 
 void LoopbackHub::post(int src, int dst, Msg m) {
@@ -56,21 +75,9 @@ LoopbackEndpoint::LoopbackEndpoint(std::shared_ptr<LoopbackHub> hub, int rank)
   RMA_CHECK_ARG(rank >= 0 && rank < hub_->size(), "rank " << rank);
 }
 
-LoopbackEndpoint::~LoopbackEndpoint() {
-  for (void* e : pool_) (void)hipEventDestroy(E(e));
-}
-
-void* LoopbackEndpoint::event() {
-  if (pool_.size() < kPool) {
-    hipEvent_t e;
-    RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    pool_.push_back(e);
-    return e;
-  }
-  void* e = pool_[next_];
-  next_ = (next_ + 1) % kPool;
-  return e;
-}
+// The events this endpoint recorded stay alive in the hub (see loopback.h):
+// a peer may still wait on the last "consumed" event after we are gone.
+LoopbackEndpoint::~LoopbackEndpoint() = default;
 
 void LoopbackEndpoint::group_start() {
   if (depth_++ == 0) {
@@ -96,7 +103,7 @@ void LoopbackEndpoint::group_end() {
   std::vector<LoopbackHub::Msg> posted;
   // 1. post every send (ready event behind the producer work on its stream)
   for (const auto& s : sends_) {
-    void* ev = event();
+    void* ev = hub_->event(rank_);
     RMA_HIP_CHECK(hipEventRecord(E(ev), as_stream(s.stream)));
     LoopbackHub::Msg m{s.buf, s.bytes, ev, std::make_shared<void*>(nullptr),
                        std::make_shared<bool>(false)};
@@ -111,7 +118,7 @@ void LoopbackEndpoint::group_end() {
     hipStream_t s = as_stream(r.stream);
     RMA_HIP_CHECK(hipStreamWaitEvent(s, E(m.ready), 0));
     RMA_HIP_CHECK(hipMemcpyAsync(r.buf, m.ptr, r.bytes, hipMemcpyDefault, s));
-    void* done = event();
+    void* done = hub_->event(rank_);
     RMA_HIP_CHECK(hipEventRecord(E(done), s));
     {
       std::lock_guard<std::mutex> lk(hub_->mu_ref());

@@ -501,6 +501,20 @@ class LoopbackComm(Communicator):
                     v.record_stream(torch.cuda.current_stream(v.device))
                 o.tensor.copy_(v)
 
+    def finalize(self) -> None:
+        """Teardown barrier (the reference brackets its device exchange with
+        ``MPI.Barrier``, ``scripts/rocmaware_test_selectdevice.jl:20,24``):
+        every rank's queued work has drained before ANY rank releases its halo
+        buffers, streams and native endpoint, which peers' copies and event
+        waits may still reference. A broken barrier (a peer already failed)
+        does not mask that peer's error."""
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+        try:
+            self.hub._barrier.wait(self.hub.timeout_s)
+        except threading.BrokenBarrierError:
+            pass
+
 
 # ---------------------------------------------------------------------------
 # bootstrap helpers

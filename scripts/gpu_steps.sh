@@ -29,8 +29,8 @@ prof() {  # name timeout rocprofv3-args... -- cmd...
 for s in "$@"; do
   case $s in
     OUT=*) ;;
-    tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 \
-             --timeout-method thread -p no:cacheprovider || exit 1 ;;
+    # the driver's exact GPU-suite command (pytest.ini: timeout 900, signal method)
+    tests) step tests 1000 python3 -m pytest tests/ -x -q -m gpu -p no:cacheprovider || exit 1 ;;
     tests_new) step tests_new 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
              tests/test_bench_gpu.py tests/test_drift_gpu.py \
              "tests/test_multirank_gpu.py::test_aligned_frames_on_partial_sides_bitwise" \

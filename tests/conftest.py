@@ -1,3 +1,4 @@
+import faulthandler
 import os
 import sys
 
@@ -8,8 +9,31 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
+# Crash evidence that survives a truncated stdout tail (the
+# faulting thread's frames of the round-4 SIGSEGV fell into the bytes the
+# driver cut): every thread's stack on a fatal signal, plus breadcrumbs of the
+# multi-rank case that was running (tests/helpers.py), in a small log under
+# the run's output directory.
+LOG_DIR = os.environ.get("RMA_TEST_LOG_DIR", os.path.join(ROOT, "gpurun_out", "pytest_faults"))
+_fault_file = None
+
+
+def breadcrumb(msg: str) -> None:
+    """Append one line to the crash log (flushed: it must be on disk before a
+    native crash can take the process down)."""
+    if _fault_file is not None:
+        _fault_file.write(msg.rstrip() + "\n")
+        _fault_file.flush()
+
 
 def pytest_configure(config):
+    global _fault_file
+    try:
+        os.makedirs(LOG_DIR, exist_ok=True)
+        _fault_file = open(os.path.join(LOG_DIR, f"faults_{os.getpid()}.log"), "a", buffering=1)
+        faulthandler.enable(file=_fault_file, all_threads=True)
+    except OSError:
+        _fault_file = None
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")
     # build the native core once per session (incremental; a no-op when fresh)
@@ -30,10 +54,11 @@ def pytest_collection_modifyitems(config, items):
 
 
 @pytest.fixture(autouse=True)
-def _fresh_grid():
+def _fresh_grid(request):
     """Every test starts and ends without a global grid."""
     from rocm_mpi_amd.parallel import implicit_grid as gg
 
+    breadcrumb(f"test {request.node.nodeid}")
     yield
     if gg.grid_is_initialized():
         try:

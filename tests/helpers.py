@@ -20,6 +20,14 @@ def run_loopback(n, fn, *args, timeout=120, **kw):
     """Run fn(rank, hub, *args) on n threads sharing one LoopbackHub."""
     from rocm_mpi_amd.parallel.comm import LoopbackHub
 
+    try:
+        from conftest import breadcrumb
+    except ImportError:  # helpers used outside pytest
+        def breadcrumb(msg):
+            pass
+    # logged before any rank thread starts: a native crash inside the threads
+    # still names the case (seed-derived arguments included)
+    breadcrumb(f"run_loopback n={n} fn={getattr(fn, '__name__', fn)} args={args!r} kw={kw!r}")
     hub = LoopbackHub(n, timeout_s=timeout)
     out = [None] * n
     err = []

@@ -1,0 +1,86 @@
+"""The threaded native path under host sanitizers (VERDICT r4
+next-step 2).
+
+tests/native/threaded_selftest.cpp drives the real loopback transport
+(csrc/runtime/loopback.cpp) and halo engine (csrc/runtime/halo.cpp) from
+2..8 rank threads against a host stand-in of the HIP runtime
+(tests/native/hip_stub): post / take / consume, plan-cache misses with pack
+buffer reallocation (per-dimension, cross and merged groups), and endpoint
+teardown while peers finish. Built with clang's ThreadSanitizer (its runtime
+intercepts pthread_cond_clockwait, which g++ 11's libtsan does not) and with
+AddressSanitizer + UBSan.
+
+The regression half rebuilds the same driver against the loopback transport
+as it was before the fix (commit 5704426, round 4: events owned by the
+endpoint) and requires both sanitizers to report the heap-use-after-free of
+the receiver's "consumed" event -- the round-4 GPU-suite SIGSEGV.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+PRE_FIX = "5704426"
+SRCS = ["tests/native/threaded_selftest.cpp", "csrc/runtime/loopback.cpp", "csrc/runtime/halo.cpp",
+        "csrc/runtime/halo_plan.cpp", "csrc/runtime/topology.cpp", "csrc/runtime/errors.cpp",
+        "csrc/kernels/cpu_kernels.cpp"]
+SAN = {"tsan": ["-fsanitize=thread"],
+       "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]}
+ENV = {"tsan": {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"},
+       "asan": {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:verify_asan_link_order=0"}}
+
+needs_clang = pytest.mark.skipif(not os.path.exists(CLANG), reason="needs ROCm's clang++")
+
+
+def _build(kind, out, srcs, extra_inc=()):
+    cmd = [CLANG, "-std=c++17", "-O1", "-g", "-ffp-contract=off", "-fno-omit-frame-pointer",
+           *SAN[kind], "-I", os.path.join(ROOT, "tests", "native", "hip_stub"),
+           *[a for d in extra_inc for a in ("-I", d)], "-I", os.path.join(ROOT, "csrc", "include"),
+           *srcs, "-o", str(out), "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+
+
+def _run(kind, exe):
+    return subprocess.run([str(exe)], capture_output=True, text=True, timeout=300,
+                          env=dict(os.environ, **ENV[kind]))
+
+
+@needs_clang
+@pytest.mark.parametrize("kind", ["tsan", "asan"])
+def test_threaded_loopback_and_halo_clean(kind, tmp_path):
+    exe = tmp_path / f"threaded_{kind}"
+    _build(kind, exe, [os.path.join(ROOT, s) for s in SRCS])
+    r = _run(kind, exe)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-6000:]
+    assert "threaded selftest OK" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr
+
+
+@needs_clang
+@pytest.mark.skipif(shutil.which("git") is None, reason="needs git")
+@pytest.mark.parametrize("kind", ["tsan", "asan"])
+def test_pre_fix_loopback_teardown_race_is_reported(kind, tmp_path):
+    """The same driver against the round-4 loopback.{h,cpp} must fail with the
+    use-after-free of the event a destroyed endpoint recorded."""
+    inc = tmp_path / "old" / "include"
+    (inc / "rma").mkdir(parents=True)
+    old_cpp = tmp_path / "old" / "loopback.cpp"
+    for rev_path, dst in (("csrc/include/rma/loopback.h", inc / "rma" / "loopback.h"),
+                          ("csrc/runtime/loopback.cpp", old_cpp)):
+        r = subprocess.run(["git", "show", f"{PRE_FIX}:{rev_path}"], capture_output=True,
+                           text=True, cwd=ROOT)
+        if r.returncode != 0:
+            pytest.skip(f"git history without {PRE_FIX}")
+        dst.write_text(r.stdout)
+    srcs = [os.path.join(ROOT, s) if s != "csrc/runtime/loopback.cpp" else str(old_cpp)
+            for s in SRCS]
+    exe = tmp_path / f"threaded_{kind}_prefix"
+    _build(kind, exe, srcs, extra_inc=[str(inc)])
+    r = _run(kind, exe)
+    assert r.returncode != 0
+    assert "heap-use-after-free" in r.stderr, r.stderr[-3000:]
+    assert "hipStreamWaitEvent" in r.stderr and "LoopbackEndpoint::~LoopbackEndpoint" in r.stderr
