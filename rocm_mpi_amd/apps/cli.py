@@ -5,6 +5,15 @@ The reference hard-codes its parameters per script (e.g.
 (un)commenting ``scripts/runme.sh:5-9``. Every entry point here keeps the
 reference's defaults and exposes them as flags, plus the BASELINE.json
 configurations as named presets (``--preset``).
+
+The reference's global problem is kept by default: one step per kernel pass,
+the canonical flux-form arithmetic, IGG's overlap 2, so ``--dims 2,1 --nx
+12288`` solves ``nx_g = 2*(12288-2)+2 = 24574`` (``diffusion_2D_perf.jl:22,
+26,28``). The measured bench path (up to 24 steps per pass, fast-math,
+``bench.py``) is opt-in: ``--bench-plan``, an explicit ``--temporal K``, or a
+BASELINE preset. K-step passes need width-K halos, i.e. grid overlap 2K, which
+changes ``nx_g``, ``dx`` and ``dt`` on a multi-rank grid: the run then prints
+both grids (``[grid]`` line) and records them (result ``extra``, checkpoint).
 """
 from __future__ import annotations
 
@@ -24,36 +33,72 @@ DEFAULTS = {
                            do_vis=False, profile=True, threads=(32, 4)),
 }
 
-# What bench.py runs (its --temporal default, fast-math on): the perf /
-# perf_hide entry points default to the same planner and kernels on tiles big
-# enough to fill the GPU with K-step tasks (below ~1.5M cells one step per
-# pass is faster, see Diffusion2D's warning), so the reference-named scripts
-# run the measured path.
+# What bench.py runs (its --temporal default, fast-math on). With
+# --bench-plan (or a BASELINE preset) the perf / perf_hide entry points run
+# the same planner and kernels on tiles big enough to fill the GPU with K-step
+# tasks (below ~1.5M cells one step per pass is faster, see Diffusion2D's
+# warning). Without it they keep the reference's one-step canonical update
+# and its overlap-2 global grid.
 BENCH_TEMPORAL = 24
 AUTO_TEMPORAL_MIN_CELLS = 1_500_000
 
 
-def auto_temporal(variant: str, nx: int, ny: int, temporal=None, fast_math=None) -> tuple:
-    """(temporal, fast_math) of a run: explicit values win; otherwise the
+def auto_temporal(variant: str, nx: int, ny: int, temporal=None, fast_math=None,
+                  bench_plan: bool = False) -> tuple:
+    """(temporal, fast_math) of a run: explicit values win; otherwise one
+    canonical step per pass (the reference), or with ``bench_plan`` the
     bench.py defaults for perf / perf_hide on tiles of >= 1.5M cells."""
     base = "perf_hide" if variant == "perf_hide_prof" else variant
     if base not in ("perf", "perf_hide"):
         return 1, False
     if temporal is None:
-        temporal = BENCH_TEMPORAL if nx * ny >= AUTO_TEMPORAL_MIN_CELLS else 1
+        temporal = (BENCH_TEMPORAL if bench_plan and nx * ny >= AUTO_TEMPORAL_MIN_CELLS
+                    else 1)
     if fast_math is None:
         fast_math = temporal > 1
     return int(temporal), bool(fast_math)
 
 
-# BASELINE.json "configs", in order.
+# BASELINE.json "configs", in order (the perf ones as bench.py measures them).
 PRESETS = {
     "ap256_cpu": dict(variant="ap", nx=256, ny=256, nt=1000, device="cpu"),
     "kp16k": dict(variant="kp", nx=16384, ny=16384, nt=1000),
-    "perf_2x1": dict(variant="perf", nx=16384, ny=16384, nt=1000, dims=(2, 1, 0)),
-    "hide_2x2": dict(variant="perf_hide", nx=16384, ny=16384, nt=1000, dims=(2, 2, 0)),
-    "hide_4x2_288GB": dict(variant="perf_hide", auto_size=True, nt=1000, dims=(4, 2, 0)),
+    "perf_2x1": dict(variant="perf", nx=16384, ny=16384, nt=1000, dims=(2, 1, 0),
+                     bench_plan=True),
+    "hide_2x2": dict(variant="perf_hide", nx=16384, ny=16384, nt=1000, dims=(2, 2, 0),
+                     bench_plan=True),
+    "hide_4x2_288GB": dict(variant="perf_hide", auto_size=True, nt=1000, dims=(4, 2, 0),
+                           bench_plan=True),
 }
+
+
+def global_sizes(nx: int, ny: int, dims, periods, nprocs: int, temporal: int) -> tuple:
+    """((nx_g, ny_g) of the run, (nx_g, ny_g) with IGG's overlap 2): K-step
+    passes (temporal K > 1) need overlap 2K (models/diffusion.py)."""
+    from ..parallel import geometry as geo
+    from ..parallel.topology import dims_create
+
+    d = dims_create(nprocs, [int(dims[0]), int(dims[1]), 1])
+    ol = 2 * temporal if temporal > 1 else 2
+    run = tuple(geo.n_global(n, d[i], ol, int(periods[i])) for i, n in enumerate((nx, ny)))
+    ref = tuple(geo.n_global(n, d[i], 2, int(periods[i])) for i, n in enumerate((nx, ny)))
+    return run, ref
+
+
+def grid_line(model) -> str | None:
+    """The loud note when the solved global grid is not the reference's
+    (overlap 2K of K-step passes on a multi-rank grid); None when equal."""
+    g, cfg = model.g, model.cfg
+    run = tuple(g.nxyz_g[:2])
+    _, ref = global_sizes(cfg.nx, cfg.ny, g.dims, g.periods, g.nprocs, 1)
+    if run == ref:
+        return None
+    dx_ref, dy_ref = cfg.lx / ref[0], cfg.ly / ref[1]
+    dt_ref = min(dx_ref * dx_ref, dy_ref * dy_ref) * cfg.Cp0 / cfg.lam / 4.1
+    return (f"[grid] global grid {run[0]}x{run[1]} (overlap {g.overlaps[0]} for "
+            f"{cfg.temporal}-step passes), dx = {model.dx:.6e}, dt = {model.dt:.6e}; the "
+            f"reference's overlap 2 gives {ref[0]}x{ref[1]}, dx = {dx_ref:.6e}, dt = "
+            f"{dt_ref:.6e} (run with --temporal 1 to solve the reference's problem)")
 
 
 def _pair(s: str) -> tuple:
@@ -103,10 +148,16 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--temporal", type=int, default=None, choices=list(range(1, 25)),
                     metavar="K",
                     help="perf/perf_hide: at most K (1..24) steps per kernel pass + width-K "
-                         "halos (grid overlap 2K); the executor plans the passes; bitwise "
-                         "identical to one-step updates without --fast-math. Default: "
-                         f"{BENCH_TEMPORAL} (what bench.py measures) on tiles of >= "
-                         f"{AUTO_TEMPORAL_MIN_CELLS:,} cells, else 1")
+                         "halos (grid overlap 2K: a multi-rank nx_g differs from the "
+                         "reference's); the executor plans the passes; bitwise identical to "
+                         "one-step updates without --fast-math. Default: 1 (the reference), "
+                         f"{BENCH_TEMPORAL} with --bench-plan on tiles of >= "
+                         f"{AUTO_TEMPORAL_MIN_CELLS:,} cells")
+    ap.add_argument("--bench-plan", dest="bench_plan", action="store_true", default=False,
+                    help=f"perf/perf_hide: run what bench.py measures (up to {BENCH_TEMPORAL} "
+                         "steps per pass, fast-math) on tiles of >= "
+                         f"{AUTO_TEMPORAL_MIN_CELLS:,} cells; on a multi-rank grid the overlap "
+                         "becomes 2K, which changes nx_g / dx / dt (printed)")
     ap.add_argument("--chunk2", type=int, default=0)
     ap.add_argument("--unroll2", type=int, default=2, choices=[2, 4])
     ap.add_argument("--fast-math", dest="fast_math", action="store_true", default=None,
@@ -179,7 +230,7 @@ def resolve(variant: str, argv=None):
             n = int(t.item())
         opts["nx"] = opts["ny"] = n
     opts["temporal"], opts["fast_math"] = auto_temporal(base, opts["nx"], opts["ny"], a.temporal,
-                                                        a.fast_math)
+                                                        a.fast_math, a.bench_plan)
     return DiffusionConfig(**opts), a
 
 
@@ -223,14 +274,26 @@ def run_variant(variant: str, argv=None) -> int:
         model.synchronize()
     if a.resume:
         ckpt.load_checkpoint(model, a.resume)
+    gline = grid_line(model)
+    if gline and model.g.me == 0:
+        import warnings
+
+        warnings.warn(gline, RuntimeWarning, stacklevel=2)
+        if not cfg.quiet:
+            print(gline, flush=True)
     res = model.run()
     if model.g.me == 0 and not cfg.quiet and cfg.variant in ("perf", "perf_hide"):
         print(plan_line(model, res.timed_steps), flush=True)
+        if gline:
+            print(gline, flush=True)
     if a.checkpoint:
         ckpt.save_checkpoint(model, a.checkpoint)
     res.extra["threads_requested"] = list(a.threads)
     res.extra["temporal"] = cfg.temporal
     res.extra["fast_math"] = bool(cfg.fast_math)
+    res.extra["overlaps"] = list(model.g.overlaps[:2])
+    res.extra["nxyz_g_reference"] = list(global_sizes(cfg.nx, cfg.ny, model.g.dims,
+                                                      model.g.periods, model.g.nprocs, 1)[1])
     if a.json and model.g.me == 0:
         print(res.to_json(), flush=True)
     model.close()

@@ -20,7 +20,8 @@ def _meta(model) -> dict:
     c = model.cfg
     return {"format": "rocm_mpi_amd.checkpoint/1", "variant": c.variant, "nx": c.nx, "ny": c.ny,
             "dims": list(g.dims), "periods": list(g.periods), "nprocs": g.nprocs,
-            "nxyz_g": list(g.nxyz_g), "steps_done": model.steps_done, "dt": model.dt,
+            "nxyz_g": list(g.nxyz_g), "overlaps": list(g.overlaps), "temporal": c.temporal,
+            "fast_math": bool(c.fast_math), "steps_done": model.steps_done, "dt": model.dt,
             "dx": model.dx, "dy": model.dy, "lam": c.lam, "Cp0": c.Cp0}
 
 
@@ -42,7 +43,11 @@ def load_checkpoint(model, path: str) -> dict:
     mine = _meta(model)
     for k in ("nx", "ny", "dims", "periods", "nprocs", "nxyz_g"):
         if meta[k] != mine[k]:
-            raise ValueError(f"checkpoint {k}={meta[k]} does not match this run ({mine[k]})")
+            hint = ""
+            if k == "nxyz_g" and meta.get("overlaps") and meta["overlaps"] != mine["overlaps"]:
+                hint = (f": written with grid overlaps {meta['overlaps']} (temporal "
+                        f"{meta.get('temporal')}), this run has {mine['overlaps']} (--temporal)")
+            raise ValueError(f"checkpoint {k}={meta[k]} does not match this run ({mine[k]}){hint}")
     for k in ("dt", "dx", "dy", "lam", "Cp0"):
         if meta[k] != mine[k]:
             raise ValueError(f"checkpoint physics {k}={meta[k]} differs from this run ({mine[k]})")

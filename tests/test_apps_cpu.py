@@ -172,11 +172,12 @@ def test_runme_and_startup_scripts(tmp_path):
 
 
 def test_preset_runs_the_bench_plan_and_kernel():
-    """the reference-named perf / perf_hide entry points
-    default to what bench.py measures (K <= 24 steps per pass, fast-math)
-    on GPU-sized tiles: `--preset hide_2x2` and `bench.py --dims 2,2` resolve
-    the same configuration, hence the same pass plan and kernel; small tiles
-    keep one step per pass and --canonical opts out of fast-math."""
+    """The BASELINE presets and --bench-plan run what bench.py measures (K <= 24
+    steps per pass, fast-math) on GPU-sized tiles: `--preset hide_2x2` and
+    `bench.py --dims 2,2` resolve the same configuration, hence the same pass
+    plan and kernel; small tiles keep one step per pass and --canonical opts
+    out of fast-math. Without them the reference-named entry points keep the
+    reference's one-step canonical update."""
     import bench
     from rocm_mpi_amd import ops
     from rocm_mpi_amd._native import native
@@ -197,10 +198,12 @@ def test_preset_runs_the_bench_plan_and_kernel():
         coef = ops.StencilCoef.from_physics(1.0, 10 / 32674, 10 / 32674, (10 / 32674) ** 2 / 4.1)
         assert (N.fast_kernel_k(max(plans[0]), cfg.ny, tuple(coef))
                 == N.fast_kernel_k(max(plans[1]), bcfg.ny, tuple(coef)))
-    # the reference's own perf default (12288^2) runs the bench path too
+    # the reference's own perf default (12288^2): its one-step canonical update
     cfg, _ = cli.resolve("perf", [])
+    assert (cfg.nx, cfg.temporal, cfg.fast_math) == (12288, 1, False)
+    cfg, _ = cli.resolve("perf", ["--bench-plan"])
     assert (cfg.nx, cfg.temporal, cfg.fast_math) == (12288, 24, True)
-    cfg, _ = cli.resolve("perf", ["--canonical"])
+    cfg, _ = cli.resolve("perf", ["--bench-plan", "--canonical"])
     assert (cfg.temporal, cfg.fast_math) == (24, False)
     cfg, _ = cli.resolve("perf", ["--temporal", "1"])
     assert (cfg.temporal, cfg.fast_math) == (1, False)
@@ -216,8 +219,53 @@ def test_perf_entry_point_prints_its_plan(capsys):
     from rocm_mpi_amd.apps import cli
 
     assert cli.run_variant("perf_hide", ["--nx", "1300", "--ny", "1200", "--nt", "60",
-                                         "--device", "cpu", "--no-vis", "--init", "random"]) == 0
+                                         "--device", "cpu", "--no-vis", "--init", "random",
+                                         "--bench-plan"]) == 0
     out = capsys.readouterr().out
     assert "Executed 60 steps in = " in out
     line = [l for l in out.splitlines() if l.startswith("[plan]")][-1]
     assert "50 timed steps" in line and "fast-math" in line and "24" in line
+
+
+def test_perf_entry_point_keeps_the_reference_global_grid():
+    """`diffusion_2D_perf --dims 2,1 --nx 12288` solves IGG's
+    overlap-2 grid, nx_g = 2*(12288-2)+2 = 24574 (diffusion_2D_perf.jl:22,26,28),
+    by default and with --temporal 1; the bench plan (overlap 2K = 48) differs
+    and says so."""
+    from rocm_mpi_amd.apps import cli
+
+    for argv in (["--dims", "2,1"], ["--dims", "2,1", "--temporal", "1"]):
+        cfg, _ = cli.resolve("perf", argv)
+        assert (cfg.temporal, cfg.fast_math) == (1, False)
+        run, ref = cli.global_sizes(cfg.nx, cfg.ny, cfg.dims, cfg.periods, 2, cfg.temporal)
+        assert run == ref == (24574, 12288)
+    cfg, _ = cli.resolve("perf", ["--dims", "2,1", "--bench-plan"])
+    run, ref = cli.global_sizes(cfg.nx, cfg.ny, cfg.dims, cfg.periods, 2, cfg.temporal)
+    assert cfg.temporal == 24 and run == (2 * (12288 - 48) + 48, 12288) and ref[0] == 24574
+
+
+def test_bench_plan_on_multi_rank_grid_prints_the_changed_grid(capsys):
+    """A K-step run on 2 ranks (loopback threads, CPU) prints both global grids
+    and records the overlaps; the one-step default prints nothing of the kind."""
+    from helpers import run_loopback
+    from rocm_mpi_amd.apps import cli
+    from rocm_mpi_amd.models import Diffusion2D
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    def rank(r, hub, argv):
+        cfg, _ = cli.resolve("perf", argv)
+        K = cfg.temporal
+        gg.init_global_grid(cfg.nx, cfg.ny, 1, dimx=2, dimy=1, quiet=True, loopback=(hub, r),
+                            device="cpu", overlaps=(2 * K if K > 1 else 2,) * 2 + (2,),
+                            halowidths=(max(1, K),) * 2 + (1,))
+        m = Diffusion2D(cfg)
+        line = cli.grid_line(m)
+        m.close()
+        gg.finalize_global_grid()
+        return line
+
+    base = ["--nx", "40", "--ny", "30", "--dims", "2,1", "--device", "cpu"]
+    assert run_loopback(2, rank, base) == [None, None]
+    lines = run_loopback(2, rank, base + ["--temporal", "4", "--canonical"])
+    assert lines[0] and "global grid 72x30 (overlap 8 for 4-step passes)" in lines[0]
+    assert "overlap 2 gives 78x30" in lines[0]
