@@ -586,9 +586,12 @@ def window_check(snap: dict, world: int, timeout_s: float, budget: float = WINDO
     return info
 
 
-# weak-scaling attribution: the N = 1 record of this tile
-# class is cached here, so the N > 1 runs of the same driver sweep can split
-# E(N) = e_gpu * e_coef * e_halo
+# weak-scaling attribution. Self-contained in
+# one job: E_in_run = t_fast_iso / t_it = e_gpu * e_coef * e_halo, with
+# t_fast_iso the fastest rank's own isotropic solo time (no exchange). The
+# N = 1 record of the same tile class (cached by the same driver sweep on the
+# same node and build) adds e_box = t(N=1) / t_fast_iso, so that
+# E(N) = t(N=1) / t_it = e_box * E_in_run.
 def _n1_cache_path() -> str:
     import tempfile
 
@@ -596,15 +599,31 @@ def _n1_cache_path() -> str:
                           os.path.join(tempfile.gettempdir(), "rma_bench_n1_record.json"))
 
 
+def _build_id() -> str:
+    """Hash of the native sources, flags and arch (rocm_mpi_amd/_build.py)."""
+    try:
+        from rocm_mpi_amd import _build
+
+        return _build.source_stamp()[:12]
+    except Exception:  # noqa: BLE001 - informational
+        return "unknown"
+
+
 def _n1_key(nx: int, ny: int, steps: int, warmup: int, K: int, fast: bool, variant: str) -> str:
-    return f"{variant}:{nx}x{ny}:s{steps}:w{warmup}:K{K}:f{int(fast)}"
+    """Tile class + build + node: a record from another build or another box
+    (another sweep) never matches."""
+    import socket
+
+    return (f"{variant}:{nx}x{ny}:s{steps}:w{warmup}:K{K}:f{int(fast)}:b{_build_id()}:"
+            f"h{socket.gethostname()}")
 
 
 def save_n1(key: str, ms_per_step: float, bus: str) -> None:
     try:
         tmp = _n1_cache_path() + f".{os.getpid()}.tmp"
         with open(tmp, "w") as f:
-            json.dump({"key": key, "ms_per_step": ms_per_step, "pci_bus_id": bus}, f)
+            json.dump({"key": key, "ms_per_step": ms_per_step, "pci_bus_id": bus,
+                       "time": time.time()}, f)
         os.replace(tmp, _n1_cache_path())
     except OSError:
         pass
@@ -620,25 +639,35 @@ def load_n1(key: str):
 
 
 def attribution(t_it: float, solo: float | None, solo_iso: float | None,
-                n1_ms: float | None) -> dict:
-    """Job-level split of the weak-scaling efficiency (max-over-ranks times):
-    e_halo = solo / t_it (exchange + frame cost, same coefficients),
-    e_coef = solo_iso / solo (the fast-math pass energy at this grid's
-    dx != dy, against dx = dy), e_gpu = t(N=1) / solo_iso (the slowest GPU of
-    this job, isotropic and without exchange, against the N = 1 record of
-    the same tile class; null without that record). Their product is
-    t(N=1)/t_it = E(N); e_halo * e_coef = weak_scaling_eff_same_run_iso."""
+                fast_iso: float | None, n1_ms: float | None) -> dict:
+    """Job-level split of the weak-scaling efficiency (times in s, max over
+    ranks unless named otherwise):
+      e_halo = solo / t_it        exchange + frame cost, same coefficients
+      e_coef = solo_iso / solo    fast-math pass energy at this grid's dx != dy
+                                  against dx = dy
+      e_gpu  = fast_iso / solo_iso  the slowest GPU against the fastest GPU of
+                                  THIS job (isotropic, no exchange): in-run
+      e_product = e_halo * e_coef * e_gpu = fast_iso / t_it  (in-run E(N))
+      e_box  = t(N=1) / fast_iso  this job's fastest GPU against the N = 1
+                                  record of the same sweep (null without it)
+      e_product_vs_n1 = e_box * e_product = t(N=1) / t_it = E(N)."""
     out = {"e_halo": None, "e_coef": None, "e_gpu": None, "e_product": None,
-           "weak_scaling_eff_same_run_iso": None, "n1_ms_per_step": n1_ms}
+           "e_box": None, "e_product_vs_n1": None,
+           "weak_scaling_eff_same_run_iso": None, "fastest_solo_iso_ms_per_step":
+               fast_iso * 1e3 if fast_iso else None, "n1_ms_per_step": n1_ms}
     if solo:
         out["e_halo"] = solo / t_it
     if solo and solo_iso:
         out["e_coef"] = solo_iso / solo
         out["weak_scaling_eff_same_run_iso"] = solo_iso / t_it
-    if solo_iso and n1_ms:
-        out["e_gpu"] = (n1_ms / 1e3) / solo_iso
+    if solo_iso and fast_iso:
+        out["e_gpu"] = fast_iso / solo_iso
     if all(out[k] is not None for k in ("e_halo", "e_coef", "e_gpu")):
         out["e_product"] = out["e_halo"] * out["e_coef"] * out["e_gpu"]
+    if fast_iso and n1_ms:
+        out["e_box"] = (n1_ms / 1e3) / fast_iso
+        if out["e_product"] is not None:
+            out["e_product_vs_n1"] = out["e_box"] * out["e_product"]
     return {k: (round(v, 6) if isinstance(v, float) else v) for k, v in out.items()}
 
 
@@ -651,14 +680,16 @@ def preflight(dims, K: int, dev: str, world: int, rank: int, gpu: bool, n: int,
     t0 = time.perf_counter()
     err = ""
     transport = "rccl" if gpu and world == 1 else "auto"
+    ring: dict = {}
     try:
-        vals = smoke.run(4, transport=transport, verbose=False, self_ring=world == 1)
+        vals = smoke.run(4, transport=transport, verbose=False, self_ring=world == 1, info=ring)
         if any(v != float((rank - 1) % world) for v in vals):
             err = f"ring received {vals}, expected {(rank - 1) % world}"
     except Exception as e:  # noqa: BLE001
         err = f"ring send/recv: {type(e).__name__}: {e}"
     agree(not err, err, world, timeout_s, "preflight ring")
-    info = {"ring_ok": True, "ring_ranks": world}
+    info = {"ring_ok": True, "ring_ranks": world, "ring_transport": ring.get("transport"),
+            "rccl_nranks": ring.get("rccl_nranks")}
     info["halo"] = halo_check(n, dims, K, dev, world, rank, timeout_s,
                               self_rccl=gpu and world == 1, inject=False)
     info["seconds"] = round(time.perf_counter() - t0, 3)
@@ -673,6 +704,19 @@ def _rccl_info() -> dict | None:
         return {"library": native().rccl_library(), "version": native().rccl_version()}
     except Exception:  # noqa: BLE001 - informational
         return None
+
+
+def _rccl_nranks(g, pre: dict | None):
+    """ncclCommCount of the halo communicator (or of the preflight ring's RCCL
+    communicator on the single-GPU RCCL-self path); None without RCCL."""
+    try:
+        from rocm_mpi_amd.parallel.comm import RcclComm
+
+        if isinstance(g.comm, RcclComm) and g.comm.native is not None:
+            return int(g.comm.native.count())
+    except Exception:  # noqa: BLE001 - informational
+        return None
+    return (pre or {}).get("rccl_nranks")
 
 
 def make_config(a, nx: int, ny: int, dev: str, dims: tuple):
@@ -941,7 +985,7 @@ def run(a, world: int, rank: int) -> int:
                   "e_halo": round(solo_own / (own_s / a.steps), 6) if solo_own else None,
                   "e_coef": (round(solo_iso_own / solo_own, 6)
                              if solo_own and solo_iso_own else None),
-                  "e_gpu": None,
+                  "e_gpu": None, "e_gpu_vs_n1": None,
                   "pass_timing": {k: (round(v, 4) if isinstance(v, float) else v)
                                   for k, v in timings.items() if k != "note"}}
         ranks_detail = gather_obj(detail, world)
@@ -1010,11 +1054,15 @@ def run(a, world: int, rank: int) -> int:
         elif world > 1:
             n1 = load_n1(n1key)
         n1_ms = n1["ms_per_step"] if n1 else None
-        if n1_ms:
-            for d in ranks_detail:
-                if d["solo_iso_ms_per_step"]:
-                    d["e_gpu"] = round(n1_ms / d["solo_iso_ms_per_step"], 6)
-        attrib = attribution(t_it, solo, solo_iso, n1_ms)
+        isos = [d["solo_iso_ms_per_step"] for d in ranks_detail if d["solo_iso_ms_per_step"]]
+        fast_iso_ms = min(isos) if len(isos) == world else None
+        for d in ranks_detail:
+            if d["solo_iso_ms_per_step"] and fast_iso_ms:
+                d["e_gpu"] = round(fast_iso_ms / d["solo_iso_ms_per_step"], 6)
+            if d["solo_iso_ms_per_step"] and n1_ms:
+                d["e_gpu_vs_n1"] = round(n1_ms / d["solo_iso_ms_per_step"], 6)
+        attrib = attribution(t_it, solo, solo_iso,
+                             fast_iso_ms / 1e3 if fast_iso_ms else None, n1_ms)
         out.update({"value": round(total, 2), "value_kind": "aggregate",
                     "teff_per_gpu": round(teff_gpu, 2), "ms_per_step": round(t_it * 1e3, 6)})
         out["config"].update({
@@ -1039,11 +1087,13 @@ def run(a, world: int, rank: int) -> int:
             "solo_iso_ms_per_step": round(solo_iso * 1e3, 6) if solo_iso else None,
             "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,
             "e_attribution": dict(attrib, note=(
-                "E(N) = t(N=1)/t_it = e_gpu * e_coef * e_halo; e_halo = solo/t_it (exchange "
-                "and frame cost), e_coef = solo_iso/solo (fast-math pass energy at dx != dy vs "
-                "dx = dy), e_gpu = t(N=1)/solo_iso (slowest GPU, isotropic, no exchange, vs the "
-                "N = 1 record of this tile class cached by the same driver sweep); value is "
-                "the aggregate N x teff_per_gpu")),
+                "in-run E = fastest_solo_iso/t_it = e_gpu * e_coef * e_halo (e_product); "
+                "e_halo = solo/t_it (exchange and frame cost), e_coef = solo_iso/solo "
+                "(fast-math pass energy at dx != dy vs dx = dy), e_gpu = fastest/slowest "
+                "isotropic solo time of this job's GPUs (no exchange); e_box = t(N=1)/"
+                "fastest_solo_iso against the N = 1 record of the same sweep, node and build "
+                "(null without it), e_product_vs_n1 = t(N=1)/t_it; value is the aggregate "
+                "N x teff_per_gpu")),
             "headline_window_check": None,
             "rccl_halo_bitwise_ok": None,
             "halo_check": None,
@@ -1067,6 +1117,7 @@ def run(a, world: int, rank: int) -> int:
             "bitwise_kstep_steps_per_pass": kc if canonical else None,
             "overlap": list(g.overlaps[:2]),
             "transport": g.transport,
+            "rccl_nranks": _rccl_nranks(g, out["config"].get("preflight")),
             "rccl": _rccl_info() if gpu else None,
             "hipgraph": bool(a.graph),
             "setup_s": round(setup_s, 3),

@@ -339,6 +339,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("nonblocking", &RcclComm::nonblocking)
       .def_property_readonly("data_blocking", &RcclComm::data_blocking)
       .def_property_readonly("device", &RcclComm::device)
+      .def("count", &RcclComm::count)
       .def("allreduce",
            [](RcclComm& c, uintptr_t sb, uintptr_t rb, size_t count, DType dt, RedOp op,
               uintptr_t s) { c.allreduce(P<const void>(sb), P<void>(rb), count, dt, op, S(s)); })

@@ -42,6 +42,8 @@ class RcclComm : public P2PTransport {
   int rank() const override { return rank_; }
   int size() const override { return nranks_; }
   int device() const { return device_; }
+  // ranks of the communicator as RCCL itself reports them (ncclCommCount)
+  int count() const;
 
   void group_start() override;
   void group_end() override;

@@ -39,6 +39,7 @@ struct RcclApi {
   decltype(&ncclCommGetAsyncError) CommGetAsyncError = &ncclCommGetAsyncError;
   decltype(&ncclCommDestroy) CommDestroy = &ncclCommDestroy;
   decltype(&ncclCommSplit) CommSplit = &ncclCommSplit;
+  decltype(&ncclCommCount) CommCount = &ncclCommCount;
   decltype(&ncclGroupStart) GroupStart = &ncclGroupStart;
   decltype(&ncclGroupEnd) GroupEnd = &ncclGroupEnd;
   decltype(&ncclSend) Send = &ncclSend;
@@ -70,6 +71,7 @@ RcclApi load_rccl_api() {
   sym(a.CommGetAsyncError, "ncclCommGetAsyncError");
   sym(a.CommDestroy, "ncclCommDestroy");
   sym(a.CommSplit, "ncclCommSplit");
+  sym(a.CommCount, "ncclCommCount");
   sym(a.GroupStart, "ncclGroupStart");
   sym(a.GroupEnd, "ncclGroupEnd");
   sym(a.Send, "ncclSend");
@@ -260,6 +262,13 @@ RcclComm::~RcclComm() {
   if (aborted_) return;  // already torn down by abort()
   if (comm_) (void)rccl().CommDestroy(C(comm_));
   if (parent_) (void)rccl().CommDestroy(C(parent_));
+}
+
+int RcclComm::count() const {
+  RMA_CHECK_ARG(comm_ != nullptr && !aborted_, "communicator is gone");
+  int n = -1;
+  RMA_NCCL_CHECK(rccl().CommCount(C(comm_), &n));
+  return n;
 }
 
 bool RcclComm::capturable() const {

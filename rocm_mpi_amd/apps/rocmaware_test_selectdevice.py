@@ -24,10 +24,12 @@ import torch
 
 
 def run(n: int = 4, transport: str = "auto", verbose: bool = True,
-        self_ring: bool = False) -> list[float]:
+        self_ring: bool = False, info: dict | None = None) -> list[float]:
     """The ring exchange; returns what this rank received. ``self_ring``: with
     one rank, still send/recv through the transport (RCCL send/recv to itself
-    on one GPU: the device-buffer P2P path without a second GPU)."""
+    on one GPU: the device-buffer P2P path without a second GPU). ``info``
+    (optional dict) receives the transport and, for RCCL, the communicator's
+    own rank count (ncclCommCount)."""
     from ..parallel import comm as C
     from ..parallel.implicit_grid import _choose_transport
 
@@ -40,12 +42,16 @@ def run(n: int = 4, transport: str = "auto", verbose: bool = True,
     dst, src = (rank + 1) % size, (rank - 1) % size
     if t == "rccl":
         comm = C.RcclComm(dev)
+        if info is not None:
+            info["rccl_nranks"] = comm.native.count()
     elif t == "ipc":  # device-to-device between processes of one node, no RCCL
         comm = C.IpcComm(dev, [dst, src])
     elif t == "self":
         comm = C.SelfComm()
     else:
         comm = C.TorchDistComm(staged=(t == "staged"))
+    if info is not None:
+        info["transport"] = t
     if verbose:
         name = torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"
         print(f"rank={rank} local_rank={local}/{lsize} (device={dev} {name}), size={size}, "

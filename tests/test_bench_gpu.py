@@ -63,7 +63,12 @@ def test_bench_small_tile_with_self_rccl_halo_check():
     assert d["value_kind"] == "aggregate" and d["teff_per_gpu"] == c["teff_per_gpu_GBps"]
     ea = c["e_attribution"]
     assert ea["e_coef"] == 1.0 and c["solo_iso_ms_per_step"] == c["solo_ms_per_step"]
+    assert ea["e_gpu"] == 1.0  # one GPU: the fastest is the slowest
     assert c["rccl"]["version"] > 0 and c["rccl"]["library"]
+    # the preflight ring went through an RCCL communicator of exactly 1 rank
+    # (ncclCommCount)
+    assert pf["ring_transport"] == "rccl" and pf["rccl_nranks"] == 1 == d["n_gpus"]
+    assert c["rccl_nranks"] == 1
 
 
 def test_bench_default_check_on_one_gpu():

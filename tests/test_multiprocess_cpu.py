@@ -98,11 +98,16 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
            "--nx", str(nx), "--single-step-steps", "4", *extra]
     K = int(extra[1])
     # the N = 1 record of this tile class, as the driver's N = 1 run of the
-    # same sweep leaves it (bench.py save_n1): e_gpu is then defined
+    # same sweep leaves it (bench.py save_n1): e_box is then defined. The
+    # in-run attribution (e_gpu included) must not need it:
+    # the 4-rank case runs without any cache file.
+    import bench
+
     cache = tmp_path / "n1.json"
-    n1_ms = 1.0
-    cache.write_text(json.dumps({"key": f"perf_hide:{nx}x{nx}:s20:w3:K{K}:f1",
-                                 "ms_per_step": n1_ms, "pci_bus_id": "cpu"}))
+    n1_ms = 1.0 if world != 4 else None
+    if n1_ms:
+        cache.write_text(json.dumps({"key": bench._n1_key(nx, nx, 20, 3, K, True, "perf_hide"),
+                                     "ms_per_step": n1_ms, "pci_bus_id": "cpu"}))
     env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_N1_CACHE=str(cache))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
                        env=env)
@@ -165,18 +170,30 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     assert d["value_kind"] == "aggregate"
     assert abs(d["teff_per_gpu"] - c["teff_per_gpu_GBps"]) <= 0.01
     ea = c["e_attribution"]
-    for k in ("e_halo", "e_coef", "e_gpu", "e_product", "weak_scaling_eff_same_run_iso"):
+    for k in ("e_halo", "e_coef", "e_gpu", "e_product", "weak_scaling_eff_same_run_iso",
+              "fastest_solo_iso_ms_per_step"):
         assert ea[k] is not None and ea[k] > 0, k
     assert abs(ea["e_halo"] - c["weak_scaling_eff_same_run"]) <= 1e-4
     assert abs(ea["e_halo"] * ea["e_coef"] - ea["weak_scaling_eff_same_run_iso"]) <= 1e-5
     t_it = d["ms_per_step"]
-    assert abs(ea["e_product"] - n1_ms / t_it) <= 1e-4 * max(1.0, n1_ms / t_it)
-    assert abs(ea["e_gpu"] - n1_ms / c["solo_iso_ms_per_step"]) <= 1e-4 * ea["e_gpu"]
+    fast = ea["fastest_solo_iso_ms_per_step"]
+    assert fast == min(r["solo_iso_ms_per_step"] for r in rd)
+    assert 0 < ea["e_gpu"] <= 1 + 1e-9
+    assert abs(ea["e_gpu"] - fast / c["solo_iso_ms_per_step"]) <= 1e-4 * ea["e_gpu"]
+    assert abs(ea["e_product"] - fast / t_it) <= 1e-4 * max(1.0, fast / t_it)
+    if n1_ms:
+        assert abs(ea["e_box"] - n1_ms / fast) <= 1e-4 * ea["e_box"]
+        assert abs(ea["e_product_vs_n1"] - n1_ms / t_it) <= 1e-4 * max(1.0, n1_ms / t_it)
+    else:
+        assert ea["e_box"] is None and ea["e_product_vs_n1"] is None
     if dims[0] == dims[1]:  # dx == dy: the isotropic re-time IS the solo time
         assert ea["e_coef"] == 1.0 and c["solo_iso_ms_per_step"] == c["solo_ms_per_step"]
     for r in rd:
         assert r["solo_iso_ms_per_step"] > 0 and r["e_halo"] > 0 and r["e_coef"] > 0
-        assert abs(r["e_gpu"] - n1_ms / r["solo_iso_ms_per_step"]) <= 1e-4 * r["e_gpu"]
+        assert abs(r["e_gpu"] - fast / r["solo_iso_ms_per_step"]) <= 1e-4 * r["e_gpu"]
+        if n1_ms:
+            assert abs(r["e_gpu_vs_n1"] - n1_ms / r["solo_iso_ms_per_step"]) <= 1e-4 * r["e_gpu_vs_n1"]
+    assert c["rccl_nranks"] is None and c["preflight"]["ring_transport"] == "gloo"
 
 
 def test_bench_window_check_detects_a_wrong_cell(tmp_path):
@@ -205,7 +222,8 @@ def test_bench_window_check_detects_a_wrong_cell(tmp_path):
     d = json.loads(lines[0])
     wc = d["config"]["headline_window_check"]
     assert wc["bitwise"] is False and "1: window rows" in wc["error"]
-    assert d["config"]["e_attribution"]["e_gpu"] is None  # no N = 1 record cached
+    assert d["config"]["e_attribution"]["e_box"] is None  # no N = 1 record cached
+    assert d["config"]["e_attribution"]["e_gpu"] is not None  # in-run: needs no record
 
 
 def test_bench_halo_check_detects_a_wrong_tile(tmp_path):
