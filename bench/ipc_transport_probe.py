@@ -6,10 +6,14 @@ share a GPU) -- run under the package launcher:
     python -m rocm_mpi_amd.launch -n 4 -- bench/ipc_transport_probe.py \\
         --transport ipc --n 2048 --K 1 --steps 400 --check
 
-Rank 0 prints one JSON line: ms per step (max over ranks), the transport, and
-with --check (canonical arithmetic) whether the gathered field equals the
-NumPy golden model bitwise. perf_hide with K = 1 exchanges every step, the
-hardest ordering test for a transport (tests/golden.py is the oracle).
+Rank 0 prints one JSON line: ms per step (max over ranks), the transport, the
+IPC mode (RMA_IPC_MODE: stream | host) and the host waits inside the
+transport's group_end during the timed steps (stream mode: 0), and with
+--check (canonical arithmetic) whether the gathered field equals the NumPy
+golden model bitwise. perf_hide with K = 1 exchanges every step, the hardest
+ordering test for a transport (tests/golden.py is the oracle). --graph
+replays the steps from a hipGraph captured by the executor (stream mode,
+RMA_IPC_GRAPH=1), checked against the same golden model.
 """
 from __future__ import annotations
 
@@ -33,8 +37,11 @@ def main(argv=None) -> int:
     ap.add_argument("--variant", default="perf_hide")
     ap.add_argument("--dims", default="0,0")
     ap.add_argument("--check", action="store_true", help="canonical arithmetic, golden compare")
+    ap.add_argument("--graph", action="store_true", help="hipGraph replay (stream-mode IPC)")
     a = ap.parse_args(argv)
     os.environ["RMA_TRANSPORT"] = a.transport
+    if a.graph:
+        os.environ["RMA_IPC_GRAPH"] = "1"
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -45,20 +52,26 @@ def main(argv=None) -> int:
     dims = tuple(int(v) for v in a.dims.split(",")) + (0,)
     m = Diffusion2D(DiffusionConfig(variant=a.variant, nx=a.n, ny=a.n, nt=a.steps, dims=dims,
                                     quiet=True, init="gaussian", init_on="host", temporal=a.K,
-                                    fast_math=a.K > 1 and not a.check, device="cuda:0"))
+                                    fast_math=a.K > 1 and not a.check, device="cuda:0",
+                                    use_graph=a.graph))
     g = gg.global_grid()
+    nat = getattr(g.comm, "native", None)
     m.step(2 * a.K)
     m.synchronize()
     dist.barrier()
+    waits0 = nat.host_waits if nat is not None and hasattr(nat, "host_waits") else None
     t0 = time.perf_counter()
     m.step(a.steps)
     m.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
+    waits = (nat.host_waits - waits0) if waits0 is not None else None
     t = torch.tensor([dt], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     out = {"transport": g.transport, "ranks": g.nprocs, "dims": list(g.dims[:2]), "tile": a.n,
            "K": a.K, "steps": a.steps, "variant": a.variant,
-           "ms_per_step_max": float(t.item()) * 1e3}
+           "ms_per_step_max": float(t.item()) * 1e3,
+           "ipc_mode": getattr(nat, "mode", None) if g.transport == "ipc" else None,
+           "host_waits_in_group_end": waits, "graph": bool(m.use_graph)}
     if a.check:
         Tv = m.gather_interior()
         if g.me == 0:

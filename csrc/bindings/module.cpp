@@ -320,13 +320,22 @@ PYBIND11_MODULE(_C, m) {
   py::class_<LoopbackEndpoint, P2PTransport>(m, "LoopbackEndpoint")
       .def(py::init<std::shared_ptr<LoopbackHub>, int>(), py::arg("hub"), py::arg("rank"));
   py::class_<IpcTransport, P2PTransport>(m, "IpcTransport")
-      .def(py::init<int, int, int, const std::vector<int>&, size_t, const std::string&, double>(),
+      .def(py::init<int, int, int, const std::vector<int>&, size_t, const std::string&, double,
+                    int>(),
            py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("peers"),
-           py::arg("mailbox_bytes"), py::arg("token"), py::arg("timeout_s") = 300.0)
+           py::arg("mailbox_bytes"), py::arg("token"), py::arg("timeout_s") = 300.0,
+           py::arg("mode") = -1)
       .def("export_for", [](const IpcTransport& t, int p) { return py::bytes(t.export_for(p)); })
       .def("connect", [](IpcTransport& t, int p, py::bytes blob) { t.connect(p, blob); })
+      .def("unlink_shm", &IpcTransport::unlink_shm)
       .def_property_readonly("connected", &IpcTransport::connected)
-      .def_property_readonly("mailbox_bytes", &IpcTransport::mailbox_bytes);
+      .def_property_readonly("mailbox_bytes", &IpcTransport::mailbox_bytes)
+      .def_property_readonly("mode",
+                             [](const IpcTransport& t) {
+                               return t.mode() == IpcTransport::Mode::kStream ? "stream" : "host";
+                             })
+      .def_property_readonly("poisoned", &IpcTransport::poisoned)
+      .def_property_readonly("host_waits", &IpcTransport::host_waits);
   py::class_<RcclComm, P2PTransport>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def(py::init([](int nranks, int rank, py::bytes uid, int device, double init_timeout_s) {

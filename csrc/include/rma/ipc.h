@@ -7,23 +7,31 @@
 // the same natively: every receiver owns, per sender, a double-buffered device
 // MAILBOX that the sender maps with hipIpcOpenMemHandle and fills with one
 // device-to-device copy per message on its own stream (over xGMI when the
-// ranks drive different GPUs, on-device when they share one). Ordering is
-// stream-ordered on the GPU and handshaked on the host:
-//   * sender, generation g of a (sender, receiver) pair: waits (host) until the
-//     receiver has published "done with g-2", copies into slot g%2, records
-//     its "sent" event, waits for it on the host, publishes g in the
-//     receiver's shared-memory flag block;
-//   * receiver: waits (host) until the sender published g, copies the slot
-//     out, records its "done" event, waits for it, publishes g.
-// (RMA_IPC_GPU_EVENTS=1: the flags mean "record enqueued" and the streams wait
-// on the peer's interprocess events instead of the host; RMA_IPC_STREAM_FLAGS=1:
-// the GPU writes the flags after the copies; see ipc.cpp.) The
-// executor enqueues the interior before the frame and the exchange for such a
-// host-synchronising transport, so the blocking costs no overlap.
-// Host waits are bounded (timeout -> rma::Error naming the peer); the GPU only
-// ever waits on event records the host has seen enqueued, so a dead peer ends
-// in an exception, not a hang. Flags live in one POSIX shared-memory block per
-// receiver (/dev/shm). Not stream-capturable (host handshake), like loopback.
+// ranks drive different GPUs, on-device when they share one). The handshake
+// flags of a (sender, receiver) pair live in the receiver's POSIX
+// shared-memory block, mapped by both. Two modes (RMA_IPC_MODE):
+//
+//   * stream (default): nothing waits on the host. Per mailbox slot a
+//     full/empty flag; the sender's stream waits for "empty"
+//     (hipStreamWaitValue64 on the flag, host-registered and mapped for the
+//     GPU), copies, and writes "full" (hipStreamWriteValue64) behind its
+//     copies; the receiver's stream waits for "full", copies the slot out and
+//     writes "empty". group_end() only enqueues. The protocol carries no
+//     generation number, so a captured group replays correctly as long as
+//     both sides replay the same sequence of groups.
+//   * host: the round-4 validation mode. Per pair a generation counter; the
+//     sender waits (host, bounded) until the receiver published "done with
+//     g-2", copies into slot g%2, waits for its own copies (a local event),
+//     publishes g; the receiver waits for g, copies out, waits for its own
+//     copies, publishes g. Timeouts name the peer.
+//
+// A group is validated as a whole before any flag or generation changes (a
+// mailbox overflow leaves the transport consistent); an error in the middle
+// of enqueueing poisons the transport (every later call throws), since the
+// peers' view of the protocol may then be out of step. Flags live in one
+// shared-memory block per receiver; unlink_shm() removes its name once every
+// peer has connected (comm.py IpcComm does it after a barrier), so a crashed
+// job leaves nothing in /dev/shm. Not stream-capturable in host mode.
 //
 // Bootstrap (rocm_mpi_amd/parallel/comm.py IpcComm): construct on every rank
 // with the peer list (neighbours and diagonals), publish export_for(p) through
@@ -41,20 +49,24 @@ namespace rma {
 
 class IpcTransport : public P2PTransport {
  public:
+  enum class Mode : int { kHost = 0, kStream = 1 };
   // token: job-unique name part of the shared-memory blocks; mailbox_bytes:
-  // capacity of ONE slot per sender (the bytes of one group to one peer)
+  // capacity of ONE slot per sender (the bytes of one group to one peer);
+  // mode -1: RMA_IPC_MODE (stream | host), default stream
   IpcTransport(int rank, int size, int device, const std::vector<int>& peers,
-               size_t mailbox_bytes, const std::string& token, double timeout_s);
+               size_t mailbox_bytes, const std::string& token, double timeout_s, int mode = -1);
   ~IpcTransport() override;
   IpcTransport(const IpcTransport&) = delete;
   IpcTransport& operator=(const IpcTransport&) = delete;
 
-  // what peer p needs from me: my mailbox for p's messages, my "done" event
-  // for p's messages, my "sent" event for my messages to p (opaque bytes)
+  // what peer p needs from me: my mailbox for p's messages (opaque bytes)
   std::string export_for(int peer) const;
   // open what peer p exported for me (and p's shared-memory flag block)
   void connect(int peer, const std::string& blob);
   bool connected() const;
+  // remove the name of my flag block (mappings stay valid): call once every
+  // peer has connected
+  void unlink_shm();
 
   int rank() const override { return rank_; }
   int size() const override { return size_; }
@@ -62,8 +74,15 @@ class IpcTransport : public P2PTransport {
   void group_end() override;
   void send(const void* buf, size_t bytes, int peer, stream_t stream) override;
   void recv(void* buf, size_t bytes, int peer, stream_t stream) override;
-  bool capturable() const override { return false; }
+  // stream mode only enqueues stream operations; whether HIP can capture
+  // them is probed by the tests (RMA_IPC_GRAPH=1 allows capture)
+  bool capturable() const override;
   size_t mailbox_bytes() const { return cap_; }
+  Mode mode() const { return mode_; }
+  bool poisoned() const { return poisoned_; }
+  // host waits inside group_end() so far (host mode: two per peer and group;
+  // stream mode: 0)
+  uint64_t host_waits() const { return host_waits_; }
 
  private:
   struct Op {
@@ -74,37 +93,34 @@ class IpcTransport : public P2PTransport {
   };
   struct Peer {
     int rank = -1;
-    // mine (receiver side): mailbox for this peer's messages + done event
-    void* mailbox = nullptr;
-    void* done_ev = nullptr;
-    // mine (sender side): sent event for my messages to this peer
-    void* sent_ev = nullptr;
-    // host-synchronised mode: plain events (a host wait on an interprocess
-    // event costs ~1 ms on this runtime)
-    void* sent_local = nullptr;
-    void* done_local = nullptr;
-    // the peer's, opened: its mailbox for my messages, its done / sent events
-    void* r_mailbox = nullptr;
-    void* r_done_ev = nullptr;
-    void* r_sent_ev = nullptr;
-    void* r_flags = nullptr;  // the peer's shared-memory flag block (mapped)
-    void* r_flags_dev = nullptr;  // ... registered for GPU writes (stream flags)
+    void* mailbox = nullptr;     // mine: 2 slots for this peer's messages
+    void* sent_local = nullptr;  // host mode: my copies to this peer done
+    void* done_local = nullptr;  // host mode: my copies out of its slot done
+    void* r_mailbox = nullptr;   // the peer's, opened: its mailbox for my messages
+    void* r_flags = nullptr;     // the peer's shared-memory flag block (mapped)
+    void* r_flags_dev = nullptr;  // ... registered for the GPU (stream mode)
     uint64_t send_gen = 0, recv_gen = 0;
     bool connected = false;
   };
   Peer& peer(int p);
-  void wait_flag(const void* addr, uint64_t want, int p, const char* what) const;
+  void wait_flag(const void* addr, uint64_t want, int p, const char* what);
+  void release() noexcept;
+  void enqueue_group();
 
   int rank_, size_, device_;
   size_t cap_;
   double timeout_s_;
   std::string token_;
+  Mode mode_;
   std::vector<Peer> peers_;
-  void* flags_ = nullptr;  // my flag block: [sender][2] = {sent, done}
-  void* flags_dev_ = nullptr;  // its device address (RMA_IPC_STREAM_FLAGS=1)
+  void* flags_ = nullptr;      // my flag block: [sender][4] = {sent, done, full0, full1}
+  void* flags_dev_ = nullptr;  // its device address (stream mode)
   size_t flags_bytes_ = 0;
   std::string shm_name_;
+  bool shm_linked_ = false;
   int depth_ = 0;
+  bool poisoned_ = false;
+  uint64_t host_waits_ = 0;
   std::vector<Op> sends_, recvs_;
 };
 

@@ -21,35 +21,13 @@ namespace rma {
 
 namespace {
 hipEvent_t E(void* p) { return reinterpret_cast<hipEvent_t>(p); }
-std::atomic<uint64_t>* slot_flag(void* block, int sender, int which) {
-  return reinterpret_cast<std::atomic<uint64_t>*>(block) + 2 * sender + which;
+// flag words of sender s in a receiver's block
+constexpr int kWords = 4, kSent = 0, kDone = 1, kFull0 = 2;
+std::atomic<uint64_t>* flag(void* block, int sender, int which) {
+  return reinterpret_cast<std::atomic<uint64_t>*>(block) + kWords * sender + which;
 }
-constexpr int kSent = 0, kDone = 1;
-// Default: the sender waits on the host for its own copies (its own event)
-// before it publishes a generation, the receiver for its own copies before it
-// frees the slot, so no process ever waits on an event it opened from another
-// one. RMA_IPC_GPU_EVENTS=1 instead makes the streams wait on the peers'
-// interprocess events (no host blocking); on the HIP 7.0 runtime in torch that
-// hipStreamWaitEvent on an opened event fails intermittently with "invalid
-// argument" (bench/ipc_transport_probe.py, profiles/SUMMARY_r4.md §9).
-bool host_sync() {
-  static const bool v = [] {
-    const char* e = std::getenv("RMA_IPC_GPU_EVENTS");
-    return !(e && e[0] == '1');
-  }();
-  return v;
-}
-// RMA_IPC_STREAM_FLAGS=1: the flags are written by the GPU, in stream order
-// after the copies (hipStreamWriteValue64 into the shared-memory block,
-// registered with hipHostRegister in every process that writes it), so the
-// sender's host never waits for its copies; the receiver's host still polls
-// for the sender's flag before it enqueues its copies
-bool stream_flags() {
-  static const bool v = [] {
-    const char* e = std::getenv("RMA_IPC_STREAM_FLAGS");
-    return e && e[0] == '1';
-  }();
-  return v;
+uint64_t* dflag(void* dev_block, int sender, int which) {
+  return reinterpret_cast<uint64_t*>(dev_block) + kWords * sender + which;
 }
 size_t page_round(size_t b) { return (b + 4095) / 4096 * 4096; }
 void* register_block(void* host, size_t bytes) {
@@ -58,6 +36,15 @@ void* register_block(void* host, size_t bytes) {
   RMA_HIP_CHECK(hipHostGetDevicePointer(&d, host, 0));
   return d;
 }
+IpcTransport::Mode mode_from(int m) {
+  if (m == 0) return IpcTransport::Mode::kHost;
+  if (m == 1) return IpcTransport::Mode::kStream;
+  const char* e = std::getenv("RMA_IPC_MODE");
+  if (e && std::strcmp(e, "host") == 0) return IpcTransport::Mode::kHost;
+  if (e && *e && std::strcmp(e, "stream") != 0)
+    throw_error("RMA_IPC_MODE must be stream or host", __FILE__, __LINE__, e);
+  return IpcTransport::Mode::kStream;
+}
 }  // namespace
 
 std::string ipc_shm_name(const std::string& token, int rank) {
@@ -65,92 +52,118 @@ std::string ipc_shm_name(const std::string& token, int rank) {
 }
 
 IpcTransport::IpcTransport(int rank, int size, int device, const std::vector<int>& peers,
-                           size_t mailbox_bytes, const std::string& token, double timeout_s)
+                           size_t mailbox_bytes, const std::string& token, double timeout_s,
+                           int mode)
     : rank_(rank), size_(size), device_(device), cap_(mailbox_bytes), timeout_s_(timeout_s),
-      token_(token) {
+      token_(token), mode_(mode_from(mode)) {
   RMA_CHECK_ARG(size >= 1 && rank >= 0 && rank < size, "rank " << rank << " of " << size);
   RMA_CHECK_ARG(mailbox_bytes >= 8, "mailbox of " << mailbox_bytes << " bytes");
   RMA_CHECK_ARG(!token.empty() && token.size() < 64 &&
                     token.find('/') == std::string::npos,
                 "shared-memory token '" << token << "'");
-  RMA_HIP_CHECK(hipSetDevice(device));
-  // my flag block: per sender {sent generation, done generation}
-  shm_name_ = ipc_shm_name(token, rank);
-  flags_bytes_ = page_round(sizeof(uint64_t) * 2 * (size_t)size);
-  const int fd = shm_open(shm_name_.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0600);
-  if (fd < 0) throw_error("shm_open failed", __FILE__, __LINE__, shm_name_);
-  if (ftruncate(fd, (off_t)flags_bytes_) != 0) {
-    close(fd);
-    throw_error("ftruncate of the IPC flag block failed", __FILE__, __LINE__, shm_name_);
-  }
-  flags_ = mmap(nullptr, flags_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  close(fd);
-  if (flags_ == MAP_FAILED) {
-    flags_ = nullptr;
-    throw_error("mmap of the IPC flag block failed", __FILE__, __LINE__, shm_name_);
-  }
-  for (int s = 0; s < size; ++s) {
-    slot_flag(flags_, s, kSent)->store(0);
-    slot_flag(flags_, s, kDone)->store(0);
-  }
-  if (stream_flags()) flags_dev_ = register_block(flags_, flags_bytes_);
-  peers_.resize(size);
-  std::vector<int> ps(peers);
-  std::sort(ps.begin(), ps.end());
-  ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
-  for (int p : ps) {
-    if (p < 0) continue;
-    RMA_CHECK_ARG(p < size, "peer " << p << " of " << size);
-    Peer& P = peers_[p];
-    P.rank = p;
-    RMA_HIP_CHECK(hipMalloc(&P.mailbox, 2 * cap_));
-    hipEvent_t e;
-    RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventInterprocess | hipEventDisableTiming));
-    P.done_ev = e;
-    RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventInterprocess | hipEventDisableTiming));
-    P.sent_ev = e;
-    RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    P.sent_local = e;
-    RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    P.done_local = e;
-    if (p == rank) {  // periodic self neighbour through the transport: no IPC
-      P.r_mailbox = P.mailbox;
-      P.r_done_ev = P.done_ev;
-      P.r_sent_ev = P.sent_ev;
-      P.r_flags = flags_;
-      P.r_flags_dev = flags_dev_;
-      P.connected = true;
+  for (int p : peers) RMA_CHECK_ARG(p < size, "peer " << p << " of " << size);
+  // every resource below is released by release() if a later step throws
+  // (the destructor does not run for a constructor that throws)
+  try {
+    RMA_HIP_CHECK(hipSetDevice(device));
+    if (mode_ == Mode::kStream) {
+      int ok = 0;
+      RMA_HIP_CHECK(hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, device));
+      RMA_CHECK_ARG(ok, "RMA_IPC_MODE=stream needs hipStreamWaitValue64 on device " << device
+                                                                             << " (use host)");
     }
+    shm_name_ = ipc_shm_name(token, rank);
+    flags_bytes_ = page_round(sizeof(uint64_t) * kWords * (size_t)size);
+    const int fd = shm_open(shm_name_.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0600);
+    if (fd < 0) throw_error("shm_open failed", __FILE__, __LINE__, shm_name_);
+    shm_linked_ = true;
+    if (ftruncate(fd, (off_t)flags_bytes_) != 0) {
+      close(fd);
+      throw_error("ftruncate of the IPC flag block failed", __FILE__, __LINE__, shm_name_);
+    }
+    void* m = mmap(nullptr, flags_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) throw_error("mmap of the IPC flag block failed", __FILE__, __LINE__, shm_name_);
+    flags_ = m;
+    for (int s = 0; s < size; ++s)
+      for (int w = 0; w < kWords; ++w) flag(flags_, s, w)->store(0);
+    if (mode_ == Mode::kStream) flags_dev_ = register_block(flags_, flags_bytes_);
+    peers_.resize(size);
+    std::vector<int> ps(peers);
+    std::sort(ps.begin(), ps.end());
+    ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
+    for (int p : ps) {
+      if (p < 0) continue;
+      Peer& P = peers_[p];
+      P.rank = p;
+      RMA_HIP_CHECK(hipMalloc(&P.mailbox, 2 * cap_));
+      if (mode_ == Mode::kHost) {
+        hipEvent_t e;
+        RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        P.sent_local = e;
+        RMA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        P.done_local = e;
+      }
+      if (p == rank) {  // periodic self neighbour through the transport: no IPC
+        P.r_mailbox = P.mailbox;
+        P.r_flags = flags_;
+        P.r_flags_dev = flags_dev_;
+        P.connected = true;
+      }
+    }
+  } catch (...) {
+    release();
+    throw;
   }
 }
 
-IpcTransport::~IpcTransport() {
+void IpcTransport::release() noexcept {
   (void)hipSetDevice(device_);
-  (void)hipDeviceSynchronize();
+  if (!peers_.empty()) (void)hipDeviceSynchronize();
   for (Peer& P : peers_) {
     if (P.rank < 0) continue;
     if (P.rank != rank_) {
       if (P.r_mailbox) (void)hipIpcCloseMemHandle(P.r_mailbox);
-      if (P.r_done_ev) (void)hipEventDestroy(E(P.r_done_ev));
-      if (P.r_sent_ev) (void)hipEventDestroy(E(P.r_sent_ev));
       if (P.r_flags_dev) (void)hipHostUnregister(P.r_flags);
       if (P.r_flags) munmap(P.r_flags, flags_bytes_);
     }
     if (P.mailbox) (void)hipFree(P.mailbox);
-    if (P.done_ev) (void)hipEventDestroy(E(P.done_ev));
-    if (P.sent_ev) (void)hipEventDestroy(E(P.sent_ev));
     if (P.sent_local) (void)hipEventDestroy(E(P.sent_local));
     if (P.done_local) (void)hipEventDestroy(E(P.done_local));
+    P = Peer();
   }
+  peers_.clear();
   if (flags_) {
     if (flags_dev_) (void)hipHostUnregister(flags_);
     munmap(flags_, flags_bytes_);
+    flags_ = flags_dev_ = nullptr;
+  }
+  if (shm_linked_) {
     shm_unlink(shm_name_.c_str());
+    shm_linked_ = false;
   }
 }
 
+IpcTransport::~IpcTransport() { release(); }
+
+void IpcTransport::unlink_shm() {
+  if (shm_linked_) {
+    shm_unlink(shm_name_.c_str());
+    shm_linked_ = false;
+  }
+}
+
+bool IpcTransport::capturable() const {
+  if (mode_ != Mode::kStream) return false;
+  static const bool allow = [] {
+    const char* e = std::getenv("RMA_IPC_GRAPH");
+    return e && e[0] == '1';
+  }();
+  return allow;
+}
+
 IpcTransport::Peer& IpcTransport::peer(int p) {
-  RMA_CHECK_ARG(p >= 0 && p < size_ && peers_[p].rank == p,
+  RMA_CHECK_ARG(p >= 0 && p < size_ && (size_t)p < peers_.size() && peers_[p].rank == p,
                 "rank " << p << " is not a peer of the IPC transport of rank " << rank_);
   Peer& P = peers_[p];
   RMA_CHECK_ARG(P.connected, "IPC transport: peer " << p << " not connected");
@@ -161,17 +174,12 @@ std::string IpcTransport::export_for(int p) const {
   RMA_CHECK_ARG(p >= 0 && p < size_ && peers_[p].rank == p, "rank " << p << " is not a peer");
   const Peer& P = peers_[p];
   hipIpcMemHandle_t mh;
-  hipIpcEventHandle_t dh, sh;
   RMA_HIP_CHECK(hipIpcGetMemHandle(&mh, P.mailbox));
-  RMA_HIP_CHECK(hipIpcGetEventHandle(&dh, E(P.done_ev)));
-  RMA_HIP_CHECK(hipIpcGetEventHandle(&sh, E(P.sent_ev)));
-  std::string blob(sizeof mh + sizeof dh + sizeof sh + sizeof(uint64_t), '\0');
+  std::string blob(sizeof mh + 2 * sizeof(uint64_t), '\0');
   char* b = &blob[0];
   std::memcpy(b, &mh, sizeof mh);
-  std::memcpy(b + sizeof mh, &dh, sizeof dh);
-  std::memcpy(b + sizeof mh + sizeof dh, &sh, sizeof sh);
-  const uint64_t cap = cap_;
-  std::memcpy(b + sizeof mh + sizeof dh + sizeof sh, &cap, sizeof cap);
+  const uint64_t meta[2] = {cap_, (uint64_t)mode_};
+  std::memcpy(b + sizeof mh, meta, sizeof meta);
   return blob;
 }
 
@@ -180,31 +188,30 @@ void IpcTransport::connect(int p, const std::string& blob) {
   Peer& P = peers_[p];
   if (P.connected) return;
   hipIpcMemHandle_t mh;
-  hipIpcEventHandle_t dh, sh;
-  uint64_t cap = 0;
-  RMA_CHECK_ARG(blob.size() == sizeof mh + sizeof dh + sizeof sh + sizeof cap,
+  uint64_t meta[2] = {0, 0};
+  RMA_CHECK_ARG(blob.size() == sizeof mh + sizeof meta,
                 "IPC export blob of " << blob.size() << " bytes from rank " << p);
-  const char* b = blob.data();
-  std::memcpy(&mh, b, sizeof mh);
-  std::memcpy(&dh, b + sizeof mh, sizeof dh);
-  std::memcpy(&sh, b + sizeof mh + sizeof dh, sizeof sh);
-  std::memcpy(&cap, b + sizeof mh + sizeof dh + sizeof sh, sizeof cap);
-  RMA_CHECK_ARG(cap == cap_, "IPC mailbox sizes differ: rank " << p << " " << cap << ", rank "
-                                                               << rank_ << " " << cap_);
-  RMA_HIP_CHECK(hipIpcOpenMemHandle(&P.r_mailbox, mh, hipIpcMemLazyEnablePeerAccess));
-  hipEvent_t e;
-  RMA_HIP_CHECK(hipIpcOpenEventHandle(&e, dh));
-  P.r_done_ev = e;
-  RMA_HIP_CHECK(hipIpcOpenEventHandle(&e, sh));
-  P.r_sent_ev = e;
+  std::memcpy(&mh, blob.data(), sizeof mh);
+  std::memcpy(meta, blob.data() + sizeof mh, sizeof meta);
+  RMA_CHECK_ARG(meta[0] == cap_, "IPC mailbox sizes differ: rank " << p << " " << meta[0]
+                                                                  << ", rank " << rank_ << " "
+                                                                  << cap_);
+  RMA_CHECK_ARG(meta[1] == (uint64_t)mode_, "IPC modes differ between rank " << p << " and rank "
+                                                                         << rank_
+                                                                         << " (RMA_IPC_MODE)");
+  // the peer's shared-memory block first: it exists only on this node, so a
+  // peer on another node fails here, before any IPC handle is opened
   const std::string name = ipc_shm_name(token_, p);
   const int fd = shm_open(name.c_str(), O_RDWR, 0600);
-  if (fd < 0) throw_error("shm_open of a peer's IPC flag block failed", __FILE__, __LINE__, name);
+  if (fd < 0)
+    throw_error("shm_open of a peer's IPC flag block failed (is the peer on this node?)",
+                __FILE__, __LINE__, name);
   void* m = mmap(nullptr, flags_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (m == MAP_FAILED) throw_error("mmap of a peer's IPC flag block failed", __FILE__, __LINE__, name);
   P.r_flags = m;
-  if (stream_flags()) P.r_flags_dev = register_block(m, flags_bytes_);
+  if (mode_ == Mode::kStream) P.r_flags_dev = register_block(m, flags_bytes_);
+  RMA_HIP_CHECK(hipIpcOpenMemHandle(&P.r_mailbox, mh, hipIpcMemLazyEnablePeerAccess));
   P.connected = true;
 }
 
@@ -214,7 +221,8 @@ bool IpcTransport::connected() const {
   return true;
 }
 
-void IpcTransport::wait_flag(const void* addr, uint64_t want, int p, const char* what) const {
+void IpcTransport::wait_flag(const void* addr, uint64_t want, int p, const char* what) {
+  ++host_waits_;
   auto* f = reinterpret_cast<const std::atomic<uint64_t>*>(addr);
   if (f->load(std::memory_order_acquire) >= want) return;
   const auto t0 = std::chrono::steady_clock::now();
@@ -231,6 +239,7 @@ void IpcTransport::wait_flag(const void* addr, uint64_t want, int p, const char*
 }
 
 void IpcTransport::group_start() {
+  RMA_CHECK_ARG(!poisoned_, "IPC transport unusable after an earlier error in group_end");
   if (depth_++ == 0) {
     sends_.clear();
     recvs_.clear();
@@ -256,85 +265,105 @@ void IpcTransport::recv(void* buf, size_t bytes, int peer_rank, stream_t stream)
 void IpcTransport::group_end() {
   RMA_CHECK_ARG(depth_ > 0, "group_end without group_start");
   if (--depth_ > 0) return;
+  RMA_CHECK_ARG(!poisoned_, "IPC transport unusable after an earlier error in group_end");
+  // validate the whole group before any flag, generation or copy: one stream
+  // per peer and direction, and every peer's bytes within the mailbox slot
+  std::map<int, size_t> out_b, in_b;
+  std::map<int, stream_t> out_s, in_s;
+  for (const Op& o : sends_) {
+    (void)peer(o.peer);
+    auto it = out_s.emplace(o.peer, o.stream).first;
+    RMA_CHECK_ARG(it->second == o.stream, "IPC transport: one stream per peer and group");
+    out_b[o.peer] += o.bytes;
+  }
+  for (const Op& o : recvs_) {
+    (void)peer(o.peer);
+    auto it = in_s.emplace(o.peer, o.stream).first;
+    RMA_CHECK_ARG(it->second == o.stream, "IPC transport: one stream per peer and group");
+    in_b[o.peer] += o.bytes;
+  }
+  for (const auto& [p, b] : out_b)
+    RMA_CHECK_ARG(b <= cap_, "IPC transport: " << b << " bytes to rank " << p
+                                               << " in one group exceed the mailbox of " << cap_
+                                               << " (RMA_IPC_MAILBOX_MB)");
+  for (const auto& [p, b] : in_b)
+    RMA_CHECK_ARG(b <= cap_, "IPC transport: " << b << " bytes from rank " << p
+                                               << " in one group exceed the mailbox of " << cap_
+                                               << " (RMA_IPC_MAILBOX_MB)");
+  try {
+    enqueue_group();
+  } catch (...) {
+    // a peer may already have seen part of this group: the protocol is out of step
+    poisoned_ = true;
+    sends_.clear();
+    recvs_.clear();
+    throw;
+  }
+  sends_.clear();
+  recvs_.clear();
+}
+
+void IpcTransport::enqueue_group() {
   // per peer, in issue order (the n-th send to p matches p's n-th recv from me)
   std::map<int, std::vector<const Op*>> out, in;
   for (const Op& o : sends_) out[o.peer].push_back(&o);
   for (const Op& o : recvs_) in[o.peer].push_back(&o);
-  const bool hs = host_sync();
   // sends first: a rank's sends of generation g wait only for its peers'
   // receives of g - 2 (completed group calls), its receives for the peers'
   // sends of g, which they publish before waiting for anything of this group
   for (auto& [p, ops] : out) {
     Peer& P = peer(p);
     hipStream_t s = as_stream(ops.front()->stream);
-    size_t total = 0;
-    for (const Op* o : ops) {
-      RMA_CHECK_ARG(as_stream(o->stream) == s, "IPC transport: one stream per peer and group");
-      total += o->bytes;
-    }
-    RMA_CHECK_ARG(total <= cap_, "IPC transport: " << total << " bytes to rank " << p
-                                                   << " in one group exceed the mailbox of "
-                                                   << cap_ << " (RMA_IPC_MAILBOX_MB)");
     const uint64_t g = ++P.send_gen;
-    if (g > 2) {  // slot g % 2 was last read by the peer's receive of g - 2
-      wait_flag(slot_flag(P.r_flags, rank_, kDone), g - 2, p, "receive done");
-      if (!hs && !P.r_flags_dev) RMA_HIP_CHECK(hipStreamWaitEvent(s, E(P.r_done_ev), 0));
+    const int slot = (int)(g & 1);
+    if (mode_ == Mode::kStream) {  // slot empty -> copies -> slot full, all on the GPU
+      RMA_HIP_CHECK(hipStreamWaitValue64(s, dflag(P.r_flags_dev, rank_, kFull0 + slot), 0,
+                                         hipStreamWaitValueEq, ~0ull));
+    } else if (g > 2) {  // slot g % 2 was last read by the peer's receive of g - 2
+      wait_flag(flag(P.r_flags, rank_, kDone), g - 2, p, "receive done");
     }
-    char* dst = static_cast<char*>(P.r_mailbox) + (g & 1) * cap_;
+    char* dst = static_cast<char*>(P.r_mailbox) + slot * cap_;
     size_t off = 0;
     for (const Op* o : ops) {
       if (o->bytes)
         RMA_HIP_CHECK(hipMemcpyAsync(dst + off, o->buf, o->bytes, hipMemcpyDeviceToDevice, s));
       off += o->bytes;
     }
-    if (P.r_flags_dev) {  // the GPU publishes g once the copies are done
-      RMA_HIP_CHECK(hipStreamWriteValue64(
-          s, slot_flag(P.r_flags_dev, rank_, kSent), g, 0));
+    if (mode_ == Mode::kStream) {
+      RMA_HIP_CHECK(hipStreamWriteValue64(s, dflag(P.r_flags_dev, rank_, kFull0 + slot), 1, 0));
       continue;
     }
-    if (hs) {
-      RMA_HIP_CHECK(hipEventRecord(E(P.sent_local), s));
-      RMA_HIP_CHECK(hipEventSynchronize(E(P.sent_local)));
-    } else {
-      RMA_HIP_CHECK(hipEventRecord(E(P.sent_ev), s));
-    }
-    slot_flag(P.r_flags, rank_, kSent)->store(g, std::memory_order_release);
+    RMA_HIP_CHECK(hipEventRecord(E(P.sent_local), s));
+    ++host_waits_;
+    RMA_HIP_CHECK(hipEventSynchronize(E(P.sent_local)));
+    flag(P.r_flags, rank_, kSent)->store(g, std::memory_order_release);
   }
   for (auto& [p, ops] : in) {
     Peer& P = peer(p);
     hipStream_t s = as_stream(ops.front()->stream);
-    size_t total = 0;
-    for (const Op* o : ops) {
-      RMA_CHECK_ARG(as_stream(o->stream) == s, "IPC transport: one stream per peer and group");
-      total += o->bytes;
-    }
-    RMA_CHECK_ARG(total <= cap_, "IPC transport: " << total << " bytes from rank " << p
-                                                   << " in one group exceed the mailbox of "
-                                                   << cap_ << " (RMA_IPC_MAILBOX_MB)");
     const uint64_t g = ++P.recv_gen;
-    wait_flag(slot_flag(flags_, p, kSent), g, p, "send");
-    if (!hs && !flags_dev_) RMA_HIP_CHECK(hipStreamWaitEvent(s, E(P.r_sent_ev), 0));
-    const char* src = static_cast<const char*>(P.mailbox) + (g & 1) * cap_;
+    const int slot = (int)(g & 1);
+    if (mode_ == Mode::kStream)
+      RMA_HIP_CHECK(hipStreamWaitValue64(s, dflag(flags_dev_, p, kFull0 + slot), 1,
+                                         hipStreamWaitValueEq, ~0ull));
+    else
+      wait_flag(flag(flags_, p, kSent), g, p, "send");
+    const char* src = static_cast<const char*>(P.mailbox) + slot * cap_;
     size_t off = 0;
     for (const Op* o : ops) {
       if (o->bytes)
         RMA_HIP_CHECK(hipMemcpyAsync(o->buf, src + off, o->bytes, hipMemcpyDeviceToDevice, s));
       off += o->bytes;
     }
-    if (flags_dev_) {  // the GPU frees the slot once the copies are done
-      RMA_HIP_CHECK(hipStreamWriteValue64(s, slot_flag(flags_dev_, p, kDone), g, 0));
+    if (mode_ == Mode::kStream) {
+      RMA_HIP_CHECK(hipStreamWriteValue64(s, dflag(flags_dev_, p, kFull0 + slot), 0, 0));
       continue;
     }
-    if (hs) {
-      RMA_HIP_CHECK(hipEventRecord(E(P.done_local), s));
-      RMA_HIP_CHECK(hipEventSynchronize(E(P.done_local)));
-    } else {
-      RMA_HIP_CHECK(hipEventRecord(E(P.done_ev), s));
-    }
-    slot_flag(flags_, p, kDone)->store(g, std::memory_order_release);
+    RMA_HIP_CHECK(hipEventRecord(E(P.done_local), s));
+    ++host_waits_;
+    RMA_HIP_CHECK(hipEventSynchronize(E(P.done_local)));
+    flag(flags_, p, kDone)->store(g, std::memory_order_release);
   }
-  sends_.clear();
-  recvs_.clear();
 }
 
 }  // namespace rma

@@ -38,7 +38,7 @@ def run(n: int = 4, transport: str = "auto", verbose: bool = True,
         C.init_distributed()
     local, lsize = C.node_local_rank(rank, size)
     dev = C.select_device(local)
-    t = _choose_transport(transport, size, dev)
+    t = _choose_transport(transport, size, dev, lsize)
     dst, src = (rank + 1) % size, (rank - 1) % size
     if t == "rccl":
         comm = C.RcclComm(dev)

@@ -337,8 +337,11 @@ class IpcComm(TorchDistComm):
     IPC (``csrc/include/rma/ipc.h``): every receiver owns a double-buffered
     device mailbox per sender, which the sender maps and fills with one
     device-to-device copy per message (over xGMI between GPUs, on-device when
-    ranks share a GPU); host handshake through POSIX shared memory, GPU
-    ordering through interprocess events. The reference's intra-node
+    ranks share a GPU). Ordering (``RMA_IPC_MODE``): ``stream`` (default) --
+    per-slot full/empty flags in POSIX shared memory that the streams wait on
+    and write (hipStreamWaitValue64 / hipStreamWriteValue64), nothing blocks
+    the host; ``host`` -- the host waits for its own copies and polls the
+    peers' generation flags (validation). The reference's intra-node
     ROCm-aware MPI path (``scripts/rocmaware_test_selectdevice.jl:16-22``) without
     MPI or RCCL. Collectives and gather stay on gloo (host-staged), as in
     ``staged``. ``peers``: the halo peers (Cartesian neighbours and diagonals).
@@ -346,7 +349,7 @@ class IpcComm(TorchDistComm):
     """
 
     def __init__(self, device: torch.device, peers, timeout_s: float = DEFAULT_TIMEOUT_S,
-                 mailbox_mb: float | None = None, store=None):
+                 mailbox_mb: float | None = None, store=None, mode: str | None = None):
         super().__init__(staged=True)
         self.name = "ipc"
         from .._native import native
@@ -365,13 +368,20 @@ class IpcComm(TorchDistComm):
         cap = max(8, int(mb * (1 << 20)))
         self.device = torch.device(device)
         self.peers = sorted({int(p) for p in peers if int(p) >= 0})
+        mode = mode or os.environ.get("RMA_IPC_MODE", "stream")
+        if mode not in ("stream", "host"):
+            raise ValueError(f"IPC mode must be stream or host, got {mode!r}")
         self._c = native().IpcTransport(self.rank, self.size, self.device.index or 0, self.peers,
-                                        cap, token, timeout_s)
+                                        cap, token, timeout_s, 1 if mode == "stream" else 0)
         others = [p for p in self.peers if p != self.rank]
-        for p in others:  # what p needs from me (my mailbox, my events)
+        for p in others:  # what p needs from me (my mailbox)
             store.set(f"{key}/{self.rank}/{p}", self._c.export_for(p))
         for p in others:  # p's shared-memory block exists: it published after creating it
             self._c.connect(p, store.get(f"{key}/{p}/{self.rank}"))
+        # every peer has mapped every block: drop the names, so that nothing
+        # stays in /dev/shm even if the job dies
+        dist.barrier(group=self._pg)
+        self._c.unlink_shm()
 
     @property
     def native(self):

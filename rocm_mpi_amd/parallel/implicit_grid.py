@@ -98,7 +98,8 @@ def grid_is_initialized() -> bool:
     return (getattr(_tls, "grid", None) or _global) is not None
 
 
-def _choose_transport(transport: str, size: int, device: torch.device) -> str:
+def _choose_transport(transport: str, size: int, device: torch.device,
+                      local_size: int | None = None) -> str:
     t = os.environ.get("RMA_TRANSPORT", transport)
     legacy = os.environ.get("IGG_ROCMAWARE_MPI")
     if t == "auto" and legacy is not None and device.type == "cuda" and size > 1:
@@ -113,6 +114,9 @@ def _choose_transport(transport: str, size: int, device: torch.device) -> str:
         raise ValueError(f"transport {t!r} needs a GPU device")
     if t == "ipc" and size == 1:
         return "self"
+    if t == "ipc" and local_size is not None and local_size != size:
+        raise ValueError(f"transport 'ipc' connects the processes of ONE node; {size} ranks "
+                         f"span nodes ({local_size} on this one): use rccl")
     return t
 
 
@@ -186,7 +190,8 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
     else:
         dev = torch.device("cpu")
 
-    tname = "loopback" if loopback is not None else _choose_transport(transport, comm_size, dev)
+    tname = ("loopback" if loopback is not None
+             else _choose_transport(transport, comm_size, dev, local_size))
     if loopback is not None:
         comm: C.Communicator = C.LoopbackComm(hub, comm_rank)
     elif tname == "self":

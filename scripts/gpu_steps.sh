@@ -208,6 +208,17 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_ipc_mailbox_overflow_fails_on_every_rank" \
              "tests/test_multirank_gpu.py::test_ipc_update_halo_device_fields" \
              -p no:cacheprovider || exit 1 ;;
+    tests_ipc5) step tests_ipc5 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+             "tests/test_multirank_gpu.py::test_ipc_modes_2000_exchanged_steps_bitwise" \
+             "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
+             "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" \
+             "tests/test_multirank_gpu.py::test_ipc_ring_smoke_test" \
+             "tests/test_multirank_gpu.py::test_ipc_mailbox_overflow_fails_on_every_rank" \
+             "tests/test_multirank_gpu.py::test_ipc_update_halo_device_fields" \
+             -p no:cacheprovider || exit 1 ;;
+    tests_ipc5g) step tests_ipc5g 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread \
+             "tests/test_multirank_gpu.py::test_ipc_stream_mode_graph_replay_matches_golden" \
+             -p no:cacheprovider || exit 1 ;;
     tests_ipc_ev) RMA_IPC_GPU_EVENTS=1 step tests_ipc_ev 400 python -u -m pytest -x -v --timeout 120 \
              --timeout-method thread "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
              "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" -p no:cacheprovider || exit 1 ;;

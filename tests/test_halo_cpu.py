@@ -192,3 +192,7 @@ def test_ipc_transport_selection():
         _choose_transport("ipc", 2, torch.device("cpu"))
     assert _choose_transport("ipc", 1, torch.device("cuda", 0)) == "self"
     assert _choose_transport("ipc", 4, torch.device("cuda", 0)) == "ipc"
+    assert _choose_transport("ipc", 4, torch.device("cuda", 0), 4) == "ipc"
+    # ranks on several nodes: IPC cannot reach them
+    with pytest.raises(ValueError, match="ONE node"):
+        _choose_transport("ipc", 8, torch.device("cuda", 0), 4)

@@ -635,3 +635,46 @@ def test_ipc_update_halo_device_fields(tmp_path, case):
               staggers, nf, env={"RMA_TRANSPORT": "ipc", "RMA_IPC_MAILBOX_MB": "1"})
     for r in range(world):
         assert open(tmp_path / f"ok{r}.txt").read() == "1 ipc"
+
+
+def _ipc_probe(*args, env=None, timeout=300):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from helpers import ROOT, free_port
+
+    e = dict(os.environ, MASTER_PORT=str(free_port()), **(env or {}))
+    r = subprocess.run([sys.executable, "-m", "rocm_mpi_amd.launch", "-n", "4", "--",
+                        os.path.join(ROOT, "bench", "ipc_transport_probe.py"), *args],
+                       capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("mode", ["stream", "host"])
+def test_ipc_modes_2000_exchanged_steps_bitwise(mode):
+    """2000 one-step perf_hide steps of a 2x2 process grid
+    (an exchange every step) over IPC == the golden model bitwise; the stream
+    mode (the default) waits on the host zero times inside group_end, the host
+    mode twice per peer and group."""
+    d = _ipc_probe("--transport", "ipc", "--n", "258", "--K", "1", "--steps", "2000", "--check",
+                   env={"RMA_IPC_MODE": mode})
+    assert d["bitwise_golden"] is True and d["transport"] == "ipc" and d["ipc_mode"] == mode
+    if mode == "stream":
+        assert d["host_waits_in_group_end"] == 0
+    else:
+        assert d["host_waits_in_group_end"] > 2000
+
+
+def test_ipc_stream_mode_graph_replay_matches_golden():
+    """The executor's hipGraph replay with the IPC exchange captured in it
+    (stream mode: only stream wait/write-value operations and copies, no host
+    handshake) == the golden model bitwise, like the eager run above."""
+    d = _ipc_probe("--transport", "ipc", "--n", "258", "--K", "1", "--steps", "400", "--check",
+                   "--graph", env={"RMA_IPC_MODE": "stream"})
+    assert d["graph"] is True and d["bitwise_golden"] is True
+    assert d["host_waits_in_group_end"] == 0
