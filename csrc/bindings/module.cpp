@@ -328,6 +328,7 @@ PYBIND11_MODULE(_C, m) {
       .def("export_for", [](const IpcTransport& t, int p) { return py::bytes(t.export_for(p)); })
       .def("connect", [](IpcTransport& t, int p, py::bytes blob) { t.connect(p, blob); })
       .def("unlink_shm", &IpcTransport::unlink_shm)
+      .def("abort_waits", &IpcTransport::abort_waits)
       .def_property_readonly("connected", &IpcTransport::connected)
       .def_property_readonly("mailbox_bytes", &IpcTransport::mailbox_bytes)
       .def_property_readonly("mode",

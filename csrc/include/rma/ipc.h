@@ -67,6 +67,11 @@ class IpcTransport : public P2PTransport {
   // remove the name of my flag block (mappings stay valid): call once every
   // peer has connected
   void unlink_shm();
+  // stream mode, teardown after a peer died: satisfy every GPU-side wait of
+  // this rank from the host (its receives see "full", its sends "empty"), so
+  // its streams drain instead of waiting forever for a dead peer's flags. The
+  // data then received is garbage; the transport is poisoned.
+  void abort_waits();
 
   int rank() const override { return rank_; }
   int size() const override { return size_; }

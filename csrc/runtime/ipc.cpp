@@ -153,6 +153,18 @@ void IpcTransport::unlink_shm() {
   }
 }
 
+void IpcTransport::abort_waits() {
+  poisoned_ = true;
+  if (mode_ != Mode::kStream) return;
+  for (const Peer& P : peers_) {
+    if (P.rank < 0 || !P.connected) continue;
+    for (int k = 0; k < 2; ++k) {
+      flag(flags_, P.rank, kFull0 + k)->store(1, std::memory_order_release);
+      flag(P.r_flags, rank_, kFull0 + k)->store(0, std::memory_order_release);
+    }
+  }
+}
+
 bool IpcTransport::capturable() const {
   if (mode_ != Mode::kStream) return false;
   static const bool allow = [] {

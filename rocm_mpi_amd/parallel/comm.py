@@ -411,10 +411,25 @@ class IpcComm(TorchDistComm):
 
     def finalize(self) -> None:
         if self._c is not None:
+            import datetime
+
+            # every peer reached teardown (so every group it owes me is
+            # enqueued); a peer that died instead leaves my stream-mode waits
+            # unsatisfiable: release them from the host before draining
+            tmo = float(os.environ.get("RMA_TEARDOWN_TIMEOUT", "30"))
+            try:
+                work = dist.barrier(group=self._pg, async_op=True)
+                work.wait(timeout=datetime.timedelta(seconds=tmo))
+            except Exception:  # noqa: BLE001 - a dead peer must not hang teardown
+                self._c.abort_waits()
             if torch.cuda.is_available() and torch.cuda.is_initialized():
                 torch.cuda.synchronize(self.device)
             # every rank is done with every mailbox before any rank unmaps its own
-            dist.barrier(group=self._pg)
+            try:
+                work = dist.barrier(group=self._pg, async_op=True)
+                work.wait(timeout=datetime.timedelta(seconds=tmo))
+            except Exception:  # noqa: BLE001
+                pass
             self._c = None
 
 

@@ -206,6 +206,7 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" \
              "tests/test_multirank_gpu.py::test_ipc_ring_smoke_test" \
              "tests/test_multirank_gpu.py::test_ipc_mailbox_overflow_fails_on_every_rank" \
+             "tests/test_multirank_gpu.py::test_ipc_overflow_of_a_later_peer_keeps_the_transport_in_step" \
              "tests/test_multirank_gpu.py::test_ipc_update_halo_device_fields" \
              -p no:cacheprovider || exit 1 ;;
     tests_ipc5) step tests_ipc5 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
@@ -214,6 +215,7 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_ipc_transport_temporal_tiles" \
              "tests/test_multirank_gpu.py::test_ipc_ring_smoke_test" \
              "tests/test_multirank_gpu.py::test_ipc_mailbox_overflow_fails_on_every_rank" \
+             "tests/test_multirank_gpu.py::test_ipc_overflow_of_a_later_peer_keeps_the_transport_in_step" \
              "tests/test_multirank_gpu.py::test_ipc_update_halo_device_fields" \
              -p no:cacheprovider || exit 1 ;;
     tests_ipc5g) step tests_ipc5g 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread \

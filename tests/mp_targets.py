@@ -170,6 +170,39 @@ def ipc_overflow(rank, world, outdir):
         f.write(msg)
 
 
+def ipc_overflow_then_ring(rank, world, outdir):
+    """a group whose LATER peer overflows the mailbox must fail
+    before any copy or flag of an EARLIER peer happened, so the transport
+    stays in step: the next, valid ring exchange works on every rank."""
+    import torch
+
+    from rocm_mpi_amd.parallel import comm as C
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    gg.init_global_grid(130, 66, 1, dimx=world, periodx=1, quiet=True, device="cuda:0")
+    comm = gg.global_grid().comm
+    assert isinstance(comm, C.IpcComm)
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
+    small = torch.full((4,), float(rank), dtype=torch.float64, device="cuda:0")
+    big = torch.zeros(comm.native.mailbox_bytes // 8 + 1, dtype=torch.float64, device="cuda:0")
+    rs, rb = torch.zeros_like(small), torch.zeros_like(big)
+    msg = ""
+    try:  # small to the next rank first, then too many bytes to the previous one
+        comm.exchange([C.P2P("send", small, nxt), C.P2P("send", big, prv),
+                       C.P2P("recv", rs, prv), C.P2P("recv", rb, nxt)])
+    except RuntimeError as e:
+        msg = str(e)
+    assert "RMA_IPC_MAILBOX_MB" in msg and not comm.native.poisoned, msg
+    for it in range(3):
+        recv = torch.full((4,), -1.0, dtype=torch.float64, device="cuda:0")
+        comm.sendrecv(small + it, nxt, recv, prv)
+        torch.cuda.synchronize()
+        assert recv.tolist() == [float(prv + it)] * 4, (it, recv.tolist())
+    gg.finalize_global_grid()
+    with open(os.path.join(outdir, f"ok{rank}.txt"), "w") as f:
+        f.write("1")
+
+
 def halo_device(rank, world, outdir, nxyz, dims, periods, overlaps, staggers, nfields):
     """update_halo_ of device fields (the native engine over RMA_TRANSPORT's
     transport, every process on cuda:0) against the global truth."""

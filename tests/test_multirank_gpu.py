@@ -621,6 +621,16 @@ def test_ipc_mailbox_overflow_fails_on_every_rank(tmp_path):
         assert "RMA_IPC_MAILBOX_MB" in open(tmp_path / f"err{r}.txt").read()
 
 
+@pytest.mark.parametrize("mode", ["stream", "host"])
+def test_ipc_overflow_of_a_later_peer_keeps_the_transport_in_step(tmp_path, mode):
+    """the mailbox check covers every peer of a group before any
+    copy or flag; after the error the next exchanges are correct."""
+    run_procs(3, "mp_targets:ipc_overflow_then_ring", str(tmp_path),
+              env={"RMA_TRANSPORT": "ipc", "RMA_IPC_MAILBOX_MB": "0.001", "RMA_IPC_MODE": mode})
+    for r in range(3):
+        assert open(tmp_path / f"ok{r}.txt").read() == "1"
+
+
 @pytest.mark.parametrize("case", [
     ((9, 7, 1), (2, 2, 1), (0, 0, 0), (2, 2, 2), [(0, 0, 0), (1, 0, 0), (0, 1, 0), (-1, 0, 0)], 4),
     ((12, 10, 1), (2, 2, 1), (1, 1, 0), (4, 4, 2), [(0, 0, 0)], 2),
