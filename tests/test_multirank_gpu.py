@@ -660,7 +660,9 @@ def _ipc_probe(*args, env=None, timeout=300):
                         os.path.join(ROOT, "bench", "ipc_transport_probe.py"), *args],
                        capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    # the launcher prefixes every line with the rank ("[0] {...}")
+    lines = [ln.split("] ", 1)[1] for ln in r.stdout.splitlines()
+             if ln.startswith("[0] {")]
     assert len(lines) == 1, r.stdout[-2000:]
     return json.loads(lines[0])
 
