@@ -37,7 +37,10 @@ def main(argv=None) -> int:
     ap.add_argument("--variant", default="perf_hide")
     ap.add_argument("--dims", default="0,0")
     ap.add_argument("--check", action="store_true", help="canonical arithmetic, golden compare")
-    ap.add_argument("--graph", action="store_true", help="hipGraph replay (stream-mode IPC)")
+    ap.add_argument("--graph", action="store_true",
+                    help="hipGraph replay (stream-mode IPC, sets RMA_IPC_GRAPH=1: experimental)")
+    ap.add_argument("--graph-request", action="store_true",
+                    help="ask for graph replay without RMA_IPC_GRAPH (the executor falls back)")
     a = ap.parse_args(argv)
     os.environ["RMA_TRANSPORT"] = a.transport
     if a.graph:
@@ -53,7 +56,7 @@ def main(argv=None) -> int:
     m = Diffusion2D(DiffusionConfig(variant=a.variant, nx=a.n, ny=a.n, nt=a.steps, dims=dims,
                                     quiet=True, init="gaussian", init_on="host", temporal=a.K,
                                     fast_math=a.K > 1 and not a.check, device="cuda:0",
-                                    use_graph=a.graph))
+                                    use_graph=a.graph or a.graph_request))
     g = gg.global_grid()
     nat = getattr(g.comm, "native", None)
     m.step(2 * a.K)

@@ -17,8 +17,10 @@
 //     GPU), copies, and writes "full" (hipStreamWriteValue64) behind its
 //     copies; the receiver's stream waits for "full", copies the slot out and
 //     writes "empty". group_end() only enqueues. The protocol carries no
-//     generation number, so a captured group replays correctly as long as
-//     both sides replay the same sequence of groups.
+//     generation number, so in principle a captured group could replay; on
+//     the HIP runtime torch bundles, a captured exchange replayed to a wrong
+//     field (profiles/r5/ipc_graph_replay_failure.log), so capture is
+//     opt-in (RMA_IPC_GRAPH=1, experimental) and off by default.
 //   * host: the round-4 validation mode. Per pair a generation counter; the
 //     sender waits (host, bounded) until the receiver published "done with
 //     g-2", copies into slot g%2, waits for its own copies (a local event),
@@ -79,8 +81,8 @@ class IpcTransport : public P2PTransport {
   void group_end() override;
   void send(const void* buf, size_t bytes, int peer, stream_t stream) override;
   void recv(void* buf, size_t bytes, int peer, stream_t stream) override;
-  // stream mode only enqueues stream operations; whether HIP can capture
-  // them is probed by the tests (RMA_IPC_GRAPH=1 allows capture)
+  // false unless RMA_IPC_GRAPH=1 in stream mode (experimental: replays were
+  // wrong on the measured runtime)
   bool capturable() const override;
   size_t mailbox_bytes() const { return cap_; }
   Mode mode() const { return mode_; }
