@@ -639,15 +639,18 @@ def load_n1(key: str):
 
 
 def attribution(t_it: float, solo: float | None, solo_iso: float | None,
-                fast_iso: float | None, n1_ms: float | None) -> dict:
+                fast_iso: float | None, n1_ms: float | None,
+                slow_iso: float | None = None) -> dict:
     """Job-level split of the weak-scaling efficiency (times in s, max over
     ranks unless named otherwise):
       e_halo = solo / t_it        exchange + frame cost, same coefficients
       e_coef = solo_iso / solo    fast-math pass energy at this grid's dx != dy
                                   against dx = dy
-      e_gpu  = fast_iso / solo_iso  the slowest GPU against the fastest GPU of
-                                  THIS job (isotropic, no exchange): in-run
-      e_product = e_halo * e_coef * e_gpu = fast_iso / t_it  (in-run E(N))
+      e_gpu  = fast_iso / slow_iso  the slowest GPU against the fastest GPU of
+                                  THIS job (each rank's own isotropic solo
+                                  time, no exchange): in-run, 1 for one GPU
+      e_product = e_halo * e_coef * e_gpu ~ fast_iso / t_it  (in-run E(N);
+                                  exact up to the barrier time in solo_iso)
       e_box  = t(N=1) / fast_iso  this job's fastest GPU against the N = 1
                                   record of the same sweep (null without it)
       e_product_vs_n1 = e_box * e_product = t(N=1) / t_it = E(N)."""
@@ -660,8 +663,8 @@ def attribution(t_it: float, solo: float | None, solo_iso: float | None,
     if solo and solo_iso:
         out["e_coef"] = solo_iso / solo
         out["weak_scaling_eff_same_run_iso"] = solo_iso / t_it
-    if solo_iso and fast_iso:
-        out["e_gpu"] = fast_iso / solo_iso
+    if fast_iso and (slow_iso or solo_iso):
+        out["e_gpu"] = fast_iso / (slow_iso or solo_iso)
     if all(out[k] is not None for k in ("e_halo", "e_coef", "e_gpu")):
         out["e_product"] = out["e_halo"] * out["e_coef"] * out["e_gpu"]
     if fast_iso and n1_ms:
@@ -1056,13 +1059,15 @@ def run(a, world: int, rank: int) -> int:
         n1_ms = n1["ms_per_step"] if n1 else None
         isos = [d["solo_iso_ms_per_step"] for d in ranks_detail if d["solo_iso_ms_per_step"]]
         fast_iso_ms = min(isos) if len(isos) == world else None
+        slow_iso_ms = max(isos) if len(isos) == world else None
         for d in ranks_detail:
             if d["solo_iso_ms_per_step"] and fast_iso_ms:
                 d["e_gpu"] = round(fast_iso_ms / d["solo_iso_ms_per_step"], 6)
             if d["solo_iso_ms_per_step"] and n1_ms:
                 d["e_gpu_vs_n1"] = round(n1_ms / d["solo_iso_ms_per_step"], 6)
         attrib = attribution(t_it, solo, solo_iso,
-                             fast_iso_ms / 1e3 if fast_iso_ms else None, n1_ms)
+                             fast_iso_ms / 1e3 if fast_iso_ms else None, n1_ms,
+                             slow_iso_ms / 1e3 if slow_iso_ms else None)
         out.update({"value": round(total, 2), "value_kind": "aggregate",
                     "teff_per_gpu": round(teff_gpu, 2), "ms_per_step": round(t_it * 1e3, 6)})
         out["config"].update({
@@ -1087,10 +1092,10 @@ def run(a, world: int, rank: int) -> int:
             "solo_iso_ms_per_step": round(solo_iso * 1e3, 6) if solo_iso else None,
             "weak_scaling_eff_same_run": round(eff_same, 4) if eff_same else None,
             "e_attribution": dict(attrib, note=(
-                "in-run E = fastest_solo_iso/t_it = e_gpu * e_coef * e_halo (e_product); "
+                "in-run E ~ fastest_solo_iso/t_it = e_gpu * e_coef * e_halo (e_product); "
                 "e_halo = solo/t_it (exchange and frame cost), e_coef = solo_iso/solo "
                 "(fast-math pass energy at dx != dy vs dx = dy), e_gpu = fastest/slowest "
-                "isotropic solo time of this job's GPUs (no exchange); e_box = t(N=1)/"
+                "own isotropic solo time of this job's GPUs (no exchange); e_box = t(N=1)/"
                 "fastest_solo_iso against the N = 1 record of the same sweep, node and build "
                 "(null without it), e_product_vs_n1 = t(N=1)/t_it; value is the aggregate "
                 "N x teff_per_gpu")),
