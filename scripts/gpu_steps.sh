@@ -209,6 +209,20 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_ipc_overflow_of_a_later_peer_keeps_the_transport_in_step" \
              "tests/test_multirank_gpu.py::test_ipc_update_halo_device_fields" \
              -p no:cacheprovider || exit 1 ;;
+    ipc_modes) for mode in stream host; do
+               for cfg in "258 1 2000" "1026 1 400" "2048 1 400" "4096 24 480"; do
+                 set -- $cfg; tag="ipc_${mode}_$1_$2"
+                 RMA_IPC_MODE=$mode step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
+                   bench/ipc_transport_probe.py --transport ipc --n $1 --K $2 --steps $3 || exit 1
+               done
+             done
+             for cfg in "258 1 2000" "2048 1 400" "4096 24 480"; do
+               set -- $cfg; tag="staged_$1_$2"
+               step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
+                 bench/ipc_transport_probe.py --transport staged --n $1 --K $2 --steps $3 || exit 1
+             done ;;
+    fuzz_soak) step fuzz_soak 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+             tests/test_fuzz_gpu.py -p no:cacheprovider || exit 1 ;;
     tests_ipc5) step tests_ipc5 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
              "tests/test_multirank_gpu.py::test_ipc_modes_2000_exchanged_steps_bitwise" \
              "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
