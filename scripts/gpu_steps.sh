@@ -221,6 +221,13 @@ for s in "$@"; do
                step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
                  bench/ipc_transport_probe.py --transport staged --n $1 --K $2 --steps $3 || exit 1
              done ;;
+    ipc_cpwait) for cw in 1 0; do
+               for cfg in "258 1 2000" "4096 24 480"; do
+                 set -- $cfg; tag="ipc_stream_cpwait${cw}_$1_$2"
+                 GPU_STREAMOPS_CP_WAIT=$cw RMA_IPC_MODE=stream step "$tag" 200 python -m rocm_mpi_amd.launch \
+                   -n 4 -- bench/ipc_transport_probe.py --transport ipc --n $1 --K $2 --steps $3 --check || exit 1
+               done
+             done ;;
     fuzz_soak) step fuzz_soak 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
              tests/test_fuzz_gpu.py -p no:cacheprovider || exit 1 ;;
     tests_ipc5) step tests_ipc5 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
