@@ -133,9 +133,10 @@ def parse(argv=None):
                     help="functional test of the multi-process path on ONE GPU: ranks share "
                          "the card over the host-staged transport; the record says so and is "
                          "never a scaling point")
-    ap.add_argument("--shared-gpu-transport", default="staged", choices=["staged", "ipc"],
-                    help="halo transport of --shared-gpu-test: host-staged gloo, or HIP IPC "
-                         "device-to-device copies between the processes")
+    ap.add_argument("--shared-gpu-transport", default="staged", choices=["staged", "ipc", "rccl"],
+                    help="halo transport of --shared-gpu-test: host-staged gloo, HIP IPC "
+                         "device-to-device copies between the processes, or RCCL with one "
+                         "fake host per rank (RMA_RCCL_SHARED_GPU: its socket transport)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the same driver on the C++ CPU twins over gloo (tests of the "
@@ -312,9 +313,13 @@ def record_rc(rank: int, rc: int) -> None:
     """RMA_BENCH_RC_DIR: every rank writes its exit status (tests)."""
     d = os.environ.get("RMA_BENCH_RC_DIR")
     if d:  # atomically: torchrun may end this rank right after (a half-written file)
-        tmp = os.path.join(d, f".rc{rank}.tmp")
+        # one temp file per thread: the check-phase watchdog thread and the main
+        # thread can both be exiting the rank at once; with one shared temp
+        # name one thread renamed the other's still-empty file into place
+        tmp = os.path.join(d, f".rc{rank}.{threading.get_ident()}.tmp")
         with open(tmp, "w") as f:
             f.write(str(rc))
+            f.flush()
         os.replace(tmp, os.path.join(d, f"rc{rank}"))
 
 
@@ -767,6 +772,8 @@ def run(a, world: int, rank: int) -> int:
     shared = a.shared_gpu_test and gpu and world > 1
     if shared:
         os.environ["RMA_TRANSPORT"] = a.shared_gpu_transport
+        if a.shared_gpu_transport == "rccl":  # RCCL's socket transport between the ranks
+            os.environ["RMA_RCCL_SHARED_GPU"] = "1"
     elif gpu and world > 1:
         # a scaling point must never silently run on the host-staged transport
         os.environ["RMA_RCCL_STRICT"] = "1"

@@ -215,6 +215,24 @@ def shutdown_distributed(barrier: bool = True, timeout_s: float | None = None) -
 _rccl_generation = 0
 
 
+def shared_gpu_rccl(rank: int, size: int) -> bool:
+    """RMA_RCCL_SHARED_GPU=1: let RCCL ranks of ONE node share a GPU, for
+    functional tests of the real multi-process RCCL path on a 1-GPU machine.
+
+    RCCL refuses two ranks on one device ("Duplicate GPU detected") only when
+    they report the same host; a per-rank NCCL_HOSTID makes each rank its own
+    "host", so RCCL connects them with its network transport (sockets over
+    NCCL_SOCKET_IFNAME, lo here) instead of xGMI P2P. Same communicator
+    bootstrap, groups, send/recv matching and stream semantics as between
+    GPUs; the wire is host memory. Never a performance path. Must run before
+    the process's first RCCL call (RCCL reads the host id at init)."""
+    if os.environ.get("RMA_RCCL_SHARED_GPU", "0") != "1" or size <= 1:
+        return False
+    os.environ.setdefault("NCCL_HOSTID", f"rma-shared-gpu-rank-{rank}")
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    return True
+
+
 class RcclComm(Communicator):
     """GPU-direct RCCL communicator (native), bootstrapped through the store.
 
@@ -241,6 +259,7 @@ class RcclComm(Communicator):
         self.size = (1 if standalone else dist.get_world_size()) if size is None else size
         self.device = torch.device(device)
         self.timeout_s = timeout_s
+        shared_gpu_rccl(self.rank, self.size)  # before this process's first RCCL call
         if self.size == 1 and store is None:
             uid = n.RcclComm.unique_id()  # single rank: nothing to distribute
         else:

@@ -230,6 +230,12 @@ for s in "$@"; do
              done ;;
     fuzz_soak) step fuzz_soak 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
              tests/test_fuzz_gpu.py -p no:cacheprovider || exit 1 ;;
+    tests_rccl_mp) step tests_rccl_mp 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+             "tests/test_multirank_gpu.py::test_rccl_ring_smoke_test_between_processes" \
+             "tests/test_multirank_gpu.py::test_rccl_between_processes_sharing_the_gpu" \
+             "tests/test_multirank_gpu.py::test_rccl_between_processes_temporal_tiles" \
+             "tests/test_bench_gpu.py::test_bench_two_processes_sharing_the_gpu" \
+             -p no:cacheprovider || exit 1 ;;
     tests_ipc5) step tests_ipc5 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
              "tests/test_multirank_gpu.py::test_ipc_modes_2000_exchanged_steps_bitwise" \
              "tests/test_multirank_gpu.py::test_ipc_transport_processes" \

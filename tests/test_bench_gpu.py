@@ -82,7 +82,7 @@ def test_bench_default_check_on_one_gpu():
     assert c["drift_check"]["steps"] == 52 and c["fast_math_drift_max"] <= 1e-14
 
 
-@pytest.mark.parametrize("transport", ["staged", "ipc"])
+@pytest.mark.parametrize("transport", ["staged", "ipc", "rccl"])
 def test_bench_two_processes_sharing_the_gpu(tmp_path, transport):
     """The multi-process bench flow on one GPU (torchrun-style ranks, staged or
     HIP-IPC halo transport, per-rank timings, solo re-time, in-run halo check):

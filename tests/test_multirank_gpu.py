@@ -692,3 +692,53 @@ def test_ipc_graph_replay_is_refused_by_default():
                    "--graph-request", env={"RMA_IPC_MODE": "stream"})
     assert d["graph"] is False and d["bitwise_golden"] is True
     assert d["host_waits_in_group_end"] == 0
+
+
+RCCL_SHARED = {"RMA_TRANSPORT": "rccl", "RMA_RCCL_SHARED_GPU": "1"}
+
+
+@pytest.mark.parametrize("variant,world,dims", [("perf_hide", 2, (2, 1)), ("perf", 4, (2, 2)),
+                                                ("kp", 2, (1, 2)), ("perf_hide", 4, (4, 1))])
+def test_rccl_between_processes_sharing_the_gpu(tmp_path, variant, world, dims):
+    """The production RCCL halo path between SEPARATE processes (multi-rank
+    communicator from the store's unique id, grouped send/recv between distinct
+    ranks, merged x+y groups with diagonal corners on 2x2): every process on
+    cuda:0, RCCL told that each rank is its own host (RMA_RCCL_SHARED_GPU ->
+    NCCL_HOSTID), so it moves the halos over its socket transport instead of
+    refusing the duplicate GPU. Gathered field == the golden model, bitwise."""
+    run_procs(world, "mp_targets:diffusion_gpu", str(tmp_path), variant, 130, 66, 25, dims,
+              env=RCCL_SHARED)
+    Tv = np.load(tmp_path / "Tv.npy")
+    nxg, nyg, transport = open(tmp_path / "meta.txt").read().split()[:3]
+    assert transport == "rccl"
+    assert np.array_equal(Tv, golden.run(int(nxg), int(nyg), 25)[1:-1, 1:-1])
+
+
+def test_rccl_between_processes_temporal_tiles(tmp_path):
+    """K-step passes (width-K halos, frame + RCCL exchange on the high-priority
+    stream, interior beside it) between 4 processes over multi-rank RCCL."""
+    from rocm_mpi_amd import ops
+
+    K, nx, ny = 8, 120, 90
+    nt = 3 * K + 1
+    run_procs(4, "mp_targets:diffusion_tiles", str(tmp_path), "perf_hide", nx, ny, nt, (2, 2), K,
+              "cuda:0", env=RCCL_SHARED)
+    metas = [open(tmp_path / f"meta{r}.txt").read().split() for r in range(4)]
+    nxg, nyg = int(metas[0][2]), int(metas[0][3])
+    assert metas[0][6] == "rccl"
+    T0 = torch.empty((nyg, nxg), dtype=torch.float64)
+    ops.init_random_(T0, ops.TileGeometry(0, 0, nxg, nyg, 1.0, 1.0), seed=1234)
+    G = golden.run(nxg, nyg, nt, T0=T0.numpy())
+    for r in range(4):
+        cx, cy, ol = int(metas[r][0]), int(metas[r][1]), int(metas[r][4])
+        T = np.load(tmp_path / f"tile{r}.npy")
+        gx0, gy0 = cx * (nx - ol), cy * (ny - ol)
+        assert np.array_equal(T, G[gy0:gy0 + ny, gx0:gx0 + nx])
+
+
+def test_rccl_ring_smoke_test_between_processes(tmp_path):
+    """The reference smoke test's device-buffer ring (rocmaware_test_selectdevice.jl)
+    over a 4-rank RCCL communicator of separate processes."""
+    run_procs(4, "mp_targets:ring_gpu", str(tmp_path), "rccl", env=RCCL_SHARED)
+    for r in range(4):
+        assert np.load(tmp_path / f"ring{r}.npy").tolist() == [float((r - 1) % 4)] * 4
