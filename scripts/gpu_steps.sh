@@ -235,6 +235,7 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_rccl_between_processes_sharing_the_gpu" \
              "tests/test_multirank_gpu.py::test_rccl_between_processes_temporal_tiles" \
              "tests/test_bench_gpu.py::test_bench_two_processes_sharing_the_gpu" \
+             "tests/test_bench_gpu.py::test_bench_rehearsal_of_the_scaling_run_over_rccl" \
              -p no:cacheprovider || exit 1 ;;
     tests_ipc5) step tests_ipc5 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
              "tests/test_multirank_gpu.py::test_ipc_modes_2000_exchanged_steps_bitwise" \

@@ -99,3 +99,26 @@ def test_bench_two_processes_sharing_the_gpu(tmp_path, transport):
     assert [r["rank"] for r in c["ranks_detail"]] == [0, 1]
     assert c["preflight"]["ring_ok"] and c["preflight"]["halo"]["transport"] == transport
     assert c["headline_window_check"]["bitwise"] is True
+
+
+@pytest.mark.parametrize("gpus,dims", [(4, (2, 2)), (8, (4, 2))])
+def test_bench_rehearsal_of_the_scaling_run_over_rccl(gpus, dims):
+    """The driver's N-GPU command shape (bench.py --gpus N: torchrun ranks,
+    preflight device ring, RCCL halo exchange, in-run halo / window / drift
+    checks, per-rank timings, E(N) attribution) with N real RCCL ranks on the
+    one GPU of this box (RMA_RCCL_SHARED_GPU: RCCL's socket transport instead
+    of xGMI). Functional, never a scaling point: the record says so."""
+    d = bench("--gpus", str(gpus), "--shared-gpu-test", "--shared-gpu-transport", "rccl",
+              "--nx", "2048", "--steps", "48", "--warmup", "4", "--single-step-steps", "0",
+              "--check-nx", "530", timeout=600)
+    c = d["config"]
+    assert c["shared_gpu_test"] is True and c["ranks"] == gpus and c["transport"] == "rccl"
+    assert c["global_grid"] == [dims[0] * (2048 - 48) + 48, dims[1] * (2048 - 48) + 48]
+    assert c["rccl_nranks"] == gpus and c["preflight"]["rccl_nranks"] == gpus
+    assert c["preflight"]["ring_ok"] and c["preflight"]["halo"]["tiles_mismatched"] == 0
+    assert c["rccl_halo_bitwise_ok"] is True and c["halo_check"]["transport"] == "rccl"
+    assert c["headline_window_check"]["bitwise"] is True
+    assert c["pass_timing"]["halo_ms"] > 0 and sum(c["passes_timed"]) == 48
+    ea = c["e_attribution"]
+    assert ea["e_gpu"] is not None and ea["e_product"] is not None
+    assert [r["rank"] for r in c["ranks_detail"]] == list(range(gpus))
