@@ -237,6 +237,10 @@ for s in "$@"; do
              "tests/test_bench_gpu.py::test_bench_two_processes_sharing_the_gpu" \
              "tests/test_bench_gpu.py::test_bench_rehearsal_of_the_scaling_run_over_rccl" \
              -p no:cacheprovider || exit 1 ;;
+    rehearse) for n in 2 4 8; do
+               step "rehearse$n" 400 python bench.py --gpus $n --shared-gpu-test --shared-gpu-transport rccl \
+                 --nx 4096 --steps 96 --warmup 4 --json-out "$OUT/rehearse$n.json" || exit 1
+             done ;;
     tests_ipc5) step tests_ipc5 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
              "tests/test_multirank_gpu.py::test_ipc_modes_2000_exchanged_steps_bitwise" \
              "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
