@@ -329,6 +329,7 @@ PYBIND11_MODULE(_C, m) {
       .def("connect", [](IpcTransport& t, int p, py::bytes blob) { t.connect(p, blob); })
       .def("unlink_shm", &IpcTransport::unlink_shm)
       .def("abort_waits", &IpcTransport::abort_waits)
+      .def("check_error", &IpcTransport::check_error)
       .def_property_readonly("connected", &IpcTransport::connected)
       .def_property_readonly("mailbox_bytes", &IpcTransport::mailbox_bytes)
       .def_property_readonly("mode",

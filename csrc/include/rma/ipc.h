@@ -12,15 +12,18 @@
 // shared-memory block, mapped by both. Two modes (RMA_IPC_MODE):
 //
 //   * stream (default): nothing waits on the host. Per mailbox slot a
-//     full/empty flag; the sender's stream waits for "empty"
-//     (hipStreamWaitValue64 on the flag, host-registered and mapped for the
-//     GPU), copies, and writes "full" (hipStreamWriteValue64) behind its
-//     copies; the receiver's stream waits for "full", copies the slot out and
-//     writes "empty". group_end() only enqueues. The protocol carries no
-//     generation number, so in principle a captured group could replay; on
-//     the HIP runtime torch bundles, a captured exchange replayed to a wrong
-//     field (profiles/r5/ipc_graph_replay_failure.log), so capture is
-//     opt-in (RMA_IPC_GRAPH=1, experimental) and off by default.
+//     full/empty flag; the sender's stream waits for "empty" (a one-wave
+//     kernel polling the flag, host-registered and mapped for the GPU,
+//     csrc/kernels/flags.hip), copies, and writes "full" (a one-wave kernel,
+//     system-scope release) behind its copies; the receiver's stream waits
+//     for "full", copies the slot out and writes "empty". group_end() only
+//     enqueues. The protocol carries no generation number and the waits are
+//     kernels, so a captured exchange replays like any other kernel node
+//     (HIP's own hipStreamWaitValue64 / WriteValue64 replayed to a wrong
+//     field once captured, profiles/r5/ipc_graph_replay_failure.log). A wait
+//     is bounded: after timeout_s it records which peer it waited for in an
+//     error word (pinned host memory) and exits; the next group or
+//     check_error() raises.
 //   * host: the round-4 validation mode. Per pair a generation counter; the
 //     sender waits (host, bounded) until the receiver published "done with
 //     g-2", copies into slot g%2, waits for its own copies (a local event),
@@ -81,9 +84,10 @@ class IpcTransport : public P2PTransport {
   void group_end() override;
   void send(const void* buf, size_t bytes, int peer, stream_t stream) override;
   void recv(void* buf, size_t bytes, int peer, stream_t stream) override;
-  // false unless RMA_IPC_GRAPH=1 in stream mode (experimental: replays were
-  // wrong on the measured runtime)
+  // stream mode: kernels and copies only (RMA_IPC_GRAPH=0 refuses capture)
   bool capturable() const override;
+  // raise if a stream-mode wait timed out (peer gone or protocol out of step)
+  void check_error();
   size_t mailbox_bytes() const { return cap_; }
   Mode mode() const { return mode_; }
   bool poisoned() const { return poisoned_; }
@@ -122,6 +126,8 @@ class IpcTransport : public P2PTransport {
   std::vector<Peer> peers_;
   void* flags_ = nullptr;      // my flag block: [sender][4] = {sent, done, full0, full1}
   void* flags_dev_ = nullptr;  // its device address (stream mode)
+  uint32_t* err_host_ = nullptr;  // stream mode: wait-timeout word (pinned, mapped)
+  uint32_t* err_dev_ = nullptr;
   size_t flags_bytes_ = 0;
   std::string shm_name_;
   bool shm_linked_ = false;

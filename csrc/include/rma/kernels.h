@@ -193,6 +193,16 @@ void stream_triad_gpu(double* c, const double* a, const double* b, double s, int
                       int blocks, stream_t stream);
 
 // ---------------------------------------------------------------------------
+// Stream-ordered flags in host-registered shared memory (flags.hip; the HIP
+// IPC transport's stream mode): wait until *flag == want (bounded: after
+// timeout_s the kernel stores `code` into *err and exits), or store value
+// with system-scope release. One 64-lane workgroup each; graph-capturable.
+// ---------------------------------------------------------------------------
+void flag_wait_gpu(const uint64_t* flag, uint64_t want, double timeout_s, uint32_t* err,
+                   uint32_t code, stream_t stream);
+void flag_write_gpu(uint64_t* flag, uint64_t value, stream_t stream);
+
+// ---------------------------------------------------------------------------
 // Reductions for verification / NaN guards. Result is written
 // to out (device memory, 1 double). workspace must hold reduce_workspace_doubles().
 // ---------------------------------------------------------------------------

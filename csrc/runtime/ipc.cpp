@@ -16,6 +16,7 @@
 #include <thread>
 
 #include "rma/hip_check.h"
+#include "rma/kernels.h"
 
 namespace rma {
 
@@ -67,10 +68,13 @@ IpcTransport::IpcTransport(int rank, int size, int device, const std::vector<int
   try {
     RMA_HIP_CHECK(hipSetDevice(device));
     if (mode_ == Mode::kStream) {
-      int ok = 0;
-      RMA_HIP_CHECK(hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, device));
-      RMA_CHECK_ARG(ok, "RMA_IPC_MODE=stream needs hipStreamWaitValue64 on device " << device
-                                                                             << " (use host)");
+      void* e = nullptr;
+      RMA_HIP_CHECK(hipHostMalloc(&e, sizeof(uint32_t), hipHostMallocMapped));
+      err_host_ = static_cast<uint32_t*>(e);
+      *err_host_ = 0;
+      void* d = nullptr;
+      RMA_HIP_CHECK(hipHostGetDevicePointer(&d, e, 0));
+      err_dev_ = static_cast<uint32_t*>(d);
     }
     shm_name_ = ipc_shm_name(token, rank);
     flags_bytes_ = page_round(sizeof(uint64_t) * kWords * (size_t)size);
@@ -142,9 +146,27 @@ void IpcTransport::release() noexcept {
     shm_unlink(shm_name_.c_str());
     shm_linked_ = false;
   }
+  if (err_host_) {
+    (void)hipHostFree(err_host_);
+    err_host_ = nullptr;
+    err_dev_ = nullptr;
+  }
 }
 
 IpcTransport::~IpcTransport() { release(); }
+
+void IpcTransport::check_error() {
+  if (!err_host_) return;
+  const uint32_t e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
+  if (e == 0) return;
+  poisoned_ = true;
+  const int p = (int)(e & 0xFFFF) - 1;
+  throw_error("IPC transport: a stream wait timed out", __FILE__, __LINE__,
+              "rank " + std::to_string(rank_) + " waited " + std::to_string(timeout_s_) +
+                  " s for rank " + std::to_string(p) + " (" +
+                  ((e >> 16) == 1 ? "empty mailbox slot" : "sent message") +
+                  "): peer gone or protocol out of step");
+}
 
 void IpcTransport::unlink_shm() {
   if (shm_linked_) {
@@ -169,7 +191,7 @@ bool IpcTransport::capturable() const {
   if (mode_ != Mode::kStream) return false;
   static const bool allow = [] {
     const char* e = std::getenv("RMA_IPC_GRAPH");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return allow;
 }
@@ -252,6 +274,7 @@ void IpcTransport::wait_flag(const void* addr, uint64_t want, int p, const char*
 
 void IpcTransport::group_start() {
   RMA_CHECK_ARG(!poisoned_, "IPC transport unusable after an earlier error in group_end");
+  check_error();
   if (depth_++ == 0) {
     sends_.clear();
     recvs_.clear();
@@ -329,8 +352,8 @@ void IpcTransport::enqueue_group() {
     const uint64_t g = ++P.send_gen;
     const int slot = (int)(g & 1);
     if (mode_ == Mode::kStream) {  // slot empty -> copies -> slot full, all on the GPU
-      RMA_HIP_CHECK(hipStreamWaitValue64(s, dflag(P.r_flags_dev, rank_, kFull0 + slot), 0,
-                                         hipStreamWaitValueEq, ~0ull));
+      flag_wait_gpu(dflag(P.r_flags_dev, rank_, kFull0 + slot), 0, timeout_s_, err_dev_,
+                    (1u << 16) | (uint32_t)(p + 1), s);
     } else if (g > 2) {  // slot g % 2 was last read by the peer's receive of g - 2
       wait_flag(flag(P.r_flags, rank_, kDone), g - 2, p, "receive done");
     }
@@ -342,7 +365,7 @@ void IpcTransport::enqueue_group() {
       off += o->bytes;
     }
     if (mode_ == Mode::kStream) {
-      RMA_HIP_CHECK(hipStreamWriteValue64(s, dflag(P.r_flags_dev, rank_, kFull0 + slot), 1, 0));
+      flag_write_gpu(dflag(P.r_flags_dev, rank_, kFull0 + slot), 1, s);
       continue;
     }
     RMA_HIP_CHECK(hipEventRecord(E(P.sent_local), s));
@@ -356,8 +379,8 @@ void IpcTransport::enqueue_group() {
     const uint64_t g = ++P.recv_gen;
     const int slot = (int)(g & 1);
     if (mode_ == Mode::kStream)
-      RMA_HIP_CHECK(hipStreamWaitValue64(s, dflag(flags_dev_, p, kFull0 + slot), 1,
-                                         hipStreamWaitValueEq, ~0ull));
+      flag_wait_gpu(dflag(flags_dev_, p, kFull0 + slot), 1, timeout_s_, err_dev_,
+                    (2u << 16) | (uint32_t)(p + 1), s);
     else
       wait_flag(flag(flags_, p, kSent), g, p, "send");
     const char* src = static_cast<const char*>(P.mailbox) + slot * cap_;
@@ -368,7 +391,7 @@ void IpcTransport::enqueue_group() {
       off += o->bytes;
     }
     if (mode_ == Mode::kStream) {
-      RMA_HIP_CHECK(hipStreamWriteValue64(s, dflag(flags_dev_, p, kFull0 + slot), 0, 0));
+      flag_write_gpu(dflag(flags_dev_, p, kFull0 + slot), 0, s);
       continue;
     }
     RMA_HIP_CHECK(hipEventRecord(E(P.done_local), s));

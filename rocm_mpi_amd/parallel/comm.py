@@ -443,6 +443,12 @@ class IpcComm(TorchDistComm):
                 self._c.abort_waits()
             if torch.cuda.is_available() and torch.cuda.is_initialized():
                 torch.cuda.synchronize(self.device)
+            timed_out = None
+            if not self._c.poisoned:
+                try:
+                    self._c.check_error()  # a stream-mode wait that gave up
+                except RuntimeError as e:
+                    timed_out = e
             # every rank is done with every mailbox before any rank unmaps its own
             try:
                 work = dist.barrier(group=self._pg, async_op=True)
@@ -450,6 +456,8 @@ class IpcComm(TorchDistComm):
             except Exception:  # noqa: BLE001
                 pass
             self._c = None
+            if timed_out is not None:
+                raise timed_out
 
 
 # ---------------------------------------------------------------------------

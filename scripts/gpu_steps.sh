@@ -251,7 +251,7 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_ipc_update_halo_device_fields" \
              -p no:cacheprovider || exit 1 ;;
     tests_ipc5g) step tests_ipc5g 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread \
-             "tests/test_multirank_gpu.py::test_ipc_graph_replay_is_refused_by_default" \
+             "tests/test_multirank_gpu.py::test_ipc_stream_mode_graph_replay_matches_golden" \
              -p no:cacheprovider || exit 1 ;;
     tests_ipc_ev) RMA_IPC_GPU_EVENTS=1 step tests_ipc_ev 400 python -u -m pytest -x -v --timeout 120 \
              --timeout-method thread "tests/test_multirank_gpu.py::test_ipc_transport_processes" \

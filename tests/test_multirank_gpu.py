@@ -682,15 +682,16 @@ def test_ipc_modes_2000_exchanged_steps_bitwise(mode):
         assert d["host_waits_in_group_end"] > 2000
 
 
-def test_ipc_graph_replay_is_refused_by_default():
-    """hipGraph replay over the IPC exchange is opt-in (RMA_IPC_GRAPH=1): on
-    this runtime the captured stream wait/write-value nodes replayed to a
-    wrong field (profiles/r5/ipc_graph_replay_failure.log: bitwise false, 13
-    ms per step), so by default the transport reports itself non-capturable
-    and the executor runs eagerly (no host waits either way)."""
-    d = _ipc_probe("--transport", "ipc", "--n", "258", "--K", "1", "--steps", "100", "--check",
-                   "--graph-request", env={"RMA_IPC_MODE": "stream"})
-    assert d["graph"] is False and d["bitwise_golden"] is True
+def test_ipc_stream_mode_graph_replay_matches_golden():
+    """the executor's hipGraph replay with the IPC exchange
+    captured in it (stream mode: copies plus the bounded flag kernels of
+    csrc/kernels/flags.hip, no host handshake) == the golden model bitwise,
+    like the eager run. (HIP's own hipStreamWaitValue64 / WriteValue64
+    replayed to a wrong field once captured:
+    profiles/r5/ipc_graph_replay_failure.log.)"""
+    d = _ipc_probe("--transport", "ipc", "--n", "258", "--K", "1", "--steps", "400", "--check",
+                   "--graph", env={"RMA_IPC_MODE": "stream"})
+    assert d["graph"] is True and d["bitwise_golden"] is True
     assert d["host_waits_in_group_end"] == 0
 
 
