@@ -221,6 +221,14 @@ for s in "$@"; do
                step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
                  bench/ipc_transport_probe.py --transport staged --n $1 --K $2 --steps $3 || exit 1
              done ;;
+    ipc_graph) for cfg in "258 1 2000" "2048 1 400" "4096 24 480"; do
+               set -- $cfg
+               for gr in "" "--graph"; do
+                 tag="ipcg_$1_$2${gr:+_graph}"
+                 RMA_IPC_MODE=stream step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
+                   bench/ipc_transport_probe.py --transport ipc --n $1 --K $2 --steps $3 --check $gr || exit 1
+               done
+             done ;;
     ipc_cpwait) for cw in 1 0; do
                for cfg in "258 1 2000" "4096 24 480"; do
                  set -- $cfg; tag="ipc_stream_cpwait${cw}_$1_$2"
