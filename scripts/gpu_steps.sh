@@ -221,11 +221,11 @@ for s in "$@"; do
                step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
                  bench/ipc_transport_probe.py --transport staged --n $1 --K $2 --steps $3 || exit 1
              done ;;
-    ipc_graph) for cfg in "258 1 2000" "2048 1 400" "4096 24 480"; do
+    ipc_graph) for cfg in "258 1 100" "2048 1 100" "4096 24 96"; do
                set -- $cfg
                for gr in "" "--graph"; do
                  tag="ipcg_$1_$2${gr:+_graph}"
-                 RMA_IPC_MODE=stream step "$tag" 200 python -m rocm_mpi_amd.launch -n 4 -- \
+                 RMA_IPC_MODE=stream step "$tag" 170 python -m rocm_mpi_amd.launch -n 4 -- \
                    bench/ipc_transport_probe.py --transport ipc --n $1 --K $2 --steps $3 --check $gr || exit 1
                done
              done ;;

@@ -689,7 +689,7 @@ def test_ipc_stream_mode_graph_replay_matches_golden():
     like the eager run. (HIP's own hipStreamWaitValue64 / WriteValue64
     replayed to a wrong field once captured:
     profiles/r5/ipc_graph_replay_failure.log.)"""
-    d = _ipc_probe("--transport", "ipc", "--n", "258", "--K", "1", "--steps", "400", "--check",
+    d = _ipc_probe("--transport", "ipc", "--n", "258", "--K", "1", "--steps", "100", "--check",
                    "--graph", env={"RMA_IPC_MODE": "stream"})
     assert d["graph"] is True and d["bitwise_golden"] is True
     assert d["host_waits_in_group_end"] == 0
