@@ -229,6 +229,12 @@ for s in "$@"; do
                    bench/ipc_transport_probe.py --transport ipc --n $1 --K $2 --steps $3 --check $gr || exit 1
                done
              done ;;
+    ipc_check24) for cfg in "ipc stream 4096 24 96" "ipc host 4096 24 96" "staged x 4096 24 96" \
+                            "ipc stream 4096 8 96" "ipc stream 1026 24 96" "ipc stream 4096 1 20"; do
+               set -- $cfg; tag="chk_$1_$2_$3_$4"
+               RMA_IPC_MODE=$2 step "$tag" 170 python -m rocm_mpi_amd.launch -n 4 -- \
+                 bench/ipc_transport_probe.py --transport $1 --n $3 --K $4 --steps $5 --check; true
+             done ;;
     ipc_cpwait) for cw in 1 0; do
                for cfg in "258 1 2000" "4096 24 480"; do
                  set -- $cfg; tag="ipc_stream_cpwait${cw}_$1_$2"
