@@ -229,8 +229,8 @@ for s in "$@"; do
                    bench/ipc_transport_probe.py --transport ipc --n $1 --K $2 --steps $3 --check $gr || exit 1
                done
              done ;;
-    ipc_check24) for cfg in "ipc stream 4096 24 96" "ipc host 4096 24 96" "staged x 4096 24 96" \
-                            "ipc stream 4096 8 96" "ipc stream 1026 24 96" "ipc stream 4096 1 20"; do
+    ipc_check24) for cfg in "ipc stream 1026 24 96" "ipc host 1026 24 96" "staged x 1026 24 96" \
+                            "ipc stream 1026 8 96" "ipc stream 258 1 200"; do
                set -- $cfg; tag="chk_$1_$2_$3_$4"
                RMA_IPC_MODE=$2 step "$tag" 170 python -m rocm_mpi_amd.launch -n 4 -- \
                  bench/ipc_transport_probe.py --transport $1 --n $3 --K $4 --steps $5 --check; true
