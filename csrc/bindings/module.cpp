@@ -268,6 +268,20 @@ PYBIND11_MODULE(_C, m) {
       copy2d_batch_cpu(c.data(), (int)c.size(), elem_bytes);
   });
   m.def("copy2d_batch_max", [] { return kCopy2dBatch; });
+  // the IPC transport's stream-ordered flag kernels (csrc/kernels/flags.hip)
+  m.def(
+      "flag_wait",
+      [](uintptr_t flag, uint64_t want, double timeout_s, uintptr_t err, uint32_t code,
+         uintptr_t stream) {
+        flag_wait_gpu(P<const uint64_t>(flag), want, timeout_s, P<uint32_t>(err), code, S(stream));
+      },
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "flag_write",
+      [](uintptr_t flag, uint64_t value, uintptr_t stream) {
+        flag_write_gpu(P<uint64_t>(flag), value, S(stream));
+      },
+      py::call_guard<py::gil_scoped_release>());
   m.def("reduce_workspace_doubles", &reduce_workspace_doubles);
   m.def("reduce_gpu", [](uintptr_t A, int64_t n, int op, uintptr_t out, uintptr_t ws,
                          uintptr_t stream) {

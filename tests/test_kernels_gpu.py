@@ -241,3 +241,29 @@ def test_stencil_int64_indexing():
     assert torch.equal(out[ny - 9:ny - 1].cpu(), ref[1:9])
     del T, iCp, out
     torch.cuda.empty_cache()
+
+
+def test_flag_kernels_write_wait_and_bounded_timeout():
+    """The IPC transport's flag kernels (csrc/kernels/flags.hip): a write is
+    seen by a later wait on the same stream; a wait whose value never comes
+    gives up after its timeout, records its code in the error word and lets
+    the stream drain (every wave exits: no hang); neighbours untouched."""
+    import time
+
+    from rocm_mpi_amd._native import native
+
+    n = native()
+    s = torch.cuda.current_stream().cuda_stream
+    guard = torch.full((3,), -7, dtype=torch.int64, device="cuda")  # [canary, flag, canary]
+    err = torch.zeros(3, dtype=torch.int32, device="cuda")
+    flag = guard.data_ptr() + 8
+    n.flag_write(flag, 5, s)
+    n.flag_wait(flag, 5, 5.0, err.data_ptr() + 4, 11, s)
+    torch.cuda.synchronize()
+    assert guard.tolist() == [-7, 5, -7] and err.tolist() == [0, 0, 0]
+    t0 = time.perf_counter()
+    n.flag_wait(flag, 6, 0.2, err.data_ptr() + 4, 12, s)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert err.tolist() == [0, 12, 0] and 0.15 < dt < 5.0, (err.tolist(), dt)
+    assert guard.tolist() == [-7, 5, -7]
