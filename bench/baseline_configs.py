@@ -10,7 +10,11 @@ record and computes the weak-scaling efficiency the reference never defines
 local tile, using a 1-GPU run of the same variant and tile as denominator.
 
 Configs needing more GPUs than ``--max-gpus`` are reported as skipped (the
-8-GPU numbers come from the driver's scaling run of ``bench.py``).
+8-GPU numbers come from the driver's scaling run of ``bench.py``), unless
+``--shared-gpu``: then the multi-rank presets run as FUNCTIONAL checks with all
+ranks on the one visible GPU, real RCCL between the processes
+(``RMA_RCCL_SHARED_GPU``: RCCL's socket transport instead of xGMI) and a
+``--shared-nx`` tile; their records say so and carry no efficiency.
 
     python bench/baseline_configs.py --out profiles/baseline_configs.json
     python bench/baseline_configs.py --only kp16k,perf_2x1 --nt 200
@@ -42,7 +46,8 @@ def gpu_count() -> int:
         return 0
 
 
-def run(preset: str, nprocs: int, nt: int | None, extra: list[str], timeout: float) -> dict:
+def run(preset: str, nprocs: int, nt: int | None, extra: list[str], timeout: float,
+        env: dict | None = None) -> dict:
     """Launch one preset (or its 1-rank reference run) and return the JSON record."""
     variant = PRESETS[preset]["variant"]
     args = ["--preset", preset, "--json", "--quiet", "--no-vis"]
@@ -53,7 +58,8 @@ def run(preset: str, nprocs: int, nt: int | None, extra: list[str], timeout: flo
     cmd = [sys.executable, "-m", "rocm_mpi_amd.launch", "-n", str(nprocs), "-m",
            f"rocm_mpi_amd.apps.diffusion_2D_{variant}", "--", *args, *extra]
     t0 = time.time()
-    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, **(env or {})))
     rec = {"preset": preset, "nprocs": nprocs, "cmd": " ".join(cmd), "rc": p.returncode,
            "wall_s": round(time.time() - t0, 2)}
     for line in p.stdout.splitlines():
@@ -73,6 +79,10 @@ def main(argv=None) -> int:
     ap.add_argument("--no-reference-runs", action="store_true",
                     help="skip the 1-GPU runs that give E(N)")
     ap.add_argument("--timeout", type=float, default=1800)
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="run the multi-rank presets on ONE GPU (functional, RCCL between "
+                         "processes over its socket transport)")
+    ap.add_argument("--shared-nx", type=int, default=2048, help="local tile of --shared-gpu runs")
     ap.add_argument("--out", default="")
     a, extra = ap.parse_known_args(argv)
     ngpu = gpu_count() if a.max_gpus is None else a.max_gpus
@@ -83,9 +93,22 @@ def main(argv=None) -> int:
     for name in names:
         need = NPROCS[name]
         on_gpu = PRESETS[name].get("device") != "cpu"
-        if on_gpu and need > ngpu:
+        shared = on_gpu and need > ngpu and a.shared_gpu and ngpu >= 1
+        if on_gpu and need > ngpu and not shared:
             report["configs"].append({"preset": name, "skipped": f"needs {need} GPUs, {ngpu} visible"})
             print(f"{name:16s} skipped (needs {need} GPUs)", flush=True)
+            continue
+        if shared:
+            rec = run(name, need, a.nt,
+                      extra + ["--no-auto-size", "--nx", str(a.shared_nx), "--ny", str(a.shared_nx)],
+                      a.timeout, env={"RMA_RCCL_SHARED_GPU": "1", "RMA_TRANSPORT": "rccl"})
+            rec["shared_gpu_functional"] = True
+            res = rec.get("result")
+            report["configs"].append(rec)
+            print(f"{name:16s} n={need} on ONE GPU (functional, RCCL sockets): "
+                  + (f"transport {res.get('transport')} local {res['nx']}x{res['ny']} global "
+                     f"{res['nxg']}x{res['nyg']}" if res else f"FAILED rc={rec['rc']}\n"
+                     f"{rec.get('error', '')}"), flush=True)
             continue
         rec = run(name, need, a.nt, extra, a.timeout)
         res = rec.get("result")

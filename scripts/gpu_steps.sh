@@ -251,6 +251,8 @@ for s in "$@"; do
              "tests/test_bench_gpu.py::test_bench_two_processes_sharing_the_gpu" \
              "tests/test_bench_gpu.py::test_bench_rehearsal_of_the_scaling_run_over_rccl" \
              -p no:cacheprovider || exit 1 ;;
+    presets_shared) step presets_shared 600 python bench/baseline_configs.py --shared-gpu --nt 120 \
+             --out "$OUT/baseline_configs_shared.json" || exit 1 ;;
     rehearse) for n in 2 4 8; do
                step "rehearse$n" 400 python bench.py --gpus $n --shared-gpu-test --shared-gpu-transport rccl \
                  --nx 4096 --steps 96 --warmup 4 --json-out "$OUT/rehearse$n.json" || exit 1
