@@ -251,6 +251,9 @@ for s in "$@"; do
              "tests/test_bench_gpu.py::test_bench_two_processes_sharing_the_gpu" \
              "tests/test_bench_gpu.py::test_bench_rehearsal_of_the_scaling_run_over_rccl" \
              -p no:cacheprovider || exit 1 ;;
+    fuzz_procs) step fuzz_procs 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+             "tests/test_fuzz_gpu.py::test_random_decompositions_between_processes" \
+             -p no:cacheprovider || exit 1 ;;
     presets_shared) step presets_shared 600 python bench/baseline_configs.py --shared-gpu --nt 120 \
              --out "$OUT/baseline_configs_shared.json" || exit 1 ;;
     rehearse) for n in 2 4 8; do

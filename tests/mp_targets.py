@@ -240,3 +240,29 @@ def halo_device(rank, world, outdir, nxyz, dims, periods, overlaps, staggers, nf
     gg.finalize_global_grid()
     with open(os.path.join(outdir, f"ok{rank}.txt"), "w") as fh:
         fh.write(f"{int(ok)} {transport}")
+
+
+def fuzz_tile(rank, world, outdir, seed):
+    """One random configuration of tests/fuzz_cases.py run by a real process
+    per rank (RMA_TRANSPORT decides the transport); saves the tile + coords."""
+    from fuzz_cases import case
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    c = case(seed)
+    K, dims, per = c["K"], c["dims"], c["periods"]
+    gg.init_global_grid(c["nx"], c["ny"], 1, dimx=dims[0], dimy=dims[1], periodx=per[0],
+                        periody=per[1], overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
+                        quiet=True, device="cuda:0")
+    g = gg.global_grid()
+    m = Diffusion2D(DiffusionConfig(variant=c["variant"], nx=c["nx"], ny=c["ny"], nt=c["nt"],
+                                    init="random", quiet=True, dims=(*dims, 0), temporal=K,
+                                    fast_math=c["fast"], b_width=c["bw"], device="cuda:0",
+                                    periods=(*per, 0)))
+    assert m.executor is not None
+    m.step(c["nt"])
+    np.save(os.path.join(outdir, f"tile{g.me}.npy"), m.field.cpu().numpy())
+    with open(os.path.join(outdir, f"meta{g.me}.txt"), "w") as f:
+        f.write(f"{g.coords[0]} {g.coords[1]} {g.nxyz_g[0]} {g.nxyz_g[1]} {g.transport}")
+    m.close()
+    gg.finalize_global_grid()

@@ -44,3 +44,38 @@ def test_random_rccl_self_send_matches_cpu(seed):
         m.close()
         gg.finalize_global_grid()
     assert outs[0].equal(outs[1]), (K, nx, ny, nt, variant, fast)
+
+
+# seeds whose process grid has 2..8 ranks (fuzz_cases.DIMS), a mix of K,
+# periodic dimensions and arithmetics
+_PROC_SEEDS = [s for s in range(64) if __import__("fuzz_cases").case(s)["dims"] != (1, 1)][:6]
+
+
+@pytest.mark.parametrize("seed", _PROC_SEEDS)
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+def test_random_decompositions_between_processes(tmp_path, seed, transport):
+    """The same random configurations with one PROCESS per rank on cuda:0:
+    multi-rank RCCL (RMA_RCCL_SHARED_GPU: its socket transport) and the HIP
+    IPC transport; every tile == the 1-rank CPU run's window, bitwise."""
+    import numpy as np
+
+    from fuzz_cases import case, spmd
+    from helpers import run_loopback, run_procs
+
+    c = case(seed)
+    P = c["dims"][0] * c["dims"][1]
+    env = {"RMA_TRANSPORT": transport}
+    if transport == "rccl":
+        env["RMA_RCCL_SHARED_GPU"] = "1"
+    run_procs(P, "mp_targets:fuzz_tile", str(tmp_path), seed, env=env, timeout=240)
+    metas = [open(tmp_path / f"meta{r}.txt").read().split() for r in range(P)]
+    assert all(m[4] == transport for m in metas)
+    nxg, nyg = int(metas[0][2]), int(metas[0][3])
+    K, ol = c["K"], 2 * c["K"]
+    one = dict(c, nx=nxg + ol * c["periods"][0], ny=nyg + ol * c["periods"][1], dims=(1, 1))
+    ref = run_loopback(1, spmd, one, "cpu", timeout=180)[0][1]
+    for r in range(P):
+        cx, cy = int(metas[r][0]), int(metas[r][1])
+        T = np.load(tmp_path / f"tile{r}.npy")
+        gx0, gy0 = cx * (c["nx"] - ol), cy * (c["ny"] - ol)
+        assert np.array_equal(T, ref[gy0:gy0 + c["ny"], gx0:gx0 + c["nx"]]), (c, (cx, cy))
