@@ -101,7 +101,7 @@ def main(argv=None):
                     "piper_u3", "piper_iso", "piper_diag_s0", "piper_w1", "piper_mask",
                     "piper_mask_ctl", "piper_nosb",
                     "piper_rot", "piper_diag_hb", "piper_u6s",
-                    "piper_sp", "piper_sp2"):
+                    "piper_sp", "piper_sp2", "piper_prio", "piper_prio_nr"):
             return N.pipe_chunk_rows(K, n, False) or N.default_chunk_k(max(K, 3), n)
         if kind == "pipec":
             return N.pipe_chunk_rows(K, n, True) or N.default_chunk_k(max(K, 3), n)

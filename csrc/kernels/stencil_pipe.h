@@ -154,12 +154,20 @@ constexpr int kArFast5RegU6S = 16;
 // moves. Same operations and rounding as piper (bitwise). kArFast5RegSP: one
 // sched_barrier per level; kArFast5RegSP2: none.
 constexpr int kArFast5RegSP = 17, kArFast5RegSP2 = 18;
+// lab: wave priority for the heaviest stage. Stage 0 (HBM stream, factor
+// formation, ~7 % more VALU and ~15x the SALU of a middle stage; ISA budget
+// profiles/r5/isa_budget.md) paces its block at every row barrier.
+// kArFast5RegPrio: the rotated stage map of kArFast5RegRot (odd blocks' stage
+// 0 on SIMD 2, so each SIMD hosts at most one stage-0 wave) plus s_setprio 2
+// on stage-0 waves, so the SIMD issues for them first; kArFast5RegPrioNR: the
+// priority without the rotation (both stage-0 waves share SIMD 0: control).
+constexpr int kArFast5RegPrio = 19, kArFast5RegPrioNR = 20;
 constexpr bool ar_reg(int Ar) {
   return Ar == kArFast5Reg || Ar == kArFast6Reg || Ar == kArFast7Reg || Ar == kArFast5RegU3 ||
          Ar == kArFast5RegIso || Ar == kArDiagS0 || Ar == kArFast5RegW1 || Ar == kArFast5RegMask ||
          Ar == kArFast5RegMaskCtl || Ar == kArFast5RegNoSB || Ar == kArFast5RegRot ||
          Ar == kArDiagHalfBarrier || Ar == kArFast5RegU6S || Ar == kArFast5RegSP ||
-         Ar == kArFast5RegSP2;
+         Ar == kArFast5RegSP2 || Ar == kArFast5RegPrio || Ar == kArFast5RegPrioNR;
 }
 constexpr bool ar_split(int Ar) { return Ar == kArFast6Reg || Ar == kArFast7Reg; }
 
@@ -312,11 +320,15 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   constexpr int kStep = G::kStep;  // output columns per strip (plan_strip_tasks, sw = WB)
   constexpr int NH = S > 1 ? S - 1 : 1;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int stage = Ar == kArFast5RegRot ? (wv + 2 * (int)(blockIdx.x & 1)) % S
+  const int stage = (Ar == kArFast5RegRot || Ar == kArFast5RegPrio)
+                        ? (wv + 2 * (int)(blockIdx.x & 1)) % S
                     : C > 1              ? wv % S
                                          : wv;  // waves c*S .. c*S+S-1: column c, one per SIMD
   const int col = C > 1 ? wv / S : 0;
   const int lane = threadIdx.x & (kWave - 1);
+  if constexpr (Ar == kArFast5RegPrio || Ar == kArFast5RegPrioNR) {
+    if (stage == 0) __builtin_amdgcn_s_setprio(2);  // wave-uniform
+  }
   const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   int ri = 0;
   while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;

@@ -41,7 +41,8 @@ bool pipe_has(int K, int S, int arith) {
     return S == 4 && (K == 20 || K == 24);
   if (arith == pipe::kArDiagHalfBarrier) return S == 4 && K == 20;
   if (arith == pipe::kArFast5RegU6S) return S == 4 && (K == 21 || K == 24);
-  if (arith == pipe::kArFast5RegSP || arith == pipe::kArFast5RegSP2)
+  if (arith == pipe::kArFast5RegSP || arith == pipe::kArFast5RegSP2 ||
+      arith == pipe::kArFast5RegPrio || arith == pipe::kArFast5RegPrioNR)
     return S == 4 && (K == 20 || K == 24);
   if (S == pipe_default_stages(K)) return true;
   // alternative stage splits instantiated for sweeps (csrc/lab/stencil_pipe_lab.hip)

@@ -67,6 +67,10 @@ bool dispatch_alt(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(24, 4, kArFast5RegSP)
   RMA_PIPE_CASE(20, 4, kArFast5RegSP2)
   RMA_PIPE_CASE(24, 4, kArFast5RegSP2)
+  RMA_PIPE_CASE(20, 4, kArFast5RegPrio)
+  RMA_PIPE_CASE(24, 4, kArFast5RegPrio)
+  RMA_PIPE_CASE(20, 4, kArFast5RegPrioNR)
+  RMA_PIPE_CASE(24, 4, kArFast5RegPrioNR)
   return false;
 }
 

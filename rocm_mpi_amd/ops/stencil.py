@@ -54,23 +54,26 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 # "piper_diag_hb" (24: a diagnosis, WRONG results: the row barrier every other row only),
 # "piper_u6s" (25: piper unrolled by 6 also at K = 21..24, spilling),
 # "piper_sp" / "piper_sp2" (26 / 27: levels software-pipelined, with / without a
-# sched_barrier per level; bitwise = piper).
+# sched_barrier per level; bitwise = piper), "piper_prio" (28: the rotated stage map
+# plus s_setprio for stage-0 waves) and its control "piper_prio_nr" (29: the
+# priority without the rotation); bitwise = piper.
 FAST5 = ("fast5", "fast5p2", "fast5p4", "fast5p8", "pipe", "pipeb", "piper", "piper_u3",
          "piper_iso", "piper_diag_s0", "piper_w1", "piper_mask", "piper_mask_ctl", "piper_nosb",
          "piper_rot", "piper_diag_hb", "piper_u6s",
-         "piper_sp", "piper_sp2")
+         "piper_sp", "piper_sp2", "piper_prio", "piper_prio_nr")
 FAST6 = ("piper6", "piper7")
 PIPE = ("pipe", "pipec", "pipeb", "piper", "pipe_diag1", "piper6", "piper7", "piper_u3",
         "piper_iso", "piper_diag_s0", "piper_w1", "piper_mask", "piper_mask_ctl", "piper_nosb",
          "piper_rot", "piper_diag_hb", "piper_u6s",
-         "piper_sp", "piper_sp2")
+         "piper_sp", "piper_sp2", "piper_prio", "piper_prio_nr")
 PIPE_MAX_K = 24
 KERNELS = {"march": 0, "lds": 1, "lds_dpp": 3, "pipe": 9, "pipec": 10, "piper": 12}
 LAB_KERNELS = {"dpp": 2, "fast": 4, "fast5": 5, "fast5p2": 6, "fast5p4": 7, "fast5p8": 8,
                "pipeb": 11, "pipe_diag1": 13, "piper6": 14, "piper7": 15,
                "piper_u3": 16, "piper_iso": 17, "piper_diag_s0": 18, "piper_w1": 19,
                "piper_mask": 20, "piper_mask_ctl": 21, "piper_nosb": 22, "piper_rot": 23,
-               "piper_diag_hb": 24, "piper_u6s": 25, "piper_sp": 26, "piper_sp2": 27}
+               "piper_diag_hb": 24, "piper_u6s": 25, "piper_sp": 26, "piper_sp2": 27,
+               "piper_prio": 28, "piper_prio_nr": 29}
 KSTEP_CORE = ("lds_dpp", "pipe", "pipec", "piper")
 
 

@@ -191,6 +191,10 @@ for s in "$@"; do
     rot_ab) step rot_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
              --pipec "" --ldsdpp "" --old "" --alt "" \
              --kinds piper:20,piper_rot:20,piper:24,piper_rot:24 --out "$OUT/rot_ab.json" || exit 1 ;;
+    prio_ab) step prio_ab 500 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
+             --pipec "" --ldsdpp "" --old "" --alt "" \
+             --kinds piper:20,piper_rot:20,piper_prio:20,piper_prio_nr:20,piper:24,piper_prio:24 \
+             --out "$OUT/prio_ab.json" || exit 1 ;;
     hb_ab) step hb_ab 400 python bench/pass_sweep.py --n 101120 --rounds 7 --pipe "" \
              --pipec "" --ldsdpp "" --old "" --alt "" \
              --kinds piper:20,piper_diag_hb:20 --out "$OUT/hb_ab.json" || exit 1 ;;

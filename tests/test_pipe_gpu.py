@@ -410,7 +410,8 @@ def test_piper_schedule_variants_bitwise(K):
     rects = [ops.interior_rect(nx, ny)]
     ref = cpu_ref(K, T, iCp, rects, "pipe")
     for chunk in (11, 64):
-        for kern in ("piper_nosb", "piper_rot", "piper_sp", "piper_sp2"):
+        for kern in ("piper_nosb", "piper_rot", "piper_sp", "piper_sp2", "piper_prio",
+                     "piper_prio_nr"):
             assert torch.equal(gpu_run(K, T, iCp, rects, kern, chunk=chunk), ref), kern
 
 
