@@ -81,7 +81,7 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
                 "pipelined K-step kernel: 1 <= K <= " << kPipeMaxK << ", got " << K);
   RMA_CHECK_ARG(pipe_has(K, S, arith), "no pipelined kernel instantiated for K=" << K << " S=" << S
                                                                              << " arithmetic " << arith);
-  RMA_CHECK_ARG(arith >= 0 && arith <= 18, "pipelined kernel arithmetic " << arith);
+  RMA_CHECK_ARG(arith >= 0 && arith <= 20, "pipelined kernel arithmetic " << arith);
   if (arith == pipe::kArFast5RegIso) {
     const double ax = (-c.mlam) * c.rdx * c.rdx, ay = (-c.mlam) * c.rdy * c.rdy;
     RMA_CHECK_ARG(ay / ax == 1.0, "the isotropic fast-math kernel needs ry = (dx/dy)^2 == 1");
