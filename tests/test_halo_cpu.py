@@ -196,3 +196,42 @@ def test_ipc_transport_selection():
     # ranks on several nodes: IPC cannot reach them
     with pytest.raises(ValueError, match="ONE node"):
         _choose_transport("ipc", 8, torch.device("cuda", 0), 4)
+
+
+def test_shared_gpu_rccl_gives_each_rank_its_own_host(monkeypatch):
+    """RMA_RCCL_SHARED_GPU=1: a per-rank NCCL_HOSTID (RCCL then refuses no
+    duplicate GPU and uses its socket transport), only with > 1 rank, never
+    overriding an explicit setting."""
+    import os
+
+    from rocm_mpi_amd.parallel import comm as C
+
+    for k in ("NCCL_HOSTID", "RMA_RCCL_SHARED_GPU"):
+        monkeypatch.delenv(k, raising=False)
+    assert not C.shared_gpu_rccl(1, 4) and "NCCL_HOSTID" not in os.environ
+    monkeypatch.setenv("RMA_RCCL_SHARED_GPU", "1")
+    assert not C.shared_gpu_rccl(0, 1) and "NCCL_HOSTID" not in os.environ
+    assert C.shared_gpu_rccl(3, 4) and os.environ["NCCL_HOSTID"] == "rma-shared-gpu-rank-3"
+    monkeypatch.setenv("NCCL_HOSTID", "mine")
+    assert C.shared_gpu_rccl(2, 4) and os.environ["NCCL_HOSTID"] == "mine"
+
+
+def test_bench_record_rc_is_atomic_across_threads(tmp_path, monkeypatch):
+    """bench.record_rc from two threads of one rank (the check watchdog and
+    the main thread exiting at once) never leaves an empty rc file."""
+    import os
+    import sys
+    import threading
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    monkeypatch.setenv("RMA_BENCH_RC_DIR", str(tmp_path))
+    for it in range(50):
+        ts = [threading.Thread(target=bench.record_rc, args=(1, 4 + (j % 3))) for j in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert int((tmp_path / "rc1").read_text()) in (4, 5, 6)
+    assert not [p for p in tmp_path.iterdir() if p.name.endswith(".tmp")]
