@@ -1,6 +1,8 @@
-// Host stand-in for the few HIP runtime calls of csrc/runtime/loopback.cpp and
-// csrc/runtime/halo.cpp, so both compile with g++ under ThreadSanitizer and
-// AddressSanitizer (tests/native/threaded_selftest.cpp).
+// Host stand-in for the few HIP runtime calls of csrc/runtime/loopback.cpp,
+// csrc/runtime/halo.cpp and csrc/runtime/ipc.cpp, so they compile with a host
+// compiler under ThreadSanitizer and AddressSanitizer
+// (tests/native/threaded_selftest.cpp). IPC "processes" are
+// threads of one process: a memory handle carries the pointer itself.
 //
 // Model: every stream operation runs synchronously on the calling thread
 // (a copy happens at enqueue time, after everything enqueued before it), so
@@ -9,13 +11,67 @@
 // heap-use-after-free for ASan, a race with the free for TSan, and a
 // "dead event" abort without any sanitizer. Allocation counters let the test
 // check that nothing leaks.
+//
+// Shared memory: rank threads that open the same POSIX shm object get ONE
+// mapping of it (refcounted), as processes would get one physical page.
+// ThreadSanitizer tracks synchronisation per virtual address, so a release
+// store through one alias and an acquire load through another would look
+// unsynchronised -- a false report about the stub, not about ipc.cpp.
 #pragma once
+
+#include <sys/mman.h>
+#include <sys/stat.h>
 
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
+
+namespace rma_stub {
+struct Mapping {
+  void* addr;
+  size_t len;
+  int refs;
+};
+inline std::mutex& map_mu() {
+  static std::mutex m;
+  return m;
+}
+inline std::map<std::pair<dev_t, ino_t>, Mapping>& mappings() {
+  static std::map<std::pair<dev_t, ino_t>, Mapping> m;
+  return m;
+}
+inline void* mmap_shared(void* a, size_t len, int prot, int flags, int fd, off_t off) {
+  struct stat st;
+  if (!(flags & MAP_SHARED) || fstat(fd, &st) != 0) return ::mmap(a, len, prot, flags, fd, off);
+  std::lock_guard<std::mutex> lk(map_mu());
+  const auto key = std::make_pair(st.st_dev, st.st_ino);
+  auto it = mappings().find(key);
+  if (it != mappings().end()) {
+    ++it->second.refs;
+    return it->second.addr;
+  }
+  void* m = ::mmap(a, len, prot, flags, fd, off);
+  if (m != MAP_FAILED) mappings()[key] = {m, len, 1};
+  return m;
+}
+inline int munmap_shared(void* a, size_t len) {
+  std::lock_guard<std::mutex> lk(map_mu());
+  for (auto it = mappings().begin(); it != mappings().end(); ++it)
+    if (it->second.addr == a) {
+      if (--it->second.refs > 0) return 0;
+      mappings().erase(it);
+      break;
+    }
+  return ::munmap(a, len);
+}
+}  // namespace rma_stub
+#define mmap rma_stub::mmap_shared
+#define munmap rma_stub::munmap_shared
 
 typedef enum hipError_t {
   hipSuccess = 0,
@@ -33,6 +89,13 @@ typedef enum hipMemcpyKind {
 
 #define hipEventDefault 0x0
 #define hipEventDisableTiming 0x2
+#define hipHostMallocMapped 0x2
+#define hipHostRegisterMapped 0x2
+#define hipIpcMemLazyEnablePeerAccess 0x1
+
+typedef struct hipIpcMemHandle_st {
+  char reserved[64];
+} hipIpcMemHandle_t;
 
 struct rma_stub_event {
   uint64_t magic;                  // kAlive until destroyed (plain: the free races with it)
@@ -66,6 +129,12 @@ inline const char* hipGetErrorName(hipError_t e) { return e == hipSuccess ? "hip
 inline const char* hipGetErrorString(hipError_t e) { return e == hipSuccess ? "no error" : "stub error"; }
 inline hipError_t hipGetLastError() { return hipSuccess; }
 inline hipError_t hipDeviceSynchronize() { return hipSuccess; }
+inline hipError_t hipSetDevice(int) { return hipSuccess; }
+inline hipError_t hipEventSynchronize(hipEvent_t e) {
+  if (!e) return hipErrorInvalidResourceHandle;
+  if (e->magic != rma_stub::kAlive) rma_stub::dead_event("hipEventSynchronize");
+  return hipSuccess;
+}
 
 inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
   if (!e) return hipErrorInvalidValue;
@@ -113,3 +182,21 @@ inline hipError_t hipFree(void* p) {
   }
   return hipSuccess;
 }
+inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) { return hipMalloc(p, n); }
+inline hipError_t hipHostFree(void* p) { return hipFree(p); }
+inline hipError_t hipHostRegister(void*, size_t, unsigned) { return hipSuccess; }
+inline hipError_t hipHostUnregister(void*) { return hipSuccess; }
+inline hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) {
+  *d = h;  // one address space
+  return hipSuccess;
+}
+inline hipError_t hipIpcGetMemHandle(hipIpcMemHandle_t* h, void* p) {
+  std::memset(h, 0, sizeof *h);
+  std::memcpy(h->reserved, &p, sizeof p);
+  return hipSuccess;
+}
+inline hipError_t hipIpcOpenMemHandle(void** p, hipIpcMemHandle_t h, unsigned) {
+  std::memcpy(p, h.reserved, sizeof *p);
+  return hipSuccess;
+}
+inline hipError_t hipIpcCloseMemHandle(void*) { return hipSuccess; }

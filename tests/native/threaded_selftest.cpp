@@ -20,6 +20,12 @@
 //      field after every exchange. Ranks then tear down in a random order.
 //   3. random_groups: P threads, random message patterns (several messages
 //      per pair, sizes, nesting), random teardown delays.
+//   4. ipc_ring: the HIP IPC transport (csrc/runtime/ipc.cpp) between P rank
+//      threads standing in for processes (shared-memory flag blocks, handle
+//      export / connect, shm unlink), in host and stream mode: ring groups of
+//      two messages per pair with random sizes, a mailbox overflow of a LATER
+//      peer that must leave the transport in step, and a stream-mode wait
+//      that times out and must surface through check_error().
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -34,7 +40,13 @@
 
 #include <hip/hip_runtime.h>  // the host stub (tests/native/hip_stub)
 
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <unistd.h>
+
 #include "rma/halo.h"
+#include "rma/ipc.h"
 #include "rma/kernels.h"
 #include "rma/loopback.h"
 #include "rma/topology.h"
@@ -44,6 +56,22 @@ namespace rma {
 // kernels become their CPU twins
 void copy2d_batch_gpu(const Copy2d* copies, int n, int elem_bytes, stream_t) {
   copy2d_batch_cpu(copies, n, elem_bytes);
+}
+// ... and the IPC flag kernels (csrc/kernels/flags.hip) a bounded host spin
+void flag_wait_gpu(const uint64_t* flag, uint64_t want, double timeout_s, uint32_t* err,
+                   uint32_t code, stream_t) {
+  auto* f = reinterpret_cast<const std::atomic<uint64_t>*>(flag);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (f->load(std::memory_order_acquire) != want) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+      __atomic_store_n(err, code, __ATOMIC_RELEASE);
+      return;
+    }
+    std::this_thread::yield();
+  }
+}
+void flag_write_gpu(uint64_t* flag, uint64_t value, stream_t) {
+  reinterpret_cast<std::atomic<uint64_t>*>(flag)->store(value, std::memory_order_release);
 }
 }  // namespace rma
 
@@ -278,6 +306,152 @@ int random_groups(int P, int rounds, unsigned seed) {
   return g_fail.load();
 }
 
+// ---------------------------------------------------------------------------
+class Barrier {  // C++17: no std::barrier
+ public:
+  explicit Barrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const int gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      ++gen_;
+      cv_.notify_all();
+      return;
+    }
+    cv_.wait(lk, [&] { return gen_ != gen; });
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int n_, count_ = 0, gen_ = 0;
+};
+
+int ipc_ring(int P, int mode, int groups, unsigned seed) {
+  const size_t cap = 4096;  // bytes of one mailbox slot
+  const std::string token = "tsel" + std::to_string(getpid()) + "m" + std::to_string(mode) + "p" +
+                            std::to_string(P);
+  Barrier bar(P);
+  std::mutex mu;
+  std::map<std::pair<int, int>, std::string> blobs;
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; ++r) {
+    th.push_back(guarded(
+        [&, r] {
+          const int nxt = (r + 1) % P, prv = (r + P - 1) % P;
+          IpcTransport t(r, P, 0, {nxt, prv}, cap, token, 30.0, mode);
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            for (int p : {nxt, prv})
+              if (p != r) blobs[{r, p}] = t.export_for(p);
+          }
+          bar.wait();
+          for (int p : {nxt, prv}) {
+            if (p == r) continue;
+            std::string b;
+            {
+              std::lock_guard<std::mutex> lk(mu);
+              b = blobs.at({p, r});
+            }
+            t.connect(p, b);
+          }
+          bar.wait();
+          t.unlink_shm();
+          std::mt19937 g(seed);  // every rank draws the same sizes
+          for (int k = 0; k < groups; ++k) {
+            const size_t n0 = 1 + g() % 200, n1 = 1 + g() % 200;  // doubles (2 msgs <= cap)
+            const bool overflow = k == groups / 2;
+            std::vector<double> s0(n0), s1(n1), r0(n0, -1), r1(n1, -1);
+            for (size_t i = 0; i < n0; ++i) s0[i] = 1e6 * k + 1e3 * r + (double)i;
+            for (size_t i = 0; i < n1; ++i) s1[i] = -(1e6 * k + 1e3 * r + (double)i);
+            if (overflow) {  // 8 B to the next rank, cap + 8 B to the previous one
+              std::vector<double> big(cap / 8 + 1, 0.0), rb(cap / 8 + 1);
+              bool threw = false;
+              try {
+                t.group_start();
+                t.send(s0.data(), 8, nxt, nullptr);
+                t.send(big.data(), big.size() * 8, prv, nullptr);
+                t.recv(r0.data(), 8, prv, nullptr);
+                t.recv(rb.data(), rb.size() * 8, nxt, nullptr);
+                t.group_end();
+              } catch (const Error&) {
+                threw = true;
+              }
+              CHECK(threw && !t.poisoned(), "rank %d: overflow must throw, unpoisoned", r);
+              continue;
+            }
+            t.group_start();
+            t.send(s0.data(), n0 * 8, nxt, nullptr);
+            t.send(s1.data(), n1 * 8, nxt, nullptr);
+            t.recv(r0.data(), n0 * 8, prv, nullptr);
+            t.recv(r1.data(), n1 * 8, prv, nullptr);
+            t.group_end();
+            for (size_t i = 0; i < n0; ++i)
+              if (r0[i] != 1e6 * k + 1e3 * prv + (double)i) {
+                CHECK(false, "ipc mode %d rank %d group %d msg 0 elem %zu", mode, r, k, i);
+                return;
+              }
+            for (size_t i = 0; i < n1; ++i)
+              if (r1[i] != -(1e6 * k + 1e3 * prv + (double)i)) {
+                CHECK(false, "ipc mode %d rank %d group %d msg 1 elem %zu", mode, r, k, i);
+                return;
+              }
+          }
+          CHECK(mode == 1 ? t.host_waits() == 0 : t.host_waits() > 0, "rank %d host waits %llu", r,
+                (unsigned long long)t.host_waits());
+          bar.wait();  // nobody unmaps while a peer still copies out of its mailbox
+        },
+        "ipc_ring", r));
+  }
+  for (auto& x : th) x.join();
+  return g_fail.load();
+}
+
+// stream mode: a receive whose sender never sends times out (bounded) and
+// surfaces at the next group / check_error
+int ipc_stream_timeout() {
+  const std::string token = "tselto" + std::to_string(getpid());
+  Barrier bar(2);
+  std::mutex mu;
+  std::map<std::pair<int, int>, std::string> blobs;
+  std::vector<std::thread> th;
+  for (int r = 0; r < 2; ++r) {
+    th.push_back(guarded(
+        [&, r] {
+          const int p = 1 - r;
+          IpcTransport t(r, 2, 0, {p}, 64, token, 0.05, 1);
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            blobs[{r, p}] = t.export_for(p);
+          }
+          bar.wait();
+          std::string b;
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            b = blobs.at({p, r});
+          }
+          t.connect(p, b);
+          bar.wait();
+          if (r == 1) {
+            double x = -1;
+            t.recv(&x, 8, 0, nullptr);  // rank 0 never sends: the wait gives up
+            bool threw = false;
+            try {
+              t.check_error();
+            } catch (const Error& e) {
+              threw = std::string(e.what()).find("timed out") != std::string::npos;
+            }
+            CHECK(threw && t.poisoned(), "stream wait timeout not reported");
+          }
+          bar.wait();
+        },
+        "ipc_stream_timeout", r));
+  }
+  for (auto& x : th) x.join();
+  return g_fail.load();
+}
+
 }  // namespace
 
 int main() {
@@ -302,6 +476,12 @@ int main() {
   for (int P : {2, 3, 5, 8})
     if (random_groups(P, 60, 100u + (unsigned)P)) return 1;
   std::printf("random_groups OK\n");
+  for (int mode : {0, 1})
+    for (int P : {2, 3, 5})
+      if (ipc_ring(P, mode, 40, 7u + (unsigned)P)) return 1;
+  std::printf("ipc_ring OK (host and stream mode, 2/3/5 ranks)\n");
+  if (ipc_stream_timeout()) return 1;
+  std::printf("ipc_stream_timeout OK\n");
   if (rma_stub::live_events() != 0 || rma_stub::live_allocs() != 0) {
     std::fprintf(stderr, "FAILED leak: %ld events, %ld allocations alive\n",
                  rma_stub::live_events().load(), rma_stub::live_allocs().load());

@@ -6,7 +6,10 @@ tests/native/threaded_selftest.cpp drives the real loopback transport
 2..8 rank threads against a host stand-in of the HIP runtime
 (tests/native/hip_stub): post / take / consume, plan-cache misses with pack
 buffer reallocation (per-dimension, cross and merged groups), and endpoint
-teardown while peers finish. Built with clang's ThreadSanitizer (its runtime
+teardown while peers finish; and the HIP IPC transport (csrc/runtime/ipc.cpp)
+between rank threads standing in for processes, in host and stream mode
+(shared-memory flags, mailbox overflow of a later peer, bounded wait
+timeout). Built with clang's ThreadSanitizer (its runtime
 intercepts pthread_cond_clockwait, which g++ 11's libtsan does not) and with
 AddressSanitizer + UBSan.
 
@@ -26,7 +29,7 @@ CLANG = "/opt/rocm/lib/llvm/bin/clang++"
 PRE_FIX = "5704426"
 SRCS = ["tests/native/threaded_selftest.cpp", "csrc/runtime/loopback.cpp", "csrc/runtime/halo.cpp",
         "csrc/runtime/halo_plan.cpp", "csrc/runtime/topology.cpp", "csrc/runtime/errors.cpp",
-        "csrc/kernels/cpu_kernels.cpp"]
+        "csrc/runtime/ipc.cpp", "csrc/kernels/cpu_kernels.cpp"]
 SAN = {"tsan": ["-fsanitize=thread"],
        "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]}
 ENV = {"tsan": {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"},
@@ -84,3 +87,21 @@ def test_pre_fix_loopback_teardown_race_is_reported(kind, tmp_path):
     assert r.returncode != 0
     assert "heap-use-after-free" in r.stderr, r.stderr[-3000:]
     assert "hipStreamWaitEvent" in r.stderr and "LoopbackEndpoint::~LoopbackEndpoint" in r.stderr
+
+
+@needs_clang
+def test_ipc_slot_reuse_without_the_done_wait_is_reported(tmp_path):
+    """Mutation check of the IPC half: with the sender's "receive done" wait
+    removed (host mode reuses mailbox slot g % 2 before the peer's receive of
+    g - 2 has copied it out), ThreadSanitizer must report the mailbox race."""
+    src = open(os.path.join(ROOT, "csrc", "runtime", "ipc.cpp")).read()
+    needle = "} else if (g > 2) {  // slot g % 2"
+    assert src.count(needle) == 1
+    mut = tmp_path / "ipc.cpp"
+    mut.write_text(src.replace(needle, "} else if (false && g > 2) {  // slot g % 2"))
+    srcs = [os.path.join(ROOT, s) if s != "csrc/runtime/ipc.cpp" else str(mut) for s in SRCS]
+    exe = tmp_path / "threaded_tsan_ipc_mut"
+    _build("tsan", exe, srcs)
+    r = _run("tsan", exe)
+    assert r.returncode != 0
+    assert "ThreadSanitizer: data race" in r.stderr and "IpcTransport::enqueue_group" in r.stderr
