@@ -116,6 +116,8 @@ class DiffusionExecutor {
   int parity() const { return parity_; }
   int64_t steps_done() const { return steps_; }
   int64_t passes_done() const { return passes_; }
+  // passes enqueued as frame-first fused launches (RMA_EXEC_FUSED)
+  int64_t fused_passes() const { return fused_passes_; }
   std::vector<Rect> frame_rects() const { return frame_; }
   Rect interior_rect() const { return interior_; }
   Rect full_rect() const { return full_; }
@@ -163,6 +165,19 @@ class DiffusionExecutor {
   // next pass's interior waits for this instead of the exchange (lag_)
   void* e_fr_ = nullptr;
   bool lag_ = true;
+  // Frame-first fused passes (RMA_EXEC_FUSED): ONE pipelined launch per pass
+  // with the frame rects' tasks dispatched first; they raise sig_[1] when all
+  // are done and the exchange stream waits for that flag (flags.hip) instead
+  // of a separate frame launch. sig_: 2 x u64 device words; ferr_*: mapped
+  // host word the bounded flag wait reports a timeout into.
+  int fused_ = 0;
+  int64_t fused_passes_ = 0;
+  double fused_timeout_s_ = 60.0;
+  uint64_t* sig_ = nullptr;
+  uint32_t* ferr_host_ = nullptr;
+  uint32_t* ferr_dev_ = nullptr;
+  bool fused_pass_ok(const PassGeom& g, const StencilTuning& tn) const;
+  void check_fused_error() const;
   void* graph_exec_ = nullptr;  // hipGraphExec_t
   int64_t graph_len_ = 0;
   int parity_ = 0;

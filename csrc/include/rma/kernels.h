@@ -35,6 +35,14 @@ struct StencilTuning {
                            // padded to 8-block multiples (same-XCD neighbours); -1: by size
   int stages = 0;          // pipelined K-step kernels 9/10: waves per strip (0: default)
   int cols = 0;            // pipelined kernels: column waves per stage (0: default, 1, 2)
+  // Frame-first fused pass (pipelined kernels only): signal != nullptr makes
+  // the first signal_rects rects' tasks dispatch first (never XCD-remapped)
+  // and count their completion in signal[0] (device memory, zero); the last
+  // one resets it and stores 1 into signal[1] with system-scope release. A
+  // flag_wait_gpu(signal + 1, 1, ...) on another stream then orders work after
+  // those rects without waiting for the rest of the launch.
+  uint64_t* signal = nullptr;
+  int signal_rects = 0;
 };
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,

@@ -35,6 +35,12 @@ struct RectList {
   int64_t gpad[kMaxRects];       // >0: row-aligned mapping with gpad blocks per chunk row,
                                  // 0: linear task mapping, -1: column mode (thin rects)
   int n;
+  // frame-first fused pass (pipelined kernels; executor RMA_EXEC_FUSED): the
+  // first sig_blocks blocks (the frame rects' tasks, dispatched first, never
+  // XCD-remapped) count their completion in sig[0]; the last one re-arms the
+  // counter and raises sig[1], which the exchange stream waits on.
+  uint64_t* sig;
+  int64_t sig_blocks;
 };
 
 template <int V, bool NTL = false>
@@ -109,6 +115,30 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nwg) {
   const int64_t q = nwg / kXcd, r = nwg % kXcd;
   const int64_t xcd = b % kXcd, slot = b / kXcd;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
+// Block b of a launch whose first `first` blocks keep dispatch order (the
+// frame tasks of a fused pass) and whose rest is XCD-remapped among itself.
+__device__ __forceinline__ int64_t xcd_remap_after(int64_t b, int64_t nwg, int64_t first) {
+  return b < first ? b : first + xcd_remap(b - first, nwg - first);
+}
+
+// End of a signalling block (RectList::sig): every wave's stores are complete
+// at workgroup scope after the barrier; thread 0's acquire-release increment
+// chains them (and, through the counter, every earlier frame block's) to the
+// last block's system-scope release of the flag. The last block re-arms the
+// counter before raising the flag; the exchange stream lowers the flag after
+// its wait (flags.hip), before the next pass can start.
+__device__ __forceinline__ void signal_block_done(uint64_t* sig, int64_t nblocks) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t old =
+        __hip_atomic_fetch_add(sig, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int64_t)old + 1 == nblocks) {
+      __hip_atomic_store(sig, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sig + 1, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // The canonical cell update (see rma/common.h StencilCoef). Compiled with

@@ -329,7 +329,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   if constexpr (Ar == kArFast5RegPrio || Ar == kArFast5RegPrioNR) {
     if (stage == 0) __builtin_amdgcn_s_setprio(2);  // wave-uniform
   }
-  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t sig_first = L.sig ? L.sig_blocks : 0;
+  const int64_t b = remap ? xcd_remap_after(blockIdx.x, gridDim.x, sig_first) : (int64_t)blockIdx.x;
   int ri = 0;
   while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
   const int64_t lb = b - (ri ? L.block_end[ri - 1] : 0);
@@ -849,6 +850,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   if constexpr (kGlds) {
     if (stage == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  if (b < sig_first) signal_block_done(L.sig, L.sig_blocks);  // block-uniform
 }
 
 template <int K, int S, int V, int Ar, int C>
@@ -872,6 +874,8 @@ struct PipeLaunch {
   StencilCoef k;
   int chunk_rows, remap;
   hipStream_t stream;
+  uint64_t* sig = nullptr;  // fused pass: the first sig_rects rects signal (RectList::sig)
+  int sig_rects = 0;
 };
 
 // Plans the (strip, chunk) tasks with this instantiation's block width
@@ -884,6 +888,13 @@ void launch(const PipeLaunch& a) {
   static_assert(Geo<K, S, V, C>::kStep == (Geo<K, S, V, C>::WB - 2 * K) / V * V, "strip step");
   if (L.n == 0) return;
   RMA_CHECK_ARG(blocks < (int64_t(1) << 31), "grid too large: " << blocks << " blocks");
+  if (a.sig) {  // the signal rects' blocks (empty rects are not planned)
+    int ns = 0;
+    for (int i = 0; i < a.sig_rects; ++i) ns += a.rects[i].empty() ? 0 : 1;
+    RMA_CHECK_ARG(ns > 0, "signalling launch without a non-empty signal rect");
+    L.sig = a.sig;
+    L.sig_blocks = L.block_end[ns - 1];
+  }
   pipe_kernel<K, S, V, Ar, C><<<dim3((unsigned)blocks), dim3(kWave * S * C), 0, a.stream>>>(
       a.T2, a.T, a.iCp, a.nx, a.ny, L, a.k, a.chunk_rows, a.remap);
 }

@@ -113,6 +113,12 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, rects, nrects, c, tune.chunk_rows, remap,
                      as_stream(stream)};
+  if (tune.signal) {
+    RMA_CHECK_ARG(tune.signal_rects >= 1 && tune.signal_rects < nrects,
+                  "signal rects " << tune.signal_rects << " of " << nrects);
+    a.sig = tune.signal;
+    a.sig_rects = tune.signal_rects;
+  }
   // V = 5 only in the lab (the core units' cases take any V other than 4 and 2 as 1)
   bool ok = C == 1 && V != 5 &&
             (pipe::dispatch_r(K, S, V, arith, a) || pipe::dispatch_a(K, S, V, arith, a) ||

@@ -197,6 +197,18 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   // RMA_EXEC_LAG=0: every pass waits for the previous exchange.
   const char* lg = std::getenv("RMA_EXEC_LAG");
   lag_ = !(lg && lg[0] == '0');
+  // Frame-first fused passes (see enqueue_pass). RMA_EXEC_FUSED=1 on, 0 off.
+  const char* fu = std::getenv("RMA_EXEC_FUSED");
+  fused_ = fu ? std::atoi(fu) : 0;
+  if (const char* ft = std::getenv("RMA_EXEC_FUSED_TIMEOUT")) fused_timeout_s_ = std::atof(ft);
+  if (fused_ && p_.mode == Mode::kHide) {
+    RMA_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&sig_), 2 * sizeof(uint64_t)));
+    RMA_HIP_CHECK(hipMemset(sig_, 0, 2 * sizeof(uint64_t)));
+    RMA_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ferr_host_), sizeof(uint32_t),
+                                hipHostMallocMapped));
+    *ferr_host_ = 0;
+    RMA_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ferr_dev_), ferr_host_, 0));
+  }
   const char* pr = std::getenv("RMA_EXEC_PRIME");
   if (!(pr && pr[0] == '0')) prime();
 }
@@ -208,6 +220,12 @@ DiffusionExecutor::~DiffusionExecutor() {
   if (e_lo_) (void)hipEventDestroy(E(e_lo_));
   if (e_in_) (void)hipEventDestroy(E(e_in_));
   if (e_fr_) (void)hipEventDestroy(E(e_fr_));
+  if (sig_ || ferr_host_) {  // the streams' flag kernels may still use them
+    (void)hipStreamSynchronize(S(s_hi_));
+    (void)hipStreamSynchronize(S(s_lo_));
+    if (sig_) (void)hipFree(sig_);
+    if (ferr_host_) (void)hipHostFree(ferr_host_);
+  }
   if (pooled_) {  // back to the pool, drained
     (void)hipStreamSynchronize(S(s_hi_));
     (void)hipStreamSynchronize(S(s_lo_));
@@ -409,6 +427,22 @@ void DiffusionExecutor::multi_step(int K, double* Tin, double* Tout, const doubl
     stencilk_rects_gpu(K, Tout, Tin, iCp, nx, ny, rects, n, p_.coef, tn, stream);
 }
 
+bool DiffusionExecutor::fused_pass_ok(const PassGeom& g, const StencilTuning& tn) const {
+  if (!sig_ || !g.aligned || tn.kernel < 9 || g.interior.empty()) return false;
+  int nf = 0;
+  for (const Rect& r : g.frame) nf += r.empty() ? 0 : 1;
+  return nf > 0 && (int)g.frame.size() + 1 <= kMaxRects;
+}
+
+void DiffusionExecutor::check_fused_error() const {
+  if (!ferr_host_) return;
+  const uint32_t e = __atomic_load_n(ferr_host_, __ATOMIC_ACQUIRE);
+  RMA_CHECK_ARG(e == 0, "frame-first fused pass: the exchange stream's wait for the frame tasks "
+                        "timed out after "
+                            << fused_timeout_s_
+                            << " s (RMA_EXEC_FUSED_TIMEOUT); the halos of that pass are wrong");
+}
+
 void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   const PassGeom& g = geometry(K);
   const StencilTuning tn = pass_tuning(K, 0);
@@ -450,6 +484,47 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     rec(2, s_lo_);
     RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
     if (ev[4]) tseq_.push_back(1);
+    return;
+  }
+  if (fused_pass_ok(g, tn)) {
+    // Frame-first fused pass: ONE launch of the pass's task grid, the frame
+    // rects (whole tasks of the same grid) first in dispatch order and never
+    // XCD-remapped, so they finish in the launch's first task wave; their last
+    // block raises sig_[1]. The exchange stream waits for that flag on the GPU
+    // (bounded, flags.hip), lowers it and exchanges while the rest of the
+    // launch runs. No frame launch beside the interior's, no frame-sized second
+    // grid. The next pass waits for this exchange (its frame tasks read the
+    // halo) and, in stream order, for this launch.
+    TraceRange tr("rma.pass.fused");
+    ++fused_passes_;
+    RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+    Rect rs[kMaxRects];
+    int n = 0;
+    for (const Rect& r : g.frame) rs[n++] = r;
+    const int nf = n;
+    rs[n++] = g.interior;
+    StencilTuning ft = tn;
+    ft.signal = sig_;
+    ft.signal_rects = nf;
+    rec(0, s_hi_);
+    rec(3, s_lo_);
+    {
+      TraceRange ti("rma.fused");
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, rs, n, ft, s_lo_);
+    }
+    rec(4, s_lo_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+    flag_wait_gpu(sig_ + 1, 1, fused_timeout_s_, ferr_dev_, 1, s_hi_);
+    flag_write_gpu(sig_ + 1, 0, s_hi_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_fr_), S(s_hi_)));
+    rec(1, s_hi_);
+    {
+      TraceRange th("rma.halo");
+      exchange(Tout, s_hi_);
+    }
+    rec(2, s_hi_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
+    if (ev[4]) tseq_.push_back(0);
     return;
   }
   TraceRange tr("rma.pass.hide");
@@ -533,6 +608,7 @@ void DiffusionExecutor::set_timing(bool on) {
 std::vector<PassTiming> DiffusionExecutor::timings() {
   RMA_HIP_CHECK(hipStreamSynchronize(S(s_hi_)));
   RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
+  check_fused_error();
   std::vector<PassTiming> out;
   for (size_t i = 0; i < tk_.size(); ++i) {
     hipEvent_t* e = reinterpret_cast<hipEvent_t*>(&tev_[5 * i]);
@@ -582,6 +658,17 @@ void DiffusionExecutor::prime() {
         continue;
       }
       multi_step(K, a, b, ic, tnx, tny, &r, 1, pass_tuning(K, 0), s_lo_);
+      if (sig_ && K == p_.temporal) {  // the flag kernels' first launches, and a signal
+        const Rect rr[2] = {Rect{1, tnx - 1, 1, 9}, Rect{1, tnx - 1, 9, tny - 1}};
+        StencilTuning st = pass_tuning(K, 0);
+        if (st.kernel >= 9) {
+          st.signal = sig_;
+          st.signal_rects = 1;
+          multi_step(K, a, b, ic, tnx, tny, rr, 2, st, s_lo_);
+          flag_wait_gpu(sig_ + 1, 1, fused_timeout_s_, ferr_dev_, 1, s_lo_);
+          flag_write_gpu(sig_ + 1, 0, s_lo_);
+        }
+      }
       if (p_.mode == Mode::kHide)
         for (int part = 1; part <= 2; ++part)
           multi_step(K, a, b, ic, tnx, tny, &r, 1, pass_tuning(K, part), s_lo_);
@@ -687,6 +774,7 @@ void DiffusionExecutor::build_graph(int64_t steps, int reps) {
 
 void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
   RMA_CHECK_ARG(nsteps >= 0, "nsteps=" << nsteps);
+  check_fused_error();
   if (nsteps == 0) return;
   hipStream_t caller = S(caller_stream);
   hipStream_t lo = S(s_lo_), hi = S(s_hi_);

@@ -366,14 +366,27 @@ for s in "$@"; do
              --steps 960 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     eqn*) # eqn<N>_<dims>[_strips][_cd<D>][_bol|_btask]: N^2 tile, K=24, equal coefficients
              t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""; fb=""; hm=""; lg=""
-             mc=""; pp=""
+             mc=""; pp=""; sk=""; va="perf_hide"; fu=""
              for tok in ${t//_/ }; do case $tok in strips) fa=0 ;; cd*) cd=${tok#cd} ;;
+               skip) sk=1 ;; perf) va=perf ;; fused) fu=1 ;;
                bol) fb=ol ;; btask) fb=task ;; nomerge) hm=0 ;; nolag) lg=0 ;;
                ch*) mc=${tok#ch} ;; pp*) pp=${tok#pp} ;; esac; done
              RMA_EXEC_LAG=$lg RMA_HALO_MERGED=$hm RMA_FRAME_BANDS=$fb RMA_FRAME_CHUNK_DIV=$cd \
-             RMA_FRAME_ALIGNED=$fa step "$s" 300 env ${mc:+NCCL_MAX_P2P_NCHANNELS=$mc} \
-             ${pp:+NCCL_NCHANNELS_PER_PEER=$pp} python bench/rccl_self_overhead.py --n "$n" --K 24 \
+             RMA_FRAME_ALIGNED=$fa RMA_DIAG_SKIP_EXCHANGE=$sk RMA_EXEC_FUSED=$fu step "$s" 300 env \
+             ${mc:+NCCL_MAX_P2P_NCHANNELS=$mc} ${pp:+NCCL_NCHANNELS_PER_PEER=$pp} \
+             python bench/rccl_self_overhead.py --n "$n" --K 24 --variants $va \
              --periodic "$d" --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    tests_fused) step tests_fused 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread \
+             "tests/test_multirank_gpu.py::test_fused_frame_first_passes_bitwise" \
+             "tests/test_multirank_gpu.py::test_fused_passes_over_rccl_self_equal_the_split_passes" \
+             -p no:cacheprovider || exit 1 ;;
+    eqfused) for t in eqn8192_xy eqn8192_xy_fused eqn2048_xy eqn2048_xy_fused eqn4096_xy \
+                      eqn4096_xy_fused eqn16384_xy eqn16384_xy_fused eqn8192_x eqn8192_x_fused \
+                      eqn8192_y eqn8192_y_fused; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    eqsplit) for t in eqn8192_xy eqn8192_xy_skip eqn8192_xy_perf eqn2048_xy eqn2048_xy_skip \
+                      eqn2048_xy_perf eqn4096_xy eqn4096_xy_skip; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     chunk_sweep) step chunk_sweep 400 python bench/pass_sweep.py --pipe 20,24 --pipec "" \
              --ldsdpp "" --old "" --alt "" --rounds 3 \
              --chunks "20:2048/3072/4096/6144,24:2048/3072/4096/6144" \

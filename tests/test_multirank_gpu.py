@@ -498,6 +498,74 @@ def test_small_tile_frame_layouts_bitwise(dims, ny):
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
 
 
+def spmd_fused(rank, hub, nx, ny, nt, dims, K, graph=False):
+    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], overlaps=(2 * K, 2 * K, 2),
+                        halowidths=(K, K, 1), quiet=True, loopback=(hub, rank))
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=nt, init="random",
+                                    quiet=True, dims=dims, temporal=K, fast_math=True,
+                                    use_graph=graph))
+    aligned = m.executor.geometry(K)["aligned"]
+    m.step(nt)
+    out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g,
+           (m.executor.fused_passes, aligned))
+    m.close()
+    gg.finalize_global_grid()
+    return out
+
+
+@pytest.mark.parametrize("dims,K,nx,ny,nt", [((2, 2), 24, 1100, 3500, 53),
+                                             ((2, 1), 20, 1100, 1500, 47),
+                                             ((1, 2), 8, 800, 2600, 19),
+                                             ((2, 2), 16, 700, 900, 37),
+                                             ((2, 2), 12, 1000, 3000, 31)])
+def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, monkeypatch):
+    """RMA_EXEC_FUSED=1: every K-step pass with a neighbour is ONE pipelined
+    launch, frame tasks first, whose last frame block raises the flag the
+    exchange stream waits on (flags.hip); every tile == its window of the
+    1-rank run, bitwise, and the passes with aligned frames (whole tasks of
+    the pass's grid) really ran fused -- the others keep the split launches."""
+    monkeypatch.setenv("RMA_EXEC_FUSED", "1")
+    P = dims[0] * dims[1]
+    res = run_loopback(P, spmd_fused, nx, ny, nt, dims, K, timeout=240)
+    nxg, nyg, _ = res[0][2]
+    monkeypatch.setenv("RMA_EXEC_FUSED", "0")
+    one = run_loopback(1, spmd_fused, nxg, nyg, nt, (1, 1), K, timeout=240)[0][1]
+    assert any(a for _, _, _, (_, a) in res)
+    for coords, T, _, (fused, aligned) in res:
+        assert (fused >= nt // K) if aligned else fused == 0, (coords, fused, aligned)
+        gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
+        assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_passes_over_rccl_self_equal_the_split_passes(graph, monkeypatch):
+    """The production exchange (RCCL send/recv to self, x and y periodic,
+    merged groups) behind fused passes -- eager and replayed from a hipGraph
+    (the flag kernels are captured nodes) -- leaves the field bitwise equal
+    to the split frame / interior passes."""
+    K, n, nt = 24, 1536, 240
+
+    def run(fused):
+        monkeypatch.setenv("RMA_EXEC_FUSED", "1" if fused else "0")
+        gg.init_global_grid(n, n, 1, periodx=1, periody=1, quiet=True, transport="rccl",
+                            overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
+                            self_via_transport=True)
+        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=n, ny=n, nt=nt, init="random",
+                                        quiet=True, periods=(1, 1, 0), temporal=K,
+                                        fast_math=True, use_graph=graph and fused))
+        m.step(nt)
+        f = m.field.cpu().numpy().copy()
+        nf = m.executor.fused_passes
+        m.close()
+        gg.finalize_global_grid()
+        return f, nf
+
+    a, nfa = run(True)
+    b, nfb = run(False)
+    assert nfb == 0 and (nfa >= nt // K or graph), nfa
+    assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("via_rccl", [False, True])
 @pytest.mark.parametrize("hw,ol", [(1, 2), (8, 16), (24, 48)])
 def test_merged_exchange_equals_dimension_ordered(via_rccl, hw, ol):
