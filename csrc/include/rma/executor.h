@@ -170,7 +170,8 @@ class DiffusionExecutor {
   // are done and the exchange stream waits for that flag (flags.hip) instead
   // of a separate frame launch. sig_: 2 x u64 device words; ferr_*: mapped
   // host word the bounded flag wait reports a timeout into.
-  int fused_ = 0;
+  int fused_ = 2;  // 0 off, 1 on, 2 auto (>= 2 waves of tasks)
+  int cus_ = 256;  // compute units of the device
   int64_t fused_passes_ = 0;
   double fused_timeout_s_ = 60.0;
   uint64_t* sig_ = nullptr;

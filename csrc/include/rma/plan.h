@@ -47,6 +47,13 @@ struct PassGeom {
   // or the ol-K rows the exchange needs (taller tasks), so frame + interior do
   // the work of ONE launch; frame launches then use the interior tuning
   bool aligned = false;
+  // task grid of the pass's pipelined launch over `out` (0: not pipelined):
+  // strip tasks of task_w output columns and task_h rows
+  int64_t task_w = 0, task_h = 0;
+  int64_t tasks() const {
+    if (task_w <= 0 || task_h <= 0 || out.empty()) return 0;
+    return ((out.x1 - out.x0 + task_w - 1) / task_w) * ((out.y1 - out.y0 + task_h - 1) / task_h);
+  }
 };
 
 // Geometry of one pass. hide: split into frame + interior so that the frame

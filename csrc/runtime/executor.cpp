@@ -197,9 +197,16 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   // RMA_EXEC_LAG=0: every pass waits for the previous exchange.
   const char* lg = std::getenv("RMA_EXEC_LAG");
   lag_ = !(lg && lg[0] == '0');
-  // Frame-first fused passes (see enqueue_pass). RMA_EXEC_FUSED=1 on, 0 off.
+  // Frame-first fused passes (see enqueue_pass). RMA_EXEC_FUSED=1 always (where
+  // the frame is aligned), 0 never, unset: by task waves (fused_pass_ok).
   const char* fu = std::getenv("RMA_EXEC_FUSED");
-  fused_ = fu ? std::atoi(fu) : 0;
+  fused_ = fu && fu[0] ? std::atoi(fu) : 2;  // 2: auto (fused_pass_ok)
+  {
+    int dev = 0, cus = 0;
+    RMA_HIP_CHECK(hipGetDevice(&dev));
+    RMA_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    cus_ = cus > 0 ? cus : 256;
+  }
   if (const char* ft = std::getenv("RMA_EXEC_FUSED_TIMEOUT")) fused_timeout_s_ = std::atof(ft);
   if (fused_ && p_.mode == Mode::kHide) {
     RMA_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&sig_), 2 * sizeof(uint64_t)));
@@ -256,6 +263,8 @@ const PassGeom& DiffusionExecutor::geometry(int K) {
     }
     geom_[K] = pass_geometry(nx_, ny_, K, nbr_, p_.mode == Mode::kHide, p_.bwx, p_.bwy, p_.olx,
                              p_.oly, tw, th, vec, frame_layout(ny_, nbr_).bands);
+    geom_[K].task_w = tw;
+    geom_[K].task_h = th;
     geom_ok_[K] = 1;
   }
   return geom_[K];
@@ -431,7 +440,13 @@ bool DiffusionExecutor::fused_pass_ok(const PassGeom& g, const StencilTuning& tn
   if (!sig_ || !g.aligned || tn.kernel < 9 || g.interior.empty()) return false;
   int nf = 0;
   for (const Rect& r : g.frame) nf += r.empty() ? 0 : 1;
-  return nf > 0 && (int)g.frame.size() + 1 <= kMaxRects;
+  if (nf == 0 || (int)g.frame.size() + 1 > kMaxRects) return false;
+  // auto: only with >= 2 waves of tasks per pass (2 blocks of 4 waves per CU
+  // at K = 10..24). Below that every task runs at once, the frame tasks end
+  // with the whole launch and the exchange is exposed; the split launches win
+  // there (RCCL-self x+y at K=24, equal coefficients, profiles/r5/fused/:
+  // 4096^2 1.2 % split vs 8.7 % fused, 2048^2 44 vs 50 %; 8192^2 5.6 -> 1.3 %)
+  return fused_ == 1 || g.tasks() >= 4 * (int64_t)cus_;
 }
 
 void DiffusionExecutor::check_fused_error() const {

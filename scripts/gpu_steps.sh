@@ -368,7 +368,7 @@ for s in "$@"; do
              t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""; fb=""; hm=""; lg=""
              mc=""; pp=""; sk=""; va="perf_hide"; fu=""
              for tok in ${t//_/ }; do case $tok in strips) fa=0 ;; cd*) cd=${tok#cd} ;;
-               skip) sk=1 ;; perf) va=perf ;; fused) fu=1 ;;
+               skip) sk=1 ;; perf) va=perf ;; fused) fu=1 ;; split) fu=0 ;;
                bol) fb=ol ;; btask) fb=task ;; nomerge) hm=0 ;; nolag) lg=0 ;;
                ch*) mc=${tok#ch} ;; pp*) pp=${tok#pp} ;; esac; done
              RMA_EXEC_LAG=$lg RMA_HALO_MERGED=$hm RMA_FRAME_BANDS=$fb RMA_FRAME_CHUNK_DIV=$cd \
@@ -380,6 +380,12 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_fused_frame_first_passes_bitwise" \
              "tests/test_multirank_gpu.py::test_fused_passes_over_rccl_self_equal_the_split_passes" \
              -p no:cacheprovider || exit 1 ;;
+    eq_xy_fused|eq_xy_split) fu=1; [ $s = eq_xy_split ] && fu=0
+             RMA_EXEC_FUSED=$fu step "$s" 400 python bench/rccl_self_overhead.py --K 24 --periodic xy \
+             --steps 320 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    eqauto) for t in eq_xy_split eq_xy_fused eqn12288_xy_split eqn12288_xy_fused eqn12288_xy \
+                     eqn8192_xy eqn4096_xy eqn2048_xy; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     eqfused) for t in eqn8192_xy eqn8192_xy_fused eqn2048_xy eqn2048_xy_fused eqn4096_xy \
                       eqn4096_xy_fused eqn16384_xy eqn16384_xy_fused eqn8192_x eqn8192_x_fused \
                       eqn8192_y eqn8192_y_fused; do

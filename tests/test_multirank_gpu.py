@@ -504,35 +504,44 @@ def spmd_fused(rank, hub, nx, ny, nt, dims, K, graph=False):
     m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=nt, init="random",
                                     quiet=True, dims=dims, temporal=K, fast_math=True,
                                     use_graph=graph))
-    aligned = m.executor.geometry(K)["aligned"]
+    plan = list(m.executor.plan(nt))
+    geos = {k: m.executor.geometry(k) for k in set(plan)}
+    # the passes the executor fuses: aligned frames (whole tasks of the pass's
+    # grid) around a non-empty interior
+    def fusable(g):
+        x0, x1, y0, y1 = g["interior"]
+        return g["aligned"] and x1 > x0 and y1 > y0 and any(r[1] > r[0] and r[3] > r[2]
+                                                            for r in g["frame"])
+    want = sum(1 for k in plan if fusable(geos[k]))
     m.step(nt)
     out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g,
-           (m.executor.fused_passes, aligned))
+           (m.executor.fused_passes, want, plan, geos))
     m.close()
     gg.finalize_global_grid()
     return out
 
 
-@pytest.mark.parametrize("dims,K,nx,ny,nt", [((2, 2), 24, 1100, 3500, 53),
-                                             ((2, 1), 20, 1100, 1500, 47),
-                                             ((1, 2), 8, 800, 2600, 19),
-                                             ((2, 2), 16, 700, 900, 37),
-                                             ((2, 2), 12, 1000, 3000, 31)])
-def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, monkeypatch):
+@pytest.mark.parametrize("dims,K,nx,ny,nt,some", [((2, 2), 24, 1100, 3500, 53, True),
+                                                  ((2, 1), 20, 1100, 1500, 47, True),
+                                                  ((1, 2), 8, 800, 2600, 19, True),
+                                                  ((2, 2), 16, 700, 900, 37, False),
+                                                  ((2, 2), 12, 1000, 3000, 31, True)])
+def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, some, monkeypatch):
     """RMA_EXEC_FUSED=1: every K-step pass with a neighbour is ONE pipelined
     launch, frame tasks first, whose last frame block raises the flag the
     exchange stream waits on (flags.hip); every tile == its window of the
     1-rank run, bitwise, and the passes with aligned frames (whole tasks of
-    the pass's grid) really ran fused -- the others keep the split launches."""
+    the pass's grid) really ran fused -- the others (all of them in the
+    700x900 case: tiles too small for aligned frames) keep the split launches."""
     monkeypatch.setenv("RMA_EXEC_FUSED", "1")
     P = dims[0] * dims[1]
     res = run_loopback(P, spmd_fused, nx, ny, nt, dims, K, timeout=240)
     nxg, nyg, _ = res[0][2]
     monkeypatch.setenv("RMA_EXEC_FUSED", "0")
     one = run_loopback(1, spmd_fused, nxg, nyg, nt, (1, 1), K, timeout=240)[0][1]
-    assert any(a for _, _, _, (_, a) in res)
-    for coords, T, _, (fused, aligned) in res:
-        assert (fused >= nt // K) if aligned else fused == 0, (coords, fused, aligned)
+    assert any(w for _, _, _, (_, w, _, _) in res) == some
+    for coords, T, _, (fused, want, plan, geos) in res:
+        assert fused == want, (coords, fused, want, plan, geos)
         gx0, gy0 = coords[0] * (nx - 2 * K), coords[1] * (ny - 2 * K)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
 
