@@ -930,6 +930,11 @@ def run(a, world: int, rank: int) -> int:
         snap = snapshot_windows(model) if a.window_check and a.variant != "kp" else None
         timings = summarize_timings(model.pass_timings(), exchange=nbrs)
         model.enable_pass_timing(False)
+        ex = getattr(model, "executor", None)
+        # passes of the warmup + timed steps and how many ran as frame-first fused launches
+        # (RMA_EXEC_FUSED: with neighbours and >= 2 waves of tasks per pass)
+        exec_passes = ({"passes": int(ex.passes_done), "fused": int(ex.fused_passes)}
+                       if ex is not None else None)
         bad = float(model.field[:: max(1, ny // 64), :: max(1, nx // 64)].isfinite().logical_not().sum())
         bad = comm.allreduce(bad, "sum")
         a_eff = 3 * nx * ny * 8 / 1e9
@@ -1132,6 +1137,7 @@ def run(a, world: int, rank: int) -> int:
             "rccl_nranks": _rccl_nranks(g, out["config"].get("preflight")),
             "rccl": _rccl_info() if gpu else None,
             "hipgraph": bool(a.graph),
+            "executor_passes": exec_passes,
             "setup_s": round(setup_s, 3),
             "nonfinite_cells_sampled": int(bad),
         })

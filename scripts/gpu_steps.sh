@@ -264,6 +264,10 @@ for s in "$@"; do
                step "rehearse$n" 400 python bench.py --gpus $n --shared-gpu-test --shared-gpu-transport rccl \
                  --nx 4096 --steps 96 --warmup 4 --json-out "$OUT/rehearse$n.json" || exit 1
              done ;;
+    rehearse_fused) for n in 2 4; do
+               step "rehearse_fused$n" 400 python bench.py --gpus $n --shared-gpu-test --shared-gpu-transport rccl \
+                 --nx 8192 --steps 96 --warmup 4 --json-out "$OUT/rehearse_fused$n.json" || exit 1
+             done ;;
     tests_ipc5) step tests_ipc5 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
              "tests/test_multirank_gpu.py::test_ipc_modes_2000_exchanged_steps_bitwise" \
              "tests/test_multirank_gpu.py::test_ipc_transport_processes" \
