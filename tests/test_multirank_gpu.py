@@ -575,6 +575,29 @@ def test_fused_passes_over_rccl_self_equal_the_split_passes(graph, monkeypatch):
     assert np.array_equal(a, b)
 
 
+def test_fused_pass_wait_timeout_is_reported_not_hung(monkeypatch):
+    """The exchange stream's wait for the frame flag is bounded: with a
+    timeout far below a frame's run time every wait gives up, the passes still
+    drain (no hang; halos of those passes are wrong) and the next run() /
+    pass_timings() raises the timeout instead of returning silently."""
+    K, n = 24, 1536
+    monkeypatch.setenv("RMA_EXEC_FUSED", "1")
+    monkeypatch.setenv("RMA_EXEC_FUSED_TIMEOUT", "1e-7")
+    gg.init_global_grid(n, n, 1, periodx=1, periody=1, quiet=True, transport="rccl",
+                        overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1), self_via_transport=True)
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=n, ny=n, nt=48, init="random",
+                                    quiet=True, periods=(1, 1, 0), temporal=K, fast_math=True))
+    try:
+        m.step(48)
+        m.synchronize()
+        assert m.executor.fused_passes == 2
+        with pytest.raises(RuntimeError, match="timed out"):  # the native module's NativeError
+            m.step(K)
+    finally:
+        m.close()
+        gg.finalize_global_grid()
+
+
 @pytest.mark.parametrize("via_rccl", [False, True])
 @pytest.mark.parametrize("hw,ol", [(1, 2), (8, 16), (24, 48)])
 def test_merged_exchange_equals_dimension_ordered(via_rccl, hw, ol):
