@@ -548,20 +548,22 @@ def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, some, monkeypatch
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_fused_passes_over_rccl_self_equal_the_split_passes(graph, monkeypatch):
-    """The production exchange (RCCL send/recv to self, x and y periodic,
-    merged groups) behind fused passes -- eager and replayed from a hipGraph
-    (the flag kernels are captured nodes) -- leaves the field bitwise equal
-    to the split frame / interior passes."""
+    """Fused passes behind the production exchange (RCCL send/recv to self, x
+    and y periodic, merged groups) eagerly, and replayed from a hipGraph (the
+    flag kernels are captured nodes; the periodic halos then go through local
+    copies, since RCCL is not captured in a torch process), leave the field
+    bitwise equal to the split frame / interior passes."""
     K, n, nt = 24, 1536, 240
 
     def run(fused):
         monkeypatch.setenv("RMA_EXEC_FUSED", "1" if fused else "0")
         gg.init_global_grid(n, n, 1, periodx=1, periody=1, quiet=True, transport="rccl",
                             overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
-                            self_via_transport=True)
+                            self_via_transport=not graph)
         m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=n, ny=n, nt=nt, init="random",
                                         quiet=True, periods=(1, 1, 0), temporal=K,
                                         fast_math=True, use_graph=graph and fused))
+        assert m.use_graph == (graph and fused)
         m.step(nt)
         f = m.field.cpu().numpy().copy()
         nf = m.executor.fused_passes
@@ -571,7 +573,7 @@ def test_fused_passes_over_rccl_self_equal_the_split_passes(graph, monkeypatch):
 
     a, nfa = run(True)
     b, nfb = run(False)
-    assert nfb == 0 and (nfa >= nt // K or graph), nfa
+    assert nfb == 0 and nfa >= 2, nfa  # (graph: counted once per captured pass)
     assert np.array_equal(a, b)
 
 
