@@ -195,17 +195,7 @@ void validate_rects(int64_t nx, int64_t ny, const Rect* rects, int nrects) {
 
 }  // namespace
 
-int stencil_vec(int64_t nx, const StencilTuning& tune) {
-  // cells per lane: 16-byte rows need an even nx; V=4 also needs nx % 4 == 0
-  // (a clamped lane past the row end must still load its own cells)
-  if (nx % 2) return 1;
-  if (tune.vec == 4 && nx % 4 == 0) return 4;
-  return 2;
-}
-
-int stencil_strip_cells(int64_t nx, const StencilTuning& tune) {
-  return kWave * stencil_vec(nx, tune);
-}
+// stencil_vec, stencil_strip_cells: kernel_select.cpp
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
                        const Rect* rects, int nrects, const StencilCoef& c,

@@ -1,0 +1,267 @@
+// The native time loop (csrc/runtime/executor.cpp DiffusionExecutor) on P rank
+// threads over the loopback transport, against a host stand-in of the HIP
+// runtime (tests/native/hip_stub) with the kernels replaced by their CPU
+// twins, so it builds with a host compiler under ThreadSanitizer and
+// AddressSanitizer (tests/test_native_host_threads.py).
+//
+// Each case decomposes one global grid over dims[0] x dims[1] rank threads
+// (open or periodic), runs n steps of perf or perf_hide with K-step passes
+// (canonical K = 1; fast-math K = 4, 8, 24: split frame / interior launches and
+// the frame-first fused pass, whose frame flag the stub raises when the launch
+// "completes") and requires every tile to equal its window of the same grid
+// run by ONE rank, bitwise: the executor's pass plan, frame / interior
+// geometry, stream / event ordering and exchanges, with the sanitizers
+// watching the threads meet in the loopback hub. Reference:
+// /root/reference/scripts/diffusion_2D_perf_hide.jl:63-101 (the overlapped
+// time loop this executor implements), diffusion_2D_perf.jl:22-58.
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <hip/hip_runtime.h>  // the host stub
+
+#include "rma/executor.h"
+#include "rma/halo.h"
+#include "rma/kernels.h"
+#include "rma/loopback.h"
+#include "rma/topology.h"
+
+namespace rma {
+// the stub runs stream work at enqueue time: every launch is its CPU twin
+void copy2d_batch_gpu(const Copy2d* copies, int n, int elem_bytes, stream_t) {
+  copy2d_batch_cpu(copies, n, elem_bytes);
+}
+void flag_wait_gpu(const uint64_t* flag, uint64_t want, double timeout_s, uint32_t* err,
+                   uint32_t code, stream_t) {
+  auto* f = reinterpret_cast<const std::atomic<uint64_t>*>(flag);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (f->load(std::memory_order_acquire) != want) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+      __atomic_store_n(err, code, __ATOMIC_RELEASE);
+      return;
+    }
+    std::this_thread::yield();
+  }
+}
+void flag_write_gpu(uint64_t* flag, uint64_t value, stream_t) {
+  reinterpret_cast<std::atomic<uint64_t>*>(flag)->store(value, std::memory_order_release);
+}
+void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                       const Rect* rects, int nrects, const StencilCoef& c, const StencilTuning&,
+                       stream_t) {
+  stencil_rects_cpu(T2, T, iCp, nx, ny, rects, nrects, c);
+}
+void stencil2_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                        const Rect* rects, int nrects, const StencilCoef& c, const StencilTuning&,
+                        stream_t) {
+  stencil2_rects_cpu(T2, T, iCp, nx, ny, rects, nrects, c);
+}
+std::atomic<long> g_signals{0};
+void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, int64_t nx,
+                        int64_t ny, const Rect* rects, int nrects, const StencilCoef& c,
+                        const StencilTuning& t, stream_t) {
+  // fast5 family: kernel 5 and the pipelined kernels except 10 (canonical)
+  const bool fast = t.kernel == 5 || (t.kernel >= 9 && t.kernel != 10);
+  if (fast)
+    stencilk5_rects_cpu(K, T2, T, iCp, nx, ny, rects, nrects, c);
+  else
+    stencilk_rects_cpu(K, T2, T, iCp, nx, ny, rects, nrects, c);
+  if (t.signal) {  // the launch's frame blocks are done: raise the flag (stencil_device.h)
+    if (t.kernel < 9) throw std::runtime_error("signal on a non-pipelined kernel");
+    reinterpret_cast<std::atomic<uint64_t>*>(t.signal + 1)->store(1, std::memory_order_release);
+    ++g_signals;
+  }
+}
+void flux_gpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,
+              double rdx, double rdy, stream_t) {
+  flux_cpu(QX, QY, T, nx, ny, mlam, rdx, rdy);
+}
+void residual_gpu(double* D, const double* QX, const double* QY, const double* iCp, int64_t nx,
+                  int64_t ny, double rdx, double rdy, stream_t) {
+  residual_cpu(D, QX, QY, iCp, nx, ny, rdx, rdy);
+}
+void update_gpu(double* T, const double* D, int64_t nx, int64_t ny, double dt, stream_t) {
+  update_cpu(T, D, nx, ny, dt);
+}
+}  // namespace rma
+
+using namespace rma;
+
+// The executor's process-wide stream pool (executor.cpp g_pool) keeps its
+// streams for the life of the process by design (reused by later executors,
+// never destroyed during HIP teardown): not a leak to report.
+extern "C" const char* __lsan_default_suppressions() {
+  return "leak:hipStreamCreateWithPriority\n";
+}
+
+namespace {
+
+std::atomic<int> g_fail{0};
+
+#define CHECK(cond, ...)                  \
+  do {                                    \
+    if (!(cond)) {                        \
+      std::fprintf(stderr, "FAIL: ");     \
+      std::fprintf(stderr, __VA_ARGS__);  \
+      std::fprintf(stderr, "\n");         \
+      ++g_fail;                           \
+    }                                     \
+  } while (0)
+
+uint64_t mix(uint64_t z) {  // splitmix64
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// a value keyed by the GLOBAL cell (wrapped on periodic dims): every
+// decomposition of the grid sees the same field, overlaps agree
+double cell_value(int64_t gx, int64_t gy, int64_t nxg, int64_t nyg, uint64_t seed, double lo,
+                  double hi) {
+  gx = ((gx % nxg) + nxg) % nxg;
+  gy = ((gy % nyg) + nyg) % nyg;
+  const uint64_t h = mix(seed ^ mix((uint64_t)(gy * nxg + gx)));
+  return lo + (hi - lo) * (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+
+struct Case {
+  const char* name;
+  std::array<int, 3> dims, periods;
+  int64_t nx, ny;  // per-rank tile (with overlaps)
+  int K;           // max steps per pass (1: canonical one-step, > 1 fast-math)
+  Mode mode;
+  int nt;
+  const char* fused;  // RMA_EXEC_FUSED for the multi-rank run ("" = auto)
+  int chunk = 0;      // K-step rows per task (ExecParams::chunk_rows2; 0: the table)
+};
+
+struct TileResult {
+  std::array<int, 3> coords;
+  std::vector<double> T;
+  int64_t fused_passes, passes;
+};
+
+// runs the case's grid on dims[0] x dims[1] rank threads; returns every tile
+std::vector<TileResult> run_ranks(const Case& c, std::array<int, 3> dims, int64_t nx, int64_t ny) {
+  const int P = dims[0] * dims[1] * dims[2];
+  const int64_t ol = std::max(2, 2 * c.K);
+  const int64_t nxg = c.periods[0] ? dims[0] * (nx - ol) : dims[0] * (nx - ol) + ol;
+  const int64_t nyg = c.periods[1] ? dims[1] * (ny - ol) : dims[1] * (ny - ol) + ol;
+  CartTopology topo(P, dims, c.periods);
+  auto hub = std::make_shared<LoopbackHub>(P, 60.0);
+  std::vector<TileResult> out((size_t)P);
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; ++r) {
+    th.emplace_back([&, r] {
+      try {
+        const auto co = topo.coords(r);
+        auto ep = std::make_unique<LoopbackEndpoint>(hub, r);
+        auto hx = std::make_unique<HaloExchanger>(ep.get(), r, topo.neighbors(r));
+        hx->set_diagonals(topo.diagonals(r));
+        const int64_t gx0 = co[0] * (nx - ol), gy0 = co[1] * (ny - ol);
+        std::vector<double> T((size_t)(nx * ny)), T2((size_t)(nx * ny)), iCp((size_t)(nx * ny));
+        for (int64_t y = 0; y < ny; ++y)
+          for (int64_t x = 0; x < nx; ++x) {
+            T[(size_t)(y * nx + x)] = cell_value(gx0 + x, gy0 + y, nxg, nyg, 11, 0.0, 1.0);
+            iCp[(size_t)(y * nx + x)] = cell_value(gx0 + x, gy0 + y, nxg, nyg, 29, 0.5, 1.5);
+          }
+        T2 = T;
+        ExecParams p;
+        p.mode = c.mode;
+        const double dx = 10.0 / (double)nxg, dy = 10.0 / (double)nyg;
+        p.coef = StencilCoef{-1.0, 1.0 / dx, 1.0 / dy, std::min(dx * dx, dy * dy) / 4.1};
+        p.temporal = c.K;
+        p.olx = p.oly = ol;
+        p.fast_math = c.K > 1 ? 1 : 0;
+        p.chunk_rows2 = c.chunk;
+        TileResult& res = out[(size_t)r];
+        {
+          DiffusionExecutor ex(T.data(), T2.data(), iCp.data(), nx, ny, p, hx.get());
+          ex.run(c.nt, nullptr);
+          (void)hipDeviceSynchronize();
+          res.fused_passes = ex.fused_passes();
+          res.passes = ex.passes_done();
+          res.T = ex.parity() ? T2 : T;
+        }
+        res.coords = co;
+        hx.reset();
+        ep.reset();
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "FAILED %s rank %d: %s\n", c.name, r, e.what());
+        ++g_fail;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  return out;
+}
+
+int run_case(const Case& c) {
+  const int fails0 = g_fail.load();
+  const int64_t ol = std::max(2, 2 * c.K);
+  if (*c.fused)
+    setenv("RMA_EXEC_FUSED", c.fused, 1);
+  else
+    unsetenv("RMA_EXEC_FUSED");
+  const auto multi = run_ranks(c, c.dims, c.nx, c.ny);
+  // the same global grid on one rank: its tile is the global grid plus the
+  // overlap cells (periodic: wrapped by the self exchange)
+  const int64_t nx1 = c.dims[0] * (c.nx - ol) + ol, ny1 = c.dims[1] * (c.ny - ol) + ol;
+  setenv("RMA_EXEC_FUSED", "0", 1);
+  const auto one = run_ranks(c, {1, 1, 1}, nx1, ny1);
+  unsetenv("RMA_EXEC_FUSED");
+  if (g_fail.load() != fails0) return 1;
+  long fused = 0;
+  for (const TileResult& t : multi) {
+    fused += t.fused_passes;
+    const int64_t gx0 = t.coords[0] * (c.nx - ol), gy0 = t.coords[1] * (c.ny - ol);
+    for (int64_t y = 0; y < c.ny; ++y)
+      for (int64_t x = 0; x < c.nx; ++x) {
+        const double a = t.T[(size_t)(y * c.nx + x)];
+        const double b = one[0].T[(size_t)((gy0 + y) * nx1 + gx0 + x)];
+        if (std::memcmp(&a, &b, sizeof a) != 0) {
+          CHECK(false, "%s: tile (%d,%d) cell (%lld,%lld) %.17g != %.17g", c.name, t.coords[0],
+                t.coords[1], (long long)x, (long long)y, a, b);
+          return 1;
+        }
+      }
+  }
+  const bool want_fused = std::string(c.fused) == "1";
+  CHECK(!want_fused || fused > 0, "%s: no fused pass ran", c.name);
+  CHECK(std::string(c.fused) != "0" || fused == 0, "%s: fused passes with RMA_EXEC_FUSED=0",
+        c.name);
+  std::printf("%s OK (%zu ranks, %lld passes on rank 0, %ld fused)\n", c.name, multi.size(),
+              (long long)multi[0].passes, fused);
+  return g_fail.load() != fails0;
+}
+
+}  // namespace
+
+int main() {
+  const Case cases[] = {
+      {"perf_hide K=1 2x2 open", {2, 2, 1}, {0, 0, 0}, 40, 36, 1, Mode::kHide, 13, ""},
+      {"perf K=1 3x1 periodic-x", {3, 1, 1}, {1, 0, 0}, 30, 28, 1, Mode::kPerf, 11, ""},
+      {"perf_hide K=4 2x2 periodic", {2, 2, 1}, {1, 1, 0}, 48, 44, 4, Mode::kHide, 19, ""},
+      {"perf_hide K=8 2x1 split", {2, 1, 1}, {0, 0, 0}, 800, 120, 8, Mode::kHide, 21, "0"},
+      {"perf_hide K=8 2x1 fused", {2, 1, 1}, {0, 0, 0}, 800, 120, 8, Mode::kHide, 21, "1"},
+      {"perf_hide K=8 2x2 fused", {2, 2, 1}, {0, 1, 0}, 760, 400, 8, Mode::kHide, 17, "1"},
+      // 64-row tasks: the table's 16 rows at this height are shorter than the
+      // 2K - 1 rows an aligned band must hold, so the frame would not be aligned
+      {"perf_hide K=24 2x1 fused", {2, 1, 1}, {0, 0, 0}, 700, 400, 24, Mode::kHide, 50, "1", 64},
+      {"perf_hide K=24 2x2 auto", {2, 2, 1}, {1, 1, 0}, 700, 400, 24, Mode::kHide, 48, "", 64},
+      {"perf K=8 1x2 periodic-y", {1, 2, 1}, {0, 1, 0}, 64, 60, 8, Mode::kPerf, 17, ""},
+  };
+  for (const Case& c : cases)
+    if (run_case(c)) return 1;
+  std::printf("frame flags raised %ld\n", g_signals.load());
+  CHECK(rma_stub::live_events() == 0, "events leaked: %ld", rma_stub::live_events().load());
+  if (g_fail.load()) return 1;
+  std::printf("executor selftest OK\n");
+  return 0;
+}

@@ -77,6 +77,7 @@ typedef enum hipError_t {
   hipSuccess = 0,
   hipErrorInvalidValue = 1,
   hipErrorInvalidResourceHandle = 400,
+  hipErrorNotSupported = 801,
 } hipError_t;
 
 typedef enum hipMemcpyKind {
@@ -92,6 +93,23 @@ typedef enum hipMemcpyKind {
 #define hipHostMallocMapped 0x2
 #define hipHostRegisterMapped 0x2
 #define hipIpcMemLazyEnablePeerAccess 0x1
+#define hipStreamNonBlocking 0x1
+
+typedef enum hipDeviceAttribute_t {
+  hipDeviceAttributeMultiprocessorCount = 63,
+  hipDeviceAttributeWallClockRate = 200,
+} hipDeviceAttribute_t;
+typedef enum hipStreamCaptureMode {
+  hipStreamCaptureModeGlobal = 0,
+  hipStreamCaptureModeThreadLocal = 1,
+  hipStreamCaptureModeRelaxed = 2,
+} hipStreamCaptureMode;
+struct ihipGraph;
+struct hipGraphExec;
+typedef ihipGraph* hipGraph_t;
+typedef hipGraphExec* hipGraphExec_t;
+struct hipGraphNode;
+typedef hipGraphNode* hipGraphNode_t;
 
 typedef struct hipIpcMemHandle_st {
   char reserved[64];
@@ -125,6 +143,66 @@ inline std::atomic<long>& waits() {
 }
 }  // namespace rma_stub
 
+// streams: distinct non-null handles (work runs at enqueue time anyway)
+namespace rma_stub {
+inline std::atomic<long>& live_streams() {
+  static std::atomic<long> n{0};
+  return n;
+}
+// the executor's fused-pass policy counts tasks per CU: a small "device"
+// (RMA_STUB_CUS, default 2) makes test-sized tiles take that path too
+inline int stub_cus() {
+  const char* e = std::getenv("RMA_STUB_CUS");
+  return e && *e ? std::atoi(e) : 2;
+}
+}  // namespace rma_stub
+inline hipError_t hipStreamCreateWithPriority(hipStream_t* s, unsigned, int) {
+  *s = reinterpret_cast<hipStream_t>(new char);
+  ++rma_stub::live_streams();
+  return hipSuccess;
+}
+inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned f) {
+  return hipStreamCreateWithPriority(s, f, 0);
+}
+inline hipError_t hipStreamDestroy(hipStream_t s) {
+  delete reinterpret_cast<char*>(s);
+  --rma_stub::live_streams();
+  return hipSuccess;
+}
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipDeviceGetStreamPriorityRange(int* least, int* greatest) {
+  *least = 0;
+  *greatest = -1;
+  return hipSuccess;
+}
+inline hipError_t hipGetDevice(int* d) {
+  *d = 0;
+  return hipSuccess;
+}
+inline hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t a, int) {
+  *v = a == hipDeviceAttributeMultiprocessorCount ? rma_stub::stub_cus() : 100000;
+  return hipSuccess;
+}
+inline hipError_t hipEventCreate(hipEvent_t* e);
+inline hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) {
+  *ms = 0.0f;
+  return hipSuccess;
+}
+// graphs: not modelled (the executor only captures with a capturable transport)
+inline hipError_t hipStreamBeginCapture(hipStream_t, hipStreamCaptureMode) {
+  return hipErrorNotSupported;
+}
+inline hipError_t hipStreamEndCapture(hipStream_t, hipGraph_t* g) {
+  *g = nullptr;
+  return hipErrorNotSupported;
+}
+inline hipError_t hipGraphInstantiate(hipGraphExec_t*, hipGraph_t, hipGraphNode_t*, char*, size_t) {
+  return hipErrorNotSupported;
+}
+inline hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t) { return hipErrorNotSupported; }
+inline hipError_t hipGraphDestroy(hipGraph_t) { return hipSuccess; }
+inline hipError_t hipGraphExecDestroy(hipGraphExec_t) { return hipSuccess; }
+
 inline const char* hipGetErrorName(hipError_t e) { return e == hipSuccess ? "hipSuccess" : "hipError"; }
 inline const char* hipGetErrorString(hipError_t e) { return e == hipSuccess ? "no error" : "stub error"; }
 inline hipError_t hipGetLastError() { return hipSuccess; }
@@ -142,6 +220,7 @@ inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
   ++rma_stub::live_events();
   return hipSuccess;
 }
+inline hipError_t hipEventCreate(hipEvent_t* e) { return hipEventCreateWithFlags(e, 0); }
 inline hipError_t hipEventDestroy(hipEvent_t e) {
   if (!e) return hipErrorInvalidResourceHandle;
   if (e->magic != rma_stub::kAlive) rma_stub::dead_event("hipEventDestroy");
@@ -175,6 +254,15 @@ inline hipError_t hipMalloc(void** p, size_t n) {
   ++rma_stub::live_allocs();
   return hipSuccess;
 }
+template <typename T>
+inline hipError_t hipMalloc(T** p, size_t n) {  // HIP's typed overload
+  return hipMalloc(reinterpret_cast<void**>(p), n);
+}
+inline hipError_t hipMemset(void* p, int v, size_t n) {
+  std::memset(p, v, n);
+  return hipSuccess;
+}
+inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { return hipMemset(p, v, n); }
 inline hipError_t hipFree(void* p) {
   if (p) {
     std::free(p);

@@ -9,7 +9,9 @@ buffer reallocation (per-dimension, cross and merged groups), and endpoint
 teardown while peers finish; and the HIP IPC transport (csrc/runtime/ipc.cpp)
 between rank threads standing in for processes, in host and stream mode
 (shared-memory flags, mailbox overflow of a later peer, bounded wait
-timeout). Built with clang's ThreadSanitizer (its runtime
+timeout); and the executor's time loop on rank threads
+(tests/native/executor_selftest.cpp, kernels as CPU twins, bitwise against
+one rank). Built with clang's ThreadSanitizer (its runtime
 intercepts pthread_cond_clockwait, which g++ 11's libtsan does not) and with
 AddressSanitizer + UBSan.
 
@@ -30,6 +32,12 @@ PRE_FIX = "5704426"
 SRCS = ["tests/native/threaded_selftest.cpp", "csrc/runtime/loopback.cpp", "csrc/runtime/halo.cpp",
         "csrc/runtime/halo_plan.cpp", "csrc/runtime/topology.cpp", "csrc/runtime/errors.cpp",
         "csrc/runtime/ipc.cpp", "csrc/kernels/cpu_kernels.cpp"]
+# the executor's time loop (csrc/runtime/executor.cpp) with the kernels' CPU twins
+EXEC_SRCS = ["tests/native/executor_selftest.cpp", "csrc/runtime/executor.cpp",
+             "csrc/runtime/plan.cpp", "csrc/runtime/loopback.cpp", "csrc/runtime/halo.cpp",
+             "csrc/runtime/halo_plan.cpp", "csrc/runtime/topology.cpp", "csrc/runtime/errors.cpp",
+             "csrc/runtime/trace.cpp", "csrc/kernels/cpu_kernels.cpp",
+             "csrc/kernels/kernel_select.cpp"]
 SAN = {"tsan": ["-fsanitize=thread"],
        "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]}
 ENV = {"tsan": {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"},
@@ -42,7 +50,7 @@ def _build(kind, out, srcs, extra_inc=()):
     cmd = [CLANG, "-std=c++17", "-O1", "-g", "-ffp-contract=off", "-fno-omit-frame-pointer",
            *SAN[kind], "-I", os.path.join(ROOT, "tests", "native", "hip_stub"),
            *[a for d in extra_inc for a in ("-I", d)], "-I", os.path.join(ROOT, "csrc", "include"),
-           *srcs, "-o", str(out), "-lpthread"]
+           *srcs, "-o", str(out), "-lpthread", "-ldl"]
     r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
 
@@ -93,7 +101,10 @@ def test_pre_fix_loopback_teardown_race_is_reported(kind, tmp_path):
 def test_ipc_slot_reuse_without_the_done_wait_is_reported(tmp_path):
     """Mutation check of the IPC half: with the sender's "receive done" wait
     removed (host mode reuses mailbox slot g % 2 before the peer's receive of
-    g - 2 has copied it out), ThreadSanitizer must report the mailbox race."""
+    g - 2 has copied it out), the build must fail: ThreadSanitizer reports the
+    mailbox race, or -- when a sender two groups ahead overwrites the slot
+    before the receiver copies it out -- the selftest's bitwise check of the
+    received data fails first (which of the two comes first is timing)."""
     src = open(os.path.join(ROOT, "csrc", "runtime", "ipc.cpp")).read()
     needle = "} else if (g > 2) {  // slot g % 2"
     assert src.count(needle) == 1
@@ -104,4 +115,25 @@ def test_ipc_slot_reuse_without_the_done_wait_is_reported(tmp_path):
     _build("tsan", exe, srcs)
     r = _run("tsan", exe)
     assert r.returncode != 0
-    assert "ThreadSanitizer: data race" in r.stderr and "IpcTransport::enqueue_group" in r.stderr
+    race = "ThreadSanitizer: data race" in r.stderr and "IpcTransport::enqueue_group" in r.stderr
+    corrupt = "ipc mode 0 rank" in r.stderr  # threaded_selftest.cpp ipc_ring's data check
+    assert race or corrupt, r.stderr[-3000:]
+
+
+@needs_clang
+@pytest.mark.parametrize("kind", ["tsan", "asan"])
+def test_executor_time_loop_on_rank_threads_clean_and_bitwise(kind, tmp_path):
+    """tests/native/executor_selftest.cpp: DiffusionExecutor on 2-4 rank
+    threads over the loopback transport (perf / perf_hide, canonical K = 1 and
+    fast-math K = 4 / 8 / 24, open and periodic grids, split launches and the
+    frame-first fused pass) == the same grid on one rank, bitwise, with the
+    kernels as their CPU twins; clean under TSan and under ASan + UBSan (the
+    process-wide stream pool's streams are kept for the process lifetime by
+    design and suppressed by name)."""
+    exe = tmp_path / f"executor_{kind}"
+    _build(kind, exe, [os.path.join(ROOT, s) for s in EXEC_SRCS])
+    r = _run(kind, exe)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-6000:]
+    assert "executor selftest OK" in r.stdout
+    assert "fused)" in r.stdout and "perf_hide K=24 2x2 auto OK" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr
