@@ -395,6 +395,10 @@ for s in "$@"; do
                       eqn4096_xy_fused eqn16384_xy eqn16384_xy_fused eqn8192_x eqn8192_x_fused \
                       eqn8192_y eqn8192_y_fused; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    k1tiles) for n in 4096 8192 12288 16384; do
+               step "k1_$n" 300 python bench/rccl_self_overhead.py --n $n --K 1 --variants perf_hide,perf \
+                 --periodic xy --steps 400 --pattern opop --spacing equal --out "$OUT/k1_$n.json" || exit 1
+             done ;;
     eqsplit) for t in eqn8192_xy eqn8192_xy_skip eqn8192_xy_perf eqn2048_xy eqn2048_xy_skip \
                       eqn2048_xy_perf eqn4096_xy eqn4096_xy_skip; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
