@@ -174,6 +174,7 @@ class DiffusionExecutor {
   int cus_ = 256;  // compute units of the device
   int64_t fused_passes_ = 0;
   double fused_timeout_s_ = 60.0;
+  int fused_fdiv_ = 1;  // frame rects' rows per task = the pass's / this (RMA_FUSED_FRAME_DIV)
   uint64_t* sig_ = nullptr;
   uint32_t* ferr_host_ = nullptr;
   uint32_t* ferr_dev_ = nullptr;

@@ -43,6 +43,7 @@ struct StencilTuning {
   // those rects without waiting for the rest of the launch.
   uint64_t* signal = nullptr;
   int signal_rects = 0;
+  int signal_chunk_rows = 0;  // rows per task of the signal rects (0: chunk_rows)
 };
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,

@@ -34,6 +34,7 @@ struct RectList {
   int64_t block_end[kMaxRects];  // inclusive prefix sum of blocks per rect
   int64_t gpad[kMaxRects];       // >0: row-aligned mapping with gpad blocks per chunk row,
                                  // 0: linear task mapping, -1: column mode (thin rects)
+  int64_t crows[kMaxRects];      // pipelined kernels: rows per task of each rect
   int n;
   // frame-first fused pass (pipelined kernels; executor RMA_EXEC_FUSED): the
   // first sig_blocks blocks (the frame rects' tasks, dispatched first, never
@@ -225,8 +226,11 @@ inline int64_t plan_rects(RectList& L, const Rect* rects, int nrects, int V, int
 // one block per (strip, chunk) task, strips as in plan_rects with halo > 0;
 // block b of a rect is (chunk = lb / strips, strip = lb % strips).
 // sw_block: input columns of one strip task (0: one wave window, 64 V).
+// rect_rows (optional): rows per task of each rect instead of chunk_rows
+// (a fused pass's frame rects, RectList::sig).
 inline int64_t plan_strip_tasks(RectList& L, const Rect* rects, int nrects, int V,
-                                int chunk_rows, int halo, int64_t sw_block = 0) {
+                                int chunk_rows, int halo, int64_t sw_block = 0,
+                                const int* rect_rows = nullptr) {
   L = RectList{};
   int64_t total = 0;
   const int64_t sw = sw_block > 0 ? sw_block : (int64_t)kWave * V;
@@ -239,7 +243,9 @@ inline int64_t plan_strip_tasks(RectList& L, const Rect* rects, int nrects, int 
     const int64_t x0 = r.x0 - halo;
     L.xa[n] = x0 - (((x0 % V) + V) % V);
     L.strips[n] = (r.x1 - (L.xa[n] + halo) + step - 1) / step;
-    L.chunks[n] = (r.y1 - r.y0 + chunk_rows - 1) / chunk_rows;
+    const int64_t cr = rect_rows && rect_rows[i] > 0 ? rect_rows[i] : chunk_rows;
+    L.crows[n] = cr;
+    L.chunks[n] = (r.y1 - r.y0 + cr - 1) / cr;
     L.gpad[n] = 0;
     total += L.strips[n] * L.chunks[n];
     L.block_end[n] = total;

@@ -263,8 +263,9 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   const int64_t strip = lb % L.strips[ri], chunk = lb / L.strips[ri];
   const Rect r = L.r[ri];
   const int64_t xs = L.xa[ri] + strip * kStep;
-  const int64_t ya = r.y0 + chunk * chunk_rows;
-  const int64_t yb = min(r.y1, ya + (int64_t)chunk_rows);
+  const int64_t crows = L.crows[ri];  // == chunk_rows unless a fused pass's frame rect
+  const int64_t ya = r.y0 + chunk * crows;
+  const int64_t yb = min(r.y1, ya + crows);
 
   // the columns [lo, hi) of this wave's window it writes to the block rows
   // (the stage boundary with the neighbouring column wave at the window
@@ -802,15 +803,22 @@ struct PipeLaunch {
   hipStream_t stream;
   uint64_t* sig = nullptr;  // fused pass: the first sig_rects rects signal (RectList::sig)
   int sig_rects = 0;
+  int sig_chunk_rows = 0;   // ...with this many rows per task (0: chunk_rows)
 };
 
 // Plans the (strip, chunk) tasks with this instantiation's block width
 // (Geo::WB, kStep), so host planning and kernel geometry cannot disagree.
 template <int K, int S, int V, int Ar, int C = 1>
 void launch(const PipeLaunch& a) {
+  int rows_buf[kMaxRects] = {};
+  const int* rows = nullptr;
+  if (a.sig && a.sig_chunk_rows > 0) {
+    for (int i = 0; i < a.sig_rects && i < kMaxRects; ++i) rows_buf[i] = a.sig_chunk_rows;
+    rows = rows_buf;
+  }
   RectList L;
   const int64_t blocks =
-      plan_strip_tasks(L, a.rects, a.nrects, V, a.chunk_rows, K, Geo<K, S, V, C>::WB);
+      plan_strip_tasks(L, a.rects, a.nrects, V, a.chunk_rows, K, Geo<K, S, V, C>::WB, rows);
   static_assert(Geo<K, S, V, C>::kStep == (Geo<K, S, V, C>::WB - 2 * K) / V * V, "strip step");
   if (L.n == 0) return;
   RMA_CHECK_ARG(blocks < (int64_t(1) << 31), "grid too large: " << blocks << " blocks");

@@ -62,6 +62,8 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
                   "signal rects " << tune.signal_rects << " of " << nrects);
     a.sig = tune.signal;
     a.sig_rects = tune.signal_rects;
+    RMA_CHECK_ARG(tune.signal_chunk_rows >= 0, "signal_chunk_rows=" << tune.signal_chunk_rows);
+    a.sig_chunk_rows = tune.signal_chunk_rows;
   }
   // V = 5 only in the lab (the core units' cases take any V other than 4 and 2 as 1)
   bool ok = C == 1 && V != 5 &&

@@ -208,6 +208,8 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
     cus_ = cus > 0 ? cus : 256;
   }
   if (const char* ft = std::getenv("RMA_EXEC_FUSED_TIMEOUT")) fused_timeout_s_ = std::atof(ft);
+  if (const char* fd = std::getenv("RMA_FUSED_FRAME_DIV"))
+    fused_fdiv_ = fd[0] ? std::max(1, std::atoi(fd)) : 1;
   if (fused_ && p_.mode == Mode::kHide) {
     RMA_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&sig_), 2 * sizeof(uint64_t)));
     RMA_HIP_CHECK(hipMemset(sig_, 0, 2 * sizeof(uint64_t)));
@@ -521,6 +523,8 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     StencilTuning ft = tn;
     ft.signal = sig_;
     ft.signal_rects = nf;
+    // shorter frame tasks finish earlier in the launch (fused_fdiv_)
+    if (fused_fdiv_ > 1) ft.signal_chunk_rows = std::max(1, tn.chunk_rows / fused_fdiv_);
     rec(0, s_hi_);
     rec(3, s_lo_);
     {

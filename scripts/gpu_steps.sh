@@ -370,13 +370,14 @@ for s in "$@"; do
              --steps 960 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
     eqn*) # eqn<N>_<dims>[_strips][_cd<D>][_bol|_btask]: N^2 tile, K=24, equal coefficients
              t=${s#eqn}; n=${t%%_*}; t=${t#*_}; d=${t%%_*}; fa=""; cd=""; fb=""; hm=""; lg=""
-             mc=""; pp=""; sk=""; va="perf_hide"; fu=""
+             mc=""; pp=""; sk=""; va="perf_hide"; fu=""; fd=""
              for tok in ${t//_/ }; do case $tok in strips) fa=0 ;; cd*) cd=${tok#cd} ;;
-               skip) sk=1 ;; perf) va=perf ;; fused) fu=1 ;; split) fu=0 ;;
+               skip) sk=1 ;; perf) va=perf ;; fused) fu=1 ;; split) fu=0 ;; fd*) fd=${tok#fd} ;;
                bol) fb=ol ;; btask) fb=task ;; nomerge) hm=0 ;; nolag) lg=0 ;;
                ch*) mc=${tok#ch} ;; pp*) pp=${tok#pp} ;; esac; done
              RMA_EXEC_LAG=$lg RMA_HALO_MERGED=$hm RMA_FRAME_BANDS=$fb RMA_FRAME_CHUNK_DIV=$cd \
-             RMA_FRAME_ALIGNED=$fa RMA_DIAG_SKIP_EXCHANGE=$sk RMA_EXEC_FUSED=$fu step "$s" 300 env \
+             RMA_FRAME_ALIGNED=$fa RMA_DIAG_SKIP_EXCHANGE=$sk RMA_EXEC_FUSED=$fu RMA_FUSED_FRAME_DIV=$fd \
+             step "$s" 300 env \
              ${mc:+NCCL_MAX_P2P_NCHANNELS=$mc} ${pp:+NCCL_NCHANNELS_PER_PEER=$pp} \
              python bench/rccl_self_overhead.py --n "$n" --K 24 --variants $va \
              --periodic "$d" --steps 2400 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
@@ -388,6 +389,10 @@ for s in "$@"; do
     eq_xy_fused|eq_xy_split) fu=1; [ $s = eq_xy_split ] && fu=0
              RMA_EXEC_FUSED=$fu step "$s" 400 python bench/rccl_self_overhead.py --K 24 --periodic xy \
              --steps 320 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    eqfdiv) for t in eqn2048_xy_split eqn2048_xy_fused eqn2048_xy_fused_fd2 eqn2048_xy_fused_fd3 \
+                     eqn4096_xy_split eqn4096_xy_fused_fd2 eqn4096_xy_fused_fd4 eqn8192_xy_fused \
+                     eqn8192_xy_fused_fd2; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     eqauto) for t in eq_xy_split eq_xy_fused eqn12288_xy_split eqn12288_xy_fused eqn12288_xy \
                      eqn8192_xy eqn4096_xy eqn2048_xy; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;

@@ -521,12 +521,13 @@ def spmd_fused(rank, hub, nx, ny, nt, dims, K, graph=False):
     return out
 
 
+@pytest.mark.parametrize("fdiv", ["1", "3"])
 @pytest.mark.parametrize("dims,K,nx,ny,nt,some", [((2, 2), 24, 1100, 3500, 53, True),
                                                   ((2, 1), 20, 1100, 1500, 47, True),
                                                   ((1, 2), 8, 800, 2600, 19, True),
                                                   ((2, 2), 16, 700, 900, 37, False),
                                                   ((2, 2), 12, 1000, 3000, 31, True)])
-def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, some, monkeypatch):
+def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, some, fdiv, monkeypatch):
     """RMA_EXEC_FUSED=1: every K-step pass with a neighbour is ONE pipelined
     launch, frame tasks first, whose last frame block raises the flag the
     exchange stream waits on (flags.hip); every tile == its window of the
@@ -534,6 +535,7 @@ def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, some, monkeypatch
     the pass's grid) really ran fused -- the others (all of them in the
     700x900 case: tiles too small for aligned frames) keep the split launches."""
     monkeypatch.setenv("RMA_EXEC_FUSED", "1")
+    monkeypatch.setenv("RMA_FUSED_FRAME_DIV", fdiv)  # 3: frame tasks of 1/3 the rows
     P = dims[0] * dims[1]
     res = run_loopback(P, spmd_fused, nx, ny, nt, dims, K, timeout=240)
     nxg, nyg, _ = res[0][2]
