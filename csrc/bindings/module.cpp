@@ -519,6 +519,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("steps_done", &DiffusionExecutor::steps_done)
       .def_property_readonly("passes_done", &DiffusionExecutor::passes_done)
       .def_property_readonly("fused_passes", &DiffusionExecutor::fused_passes)
+      .def("check_error", &DiffusionExecutor::check_error)
       .def("plan", &DiffusionExecutor::plan, py::arg("nsteps"))
       .def_property_readonly("pass_costs", &DiffusionExecutor::pass_costs)
       .def("prime", &DiffusionExecutor::prime, py::call_guard<py::gil_scoped_release>())

@@ -118,6 +118,9 @@ class DiffusionExecutor {
   int64_t passes_done() const { return passes_; }
   // passes enqueued as frame-first fused launches (RMA_EXEC_FUSED)
   int64_t fused_passes() const { return fused_passes_; }
+  // throws if a fused pass's bounded wait for its frame flag timed out (the
+  // halos of that pass are wrong); also checked at every run() and timings()
+  void check_error() const { check_fused_error(); }
   std::vector<Rect> frame_rects() const { return frame_; }
   Rect interior_rect() const { return interior_; }
   Rect full_rect() const { return full_; }

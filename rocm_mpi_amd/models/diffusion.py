@@ -527,6 +527,8 @@ class Diffusion2D:
     def synchronize(self) -> None:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+        if self.executor is not None and hasattr(self.executor, "check_error"):
+            self.executor.check_error()  # a fused pass's timed-out frame wait, if any
 
     def check_finite(self) -> None:
         bad = float(ops.reduce(self.field, "nonfinite"))
@@ -632,8 +634,10 @@ class Diffusion2D:
         return info
 
     def close(self) -> None:
-        self.synchronize()
-        self.executor = None
-        self._ap_graph = None
-        if self._owns_grid:
-            gg.finalize_global_grid()
+        try:
+            self.synchronize()  # raises a pending executor error; resources go either way
+        finally:
+            self.executor = None
+            self._ap_graph = None
+            if self._owns_grid:
+                gg.finalize_global_grid()

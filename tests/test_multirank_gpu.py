@@ -582,8 +582,8 @@ def test_fused_passes_over_rccl_self_equal_the_split_passes(graph, monkeypatch):
 def test_fused_pass_wait_timeout_is_reported_not_hung(monkeypatch):
     """The exchange stream's wait for the frame flag is bounded: with a
     timeout far below a frame's run time every wait gives up, the passes still
-    drain (no hang; halos of those passes are wrong) and the next run() /
-    pass_timings() raises the timeout instead of returning silently."""
+    drain (no hang; halos of those passes are wrong) and synchronize() and
+    the next run() raise the timeout instead of returning silently."""
     K, n = 24, 1536
     monkeypatch.setenv("RMA_EXEC_FUSED", "1")
     monkeypatch.setenv("RMA_EXEC_FUSED_TIMEOUT", "1e-7")
@@ -593,12 +593,15 @@ def test_fused_pass_wait_timeout_is_reported_not_hung(monkeypatch):
                                     quiet=True, periods=(1, 1, 0), temporal=K, fast_math=True))
     try:
         m.step(48)
-        m.synchronize()
-        assert m.executor.fused_passes == 2
         with pytest.raises(RuntimeError, match="timed out"):  # the native module's NativeError
+            m.synchronize()
+        assert m.executor.fused_passes == 2
+        with pytest.raises(RuntimeError, match="timed out"):
             m.step(K)
     finally:
-        m.close()
+        with pytest.raises(RuntimeError, match="timed out"):  # and close() still releases
+            m.close()
+        assert m.executor is None
         gg.finalize_global_grid()
 
 
