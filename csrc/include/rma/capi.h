@@ -103,6 +103,11 @@ int rma_executor_create_g(rma_grid* g, int mode, double* T, double* T2, const do
 int rma_grid_self_via_rccl(rma_grid* g);
 int rma_executor_run(rma_executor* e, int64_t nsteps, void* stream);
 int rma_executor_parity(const rma_executor* e);
+/* After the caller synchronised: nonzero (with rma_last_error) if a
+ * frame-first fused pass's bounded wait for its frame flag timed out (the
+ * halos of that pass are wrong); also reported by the next rma_executor_run.
+ * out_fused (may be NULL): passes run as fused launches so far. */
+int rma_executor_check(const rma_executor* e, int64_t* out_fused);
 int rma_executor_destroy(rma_executor* e);
 
 #ifdef __cplusplus

@@ -312,6 +312,13 @@ int rma_executor_run(rma_executor* e, int64_t nsteps, void* stream) {
 
 int rma_executor_parity(const rma_executor* e) { return e->ex->parity(); }
 
+int rma_executor_check(const rma_executor* e, int64_t* out_fused) {
+  return guard([&] {
+    if (out_fused) *out_fused = e->ex->fused_passes();
+    e->ex->check_error();
+  });
+}
+
 int rma_executor_destroy(rma_executor* e) {
   return guard([&] {
     if (!e) return;

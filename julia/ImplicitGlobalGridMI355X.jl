@@ -21,7 +21,7 @@ module ImplicitGlobalGridMI355X
 using Libdl
 
 export init_global_grid, finalize_global_grid, update_halo!, gather!, nx_g, ny_g, nz_g,
-       x_g, y_g, z_g, tic, toc, DiffusionExecutor, run!, current_field
+       x_g, y_g, z_g, tic, toc, DiffusionExecutor, run!, current_field, check_executor
 
 const LIB = Ref{Ptr{Cvoid}}(C_NULL)
 const GRID = Ref{Ptr{Cvoid}}(C_NULL)
@@ -162,5 +162,13 @@ run!(ex::DiffusionExecutor, n::Integer; stream::Ptr{Cvoid}=C_NULL) =
 
 current_field(ex::DiffusionExecutor) =
     ex.T2 === nothing || ccall(sym(:rma_executor_parity), Cint, (Ptr{Cvoid},), ex.ptr) == 0 ? ex.T : ex.T2
+
+# after synchronising the stream: throws if a frame-first fused pass timed out
+# waiting for its frame flag (rma_executor_check); returns the fused-pass count
+function check_executor(ex::DiffusionExecutor)
+    nf = Ref{Int64}(0)
+    check(ccall(sym(:rma_executor_check), Cint, (Ptr{Cvoid}, Ref{Int64}), ex.ptr, nf))
+    return nf[]
+end
 
 end # module

@@ -385,6 +385,7 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_fused_frame_first_passes_bitwise" \
              "tests/test_multirank_gpu.py::test_fused_passes_over_rccl_self_equal_the_split_passes" \
              "tests/test_multirank_gpu.py::test_fused_pass_wait_timeout_is_reported_not_hung" \
+             "tests/test_capi_gpu.py::test_capi_fused_passes_checked_and_bitwise" \
              -p no:cacheprovider || exit 1 ;;
     eq_xy_fused|eq_xy_split) fu=1; [ $s = eq_xy_split ] && fu=0
              RMA_EXEC_FUSED=$fu step "$s" 400 python bench/rccl_self_overhead.py --K 24 --periodic xy \

@@ -132,6 +132,44 @@ def test_capi_fast_math_executor_close(mode, K):
         ck(L, L.rma_finalize_global_grid(g))
 
 
+def test_capi_fused_passes_checked_and_bitwise(monkeypatch):
+    """A periodic fast-math perf_hide executor through the C ABI: with
+    RMA_EXEC_FUSED=1 its K=24 passes run as frame-first fused launches
+    (rma_executor_check: no timed-out frame wait, the fused-pass count) and
+    the field equals the split passes' bitwise."""
+    L = lib()
+    n, K, nt = 1536, 24, 72
+
+    def run(fused):
+        monkeypatch.setenv("RMA_EXEC_FUSED", "1" if fused else "0")
+        g = grid(L, n, n, K, periods=(1, 1, 0))
+        s = torch.cuda.current_stream().cuda_stream
+        T = torch.from_numpy(golden.initial(n, n)).cuda()
+        T2 = T.clone()
+        iCp = torch.ones_like(T)
+        ex = ctypes.c_void_p()
+        ck(L, L.rma_executor_create_kf(g, 1, ctypes.c_void_p(T.data_ptr()),
+                                       ctypes.c_void_p(T2.data_ptr()),
+                                       ctypes.c_void_p(iCp.data_ptr()), ctypes.c_int64(n),
+                                       ctypes.c_int64(n), coef4(L, g, n, n), ctypes.c_int64(1),
+                                       ctypes.c_int64(1), K, 1, None, None, None,
+                                       ctypes.byref(ex)))
+        ck(L, L.rma_executor_run(ex, ctypes.c_int64(nt), ctypes.c_void_p(s)))
+        par = L.rma_executor_parity(ex)
+        torch.cuda.synchronize()
+        nf = ctypes.c_int64(-1)
+        ck(L, L.rma_executor_check(ex, ctypes.byref(nf)))
+        field = (T2 if par else T).cpu().numpy()
+        ck(L, L.rma_executor_destroy(ex))
+        ck(L, L.rma_finalize_global_grid(g))
+        return field, nf.value
+
+    a, nfa = run(True)
+    b, nfb = run(False)
+    assert nfa == nt // K and nfb == 0
+    assert np.array_equal(a, b)
+
+
 def test_capi_update_halo_periodic_and_gather():
     L = lib()
     nx, ny = 130, 67

@@ -1,0 +1,54 @@
+"""The Julia front end (julia/ImplicitGlobalGridMI355X.jl) is a ccall shim over
+the C ABI; Julia is not installed here, so its behaviour stays unpinned. What
+can be pinned on the CPU: every C function the shim calls is declared in
+csrc/include/rma/capi.h and exported by the built librma_core.so, with the
+same number of arguments as the ccall passes."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from helpers import ROOT
+
+JL = os.path.join(ROOT, "julia", "ImplicitGlobalGridMI355X.jl")
+CAPI = os.path.join(ROOT, "csrc", "include", "rma", "capi.h")
+LIB = os.path.join(ROOT, "rocm_mpi_amd", "librma_core.so")
+
+
+def _ccalls():
+    src = open(JL).read()
+    out = {}
+    # ccall(sym(:name), Ret, (T1, T2, ...), args...)
+    for m in re.finditer(r"ccall\(sym\(:(\w+)\),\s*[\w{}]+,\s*\(([^()]*(?:\([^()]*\)[^()]*)*)\)",
+                         src):
+        types = [t for t in m.group(2).split(",") if t.strip()]
+        out.setdefault(m.group(1), set()).add(len(types))
+    return out
+
+
+def _capi_arity():
+    src = re.sub(r"/\*.*?\*/|//[^\n]*", "", open(CAPI).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(rma_\w+)\s*\(([^;{]*?)\)\s*;", src):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_every_shim_ccall_is_declared_with_its_arity():
+    calls, decl = _ccalls(), _capi_arity()
+    assert len(calls) >= 10
+    for name, arities in calls.items():
+        assert name in decl, f"{name} is called by the Julia shim but not declared in capi.h"
+        assert arities == {decl[name]}, (name, arities, decl[name])
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="librma_core.so not built")
+def test_every_shim_ccall_is_exported():
+    nm = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True)
+    if nm.returncode != 0:
+        pytest.skip("nm unavailable")
+    exported = {line.split()[-1] for line in nm.stdout.splitlines() if line.strip()}
+    missing = sorted(set(_ccalls()) - exported)
+    assert not missing, missing
