@@ -212,7 +212,13 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
     fused_fdiv_ = fd[0] ? std::max(1, std::atoi(fd)) : 1;
   if (fused_ && p_.mode == Mode::kHide) {
     RMA_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&sig_), 2 * sizeof(uint64_t)));
-    RMA_HIP_CHECK(hipMemset(sig_, 0, 2 * sizeof(uint64_t)));
+    // zeroed ON the executor's stream and waited for: a null-stream hipMemset
+    // is not ordered before work on these non-blocking streams, and a counter
+    // zeroed after (or never before) the first signalling launch never reaches
+    // its target, so the frame wait times out (seen with 4 processes sharing
+    // a GPU: the bench's shared-GPU rehearsal, profiles/SUMMARY_r5.md §6)
+    RMA_HIP_CHECK(hipMemsetAsync(sig_, 0, 2 * sizeof(uint64_t), S(s_lo_)));
+    RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
     RMA_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ferr_host_), sizeof(uint32_t),
                                 hipHostMallocMapped));
     *ferr_host_ = 0;

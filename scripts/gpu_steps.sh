@@ -264,7 +264,7 @@ for s in "$@"; do
                step "rehearse$n" 400 python bench.py --gpus $n --shared-gpu-test --shared-gpu-transport rccl \
                  --nx 4096 --steps 96 --warmup 4 --json-out "$OUT/rehearse$n.json" || exit 1
              done ;;
-    rehearse_fused) for n in 2 4; do
+    rehearse_fused) for n in 2 4 8; do
                step "rehearse_fused$n" 400 python bench.py --gpus $n --shared-gpu-test --shared-gpu-transport rccl \
                  --nx 8192 --steps 96 --warmup 4 --json-out "$OUT/rehearse_fused$n.json" || exit 1
              done ;;
