@@ -449,12 +449,14 @@ bool DiffusionExecutor::fused_pass_ok(const PassGeom& g, const StencilTuning& tn
   int nf = 0;
   for (const Rect& r : g.frame) nf += r.empty() ? 0 : 1;
   if (nf == 0 || (int)g.frame.size() + 1 > kMaxRects) return false;
-  // auto: only with >= 2 waves of tasks per pass (2 blocks of 4 waves per CU
-  // at K = 10..24). Below that every task runs at once, the frame tasks end
-  // with the whole launch and the exchange is exposed; the split launches win
-  // there (RCCL-self x+y at K=24, equal coefficients, profiles/r5/fused/:
-  // 4096^2 1.2 % split vs 8.7 % fused, 2048^2 44 vs 50 %; 8192^2 5.6 -> 1.3 %)
-  return fused_ == 1 || g.tasks() >= 4 * (int64_t)cus_;
+  // auto: with more than one wave of tasks per pass (2 blocks of 4 waves per
+  // CU at K = 10..24). Within one wave every task runs at once, the frame
+  // tasks end with the whole launch and the exchange is exposed; the split
+  // launches win there. RCCL-self x+y at K=24, equal coefficients
+  // (profiles/r5/fused/): 2048^2 (~430 tasks) 44 % split vs 50 % fused, 4096^2
+  // (440) 1.2 vs 8.7 %; 5120^2 (675) 12.2 vs 2.7 %, 6144^2 (720) 11.3 vs 2.0 %,
+  // 7168^2 (980) 11.1 vs 0.4 %, 8192^2 5.6 vs 1.3 %
+  return fused_ == 1 || g.tasks() > 2 * (int64_t)cus_;
 }
 
 void DiffusionExecutor::check_fused_error() const {

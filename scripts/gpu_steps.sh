@@ -390,6 +390,15 @@ for s in "$@"; do
     eq_xy_fused|eq_xy_split) fu=1; [ $s = eq_xy_split ] && fu=0
              RMA_EXEC_FUSED=$fu step "$s" 400 python bench/rccl_self_overhead.py --K 24 --periodic xy \
              --steps 320 --pattern opop --spacing equal --out "$OUT/$s.json" || exit 1 ;;
+    eqauto2) for t in eqn4096_xy eqn5120_xy eqn6144_xy eqn7168_xy eqn8192_xy eqn2048_xy eqn4096_x \
+                      eqn4096_y eqn6144_x eqn6144_y; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    eqy) for t in eqn6144_y_split eqn6144_y_fused eqn6144_y_split eqn6144_y_fused eqn5120_y_split \
+                  eqn5120_y_fused eqn6144_x_split eqn6144_x_fused; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    eqbound) for t in eqn6144_xy_split eqn6144_xy_fused eqn7168_xy_split eqn7168_xy_fused \
+                      eqn5120_xy_split eqn5120_xy_fused eqn8192_y_split eqn8192_y_fused; do
+               bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
     eqfdiv) for t in eqn2048_xy_split eqn2048_xy_fused eqn2048_xy_fused_fd2 eqn2048_xy_fused_fd3 \
                      eqn4096_xy_split eqn4096_xy_fused_fd2 eqn4096_xy_fused_fd4 eqn8192_xy_fused \
                      eqn8192_xy_fused_fd2; do
