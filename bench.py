@@ -1053,9 +1053,12 @@ def run(a, world: int, rank: int) -> int:
             tdesc = {"rccl": "RCCL send/recv over xGMI", "staged": "host-staged copies + gloo",
                      "gloo": "gloo (CPU twin)", "loopback": "in-process loopback",
                      "self": "periodic self copies"}.get(g.transport, g.transport)
-            par = f"halo: {tdesc}" + (", boundary frame + exchange on a high-priority stream "
-                                      "overlapped with the interior" if a.variant == "perf_hide"
-                                      else ", exchange after each pass")
+            fused_run = bool(exec_passes and exec_passes["fused"])
+            par = f"halo: {tdesc}" + (
+                (", frame-first fused launch per pass, exchange on a high-priority stream "
+                 "started by the frame tasks' device flag" if fused_run else
+                 ", boundary frame + exchange on a high-priority stream overlapped with the "
+                 "interior") if a.variant == "perf_hide" else ", exchange after each pass")
         # without a neighbour the solo re-time IS the run: no same-run efficiency
         eff_same = (solo / t_it) if solo and nbrs else None
         if shared:
