@@ -396,6 +396,9 @@ for s in "$@"; do
     eqy) for t in eqn6144_y_split eqn6144_y_fused eqn6144_y_split eqn6144_y_fused eqn5120_y_split \
                   eqn5120_y_fused eqn6144_x_split eqn6144_x_fused; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
+    trace_fused) prof trace_fused 300 --kernel-trace -d "$R/$OUT/trace_fused" -o run -- python3 \
+             "$R/bench/rccl_self_overhead.py" --n 8192 --K 24 --periodic xy --steps 240 --pattern p \
+             --spacing equal --out "$R/$OUT/trace_fused.json" || exit 1 ;;
     eqbound) for t in eqn6144_xy_split eqn6144_xy_fused eqn7168_xy_split eqn7168_xy_fused \
                       eqn5120_xy_split eqn5120_xy_fused eqn8192_y_split eqn8192_y_fused; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
