@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -259,6 +260,31 @@ int main() {
   };
   for (const Case& c : cases)
     if (run_case(c)) return 1;
+  // random fused-pass geometries (fixed seed): dims, periods, depth, rows per
+  // task, steps; tiles wide and tall enough for aligned frames
+  std::mt19937 rng(20251018u);
+  static std::vector<std::string> names;
+  names.reserve(8);
+  for (int i = 0; i < 6; ++i) {
+    const std::array<int, 3> dimsets[4] = {{2, 1, 1}, {1, 2, 1}, {2, 2, 1}, {3, 1, 1}};
+    Case c{};
+    c.dims = dimsets[rng() % 4];
+    c.periods = {(int)(rng() % 2), (int)(rng() % 2), 0};
+    c.K = 8 + (int)(rng() % 17);                          // 8..24
+    c.nx = 3 * (256 - 2 * c.K) + 2 * c.K + 8 + (int64_t)(rng() % 64);
+    c.chunk = 32 + 16 * (int)(rng() % 3);                 // 32, 48, 64
+    c.ny = 3 * c.chunk + 4 * c.K + (int64_t)(rng() % 80);
+    c.mode = Mode::kHide;
+    c.nt = c.K + 1 + (int)(rng() % (2 * c.K));
+    c.fused = "1";
+    names.push_back("random fused " + std::to_string(i) + " dims " + std::to_string(c.dims[0]) +
+                    "x" + std::to_string(c.dims[1]) + " per " + std::to_string(c.periods[0]) +
+                    std::to_string(c.periods[1]) + " K=" + std::to_string(c.K) + " tile " +
+                    std::to_string(c.nx) + "x" + std::to_string(c.ny) + " rows " +
+                    std::to_string(c.chunk) + " nt " + std::to_string(c.nt));
+    c.name = names.back().c_str();
+    if (run_case(c)) return 1;
+  }
   std::printf("frame flags raised %ld\n", g_signals.load());
   CHECK(rma_stub::live_events() == 0, "events leaked: %ld", rma_stub::live_events().load());
   if (g_fail.load()) return 1;
