@@ -399,6 +399,9 @@ for s in "$@"; do
     trace_fused) prof trace_fused 300 --kernel-trace -d "$R/$OUT/trace_fused" -o run -- python3 \
              "$R/bench/rccl_self_overhead.py" --n 8192 --K 24 --periodic xy --steps 240 --pattern p \
              --spacing equal --out "$R/$OUT/trace_fused.json" || exit 1 ;;
+    trace_fused_y) RMA_EXEC_FUSED=1 prof trace_fused_y 300 --kernel-trace -d "$R/$OUT/trace_fused_y" -o run \
+             -- python3 "$R/bench/rccl_self_overhead.py" --n 6144 --K 24 --periodic y --steps 240 \
+             --pattern op --spacing equal --out "$R/$OUT/trace_fused_y.json" || exit 1 ;;
     eqbound) for t in eqn6144_xy_split eqn6144_xy_fused eqn7168_xy_split eqn7168_xy_fused \
                       eqn5120_xy_split eqn5120_xy_fused eqn8192_y_split eqn8192_y_fused; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
