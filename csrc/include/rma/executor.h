@@ -182,6 +182,8 @@ class DiffusionExecutor {
   uint32_t* ferr_host_ = nullptr;
   uint32_t* ferr_dev_ = nullptr;
   bool fused_pass_ok(const PassGeom& g, const StencilTuning& tn) const;
+  bool fused_step_ok() const;
+  bool fused_step_ = false;  // one-step passes fused too (RMA_EXEC_FUSED_STEP=1)
   void check_fused_error() const;
   void* graph_exec_ = nullptr;  // hipGraphExec_t
   int64_t graph_len_ = 0;

@@ -38,16 +38,13 @@ namespace rma {
 namespace {
 using namespace march;
 
-template <int V, bool NT, int kUnroll, bool NTL, bool NTT = false>
-__global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restrict__ T2,
-                                                               const double* __restrict__ T,
-                                                               const double* __restrict__ iCp,
-                                                               int64_t nx, RectList L,
-                                                               StencilCoef k, int chunk_rows,
-                                                               int remap) {
+template <int V, bool NT, int kUnroll, bool NTL, bool NTT>
+__device__ __forceinline__ void march_body(double* __restrict__ T2, const double* __restrict__ T,
+                                           const double* __restrict__ iCp, int64_t nx,
+                                           const RectList& L, const StencilCoef& k,
+                                           int chunk_rows, int64_t b) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   int ri = 0;
   while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;  // wave-uniform, <= 8 steps
   const int64_t bstart = ri ? L.block_end[ri - 1] : 0;
@@ -125,6 +122,22 @@ __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restric
       rows[1][v] = rows[2][v];
     }
   }
+}
+
+template <int V, bool NT, int kUnroll, bool NTL, bool NTT = false>
+__global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restrict__ T2,
+                                                               const double* __restrict__ T,
+                                                               const double* __restrict__ iCp,
+                                                               int64_t nx, RectList L,
+                                                               StencilCoef k, int chunk_rows,
+                                                               int remap) {
+  // a fused one-step pass (RectList::sig): the frame rects' blocks come first,
+  // never XCD-remapped, and every one of their waves counts its completion
+  // (waves leave the body independently: column mode, padding waves)
+  const int64_t sig_first = L.sig ? L.sig_blocks : 0;
+  const int64_t b = remap ? xcd_remap_after(blockIdx.x, gridDim.x, sig_first) : (int64_t)blockIdx.x;
+  march_body<V, NT, kUnroll, NTL, NTT>(T2, T, iCp, nx, L, k, chunk_rows, b);
+  if (b < sig_first) signal_wave_done(L.sig, (int64_t)kWavesPerBlock * L.sig_blocks);
 }
 
 // ---------------------------------------------------------------------------
@@ -230,6 +243,16 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
   }
   if (L.n == 0) return;
   RMA_CHECK_ARG(total < (int64_t(1) << 31), "grid too large: " << total << " blocks");
+  if (tune.signal) {  // fused one-step pass: the first signal_rects rects' waves signal
+    RMA_CHECK_ARG(!lds, "a signalling launch needs the march kernel");
+    RMA_CHECK_ARG(tune.signal_rects >= 1 && tune.signal_rects < nrects,
+                  "signal rects " << tune.signal_rects << " of " << nrects);
+    int ns = 0;
+    for (int i = 0; i < tune.signal_rects; ++i) ns += rects[i].empty() ? 0 : 1;
+    RMA_CHECK_ARG(ns > 0, "signalling launch without a non-empty signal rect");
+    L.sig = tune.signal;
+    L.sig_blocks = L.block_end[ns - 1];
+  }
   const dim3 grid((unsigned)total), block(kBlock);
   hipStream_t s = as_stream(stream);
   if (lds) {

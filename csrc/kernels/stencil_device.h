@@ -142,6 +142,21 @@ __device__ __forceinline__ void signal_block_done(uint64_t* sig, int64_t nblocks
   }
 }
 
+// Per-wave variant for kernels whose waves leave independently (the one-step
+// march: column-mode threads, padding waves): lane 0 of every wave of the
+// signalling blocks counts, after the wave's own stores (the release fence
+// waits for all of the wave's memory operations, whatever the EXEC mask).
+__device__ __forceinline__ void signal_wave_done(uint64_t* sig, int64_t nwaves) {
+  if ((threadIdx.x & 63) == 0) {
+    const uint64_t old =
+        __hip_atomic_fetch_add(sig, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int64_t)old + 1 == nwaves) {
+      __hip_atomic_store(sig, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sig + 1, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // The canonical cell update (see rma/common.h StencilCoef). Compiled with
 // -ffp-contract=off: every operation rounds exactly as written, in this order.
 __device__ __forceinline__ double cell(double xl, double c, double xr, double up, double dn,

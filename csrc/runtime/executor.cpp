@@ -208,6 +208,7 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
     cus_ = cus > 0 ? cus : 256;
   }
   if (const char* ft = std::getenv("RMA_EXEC_FUSED_TIMEOUT")) fused_timeout_s_ = std::atof(ft);
+  if (const char* fs = std::getenv("RMA_EXEC_FUSED_STEP")) fused_step_ = fs[0] == '1';
   if (const char* fd = std::getenv("RMA_FUSED_FRAME_DIV"))
     fused_fdiv_ = fd[0] ? std::max(1, std::atoi(fd)) : 1;
   if (fused_ && p_.mode == Mode::kHide) {
@@ -396,6 +397,42 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
     if (p_.mode == Mode::kHide) RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
     return;
   }
+  if (fused_step_ok()) {
+    // frame-first fused one-step pass (as enqueue_pass): one march launch over
+    // the frame rects (first, never XCD-remapped) and the interior, whose
+    // frame waves raise sig_[1] for the exchange stream
+    TraceRange tr("rma.step.fused");
+    ++fused_passes_;
+    RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+    Rect rs[kMaxRects];
+    int n = 0;
+    for (const Rect& r : frame_) rs[n++] = r;
+    const int nf = n;
+    rs[n++] = interior_;
+    StencilTuning ft = p_.tune;
+    ft.signal = sig_;
+    ft.signal_rects = nf;
+    rec(0, s_hi_);
+    rec(3, s_lo_);
+    {
+      TraceRange ti("rma.fused");
+      stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, rs, n, c, ft, s_lo_);
+    }
+    rec(4, s_lo_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+    flag_wait_gpu(sig_ + 1, 1, fused_timeout_s_, ferr_dev_, 1, s_hi_);
+    flag_write_gpu(sig_ + 1, 0, s_hi_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_fr_), S(s_hi_)));
+    rec(1, s_hi_);
+    {
+      TraceRange th("rma.halo");
+      exchange(Tout, s_hi_);
+    }
+    rec(2, s_hi_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
+    if (ev[4]) tseq_.push_back(0);
+    return;
+  }
   TraceRange tr("rma.step.hide");
   // the frame waits for the previous step on both streams; the interior for
   // the previous frame and interior (lag_: not the previous exchange)
@@ -457,6 +494,15 @@ bool DiffusionExecutor::fused_pass_ok(const PassGeom& g, const StencilTuning& tn
   // (440) 1.2 vs 8.7 %; 5120^2 (675) 12.2 vs 2.7 %, 6144^2 (720) 11.3 vs 2.0 %,
   // 7168^2 (980) 11.1 vs 0.4 %, 8192^2 5.6 vs 1.3 %
   return fused_ == 1 || g.tasks() > 2 * (int64_t)cus_;
+}
+
+bool DiffusionExecutor::fused_step_ok() const {
+  // one-step passes: only on request (RMA_EXEC_FUSED_STEP=1; A/B, see
+  // profiles/SUMMARY_r5.md section 6), the march kernel, a frame and an interior
+  if (!sig_ || !fused_step_ || p_.tune.kernel == 1 || interior_.empty()) return false;
+  int nf = 0;
+  for (const Rect& r : frame_) nf += r.empty() ? 0 : 1;
+  return nf > 0 && (int)frame_.size() + 1 <= kMaxRects;
 }
 
 void DiffusionExecutor::check_fused_error() const {

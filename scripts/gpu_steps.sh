@@ -386,6 +386,8 @@ for s in "$@"; do
              "tests/test_multirank_gpu.py::test_fused_passes_over_rccl_self_equal_the_split_passes" \
              "tests/test_multirank_gpu.py::test_fused_pass_wait_timeout_is_reported_not_hung" \
              "tests/test_capi_gpu.py::test_capi_fused_passes_checked_and_bitwise" \
+             "tests/test_multirank_gpu.py::test_fused_one_step_passes_bitwise" \
+             "tests/test_multirank_gpu.py::test_fused_one_step_passes_over_rccl_self_equal_split" \
              -p no:cacheprovider || exit 1 ;;
     eq_xy_fused|eq_xy_split) fu=1; [ $s = eq_xy_split ] && fu=0
              RMA_EXEC_FUSED=$fu step "$s" 400 python bench/rccl_self_overhead.py --K 24 --periodic xy \
@@ -402,6 +404,13 @@ for s in "$@"; do
     trace_fused_y) RMA_EXEC_FUSED=1 prof trace_fused_y 300 --kernel-trace -d "$R/$OUT/trace_fused_y" -o run \
              -- python3 "$R/bench/rccl_self_overhead.py" --n 6144 --K 24 --periodic y --steps 240 \
              --pattern op --spacing equal --out "$R/$OUT/trace_fused_y.json" || exit 1 ;;
+    k1fused) for n in 8192 12288 16384 4096; do
+               for fs in 0 1; do
+                 RMA_EXEC_FUSED_STEP=$fs step "k1_${n}_fs$fs" 300 python bench/rccl_self_overhead.py --n $n \
+                   --K 1 --variants perf_hide --periodic xy --steps 400 --pattern opop --spacing equal \
+                   --out "$OUT/k1_${n}_fs$fs.json" || exit 1
+               done
+             done ;;
     eqbound) for t in eqn6144_xy_split eqn6144_xy_fused eqn7168_xy_split eqn7168_xy_fused \
                       eqn5120_xy_split eqn5120_xy_fused eqn8192_y_split eqn8192_y_fused; do
                bash "$0" OUT="$OUT" "$t" || exit 1; done ;;
