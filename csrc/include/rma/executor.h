@@ -183,6 +183,12 @@ class DiffusionExecutor {
   uint32_t* ferr_dev_ = nullptr;
   bool fused_pass_ok(const PassGeom& g, const StencilTuning& tn) const;
   bool fused_step_ok() const;
+  // the frame-first fused pass around `launch(rects, n, tuning)`: one launch
+  // of the frame rects + interior on the low stream, the frame-flag wait and
+  // the exchange on the high one (tn gets the signal fields)
+  template <typename Launch>
+  void enqueue_fused(const std::vector<Rect>& frame, const Rect& interior, StencilTuning tn,
+                     double* Tout, void* const* ev, Launch&& launch);
   bool fused_step_ = false;  // one-step passes fused too (RMA_EXEC_FUSED_STEP=1)
   void check_fused_error() const;
   void* graph_exec_ = nullptr;  // hipGraphExec_t

@@ -398,39 +398,14 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
     return;
   }
   if (fused_step_ok()) {
-    // frame-first fused one-step pass (as enqueue_pass): one march launch over
+    // frame-first fused one-step pass (enqueue_fused): one march launch over
     // the frame rects (first, never XCD-remapped) and the interior, whose
     // frame waves raise sig_[1] for the exchange stream
     TraceRange tr("rma.step.fused");
-    ++fused_passes_;
-    RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
-    Rect rs[kMaxRects];
-    int n = 0;
-    for (const Rect& r : frame_) rs[n++] = r;
-    const int nf = n;
-    rs[n++] = interior_;
-    StencilTuning ft = p_.tune;
-    ft.signal = sig_;
-    ft.signal_rects = nf;
-    rec(0, s_hi_);
-    rec(3, s_lo_);
-    {
-      TraceRange ti("rma.fused");
-      stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, rs, n, c, ft, s_lo_);
-    }
-    rec(4, s_lo_);
-    RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
-    flag_wait_gpu(sig_ + 1, 1, fused_timeout_s_, ferr_dev_, 1, s_hi_);
-    flag_write_gpu(sig_ + 1, 0, s_hi_);
-    RMA_HIP_CHECK(hipEventRecord(E(e_fr_), S(s_hi_)));
-    rec(1, s_hi_);
-    {
-      TraceRange th("rma.halo");
-      exchange(Tout, s_hi_);
-    }
-    rec(2, s_hi_);
-    RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
-    if (ev[4]) tseq_.push_back(0);
+    enqueue_fused(frame_, interior_, p_.tune, Tout, ev,
+                  [&](const Rect* rs, int n, const StencilTuning& t) {
+                    stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, rs, n, c, t, s_lo_);
+                  });
     return;
   }
   TraceRange tr("rma.step.hide");
@@ -505,6 +480,45 @@ bool DiffusionExecutor::fused_step_ok() const {
   return nf > 0 && (int)frame_.size() + 1 <= kMaxRects;
 }
 
+template <typename Launch>
+void DiffusionExecutor::enqueue_fused(const std::vector<Rect>& frame, const Rect& interior,
+                                      StencilTuning tn, double* Tout, void* const* ev,
+                                      Launch&& launch) {
+  ++fused_passes_;
+  auto rec = [&](int i, void* stream) {
+    if (ev[4]) RMA_HIP_CHECK(hipEventRecord(E(ev[i]), S(stream)));
+  };
+  // the whole launch waits for the previous exchange (its frame tasks read the
+  // halo) and, in stream order, for the previous launch
+  RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+  Rect rs[kMaxRects];
+  int n = 0;
+  for (const Rect& r : frame) rs[n++] = r;
+  tn.signal = sig_;
+  tn.signal_rects = n;
+  rs[n++] = interior;
+  rec(0, s_hi_);
+  rec(3, s_lo_);
+  {
+    TraceRange ti("rma.fused");
+    launch(rs, n, tn);
+  }
+  rec(4, s_lo_);
+  RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
+  // exchange stream: the frame flag (bounded wait), lowered for the next pass
+  flag_wait_gpu(sig_ + 1, 1, fused_timeout_s_, ferr_dev_, 1, s_hi_);
+  flag_write_gpu(sig_ + 1, 0, s_hi_);
+  RMA_HIP_CHECK(hipEventRecord(E(e_fr_), S(s_hi_)));
+  rec(1, s_hi_);
+  {
+    TraceRange th("rma.halo");
+    exchange(Tout, s_hi_);
+  }
+  rec(2, s_hi_);
+  RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
+  if (ev[4]) tseq_.push_back(0);
+}
+
 void DiffusionExecutor::check_fused_error() const {
   if (!ferr_host_) return;
   const uint32_t e = __atomic_load_n(ferr_host_, __ATOMIC_ACQUIRE);
@@ -567,37 +581,13 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     // grid. The next pass waits for this exchange (its frame tasks read the
     // halo) and, in stream order, for this launch.
     TraceRange tr("rma.pass.fused");
-    ++fused_passes_;
-    RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
-    Rect rs[kMaxRects];
-    int n = 0;
-    for (const Rect& r : g.frame) rs[n++] = r;
-    const int nf = n;
-    rs[n++] = g.interior;
     StencilTuning ft = tn;
-    ft.signal = sig_;
-    ft.signal_rects = nf;
     // shorter frame tasks finish earlier in the launch (fused_fdiv_)
     if (fused_fdiv_ > 1) ft.signal_chunk_rows = std::max(1, tn.chunk_rows / fused_fdiv_);
-    rec(0, s_hi_);
-    rec(3, s_lo_);
-    {
-      TraceRange ti("rma.fused");
-      multi_step(K, Tin, Tout, iCp_, nx_, ny_, rs, n, ft, s_lo_);
-    }
-    rec(4, s_lo_);
-    RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
-    flag_wait_gpu(sig_ + 1, 1, fused_timeout_s_, ferr_dev_, 1, s_hi_);
-    flag_write_gpu(sig_ + 1, 0, s_hi_);
-    RMA_HIP_CHECK(hipEventRecord(E(e_fr_), S(s_hi_)));
-    rec(1, s_hi_);
-    {
-      TraceRange th("rma.halo");
-      exchange(Tout, s_hi_);
-    }
-    rec(2, s_hi_);
-    RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
-    if (ev[4]) tseq_.push_back(0);
+    enqueue_fused(g.frame, g.interior, ft, Tout, ev,
+                  [&](const Rect* rs, int n, const StencilTuning& t) {
+                    multi_step(K, Tin, Tout, iCp_, nx_, ny_, rs, n, t, s_lo_);
+                  });
     return;
   }
   TraceRange tr("rma.pass.hide");
