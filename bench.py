@@ -771,6 +771,7 @@ def run(a, world: int, rank: int) -> int:
     gpu = a.device == "cuda"
     shared = a.shared_gpu_test and gpu and world > 1
     if shared:
+        os.environ["RMA_SHARED_GPU"] = "1"  # select_device: ranks may share cuda:0
         os.environ["RMA_TRANSPORT"] = a.shared_gpu_transport
         if a.shared_gpu_transport == "rccl":  # RCCL's socket transport between the ranks
             os.environ["RMA_RCCL_SHARED_GPU"] = "1"

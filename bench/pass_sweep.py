@@ -101,7 +101,8 @@ def main(argv=None):
                     "piper_u3", "piper_iso", "piper_diag_s0", "piper_w1", "piper_mask",
                     "piper_mask_ctl", "piper_nosb",
                     "piper_rot", "piper_diag_hb", "piper_u6s",
-                    "piper_sp", "piper_sp2", "piper_prio", "piper_prio_nr"):
+                    "piper_sp", "piper_sp2", "piper_prio", "piper_prio_nr", "piper2",
+                    "piper_rot2"):
             return N.pipe_chunk_rows(K, n, False) or N.default_chunk_k(max(K, 3), n)
         if kind == "pipec":
             return N.pipe_chunk_rows(K, n, True) or N.default_chunk_k(max(K, 3), n)
@@ -158,9 +159,11 @@ def main(argv=None):
             ops.stencilk_step(K, T2, T, iCp, coef, rect, tn)
         else:
             vec = 2 if kind in ("lds_dpp", "fast5") else 5 if kind == "pipe5" else 4
-            tn = ops.StencilTuning(chunk_rows=chunk(K, c, kind),
-                                   kernel="pipe" if kind in ("pipe2", "pipe5") else kind,
-                                   vec=vec, xcd_remap=1, stages=S, cols=2 if kind == "pipe2" else 0)
+            # "<kernel>2": two column waves per stage (pipe2, piper2, piper_rot2)
+            cols2 = kind in ("pipe2", "piper2", "piper_rot2")
+            kern = "pipe" if kind in ("pipe2", "pipe5") else kind[:-1] if cols2 else kind
+            tn = ops.StencilTuning(chunk_rows=chunk(K, c, kind), kernel=kern,
+                                   vec=vec, xcd_remap=1, stages=S, cols=2 if cols2 else 0)
             ops.stencilk_step(K, T2, T, iCp, coef, rect, tn)
 
     times: dict = {c: [] for c in cfgs}

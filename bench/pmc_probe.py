@@ -39,6 +39,21 @@ if which == "fast":  # fast-math K-step kernels at the executor's tuning (bench 
     torch.cuda.synchronize()
     print(f"probe done n={n} reps={reps} set={which} K={K} chunk={ch}")
     sys.exit(0)
+if which == "cols":  # piper with 1 vs 2 column waves per stage
+    from rocm_mpi_amd._native import load_lab
+
+    load_lab()
+    K = int(os.environ.get("RMA_PROBE_K", "20"))
+    ch = nat.pipe_chunk_rows(K, n, False) or nat.default_chunk_k(K, n)
+    rect = [ops.interior_rect(n, n)]
+    for kern, cols in (("piper", 1), ("piper", 2), ("piper_rot", 2)):
+        for _ in range(reps):
+            ops.stencilk_step(K, T2, T, iCp, c, rect,
+                              ops.StencilTuning(chunk_rows=ch, xcd_remap=1, kernel=kern, vec=4,
+                                                cols=cols))
+    torch.cuda.synchronize()
+    print(f"probe done n={n} reps={reps} set={which} K={K} chunk={ch}")
+    sys.exit(0)
 if which in ("all", "tbk"):  # multi-step kernels (temporal blocking)
     for K, ch in ((2, 16), (3, 128), (4, 128), (6, 128), (8, 128)):
         for _ in range(reps):

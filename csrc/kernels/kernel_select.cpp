@@ -50,13 +50,17 @@ bool pipe_has(int K, int S, int arith) {
 
 bool pipe_has_cols(int K, int S, int arith, int cols) {
   if (cols <= 1) return pipe_has(K, S, arith);
-  return cols == 2 && arith == pipe::kArFast5 && S == 4 && (K == 16 || K == 20 || K == 24);
+  if (cols != 2 || S != 4) return false;
+  if (arith == pipe::kArFast5 || arith == pipe::kArFast5Reg) return K == 16 || K == 20 || K == 24;
+  return arith == pipe::kArFast5RegRot && (K == 20 || K == 24);
 }
 
 int pipe_default_cols(int K, int S, int arith) {
-  // one column wave: the 2-column blocks (csrc/lab/stencil_pipe_lab.hip) do 8 % less
-  // arithmetic at K=24 but run one block per CU and lose 5-20 % to the
-  // unhidden per-row barrier (profiles/pass_sweep_cols2_r2.json)
+  // one column wave: the 2-column blocks (csrc/lab/stencil_pipe_lab.hip) do 6-8 % less
+  // arithmetic but run one 8-wave block per CU and lose more to the unhidden
+  // per-row barrier: ring kernel 5-20 % (profiles/pass_sweep_cols2_r2.json), piper
+  // +5.3 % at K=20 and +11.9 % at K=24 with the rotated map, +34-38 % wait cycles
+  // (profiles/r6/cols2_piper.md)
   (void)K;
   (void)S;
   (void)arith;

@@ -174,10 +174,13 @@ template <int K, int S, int Ar>
 constexpr int staging_rows() {
   return pipe_u6<K, S, Ar>() ? 6 : 3;
 }
-template <int K, int S, int V, int Ar>
-constexpr int lds_bytes_reg() {  // T + factor hand-off rows, LDS-DMA staging (V = 2, 4)
-  return (4 * (S > 1 ? S - 1 : 1) + (V == 2 || V == 4 ? 2 * staging_rows<K, S, Ar>() : 0)) *
-             Geo<K, S, V, 1>::WB * 8 +
+// T + factor hand-off rows (block-wide, WB columns), LDS-DMA staging (V = 2, 4;
+// private to each column's stage-0 wave, W columns each)
+template <int K, int S, int V, int Ar, int C = 1>
+constexpr int lds_bytes_reg() {
+  return (4 * (S > 1 ? S - 1 : 1) * Geo<K, S, V, C>::WB +
+          (V == 2 || V == 4 ? 2 * staging_rows<K, S, Ar>() * Geo<K, S, V, C>::W * C : 0)) *
+             8 +
          8;
 }
 template <int K, int S, int V, int Ar, int C>
@@ -187,7 +190,7 @@ constexpr int kernel_waves() {
     constexpr int H = Plan<K, S>::H;
     constexpr int vgpr = 8 * H * V + 8 * V + 40;
     constexpr int by_vgpr = 512 / ((vgpr + 7) / 8 * 8);
-    constexpr int w = occupancy<K, S, V, false, C>(lds_bytes_reg<K, S, V, Ar>());
+    constexpr int w = occupancy<K, S, V, false, C>(lds_bytes_reg<K, S, V, Ar, C>());
     if constexpr (Ar == kArFast5RegW1) return 1;
     return by_vgpr < 2 ? 2 : (by_vgpr < w ? by_vgpr : w);
   } else {
@@ -225,7 +228,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
                                           int remap) {
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = ar_reg(Ar);
-  static_assert(!kRegG || (C == 1 && V != 5), "register factors: V <= 4, one column wave");
+  static_assert(!kRegG || (V != 5 && (C == 1 || V == 4)),
+                "register factors: V <= 4; two column waves at V = 4 only");
   // register factors, 2 or 4 cells per lane: stage 0 prefetches T / 1/Cp three
   // rows ahead by LDS-DMA (global_load_lds_dwordx4 into three staging rows per
   // array) instead of two rows ahead into 4 rows of registers, which the
@@ -246,11 +250,13 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   constexpr int kStep = G::kStep;  // output columns per strip (plan_strip_tasks, sw = WB)
   constexpr int NH = S > 1 ? S - 1 : 1;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int stage = (Ar == kArFast5RegRot || Ar == kArFast5RegPrio)
-                        ? (wv + 2 * (int)(blockIdx.x & 1)) % S
-                    : C > 1              ? wv % S
-                                         : wv;  // waves c*S .. c*S+S-1: column c, one per SIMD
   const int col = C > 1 ? wv / S : 0;
+  // waves c*S .. c*S+S-1: column c, one per SIMD (waves are dealt to SIMDs in
+  // order). Rotated maps: odd blocks (C = 1) / column 1 (C = 2) start at SIMD
+  // 2, so no SIMD hosts two stage-0 waves
+  const int stage = (Ar == kArFast5RegRot || Ar == kArFast5RegPrio)
+                        ? (C > 1 ? (wv % S + 2 * col) % S : (wv + 2 * (int)(blockIdx.x & 1)) % S)
+                        : wv % S;
   const int lane = threadIdx.x & (kWave - 1);
   if constexpr (Ar == kArFast5RegPrio || Ar == kArFast5RegPrioNR) {
     if (stage == 0) __builtin_amdgcn_s_setprio(2);  // wave-uniform
@@ -336,7 +342,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   constexpr int kRing = kRegG ? 1 : (R + M) * WB, kHand = kRegG ? 4 : 2;
   __shared__ double ring[kRing];
   __shared__ double hand[kHand][NH][WB];
-  __shared__ double staging[kGlds ? 2 * NST * WB : 1];
+  __shared__ double staging[kGlds ? 2 * NST * W * C : 1];  // per column wave
   if constexpr (!kRegG)
     for (int t = threadIdx.x; t < kRing; t += S * C * kWave) ring[t] = 0.0;
   for (int t = threadIdx.x; t < kHand * NH * WB; t += S * C * kWave) (&hand[0][0][0])[t] = 0.0;
@@ -359,10 +365,11 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
       for (int v = 0; v < V; ++v) gr[q][v] = gr[q - 1][v];
   };
   __syncthreads();
-  // LDS-DMA staging row of T (a = 0) / 1/Cp (a = 1) for relative row r (mod NST):
+  // LDS-DMA staging row of T (a = 0) / 1/Cp (a = 1) for relative row r (mod NST),
+  // the column wave's own (only its stage-0 wave writes and reads it):
   // instruction h, lane l loads the cell pair 2l+h of the lane's window, which
-  // lands at dbl2 slot h*64 + l: the pair-interleaved row layout rd2 reads
-  auto stg = [&](int a, int r) { return &staging[(NST * a + r) * WB]; };
+  // lands at dbl2 slot h*64 + l (the one-window layout rds reads)
+  auto stg = [&](int a, int r) { return &staging[((2 * col + a) * NST + r) * W]; };
   auto glds_row = [&](int a, int y, int r) {
     const double* rb = (a ? iCp : T) + rowc(y) * nx;
 #pragma unroll
@@ -397,6 +404,14 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         out[2 * h] = t2.x;
         out[2 * h + 1] = t2.y;
       }
+    }
+  };
+  auto rds = [&](const double* row, double (&out)[V]) {  // a staging row (V = 2, 4)
+#pragma unroll
+    for (int h = 0; h < V / 2; ++h) {
+      const dbl2 t2 = reinterpret_cast<const dbl2*>(row)[h * kWave + lane];
+      out[2 * h] = t2.x;
+      out[2 * h + 1] = t2.y;
     }
   };
   auto wr2 = [&](double* row, const double (&in)[V]) {
@@ -461,8 +476,8 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         static_assert(kVm < 64, "vmcnt");
         __builtin_amdgcn_s_waitcnt(0x0F70 | (kVm & 15) | ((kVm >> 4) << 14));
         asm volatile("" ::: "memory");
-        rd2(stg(0, Ps), pT);
-        rd2(stg(1, Ps), pC);
+        rds(stg(0, Ps), pT);
+        rds(stg(1, Ps), pC);
       }
 #pragma unroll
       for (int v = 0; v < V; ++v) w[0][Pr][v] = pT[v];

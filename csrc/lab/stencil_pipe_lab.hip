@@ -8,7 +8,9 @@
 //     columns instead of a second strip's 2K. 8 % less arithmetic at K=24 but
 //     one block per CU (152 KB LDS), whose per-row barrier no second block
 //     hides: 85.2 vs 80.9 ms per K=24 pass at 101376^2, 65.7 vs 55.4 ms at
-//     K=16 (profiles/pass_sweep_cols2_r2.json);
+//     K=16 (profiles/pass_sweep_cols2_r2.json); the same with piper's register
+//     factors (K = 16, 20, 24; piper_rot at 20, 24), round 6: VALU -5.9 % but
+//     +34-38 % wait cycles, 70.8 vs 67.2 ms at K=20 (profiles/r6/cols2_piper.md);
 //   * 5 cells per lane (fast5, K = 16..20, stencil_pipe5_lab.hip);
 //   * a diagnosis variant with one factor-ring read per stage and row (wrong
 //     results; what the ring reads cost: -5 % per K=24 pass, SUMMARY_r3);
@@ -86,6 +88,11 @@ bool dispatch_cols2(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE2_CASE(16, 4, kArFast5)
   RMA_PIPE2_CASE(20, 4, kArFast5)
   RMA_PIPE2_CASE(24, 4, kArFast5)
+  RMA_PIPE2_CASE(16, 4, kArFast5Reg)
+  RMA_PIPE2_CASE(20, 4, kArFast5Reg)
+  RMA_PIPE2_CASE(24, 4, kArFast5Reg)
+  RMA_PIPE2_CASE(20, 4, kArFast5RegRot)
+  RMA_PIPE2_CASE(24, 4, kArFast5RegRot)
   return false;
 }
 

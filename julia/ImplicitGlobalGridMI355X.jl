@@ -36,6 +36,17 @@ end
 
 check(rc) = rc == 0 || error("rocm_mpi_amd: " * unsafe_string(ccall(sym(:rma_last_error), Cstring, ())))
 
+"""Node-local rank from the launcher (torchrun, SLURM, Open MPI, MPICH/Intel MPI), never
+the global rank: on a second node the global rank names a GPU that does not exist there.
+Without any of these variables the process is the node's only rank (device 0)."""
+function launcher_local_rank()
+    for name in ("LOCAL_RANK", "SLURM_LOCALID", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID")
+        v = get(ENV, name, "")
+        isempty(v) || return parse(Int, v)
+    end
+    return 0
+end
+
 """init_global_grid(nx, ny, nz; dimx=0, dimy=0, dimz=0, periodx=0, periody=0, periodz=0,
 overlaps=(2,2,2), halowidths=(1,1,1), comm=nothing, device=-1) -> (me, dims, nprocs, coords, comm)"""
 function init_global_grid(nx::Integer, ny::Integer, nz::Integer; dimx=0, dimy=0, dimz=0,
@@ -43,13 +54,19 @@ function init_global_grid(nx::Integer, ny::Integer, nz::Integer; dimx=0, dimy=0,
                           halowidths=(1, 1, 1), comm=nothing, device::Integer=-1)
     nprocs, rank = 1, 0
     uid = zeros(UInt8, 128)
+    local_rank = -1
     if comm !== nothing  # an MPI.Comm from MPI.jl
         MPI = Base.require(Base.PkgId(Base.UUID("da04e1cc-30fd-572f-bb4f-1f8673147195"), "MPI"))
         nprocs, rank = MPI.Comm_size(comm), MPI.Comm_rank(comm)
         rank == 0 && check(ccall(sym(:rma_unique_id), Cint, (Ptr{UInt8},), uid))
         MPI.Bcast!(uid, 0, comm)
+        # node-local rank from the shared-memory split, as the reference does
+        # (scripts/rocmaware_test_selectdevice.jl:7-9)
+        comm_l = MPI.Comm_split_type(comm, MPI.COMM_TYPE_SHARED, rank)
+        local_rank = MPI.Comm_rank(comm_l)
+        MPI.free(comm_l)
     end
-    dev = device >= 0 ? device : parse(Int, get(ENV, "LOCAL_RANK", string(rank)))
+    dev = device >= 0 ? device : local_rank >= 0 ? local_rank : launcher_local_rank()
     g = Ref{Ptr{Cvoid}}(C_NULL)
     me = Ref{Cint}(0)
     dims = zeros(Cint, 3)

@@ -11,6 +11,15 @@ Public API (ImplicitGlobalGrid names, torch tensors, 0-based indices)::
     update_halo_(T); gather_(T_nh, T_v); nx_g(); x_g(ix, dx, T); tic(); toc()
     finalize_global_grid()
 """
+import os as _os
+
+# RCCL / HIP IPC between the processes of a node need the dmabuf IPC mode on
+# this driver (hipIpcGetMemHandle fails with "invalid argument" otherwise;
+# scripts/setenv.sh). The HSA runtime reads it when it initialises, so it is
+# set on import, before any GPU call, for every entry path (torchrun -m
+# rocm_mpi_amd.apps.*, user scripts) and not only through setenv.sh / bench.py.
+_os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 from .parallel import (CartTopology, dims_create, finalize_global_grid, gather, gather_,
                        global_grid, grid_is_initialized, init_global_grid, me, nx_g, ny_g, nz_g,
                        tic, toc, update_halo, update_halo_, x_g, y_g, z_g)

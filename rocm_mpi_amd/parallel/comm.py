@@ -629,13 +629,34 @@ def visible_devices() -> int:
     return n
 
 
+def shared_gpu_allowed() -> bool:
+    """May several ranks of a node share one GPU? Only in the functional test
+    modes: ``RMA_SHARED_GPU=1`` (multi-process tests and rehearsals on a
+    1-GPU box) or ``RMA_RCCL_SHARED_GPU=1`` (which implies it)."""
+    return (os.environ.get("RMA_SHARED_GPU", "0") == "1"
+            or os.environ.get("RMA_RCCL_SHARED_GPU", "0") == "1")
+
+
 def select_device(local_rank: int) -> torch.device:
-    """One GPU per process: device = local_rank mod visible devices."""
+    """One GPU per process: device = the node-local rank (the reference's
+    ``AMDGPU.device!(rank_l+1)``, ``scripts/rocmaware_test_selectdevice.jl:9``).
+
+    More local ranks than visible GPUs is an error (two ranks would silently
+    share a device and every timing would be wrong), unless a shared-GPU test
+    mode is on (:func:`shared_gpu_allowed`): then device = local_rank mod
+    visible devices."""
     if not torch.cuda.is_available():
         return torch.device("cpu")
     n = visible_devices()
     if n <= 0:
         raise RuntimeError("torch reports a GPU but no visible device")
+    if local_rank < 0:
+        raise ValueError(f"local rank {local_rank} < 0")
+    if local_rank >= n and not shared_gpu_allowed():
+        raise RuntimeError(
+            f"node-local rank {local_rank} but only {n} visible GPU(s): one process per GPU "
+            f"(launch at most {n} ranks per node, or set RMA_SHARED_GPU=1 for a functional "
+            f"test that shares a GPU)")
     dev = torch.device("cuda", local_rank % n)
     torch.cuda.set_device(dev)
     return dev

@@ -8,6 +8,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# the multi-process GPU tests run every rank on the one GPU of the test box:
+# select_device refuses that outside this functional mode (inherited by the
+# ranks the tests spawn; tests of the refusal unset it)
+os.environ.setdefault("RMA_SHARED_GPU", "1")
 
 # Crash evidence that survives a truncated stdout tail (the
 # faulting thread's frames of the round-4 SIGSEGV fell into the bytes the

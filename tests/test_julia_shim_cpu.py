@@ -52,3 +52,27 @@ def test_every_shim_ccall_is_exported():
     exported = {line.split()[-1] for line in nm.stdout.splitlines() if line.strip()}
     missing = sorted(set(_ccalls()) - exported)
     assert not missing, missing
+
+
+def test_shim_device_index_is_node_local_never_global():
+    """the shim's device index comes from the MPI
+    shared-memory split when a comm is given (the reference's
+    ``Comm_split_type(COMM_TYPE_SHARED)``, scripts/rocmaware_test_selectdevice.jl:7-9),
+    else from the launcher's node-local rank variables (the same list as the
+    Python side, comm.env_world), and never from the global rank."""
+    src = open(JL).read()
+    dev_line = [ln for ln in src.splitlines() if re.match(r"\s*dev\s*=", ln)]
+    assert len(dev_line) == 1, dev_line
+    assert "local_rank" in dev_line[0] and "launcher_local_rank()" in dev_line[0]
+    assert not re.search(r"\brank\b", dev_line[0].replace("local_rank", "")), dev_line[0]
+    assert "MPI.Comm_split_type(comm, MPI.COMM_TYPE_SHARED" in src
+    assert re.search(r"local_rank\s*=\s*MPI\.Comm_rank\(comm_l\)", src)
+    m = re.search(r"function launcher_local_rank\(\)(.*?)\nend", src, re.S)
+    assert m, "launcher_local_rank missing"
+    names = re.findall(r'"([A-Z_]+)"', m.group(1))
+    from rocm_mpi_amd.parallel import comm as C
+    import inspect
+    py = inspect.getsource(C.env_world)
+    py_local = re.search(r'local = first\(([^)]*)\)', py).group(1)
+    assert names == re.findall(r'"([A-Z_]+)"', py_local)
+    assert "return 0" in m.group(1)  # no launcher variable: the node's only rank

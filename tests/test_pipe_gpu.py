@@ -88,6 +88,25 @@ def test_pipe_two_column_waves_bitwise(nx, K):
     assert torch.equal(gpu_run(K, T, iCp, sub, "pipe", chunk=23, cols=2, xcd=0), ref)
 
 
+@pytest.mark.parametrize("nx", [516, 1028, 1500, 2052])
+@pytest.mark.parametrize("K,kern", [(16, "piper"), (20, "piper"), (24, "piper"), (20, "piper_rot"),
+                                    (24, "piper_rot")])
+def test_piper_two_column_waves_bitwise(nx, K, kern):
+    """piper (register factors, per-column LDS-DMA staging) with 2 column waves
+    per stage: the block-wide T and factor hand-off rows are written by both
+    column waves (each its [lo, hi) share); bitwise equal to the CPU twin on
+    whole interiors, rect lists whose strips end mid-block, short chunks."""
+    ny = 149
+    T, iCp = rand((ny, nx), 101 + K), rand((ny, nx), 102, 0.5, 1.0)
+    rects = [ops.interior_rect(nx, ny)]
+    ref = cpu_ref(K, T, iCp, rects, "pipe")
+    for chunk in (5, 41):
+        assert torch.equal(gpu_run(K, T, iCp, rects, kern, chunk=chunk, cols=2), ref)
+    sub = [(K + 3, nx - K - 7, K + 2, ny - K - 5), (1, K + 3, 1, ny - 1)]
+    ref = cpu_ref(K, T, iCp, sub, "pipe")
+    assert torch.equal(gpu_run(K, T, iCp, sub, kern, chunk=23, cols=2, xcd=0), ref)
+
+
 def test_pipe_two_column_waves_need_vec4():
     """cols=2 on a tile that only allows 2 cells per lane runs the 1-column kernel."""
     ny, nx, K = 67, 518, 20
@@ -184,6 +203,32 @@ def test_pipe_guard_bands(kernel, K, vec, nx):
     mask = torch.ones((ny, nx), dtype=torch.bool, device=DEV)
     mask[K:ny - K, K:nx - K] = False
     assert torch.equal(out[mask], before[mask])
+
+
+@pytest.mark.parametrize("K,nx", [(20, 1028), (24, 776), (16, 1500)])
+def test_piper_two_column_waves_guard_bands(K, nx):
+    """2-column piper: no write outside the output rect or the arrays."""
+    ny = 197
+    bufs, fields = [], []
+    for seed in (17, 18, 19):
+        b = torch.full((G + ny * nx + G,), CANARY, dtype=torch.float64, device=DEV)
+        f = b[G:G + ny * nx].view(ny, nx)
+        f.copy_(rand((ny, nx), seed, 0.5, 1.0))
+        bufs.append(b)
+        fields.append(f)
+    T, iCp, out = fields
+    before = out.clone()
+    rects = [(K, nx - K, K, ny - K)]
+    ops.stencilk_step(K, out, T, iCp, coef(), rects,
+                      ops.StencilTuning(kernel="piper", chunk_rows=29, vec=4, cols=2))
+    torch.cuda.synchronize()
+    for b in bufs:
+        assert bool((b[:G] == CANARY).all()) and bool((b[-G:] == CANARY).all())
+    mask = torch.ones((ny, nx), dtype=torch.bool, device=DEV)
+    mask[K:ny - K, K:nx - K] = False
+    assert torch.equal(out[mask], before[mask])
+    ref = cpu_ref(K, T.cpu(), iCp.cpu(), rects, "pipe")
+    assert torch.equal(out.cpu()[~mask.cpu()], ref[~mask.cpu()])
 
 
 def test_piper_tiny_tiles_and_short_chunks():
