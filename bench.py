@@ -48,23 +48,16 @@ import os
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 import argparse  # noqa: E402
-import datetime  # noqa: E402
-import hashlib  # noqa: E402
 import json  # noqa: E402
 import math  # noqa: E402
 import subprocess  # noqa: E402
 import sys  # noqa: E402
-import threading  # noqa: E402
 import time  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "T_eff (GB/s) + weak-scaling eff., 2D diffusion 1000 steps at 1/2/4/8 MI355X"
-# fast-math drift bound (max |fast - canonical| after the run's steps on a
-# random field in [0, 1)): diffusion is contractive, rounding differences do
-# not accumulate (3.3e-16 after 24..5000 steps, CPU twins, 514^2)
-DRIFT_BOUND = 1e-14
 
 
 def parse(argv=None):
@@ -113,6 +106,9 @@ def parse(argv=None):
                          "efficiency (-1: = --steps; 0: skip)")
     ap.add_argument("--preflight", type=int, default=1,
                     help="ring send/recv + tiny halo check before the tile is allocated (1/0)")
+    ap.add_argument("--link-probe", type=int, default=1,
+                    help="preflight: time one exchange per halo neighbour at the timed tile's "
+                         "message sizes and record RCCL's transport per connection (1/0)")
     ap.add_argument("--check", type=int, default=-1,
                     help="halo bitwise check after the run (1 on, 0 off, -1: on with a GPU "
                          "or N > 1)")
@@ -127,6 +123,10 @@ def parse(argv=None):
     ap.add_argument("--window-check", type=int, default=1,
                     help="after the timed run, compare three full-width row windows of the "
                          "timed field bitwise with the CPU twin (1/0)")
+    ap.add_argument("--full-field-check", type=int, default=1,
+                    help="after the timed run, one device pass over every cell of the timed "
+                         "field: finite and within the initial field's bounds (maximum "
+                         "principle of the explicit scheme) (1/0)")
     ap.add_argument("--drift-steps", type=int, default=-1,
                     help="steps of the fast-math drift measurement (-1: warmup + steps; 0: off)")
     ap.add_argument("--shared-gpu-test", action="store_true",
@@ -155,576 +155,14 @@ def auto_tile(frac: float, cap: int) -> int:
     return max(n, 512)
 
 
-def log(rank: int, msg: str) -> None:
-    print(f"bench.py rank {rank}: {msg}", file=sys.stderr, flush=True)
-
-
-class CheckFailed(RuntimeError):
-    """A correctness check failed (on this or another rank)."""
-
-
-# ---------------------------------------------------------------------------
-# bounded collectives over the gloo group (metadata only)
-# ---------------------------------------------------------------------------
-def gather_obj(obj, world: int):
-    """All-gather a small picklable object over the gloo group (main phase:
-    every rank reaches it; torchrun ends the job if one rank dies)."""
-    if world == 1:
-        return [obj]
-    import torch.distributed as dist
-
-    from rocm_mpi_amd.parallel import comm as C
-
-    out: list = [None] * world
-    dist.all_gather_object(out, obj, group=C._gloo_group())
-    return out
-
-
-def _wait(work, timeout_s: float, what: str) -> None:
-    try:
-        work.wait(timeout=datetime.timedelta(seconds=timeout_s))
-    except Exception as e:  # noqa: BLE001 - a peer is gone or stuck
-        raise CheckFailed(f"{what}: no answer from every rank within {timeout_s:.0f} s ({e})") \
-            from None
-
-
-def bounded_status(ok: bool, msg: str, world: int, timeout_s: float) -> list:
-    """All-gather (ok, message) from every rank, bounded: every rank learns
-    whether any rank failed and why, and nobody blocks longer than timeout_s."""
-    if world == 1:
-        return [(ok, msg)]
-    import torch
-    import torch.distributed as dist
-
-    from rocm_mpi_amd.parallel import comm as C
-
-    raw = msg.encode("utf-8", "replace")[:480]
-    buf = torch.zeros(512, dtype=torch.uint8)
-    buf[0] = 1 if ok else 0
-    buf[1] = len(raw) >> 8
-    buf[2] = len(raw) & 0xFF
-    if raw:
-        buf[3:3 + len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
-    out = [torch.empty_like(buf) for _ in range(world)]
-    _wait(dist.all_gather(out, buf, group=C._gloo_group(), async_op=True), timeout_s,
-          "status exchange")
-    res = []
-    for b in out:
-        n = (int(b[1]) << 8) | int(b[2])
-        res.append((bool(b[0]), bytes(b[3:3 + n].tolist()).decode("utf-8", "replace")))
-    return res
-
-
-def agree(ok: bool, msg: str, world: int, timeout_s: float, what: str) -> None:
-    """Raise CheckFailed on EVERY rank if any rank failed (bounded)."""
-    st = bounded_status(ok, msg, world, timeout_s)
-    bad = [(r, m) for r, (o, m) in enumerate(st) if not o]
-    if bad:
-        raise CheckFailed(f"{what} failed on rank(s) " +
-                          "; ".join(f"{r}: {m}" for r, m in bad))
-
-
-def bounded_gather_tiles(field, world: int, timeout_s: float):
-    """The equal-shape tiles of every rank on rank 0 (host copies), bounded."""
-    host = field.detach().cpu().contiguous()
-    if world == 1:
-        return [host]
-    import torch
-    import torch.distributed as dist
-
-    from rocm_mpi_amd.parallel import comm as C
-
-    lst = [torch.empty_like(host) for _ in range(world)] if dist.get_rank() == 0 else None
-    _wait(dist.gather(host, lst, dst=0, group=C._gloo_group(), async_op=True), timeout_s,
-          "tile gather")
-    return lst
-
-
-_DONE_KEY = "rma/bench/rank0_reported"
-
-
-def signal_reported(world: int) -> None:
-    """Rank 0 has printed its record (or is about to exit without one)."""
-    if world > 1:
-        try:
-            import torch.distributed as dist
-
-            dist.distributed_c10d._get_default_store().set(_DONE_KEY, "1")
-        except Exception:  # noqa: BLE001 - best effort on an error path
-            pass
-
-
-def wait_reported(world: int, timeout_s: float) -> None:
-    """A failing rank > 0 waits (bounded) for rank 0's record before it exits:
-    torchrun ends the whole job as soon as one rank exits non-zero."""
-    if world > 1:
-        try:
-            import torch.distributed as dist
-
-            dist.distributed_c10d._get_default_store().wait(
-                [_DONE_KEY], datetime.timedelta(seconds=timeout_s))
-        except Exception:  # noqa: BLE001
-            pass
-
-
-class Watchdog:
-    """Ends this rank if a phase outlives its deadline (a rank stuck inside
-    the GPU runtime, RCCL or a gloo receive cannot be interrupted from
-    Python): rank 0 first prints the record it has, with the failure, so the
-    run still reports; the other ranks give it time to do so."""
-
-    def __init__(self, rank: int, world: int, seconds: float, what: str, on_fire=None):
-        self.rank, self.world, self.what, self.on_fire = rank, world, what, on_fire
-        self._t = threading.Timer(seconds, self._fire)
-        self._t.daemon = True
-        self._t.start()
-
-    def _fire(self) -> None:
-        msg = f"watchdog: {self.what} did not finish in time"
-        log(self.rank, msg + "; exiting")
-        try:
-            if self.rank == 0 and self.on_fire is not None:
-                self.on_fire(msg)
-        finally:
-            finish_failed(self.rank, self.world, 6, 30.0)
-
-    def cancel(self) -> None:
-        self._t.cancel()
-
-
-def finish_failed(rank: int, world: int, rc: int, wait_s: float) -> None:
-    """Exit a failed run on this rank without touching the (possibly broken)
-    process groups: rank 0 after its record, the others after rank 0's."""
-    if rank == 0:
-        signal_reported(world)
-    else:
-        wait_reported(world, wait_s)
-    hard_exit(rank, rc)
-
-
-def hard_exit(rank: int, rc: int) -> None:
-    record_rc(rank, rc)
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(rc)
-
-
-def record_rc(rank: int, rc: int) -> None:
-    """RMA_BENCH_RC_DIR: every rank writes its exit status (tests)."""
-    d = os.environ.get("RMA_BENCH_RC_DIR")
-    if d:  # atomically: torchrun may end this rank right after (a half-written file)
-        # one temp file per thread: the check-phase watchdog thread and the main
-        # thread can both be exiting the rank at once; with one shared temp
-        # name one thread renamed the other's still-empty file into place
-        tmp = os.path.join(d, f".rc{rank}.{threading.get_ident()}.tmp")
-        with open(tmp, "w") as f:
-            f.write(str(rc))
-            f.flush()
-        os.replace(tmp, os.path.join(d, f"rc{rank}"))
-
-
-# ---------------------------------------------------------------------------
-# checks
-# ---------------------------------------------------------------------------
-def summarize_timings(ts: list, exchange: bool = True) -> dict:
-    """Mean per-pass frame / halo / interior / exposed-halo ms of one rank.
-    Without a neighbour (exchange=False) the halo events bracket an empty
-    exchange: the halo keys are event-gap noise and the overlap fraction is
-    not defined (None)."""
-    if not ts:
-        return {}
-    n = len(ts)
-    mean = {k: sum(t[k] for t in ts) / n for k in ("frame_ms", "halo_ms", "interior_ms",
-                                                   "pass_ms", "exposed_halo_ms")}
-    halo = sum(t["halo_ms"] for t in ts)
-    exposed = sum(t["exposed_halo_ms"] for t in ts)
-    mean["passes"] = n
-    mean["depths"] = sorted({int(t["K"]) for t in ts}, reverse=True)
-    mean["overlap_fraction"] = (1.0 - exposed / halo) if halo > 0 and exchange else None
-    if not exchange:
-        mean["note"] = "no neighbour: no halo exchange ran; halo_ms / exposed_halo_ms are event gaps"
-    return mean
-
-
-def _run_grid(nx, ny, dims_, K, steps_fast, steps_can, periodic, loopback=None, device=None,
-              via=False):
-    """A small grid through the production path: steps_fast fast-math steps,
-    then steps_can canonical steps. Returns (field, coords, nxyz_g, transport, plan)."""
-    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
-    from rocm_mpi_amd.parallel import implicit_grid as gg
-
-    ol = 2 * K
-    per = 1 if periodic else 0
-    kw = dict(dimx=dims_[0], dimy=dims_[1], overlaps=(ol, ol, 2), halowidths=(K, K, 1),
-              quiet=True, periodx=per, periody=per)
-    if loopback is not None:
-        kw.update(loopback=loopback, device=device)
-    elif via:
-        kw.update(transport="rccl", self_via_transport=True)
-    gg.init_global_grid(nx, ny, 1, **kw)
-    try:
-        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny,
-                                        nt=max(1, steps_fast + steps_can), init="random",
-                                        quiet=True, dims=(*dims_, 0), temporal=K,
-                                        periods=(per, per, 0), fast_math=True, device=device))
-        plan = m.plan(steps_fast)
-        m.step(steps_fast)
-        if steps_can:
-            m.set_temporal(K, fast_math=False)
-            m.step(steps_can)
-        m.synchronize()
-        out = (m.field.clone(), m.g.coords, m.g.nxyz_g, m.g.transport, plan)
-        m.close()
-    finally:
-        gg.finalize_global_grid(finalize_dist=False)
-    return out
-
-
-def _local_device(dev: str) -> str:
-    import torch
-
-    return dev if dev == "cpu" else f"cuda:{torch.cuda.current_device()}"
-
-
-def _restore_stream(dev: str):
-    """The loopback grid installs its own stream: put the caller's back."""
-    import torch
-
-    prev = torch.cuda.current_stream() if dev != "cpu" else None
-
-    class _R:
-        def __enter__(self):
-            return self
-
-        def __exit__(self, *exc):
-            if prev is not None:
-                torch.cuda.set_stream(prev)
-            return False
-
-    return _R()
-
-
-def halo_check(n: int, dims, K: int, dev: str, world: int, rank: int, timeout_s: float,
-               self_rccl: bool = False, inject: bool = True) -> dict:
-    """Run a small grid with the bench's process grid through the real halo
-    path (37 fast-math steps, then 23 canonical), gather every rank's tile on
-    rank 0 and compare bitwise with a 1-rank run of the global grid on rank
-    0's device. Raises CheckFailed on every rank on any error or mismatch.
-
-    self_rccl (one rank): the check grid is periodic and its halos go through
-    RCCL send/recv to itself; the reference is the same periodic tile with
-    local self copies (exercises this path with real RCCL traffic on 1 GPU)."""
-    import numpy as np
-
-    from rocm_mpi_amd.parallel import comm as C
-
-    n_fast, n_can = 37, 23
-    ol = 2 * K
-    t0 = time.perf_counter()
-    err = ""
-    field = coords = None
-    info = {"local_tile": [n, n], "steps": [n_fast, n_can], "self_rccl": self_rccl}
-    try:
-        fault = os.environ.get("RMA_BENCH_CHECK_RAISE", "") if inject and rank == world - 1 else ""
-        if fault == "before":  # peers then block in the exchange: the watchdog path
-            raise RuntimeError("injected halo-check failure before the run")
-        field, coords, nxyz_g, transport, plan = _run_grid(n, n, dims, K, n_fast, n_can,
-                                                           self_rccl, via=self_rccl)
-        if fault == "after":
-            raise RuntimeError("injected halo-check failure after the run")
-        info.update(global_grid=list(nxyz_g[:2]), transport=transport, fast_math_plan=plan)
-        if inject and os.environ.get("RMA_BENCH_CHECK_CORRUPT") == "1" and rank == world - 1:
-            field[n // 2, n // 2] += 1e-12  # negative test (tests/test_multiprocess_cpu.py)
-    except Exception as e:  # noqa: BLE001 - reported to every rank below
-        err = f"{type(e).__name__}: {e}"
-    agree(not err, err, world, timeout_s, "halo check run")
-    import torch
-
-    cxy = torch.tensor([coords[0], coords[1]], dtype=torch.float64)
-    all_xy = bounded_gather_tiles(cxy, world, timeout_s)
-    tiles = bounded_gather_tiles(field, world, timeout_s)
-    bad, err = 0, ""
-    if rank == 0:
-        try:
-            with _restore_stream(dev):
-                rn = (n, n) if self_rccl else tuple(info["global_grid"])
-                ref = _run_grid(*rn, (1, 1), K, n_fast, n_can, self_rccl,
-                                loopback=(C.LoopbackHub(1), 0), device=_local_device(dev))[0]
-            ref = ref.cpu().numpy()
-            for xy, T in zip(all_xy, tiles):
-                gx0, gy0 = int(xy[0]) * (n - ol), int(xy[1]) * (n - ol)
-                if not np.array_equal(T.numpy(), ref[gy0:gy0 + n, gx0:gx0 + n]):
-                    bad += 1
-        except Exception as e:  # noqa: BLE001
-            err = f"reference run: {type(e).__name__}: {e}"
-    st = bounded_status(not err and bad == 0, err or f"{bad} tile(s) differ", world, timeout_s)
-    info["tiles_mismatched"] = bad if rank == 0 else None
-    info["seconds"] = round(time.perf_counter() - t0, 3)
-    if not st[0][0]:
-        info["tiles_mismatched"] = bad if rank == 0 else -1
-        raise CheckFailed(f"halo check: {st[0][1]}", info)
-    return info
-
-
-def drift_check(n: int, K: int, steps: int, dev: str, world: int, timeout_s: float) -> dict:
-    """max |fast - canonical| on an n x n random tile after `steps` steps
-    (every rank on its own GPU, 1-rank grid); the fast fields must agree
-    bitwise across ranks (same kernels, same data) and stay within DRIFT_BOUND."""
-    from rocm_mpi_amd.parallel import comm as C
-
-    t0 = time.perf_counter()
-    err, drift, digest = "", None, ""
-    try:
-        with _restore_stream(dev):
-            kw = dict(loopback=(C.LoopbackHub(1), 0), device=_local_device(dev))
-            fast = _run_grid(n, n, (1, 1), K, steps, 0, False, **kw)
-            can = _run_grid(n, n, (1, 1), K, 0, steps, False, **kw)
-        drift = float((fast[0] - can[0]).abs().max())
-        digest = hashlib.sha1(fast[0].cpu().numpy().tobytes()).hexdigest()[:16]
-        if not drift <= DRIFT_BOUND:
-            err = f"fast-math drift {drift:.3e} > bound {DRIFT_BOUND:.0e}"
-    except Exception as e:  # noqa: BLE001
-        err = f"{type(e).__name__}: {e}"
-    st = bounded_status(not err, err or f"{digest} {drift!r}", world, timeout_s)
-    bad = [f"{r}: {m}" for r, (o, m) in enumerate(st) if not o]
-    if not bad and len({m.split()[0] for _, m in st}) != 1:
-        bad = ["fast-math fields differ across GPUs: " + ", ".join(m for _, m in st)]
-    info = {"tile": [n, n], "steps": steps, "fast_math_drift_max": drift, "bound": DRIFT_BOUND,
-            "fast_field_sha1_16": digest, "seconds": round(time.perf_counter() - t0, 3)}
-    if bad:
-        raise CheckFailed("fast-math drift check: " + "; ".join(bad), info)
-    return info
-
-
-WINDOW_ROWS = 8
-WINDOW_BUDGET = 3.0e9  # cell updates of the CPU twin for all windows of a rank
-
-
-def snapshot_windows(model, h: int = WINDOW_ROWS) -> dict:
-    """Three full-width row windows of this rank's field (top edge, middle,
-    bottom edge), copied to the host right after the timed run, with what the
-    CPU twin needs to recompute them from the initial condition."""
-    import torch
-
-    cfg, g = model.cfg, model.g
-    ny, nx = model.field.shape
-    h = min(h, ny)
-    rows = sorted({0, max(0, ny // 2 - h // 2), ny - h})
-    geo = model.geometry()
-    tiles = [model.field[r:r + h].detach().cpu().clone() for r in rows]
-    if os.environ.get("RMA_BENCH_WINDOW_CORRUPT") == "1" and g.me == g.nprocs - 1:
-        tiles[-1][h // 2, nx // 2] += 1e-12  # negative test (tests/test_multiprocess_cpu.py)
-    return {"rows": rows, "h": h, "tiles": tiles,
-            "nx": nx, "ny": ny, "geom": geo, "coef": model.coef, "seed": cfg.seed,
-            "icp": 1.0 / cfg.Cp0, "fast": bool(cfg.fast_math), "steps": model.steps_done,
-            "dtype": torch.float64}
-
-
-def window_check(snap: dict, world: int, timeout_s: float, budget: float = WINDOW_BUDGET) -> dict:
-    """the headline field itself, not a small proxy tile.
-    Each window is recomputed on the CPU twin (the C++ fast5 / canonical
-    arithmetic, bitwise equal to the GPU kernels) from the counter-based
-    initial condition of the global grid (csrc/kernels/misc.hip init_random),
-    over the window plus `steps` rows / columns of margin on every side that
-    is not a global boundary (the dependency cone of `steps` updates), and
-    compared bitwise. Full-width windows when the twin's cost fits `budget`
-    cell updates, else three 64-column boxes per window (left edge, centre,
-    right edge). Raises CheckFailed on every rank on any mismatch."""
-    import torch
-
-    from rocm_mpi_amd import ops
-
-    t0 = time.perf_counter()
-    S, h, nx, ny = snap["steps"], snap["h"], snap["nx"], snap["ny"]
-    geo = snap["geom"]
-    nxg, nyg = geo.nxg, geo.nyg
-    per = geo.periodx or geo.periody
-    full = (nx + 2 * S) * (h + 2 * S) * S * len(snap["rows"]) <= budget
-    bw = nx if full else min(64, nx)
-    cols = [0] if full else sorted({0, max(0, nx // 2 - bw // 2), nx - bw})
-    tn = ops.StencilTuning(kernel="pipe" if snap["fast"] else "pipec")
-    err, boxes, mism = "", 0, 0
-    try:
-        if per:
-            raise CheckFailed("window check: periodic grids are not covered")
-        for r0, tile in zip(snap["rows"], snap["tiles"]):
-            for c0 in cols:
-                # the box in global coordinates, with the margin, clipped to the grid
-                gy_lo, gy_hi = geo.gy0 + r0, geo.gy0 + r0 + h
-                gx_lo, gx_hi = geo.gx0 + c0, geo.gx0 + c0 + bw
-                wy0, wy1 = max(0, gy_lo - S), min(nyg, gy_hi + S)
-                wx0, wx1 = max(0, gx_lo - S), min(nxg, gx_hi + S)
-                wg = ops.TileGeometry(gx0=wx0, gy0=wy0, nxg=nxg, nyg=nyg, dx=geo.dx, dy=geo.dy)
-                a = torch.empty((wy1 - wy0, wx1 - wx0), dtype=snap["dtype"])
-                ops.init_random_(a, wg, seed=snap["seed"])
-                icp = torch.full_like(a, snap["icp"])
-                b = a.clone()
-                done = 0
-                while done < S:
-                    k = min(24, S - done)
-                    if a.shape[0] >= 3 and a.shape[1] >= 3:
-                        ops.stencilk_step(k, b, a, icp, snap["coef"], None, tn)
-                    a, b = b, a
-                    done += k
-                want = a[gy_lo - wy0:gy_hi - wy0, gx_lo - wx0:gx_hi - wx0]
-                got = tile[:, c0:c0 + bw]
-                boxes += 1
-                if not torch.equal(got, want):
-                    mism += 1
-                    d = (got - want).abs().max().item()
-                    err = (f"window rows {r0}..{r0 + h} cols {c0}..{c0 + bw}: "
-                           f"{int((got != want).sum())} cells differ (max |diff| {d:.3e})")
-    except CheckFailed as e:
-        err = str(e.args[0])
-    except Exception as e:  # noqa: BLE001
-        err = f"{type(e).__name__}: {e}"
-    info = {"windows": len(snap["rows"]), "rows_each": h, "row_starts": snap["rows"],
-            "full_width": bool(full), "box_cols": None if full else bw, "boxes": boxes,
-            "steps": S, "bitwise": not err and mism == 0,
-            "arithmetic": "fast-math twin" if snap["fast"] else "canonical twin",
-            "seconds": round(time.perf_counter() - t0, 3)}
-    st = bounded_status(not err, err, world, timeout_s)
-    bad = [f"{r}: {m}" for r, (o, m) in enumerate(st) if not o]
-    if bad:
-        info["bitwise"] = False
-        raise CheckFailed("headline window check: " + "; ".join(bad), info)
-    return info
-
-
-# weak-scaling attribution (VERDICT r3 next 3, r4 next 3). Self-contained in
-# one job: E_in_run = t_fast_iso / t_it = e_gpu * e_coef * e_halo, with
-# t_fast_iso the fastest rank's own isotropic solo time (no exchange). The
-# N = 1 record of the same tile class (cached by the same driver sweep on the
-# same node and build) adds e_box = t(N=1) / t_fast_iso, so that
-# E(N) = t(N=1) / t_it = e_box * E_in_run.
-def _n1_cache_path() -> str:
-    import tempfile
-
-    return os.environ.get("RMA_BENCH_N1_CACHE",
-                          os.path.join(tempfile.gettempdir(), "rma_bench_n1_record.json"))
-
-
-def _build_id() -> str:
-    """Hash of the native sources, flags and arch (rocm_mpi_amd/_build.py)."""
-    try:
-        from rocm_mpi_amd import _build
-
-        return _build.source_stamp()[:12]
-    except Exception:  # noqa: BLE001 - informational
-        return "unknown"
-
-
-def _n1_key(nx: int, ny: int, steps: int, warmup: int, K: int, fast: bool, variant: str) -> str:
-    """Tile class + build + node: a record from another build or another box
-    (another sweep) never matches."""
-    import socket
-
-    return (f"{variant}:{nx}x{ny}:s{steps}:w{warmup}:K{K}:f{int(fast)}:b{_build_id()}:"
-            f"h{socket.gethostname()}")
-
-
-def save_n1(key: str, ms_per_step: float, bus: str) -> None:
-    try:
-        tmp = _n1_cache_path() + f".{os.getpid()}.tmp"
-        with open(tmp, "w") as f:
-            json.dump({"key": key, "ms_per_step": ms_per_step, "pci_bus_id": bus,
-                       "time": time.time()}, f)
-        os.replace(tmp, _n1_cache_path())
-    except OSError:
-        pass
-
-
-def load_n1(key: str):
-    try:
-        with open(_n1_cache_path()) as f:
-            d = json.load(f)
-        return d if d.get("key") == key else None
-    except (OSError, ValueError):
-        return None
-
-
-def attribution(t_it: float, solo: float | None, solo_iso: float | None,
-                fast_iso: float | None, n1_ms: float | None,
-                slow_iso: float | None = None) -> dict:
-    """Job-level split of the weak-scaling efficiency (times in s, max over
-    ranks unless named otherwise):
-      e_halo = solo / t_it        exchange + frame cost, same coefficients
-      e_coef = solo_iso / solo    fast-math pass energy at this grid's dx != dy
-                                  against dx = dy
-      e_gpu  = fast_iso / slow_iso  the slowest GPU against the fastest GPU of
-                                  THIS job (each rank's own isotropic solo
-                                  time, no exchange): in-run, 1 for one GPU
-      e_product = e_halo * e_coef * e_gpu ~ fast_iso / t_it  (in-run E(N);
-                                  exact up to the barrier time in solo_iso)
-      e_box  = t(N=1) / fast_iso  this job's fastest GPU against the N = 1
-                                  record of the same sweep (null without it)
-      e_product_vs_n1 = e_box * e_product = t(N=1) / t_it = E(N)."""
-    out = {"e_halo": None, "e_coef": None, "e_gpu": None, "e_product": None,
-           "e_box": None, "e_product_vs_n1": None,
-           "weak_scaling_eff_same_run_iso": None, "fastest_solo_iso_ms_per_step":
-               fast_iso * 1e3 if fast_iso else None, "n1_ms_per_step": n1_ms}
-    if solo:
-        out["e_halo"] = solo / t_it
-    if solo and solo_iso:
-        out["e_coef"] = solo_iso / solo
-        out["weak_scaling_eff_same_run_iso"] = solo_iso / t_it
-    if fast_iso and (slow_iso or solo_iso):
-        out["e_gpu"] = fast_iso / (slow_iso or solo_iso)
-    if all(out[k] is not None for k in ("e_halo", "e_coef", "e_gpu")):
-        out["e_product"] = out["e_halo"] * out["e_coef"] * out["e_gpu"]
-    if fast_iso and n1_ms:
-        out["e_box"] = (n1_ms / 1e3) / fast_iso
-        if out["e_product"] is not None:
-            out["e_product_vs_n1"] = out["e_box"] * out["e_product"]
-    return {k: (round(v, 6) if isinstance(v, float) else v) for k, v in out.items()}
-
-
-def preflight(dims, K: int, dev: str, world: int, rank: int, gpu: bool, n: int,
-              timeout_s: float) -> dict:
-    """Before the HBM-sized tile: the ring send/recv of the reference's smoke
-    test over the halo transport, then the halo check on a tiny grid."""
-    from rocm_mpi_amd.apps import rocmaware_test_selectdevice as smoke
-
-    t0 = time.perf_counter()
-    err = ""
-    transport = "rccl" if gpu and world == 1 else "auto"
-    ring: dict = {}
-    try:
-        vals = smoke.run(4, transport=transport, verbose=False, self_ring=world == 1, info=ring)
-        if any(v != float((rank - 1) % world) for v in vals):
-            err = f"ring received {vals}, expected {(rank - 1) % world}"
-    except Exception as e:  # noqa: BLE001
-        err = f"ring send/recv: {type(e).__name__}: {e}"
-    agree(not err, err, world, timeout_s, "preflight ring")
-    info = {"ring_ok": True, "ring_ranks": world, "ring_transport": ring.get("transport"),
-            "rccl_nranks": ring.get("rccl_nranks")}
-    info["halo"] = halo_check(n, dims, K, dev, world, rank, timeout_s,
-                              self_rccl=gpu and world == 1, inject=False)
-    info["seconds"] = round(time.perf_counter() - t0, 3)
-    return info
-
-
-def _rccl_info() -> dict | None:
-    """Which RCCL carries the halo traffic (RMA_RCCL_LIB may swap it)."""
-    try:
-        from rocm_mpi_amd._native import native
-
-        return {"library": native().rccl_library(), "version": native().rccl_version()}
-    except Exception:  # noqa: BLE001 - informational
-        return None
-
-
-def _rccl_nranks(g, pre: dict | None):
-    """ncclCommCount of the halo communicator (or of the preflight ring's RCCL
-    communicator on the single-GPU RCCL-self path); None without RCCL."""
-    try:
-        from rocm_mpi_amd.parallel.comm import RcclComm
-
-        if isinstance(g.comm, RcclComm) and g.comm.native is not None:
-            return int(g.comm.native.count())
-    except Exception:  # noqa: BLE001 - informational
-        return None
-    return (pre or {}).get("rccl_nranks")
+from rocm_mpi_amd.benchmark.attribution import (_n1_key, attribution, load_n1,  # noqa: E402
+                                                save_n1, summarize_timings)
+from rocm_mpi_amd.benchmark.checks import (DRIFT_BOUND, drift_check,  # noqa: E402,F401
+                                           field_stats_global, full_field_check, halo_check,
+                                           snapshot_windows, window_check)
+from rocm_mpi_amd.benchmark.common import (CheckFailed, Watchdog, finish_failed,  # noqa: E402
+                                           gather_obj, log, record_rc)
+from rocm_mpi_amd.benchmark.preflight import _rccl_info, _rccl_nranks, preflight  # noqa: E402
 
 
 def make_config(a, nx: int, ny: int, dev: str, dims: tuple):
@@ -770,6 +208,18 @@ def run(a, world: int, rank: int) -> int:
 
     gpu = a.device == "cuda"
     shared = a.shared_gpu_test and gpu and world > 1
+    if gpu and a.link_probe and (os.environ.get("NCCL_DEBUG", "").upper() in ("", "VERSION", "WARN")
+                                 or not os.environ.get("NCCL_DEBUG_FILE")):
+        # RCCL's connection log (which transport each peer link uses), one file
+        # per process, before this process's first RCCL call
+        import tempfile
+
+        from rocm_mpi_amd.benchmark.preflight import rccl_debug_env
+
+        ld = os.environ.get("RMA_BENCH_RCCL_LOG_DIR") or os.path.join(
+            tempfile.gettempdir(), f"rma_rccl_{os.environ.get('MASTER_PORT', 'solo')}")
+        os.makedirs(ld, exist_ok=True)
+        os.environ.update(rccl_debug_env(ld))
     if shared:
         os.environ["RMA_SHARED_GPU"] = "1"  # select_device: ranks may share cuda:0
         os.environ["RMA_TRANSPORT"] = a.shared_gpu_transport
@@ -853,6 +303,7 @@ def run(a, world: int, rank: int) -> int:
            "data": "synthetic: counter-based uniform [0,1) random-init temperature field",
            "config": {"model": f"diffusion_2D_{a.variant}", "ranks": world,
                       "pci_bus_ids": buses if gpu else None, "shared_gpu_test": bool(shared),
+                      "scaling_point": (not shared) if world > 1 and gpu else None,
                       "diag_env": diag}}
     printed = [False]
 
@@ -880,13 +331,26 @@ def run(a, world: int, rank: int) -> int:
     if a.preflight and a.variant != "kp":
         wd = Watchdog(rank, world, 3 * tmo, "preflight", emit)
         try:
+            # the halo messages of the timed tile: K-wide x- and y-planes
+            nx_est = a.nx or (auto_tile(a.hbm_frac, a.max_tile) if gpu else 130)
+            ny_est = a.ny or nx_est
+            sizes = ({"latency_8B": 8, "x_plane": K * ny_est * 8, "y_plane": K * nx_est * 8}
+                     if a.link_probe else None)
             out["config"]["preflight"] = preflight(dims[:2], K, dev, world, rank, gpu,
-                                                   max(130, 6 * K + 2), tmo)
+                                                   max(130, 6 * K + 2), tmo, sizes)
         except CheckFailed as e:
             out["config"]["preflight"] = {"error": str(e.args[0])}
             return fail_run("preflight", e, 5)
         finally:
             wd.cancel()
+        lk = out["config"]["preflight"].get("links") or {}
+        if gpu and world > 1 and not shared and lk.get("all_p2p") is False:
+            # RCCL chose a host path (sockets, shared memory) for a halo connection
+            out["config"]["scaling_point"] = False
+            out["config"]["non_scaling_reason"] = (
+                "RCCL halo connections are not all GPU-direct P2P: " +
+                ", ".join(f"rank {r['rank']}: {r['transport']}" for r in lk["ranks"]))
+            log(rank, out["config"]["non_scaling_reason"])
 
     try:
         nx = a.nx or auto_tile(a.hbm_frac, a.max_tile)
@@ -911,6 +375,7 @@ def run(a, world: int, rank: int) -> int:
         model.synchronize()
         comm.barrier()
         setup_s = time.perf_counter() - t_setup
+        init_stats = field_stats_global(model.field, comm) if a.full_field_check else None
 
         fast_used = bool(model.cfg.fast_math)  # the side measurements below switch it off
         plan_warm = model.plan(a.warmup)
@@ -936,8 +401,15 @@ def run(a, world: int, rank: int) -> int:
         # (RMA_EXEC_FUSED: with neighbours and >= 2 waves of tasks per pass)
         exec_passes = ({"passes": int(ex.passes_done), "fused": int(ex.fused_passes)}
                        if ex is not None else None)
-        bad = float(model.field[:: max(1, ny // 64), :: max(1, nx // 64)].isfinite().logical_not().sum())
-        bad = comm.allreduce(bad, "sum")
+        # every cell of the timed field, before the side measurements step it further
+        ffc = None
+        if init_stats is not None:
+            try:
+                ffc = full_field_check(model.field, init_stats, model.steps_done, comm, world,
+                                       rank, tmo)
+            except CheckFailed as e:
+                out["config"]["full_field_check"] = e.args[1] if len(e.args) > 1 else None
+                return fail_run("check", CheckFailed(e.args[0]), 3)
         a_eff = 3 * nx * ny * 8 / 1e9
 
         def side_teff(Kside, fast, steps):
@@ -1051,7 +523,13 @@ def run(a, world: int, rank: int) -> int:
         if not nbrs:
             par = "single rank, no halo exchange (one launch per pass)"
         else:
-            tdesc = {"rccl": "RCCL send/recv over xGMI", "staged": "host-staged copies + gloo",
+            lk = (out["config"].get("preflight") or {}).get("links") or {}
+            verdicts = sorted({r["transport"] for r in lk.get("ranks", [])})
+            rccl_desc = ("RCCL send/recv over xGMI (every connection P2P in RCCL's log)"
+                         if lk.get("all_p2p") else
+                         f"RCCL send/recv (RCCL-logged transport: {', '.join(verdicts)})"
+                         if verdicts else "RCCL send/recv")
+            tdesc = {"rccl": rccl_desc, "staged": "host-staged copies + gloo",
                      "gloo": "gloo (CPU twin)", "loopback": "in-process loopback",
                      "self": "periodic self copies"}.get(g.transport, g.transport)
             fused_run = bool(exec_passes and exec_passes["fused"])
@@ -1064,6 +542,8 @@ def run(a, world: int, rank: int) -> int:
         eff_same = (solo / t_it) if solo and nbrs else None
         if shared:
             par = f"SHARED-GPU FUNCTIONAL TEST, {world} ranks on {n_gpus} GPU, not a scaling point; {par}"
+        elif out["config"].get("scaling_point") is False:
+            par = f"NOT A SCALING POINT ({out['config']['non_scaling_reason']}); {par}"
         fast_plan = bool(fast_used)
         n1key = _n1_key(nx, ny, a.steps, a.warmup, K, fast_plan, a.variant)
         n1 = None
@@ -1143,11 +623,11 @@ def run(a, world: int, rank: int) -> int:
             "hipgraph": bool(a.graph),
             "executor_passes": exec_passes,
             "setup_s": round(setup_s, 3),
-            "nonfinite_cells_sampled": int(bad),
+            "full_field_check": ffc,
         })
 
         # --- correctness of this run's code paths (bounded; any failure fails all)
-        rc = 0 if bad == 0 else 3
+        rc = 0
         drift_steps = (a.warmup + a.steps) if a.drift_steps < 0 else a.drift_steps
         if (check_on or drift_steps or snap is not None) and a.variant != "kp":
             wd = Watchdog(rank, world, 3 * tmo, "check phase", emit)

@@ -289,6 +289,16 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("reduce_cpu",
         [](uintptr_t A, int64_t n, int op) { return reduce_cpu(P<const double>(A), n, op); });
+  m.def("field_stats_workspace_doubles", &field_stats_workspace_doubles);
+  m.def("field_stats_gpu", [](uintptr_t A, int64_t n, uintptr_t out3, uintptr_t ws,
+                              uintptr_t stream) {
+    field_stats_gpu(P<const double>(A), n, P<double>(out3), P<double>(ws), S(stream));
+  });
+  m.def("field_stats_cpu", [](uintptr_t A, int64_t n) {
+    double o[3];
+    field_stats_cpu(P<const double>(A), n, o);
+    return std::make_tuple(o[0], o[1], o[2]);
+  });
 
   // ---------------- topology ----------------
   m.def("dims_create", &dims_create, py::arg("nprocs"), py::arg("dims"));

@@ -220,5 +220,12 @@ int64_t reduce_workspace_doubles();
 void reduce_gpu(const double* A, int64_t n, int op, double* out, double* workspace,
                 stream_t stream);
 double reduce_cpu(const double* A, int64_t n, int op);
+// One pass over a field: out3 = {non-finite count, min, max of the finite cells}
+// (device memory; workspace: field_stats_workspace_doubles()). The full-field
+// check of a timed run (bench.py).
+int64_t field_stats_workspace_doubles();
+void field_stats_gpu(const double* A, int64_t n, double* out3, double* workspace,
+                     stream_t stream);
+void field_stats_cpu(const double* A, int64_t n, double* out3);
 
 }  // namespace rma

@@ -238,4 +238,21 @@ double reduce_cpu(const double* A, int64_t n, int op) {
   return v;
 }
 
+// CPU twin of field_stats_gpu (misc.hip)
+void field_stats_cpu(const double* A, int64_t n, double* out3) {
+  double bad = 0.0, lo = INFINITY, hi = -INFINITY;
+  for (int64_t i = 0; i < n; ++i) {
+    const double v = A[i];
+    if (!std::isfinite(v)) {
+      bad += 1.0;
+      continue;
+    }
+    lo = std::fmin(lo, v);
+    hi = std::fmax(hi, v);
+  }
+  out3[0] = bad;
+  out3[1] = lo;
+  out3[2] = hi;
+}
+
 }  // namespace rma

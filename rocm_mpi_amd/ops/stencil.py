@@ -541,3 +541,29 @@ def reduce(A: torch.Tensor, op: str = "sum") -> torch.Tensor:
     f = {"sum": torch.sum, "max": torch.max, "min": torch.min,
          "maxabs": lambda a: a.abs().max(), "nonfinite": lambda a: (~torch.isfinite(a)).sum()}[op]
     return f(A).to(torch.float64)
+
+
+def field_stats(A: torch.Tensor) -> tuple[float, float, float]:
+    """(non-finite cell count, min, max of the finite cells) of a float64 field
+    in ONE pass (native kernel on the GPU and its CPU twin): the full-field
+    check of a timed run. Synchronises the field's stream (returns floats)."""
+    if not (A.dtype == torch.float64 and A.is_contiguous()):
+        raise TypeError("field_stats expects a contiguous float64 tensor")
+    if A.is_cuda:
+        key = ("stats", A.device)
+        ws = _ws_cache.get(key)
+        if ws is None:
+            ws = torch.empty(native().field_stats_workspace_doubles(), dtype=torch.float64,
+                             device=A.device)
+            _ws_cache[key] = ws
+        out = torch.empty(3, dtype=torch.float64, device=A.device)
+        native().field_stats_gpu(_ptr(A), A.numel(), _ptr(out), _ptr(ws), stream_handle(A))
+        bad, lo, hi = out.tolist()
+        return bad, lo, hi
+    if _use_native_cpu():
+        return tuple(native().field_stats_cpu(_ptr(A), A.numel()))
+    fin = torch.isfinite(A)
+    v = A[fin]
+    return (float((~fin).sum()), float(v.min()) if v.numel() else float("inf"),
+            float(v.max()) if v.numel() else float("-inf"))
+

@@ -356,11 +356,14 @@ class IpcComm(TorchDistComm):
     IPC (``csrc/include/rma/ipc.h``): every receiver owns a double-buffered
     device mailbox per sender, which the sender maps and fills with one
     device-to-device copy per message (over xGMI between GPUs, on-device when
-    ranks share a GPU). Ordering (``RMA_IPC_MODE``): ``stream`` (default) --
-    per-slot full/empty flags in POSIX shared memory that the streams wait on
-    and write (hipStreamWaitValue64 / hipStreamWriteValue64), nothing blocks
-    the host; ``host`` -- the host waits for its own copies and polls the
-    peers' generation flags (validation). The reference's intra-node
+    ranks share a GPU). Ordering (``RMA_IPC_MODE``): ``stream`` -- per-slot
+    full/empty flags in POSIX shared memory that bounded one-wave flag
+    kernels (``csrc/kernels/flags.hip``: system-scope acquire / release,
+    timeout with an error word) wait on and write on the streams, nothing
+    blocks the host (the default when every rank shares one GPU, the only
+    case it has run on); ``host`` -- the host waits for its own copies and
+    polls the peers' generation flags (the default across GPUs, see
+    :meth:`_auto_mode`). The reference's intra-node
     ROCm-aware MPI path (``scripts/rocmaware_test_selectdevice.jl:16-22``) without
     MPI or RCCL. Collectives and gather stay on gloo (host-staged), as in
     ``staged``. ``peers``: the halo peers (Cartesian neighbours and diagonals).
@@ -387,9 +390,10 @@ class IpcComm(TorchDistComm):
         cap = max(8, int(mb * (1 << 20)))
         self.device = torch.device(device)
         self.peers = sorted({int(p) for p in peers if int(p) >= 0})
-        mode = mode or os.environ.get("RMA_IPC_MODE", "stream")
+        mode = mode or os.environ.get("RMA_IPC_MODE", "") or self._auto_mode()
         if mode not in ("stream", "host"):
             raise ValueError(f"IPC mode must be stream or host, got {mode!r}")
+        self.mode = mode
         self._c = native().IpcTransport(self.rank, self.size, self.device.index or 0, self.peers,
                                         cap, token, timeout_s, 1 if mode == "stream" else 0)
         others = [p for p in self.peers if p != self.rank]
@@ -401,6 +405,25 @@ class IpcComm(TorchDistComm):
         # stays in /dev/shm even if the job dies
         dist.barrier(group=self._pg)
         self._c.unlink_shm()
+
+    def _auto_mode(self) -> str:
+        """Stream mode (flag kernels, nothing blocks the host) is verified only
+        with every rank on ONE GPU: whether a peer GPU's xGMI writes into this
+        GPU's mailbox are visible to the copy-out under the flag kernels'
+        system-scope acquire has not run on a multi-GPU node. So
+        stream mode is the default only when every rank of the job shares one
+        physical GPU; ranks on different GPUs default to host mode (the host
+        waits on its own copies' events and polls the peers' generation flags,
+        which needs no cross-GPU memory-scope argument). RMA_IPC_MODE overrides."""
+        try:
+            from .._native import native
+
+            bus = native().device_pci_bus_id(self.device.index or 0)
+        except Exception:  # noqa: BLE001 - unknown: the conservative mode
+            bus = f"unknown-{self.rank}"
+        buses: list = [None] * self.size
+        dist.all_gather_object(buses, bus, group=self._pg)
+        return "stream" if len(set(buses)) == 1 else "host"
 
     @property
     def native(self):
@@ -435,11 +458,16 @@ class IpcComm(TorchDistComm):
             # every peer reached teardown (so every group it owes me is
             # enqueued); a peer that died instead leaves my stream-mode waits
             # unsatisfiable: release them from the host before draining
-            tmo = float(os.environ.get("RMA_TEARDOWN_TIMEOUT", "30"))
+            # long: a live peer may be late (rank 0 gathering, checkpointing),
+            # and releasing the waits under it corrupts its receives
+            tmo = float(os.environ.get("RMA_IPC_TEARDOWN_TIMEOUT",
+                                       os.environ.get("RMA_TEARDOWN_TIMEOUT", "300")))
+            aborted = None
             try:
                 work = dist.barrier(group=self._pg, async_op=True)
                 work.wait(timeout=datetime.timedelta(seconds=tmo))
-            except Exception:  # noqa: BLE001 - a dead peer must not hang teardown
+            except Exception as e:  # noqa: BLE001 - a dead peer must not hang teardown
+                aborted = e
                 self._c.abort_waits()
             if torch.cuda.is_available() and torch.cuda.is_initialized():
                 torch.cuda.synchronize(self.device)
@@ -456,6 +484,13 @@ class IpcComm(TorchDistComm):
             except Exception:  # noqa: BLE001
                 pass
             self._c = None
+            if aborted is not None:
+                # the released waits let pending receives copy stale mailbox
+                # data: never a normal return
+                raise RuntimeError(
+                    f"IPC teardown (rank {self.rank}): the peers' barrier did not complete "
+                    f"within {tmo:.0f} s ({type(aborted).__name__}: {aborted}); pending "
+                    f"stream waits were released, received halos may be incomplete")
             if timed_out is not None:
                 raise timed_out
 

@@ -54,7 +54,17 @@ def test_bench_small_tile_with_self_rccl_halo_check():
     assert len(rd) == 1 and rd[0]["pci_bus_id"] == c["pci_bus_ids"][0]
     assert c["teff_single_step_kernel_GBps"] > 0 and c["teff_bitwise_kstep_GBps"] > 0
     assert c["pci_bus_ids"] and len(c["pci_bus_ids"]) == 1
-    assert c["nonfinite_cells_sampled"] == 0
+    # every cell of the timed field: finite, inside the initial bounds (max principle)
+    ff = c["full_field_check"]
+    assert ff["ok"] and ff["nonfinite"] == 0 and ff["cells"] == 4096 * 4096 and ff["steps"] == 25
+    assert ff["init_min"] <= ff["min"] <= ff["max"] <= ff["init_max"]
+    # per-link probe at the timed tile's message sizes (one GPU: RCCL to itself)
+    lk = pf["links"]
+    assert lk["sizes"]["x_plane"] == 24 * 4096 * 8 and lk["all_p2p"] is None
+    r0 = lk["ranks"][0]
+    assert r0["transport"].startswith("self") and r0["peers"] == [0]
+    assert [t["message"] for t in r0["timed"]] == ["latency_8B", "x_plane", "y_plane"]
+    assert all(t["data_ok"] and t["us"] > 0 for t in r0["timed"])
     # the timed field itself: three full-width row windows bitwise vs the CPU twin
     wc = c["headline_window_check"]
     assert wc["windows"] == 3 and wc["bitwise"] is True and wc["full_width"] is True
@@ -95,7 +105,14 @@ def test_bench_two_processes_sharing_the_gpu(tmp_path, transport):
     assert c["ranks"] == 2 and d["n_gpus"] == 1 and c["transport"] == transport
     assert c["rccl_halo_bitwise_ok"] is True and c["halo_check"]["tiles_mismatched"] == 0
     assert c["pass_timing"]["passes"] == len(c["passes_timed"]) and sum(c["passes_timed"]) == 24
-    assert len(c["pci_bus_ids"]) == 2 and c["nonfinite_cells_sampled"] == 0
+    assert len(c["pci_bus_ids"]) == 2 and c["full_field_check"]["ok"]
+    assert c["scaling_point"] is False
+    lk = c["preflight"]["links"]
+    assert [r["peers"] for r in lk["ranks"]] == [[1], [0]]
+    assert all(t["data_ok"] for r in lk["ranks"] for t in r["timed"])
+    if transport == "rccl":  # RCCL between processes sharing cuda:0: its socket transport
+        assert [r["transport"] for r in lk["ranks"]] == ["socket", "socket"]
+        assert lk["all_p2p"] is False and "NET/Socket" in lk["ranks"][0]["transport_kinds"]
     assert [r["rank"] for r in c["ranks_detail"]] == [0, 1]
     assert c["preflight"]["ring_ok"] and c["preflight"]["halo"]["transport"] == transport
     assert c["headline_window_check"]["bitwise"] is True
@@ -122,3 +139,9 @@ def test_bench_rehearsal_of_the_scaling_run_over_rccl(gpus, dims):
     ea = c["e_attribution"]
     assert ea["e_gpu"] is not None and ea["e_product"] is not None
     assert [r["rank"] for r in c["ranks_detail"]] == list(range(gpus))
+    # the record proves its own transport and links
+    lk = c["preflight"]["links"]
+    assert {r["transport"] for r in lk["ranks"]} == {"socket"} and lk["all_p2p"] is False
+    assert all(len(r["timed"]) == 3 * len(r["peers"]) and r["peers"] for r in lk["ranks"])
+    assert c["scaling_point"] is False and c["full_field_check"]["ok"]
+    assert "socket" in c["parallelism"] or "NET" in c["parallelism"] or "socket" in str(lk)

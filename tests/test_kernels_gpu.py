@@ -267,3 +267,21 @@ def test_flag_kernels_write_wait_and_bounded_timeout():
     dt = time.perf_counter() - t0
     assert err.tolist() == [0, 12, 0] and 0.15 < dt < 5.0, (err.tolist(), dt)
     assert guard.tolist() == [-7, 5, -7]
+
+
+@pytest.mark.parametrize("n,offset", [(1, 0), (7, 0), (4097, 0), (4097, 1), (3 * 2**20 + 5, 1),
+                                      (2**24, 0)])
+def test_field_stats_gpu_equals_cpu_twin(n, offset):
+    """One-pass field statistics (bench.py full-field check): non-finite
+    count, min and max of the finite cells, on aligned and 8-byte-offset
+    views, odd lengths, with NaN / +-inf planted; equal to the CPU twin."""
+    g = torch.Generator().manual_seed(n + offset)
+    base = torch.rand(n + offset, generator=g, dtype=torch.float64) * 6 - 3
+    a = base[offset:]
+    if n > 8:
+        a[n // 3] = float("nan")
+        a[n - 1] = float("inf")
+        a[0] = -float("inf")
+    ref = ops.field_stats(a.contiguous())
+    d = base.to("cuda")[offset:]
+    assert ops.field_stats(d) == ref

@@ -125,7 +125,7 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     dims = [int(v) for v in extra[3].split(",")]
     assert c["global_grid"] == [dims[0] * (nx - 2 * K) + 2 * K, dims[1] * (nx - 2 * K) + 2 * K]
     assert abs(d["value"] - world * c["teff_per_gpu_GBps"]) <= 1e-6 * d["value"] + 0.005 * world + 0.01
-    assert c["nonfinite_cells_sampled"] == 0
+    assert c["full_field_check"]["ok"] and c["full_field_check"]["nonfinite"] == 0
     # self-validation of a multi-rank point
     assert c["ranks"] == world and c["transport"] == "gloo"
     assert sum(c["passes_timed"]) == 20 and max(c["passes_timed"]) <= K
