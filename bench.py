@@ -163,6 +163,7 @@ from rocm_mpi_amd.benchmark.checks import (DRIFT_BOUND, drift_check,  # noqa: E4
 from rocm_mpi_amd.benchmark.common import (CheckFailed, Watchdog, finish_failed,  # noqa: E402
                                            gather_obj, log, record_rc)
 from rocm_mpi_amd.benchmark.preflight import _rccl_info, _rccl_nranks, preflight  # noqa: E402
+from rocm_mpi_amd.config import diag_entries, diag_flag, diag_value  # noqa: E402
 
 
 def make_config(a, nx: int, ny: int, dev: str, dims: tuple):
@@ -216,7 +217,7 @@ def run(a, world: int, rank: int) -> int:
 
         from rocm_mpi_amd.benchmark.preflight import rccl_debug_env
 
-        ld = os.environ.get("RMA_BENCH_RCCL_LOG_DIR") or os.path.join(
+        ld = diag_value("bench_rccl_log_dir") or os.path.join(
             tempfile.gettempdir(), f"rma_rccl_{os.environ.get('MASTER_PORT', 'solo')}")
         os.makedirs(ld, exist_ok=True)
         os.environ.update(rccl_debug_env(ld))
@@ -229,20 +230,18 @@ def run(a, world: int, rank: int) -> int:
         # a scaling point must never silently run on the host-staged transport
         os.environ["RMA_RCCL_STRICT"] = "1"
         os.environ["RMA_TRANSPORT"] = "rccl"
+    # every diagnostic switch of this run (RMA_DIAG, validated) and the tuning
+    # knobs that change what the timed passes run
     diag = {k: v for k, v in sorted(os.environ.items())
-            if k.startswith("RMA_DIAG") or k in ("RMA_FRAME_SIDES", "RMA_FRAME_ALIGNED",
-                                                 "RMA_PASS_COSTS", "RMA_HALO_BATCH",
-                                                 "RMA_FRAME_FILL", "RMA_EXEC_STREAMS",
-                                                 "RMA_PIPE_FAST", "RMA_HALO_CROSS",
-                                                 "RMA_FRAME_BANDS", "RMA_RCCL_LIB",
-                                                 "RMA_FRAME_CHUNK_DIV")}
-    if gpu and os.environ.get("RMA_PIPE_FAST") == "pipe5":  # an A/B of the lab kernel
+            if k in ("RMA_DIAG", "RMA_RCCL_LIB", "RMA_EXEC_FUSED", "RMA_EXEC_FUSED_TIMEOUT")}
+    diag_entries()  # an unknown RMA_DIAG key fails the run here, before any work
+    if gpu and diag_value("pipe_fast") == "pipe5":  # an A/B of the lab kernel
         from rocm_mpi_amd._native import load_lab
 
         load_lab()
     check_on = a.check == 1 or (a.check < 0 and (gpu or world > 1))
-    if check_on and os.environ.get("RMA_DIAG_SKIP_EXCHANGE", "0") == "1":
-        log(rank, "RMA_DIAG_SKIP_EXCHANGE=1 skips every halo exchange: refused with the halo "
+    if check_on and diag_flag("skip_exchange"):
+        log(rank, "RMA_DIAG=skip_exchange skips every halo exchange: refused with the halo "
                   "check on (--check 0 for a diagnosis run)")
         return 2
 

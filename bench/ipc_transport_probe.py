@@ -13,7 +13,7 @@ transport's group_end during the timed steps (stream mode: 0), and with
 golden model bitwise. perf_hide with K = 1 exchanges every step, the hardest
 ordering test for a transport (tests/golden.py is the oracle). --graph
 replays the steps from a hipGraph captured by the executor (stream mode,
-RMA_IPC_GRAPH=1), checked against the same golden model.
+RMA_DIAG no_ipc_graph unset), checked against the same golden model.
 """
 from __future__ import annotations
 
@@ -38,13 +38,15 @@ def main(argv=None) -> int:
     ap.add_argument("--dims", default="0,0")
     ap.add_argument("--check", action="store_true", help="canonical arithmetic, golden compare")
     ap.add_argument("--graph", action="store_true",
-                    help="hipGraph replay (stream-mode IPC, sets RMA_IPC_GRAPH=1: experimental)")
+                    help="hipGraph replay (stream-mode IPC, experimental)")
     ap.add_argument("--graph-request", action="store_true",
-                    help="ask for graph replay without RMA_IPC_GRAPH (the executor falls back)")
+                    help="ask for graph replay with RMA_DIAG=no_ipc_graph (the executor falls back)")
     a = ap.parse_args(argv)
     os.environ["RMA_TRANSPORT"] = a.transport
-    if a.graph:
-        os.environ["RMA_IPC_GRAPH"] = "1"
+    if a.graph_request:
+        from rocm_mpi_amd.config import diag_with
+
+        os.environ["RMA_DIAG"] = diag_with(no_ipc_graph=True)
     import numpy as np
     import torch
     import torch.distributed as dist

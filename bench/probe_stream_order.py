@@ -14,7 +14,7 @@ low-priority stream). Each stream-creation mode runs in its own subprocess:
 
 Run under ``rocprofv3 --kernel-trace`` to see the hardware queue of every
 dispatch; the JSON line per mode lists GB/s per instance and the HIP stream
-handles the executor reported (RMA_EXEC_VERBOSE=1).
+handles the executor reported (RMA_DIAG exec_verbose).
 
     python bench/probe_stream_order.py --n 16384 --modes lofirst,hifirst,plain,pool
 """
@@ -74,7 +74,7 @@ def main(argv=None) -> int:
         return 0
     out = {}
     for mode in a.modes.split(","):
-        env = dict(os.environ, RMA_EXEC_STREAMS=mode, RMA_EXEC_VERBOSE="1")
+        env = dict(os.environ, RMA_DIAG=f"exec_streams={mode},exec_verbose")
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--n",
                             str(a.n), "--steps", str(a.steps)], capture_output=True, text=True,
                            env=env, timeout=600)

@@ -10,7 +10,7 @@ its own child process (a crash stays contained, each child has a time limit):
   lib = linked  (the RCCL the core binds to in a torch process: torch's)
   lib = system  (RMA_RCCL_LIB=system: /opt/rocm/lib/librccl.so.1 loaded
                  privately for the native communicators)
-  x graph = 0 / 1 (RMA_RCCL_GRAPH=1 lets the executor capture the exchange)
+  x graph = 0 / 1 (RMA_DIAG=rccl_graph lets the executor capture the exchange)
 
 on one GPU: a periodic perf_hide tile whose four halo planes go through RCCL
 send/recv to self, one-step passes (the small-tile regime). A child reports
@@ -83,7 +83,7 @@ def main(argv=None) -> int:
     ref = None
     for cfg in a.configs.split(","):
         lib, graph = cfg.split(":")
-        env = dict(os.environ, RMA_RCCL_GRAPH=graph, RMA_RCCL_BLOCKING="1")
+        env = dict(os.environ, RMA_DIAG="rccl_graph" if graph == "1" else "", RMA_RCCL_BLOCKING="1")
         if lib == "system":
             env["RMA_RCCL_LIB"] = "system"
         else:

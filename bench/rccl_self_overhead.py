@@ -106,7 +106,7 @@ def main(argv=None) -> int:
            "spacing": a.spacing,
            "periodic_via": "local copies" if a.self_copies else "rccl self send/recv",
            "init": a.init,
-           "frame_sides": os.environ.get("RMA_FRAME_SIDES", "neighbours"), "variants": {}}
+           "frame_sides": os.environ.get("RMA_DIAG", "") or "neighbours", "variants": {}}
     for variant in a.variants.split(","):
         rows = []
         for periodic in (c == "p" for c in a.pattern):

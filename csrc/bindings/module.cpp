@@ -11,6 +11,7 @@
 #include <tuple>
 #include <vector>
 
+#include "rma/config.h"
 #include "rma/comm.h"
 #include "rma/common.h"
 #include "rma/executor.h"
@@ -289,6 +290,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("reduce_cpu",
         [](uintptr_t A, int64_t n, int op) { return reduce_cpu(P<const double>(A), n, op); });
+  m.def("diag_string", &diag_string);  // RMA_DIAG, validated (unknown key: error)
+  m.def("diag_value", [](const std::string& k) { return diag_value(k.c_str()); });
+  m.def("env_double", &env_double);
+  m.def("env_choice", &env_choice);
   m.def("field_stats_workspace_doubles", &field_stats_workspace_doubles);
   m.def("field_stats_gpu", [](uintptr_t A, int64_t n, uintptr_t out3, uintptr_t ws,
                               uintptr_t stream) {

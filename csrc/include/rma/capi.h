@@ -91,7 +91,7 @@ int rma_executor_create_kf(rma_grid* g, int mode, double* T, double* T2, const d
                            double* qy, double* dTdt, rma_executor** out);
 // Same with `graph_steps` > 0: steps are replayed from a hipGraph capturing
 // `graph_steps` steps (the host enqueue cost of a step drops to a graph launch);
-// needs a capturable halo transport (RCCL: RMA_RCCL_GRAPH=1, see README).
+// needs a capturable halo transport (RCCL: RMA_DIAG=rccl_graph, see README).
 int rma_executor_create_g(rma_grid* g, int mode, double* T, double* T2, const double* iCp,
                           int64_t nx, int64_t ny, const double coef[4], int64_t bwx, int64_t bwy,
                           int steps_per_pass, int fast_math, int graph_steps, double* qx,

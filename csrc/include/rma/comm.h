@@ -51,7 +51,7 @@ class RcclComm : public P2PTransport {
   void recv(void* buf, size_t bytes, int peer, stream_t stream) override;
   // RCCL P2P inside hipStreamBeginCapture crashed (SIGSEGV) with the RCCL
   // 2.26 bundled by torch on MI355X (scripts/rccl_probe.py, 2026-10-15):
-  // graph replay is refused unless RMA_RCCL_GRAPH=1.
+  // graph replay is refused unless RMA_DIAG=rccl_graph.
   bool capturable() const override;
   void allreduce(const void* sendbuf, void* recvbuf, size_t count, DType dt, RedOp op,
                  stream_t stream);
@@ -71,7 +71,7 @@ class RcclComm : public P2PTransport {
   // nonblocking(): the communicator was created non-blocking (init with a
   // timeout; group ends are then polled until RCCL has enqueued them);
   // data_blocking(): the data path runs on a blocking communicator
-  // (RMA_RCCL_BLOCKING=1 init, or RMA_RCCL_DATA_BLOCKING=1: split from the
+  // (RMA_RCCL_BLOCKING=1 init, or RMA_DIAG rccl_data_blocking: split from the
   // non-blocking one after init; no host-time gain measured, see comm.cpp).
   bool nonblocking() const { return nonblocking_; }
   bool data_blocking() const { return parent_ != nullptr || !nonblocking_; }

@@ -100,7 +100,7 @@ class DiffusionExecutor {
   const std::vector<double>& pass_costs() const { return cost_; }
   // Launch every kernel a run may use once on a tiny scratch field (first
   // launches stay out of timed regions); synchronous. Done by the constructor
-  // unless RMA_EXEC_PRIME=0.
+  // unless RMA_DIAG=no_prime.
   void prime();
   // Record per-pass HIP events from now on (clears earlier records); read
   // them with timings() once the work is done (synchronises).
@@ -177,19 +177,16 @@ class DiffusionExecutor {
   int cus_ = 256;  // compute units of the device
   int64_t fused_passes_ = 0;
   double fused_timeout_s_ = 60.0;
-  int fused_fdiv_ = 1;  // frame rects' rows per task = the pass's / this (RMA_FUSED_FRAME_DIV)
   uint64_t* sig_ = nullptr;
   uint32_t* ferr_host_ = nullptr;
   uint32_t* ferr_dev_ = nullptr;
   bool fused_pass_ok(const PassGeom& g, const StencilTuning& tn) const;
-  bool fused_step_ok() const;
   // the frame-first fused pass around `launch(rects, n, tuning)`: one launch
   // of the frame rects + interior on the low stream, the frame-flag wait and
   // the exchange on the high one (tn gets the signal fields)
   template <typename Launch>
   void enqueue_fused(const std::vector<Rect>& frame, const Rect& interior, StencilTuning tn,
                      double* Tout, void* const* ev, Launch&& launch);
-  bool fused_step_ = false;  // one-step passes fused too (RMA_EXEC_FUSED_STEP=1)
   void check_fused_error() const;
   void* graph_exec_ = nullptr;  // hipGraphExec_t
   int64_t graph_len_ = 0;
@@ -208,6 +205,7 @@ class DiffusionExecutor {
   size_t tused_ = 0;
   void* tevent();
   void release_timing();
+  void release_resources();  // destructor and a throwing constructor
 };
 
 }  // namespace rma

@@ -84,7 +84,7 @@ class IpcTransport : public P2PTransport {
   void group_end() override;
   void send(const void* buf, size_t bytes, int peer, stream_t stream) override;
   void recv(void* buf, size_t bytes, int peer, stream_t stream) override;
-  // stream mode: kernels and copies only (RMA_IPC_GRAPH=0 refuses capture)
+  // stream mode: kernels and copies only (RMA_DIAG=no_ipc_graph refuses capture)
   bool capturable() const override;
   // raise if a stream-mode wait timed out (peer gone or protocol out of step)
   void check_error();

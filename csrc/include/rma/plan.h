@@ -32,7 +32,7 @@ Rect owned_rect(int64_t nx, int64_t ny, int K, const Neighbors& nbr);
 
 // Sides [dim][lo/hi] whose cells perf_hide computes ahead of the exchange:
 // those with a neighbour (their send planes), all four under
-// RMA_FRAME_SIDES=all (the r1-r2 layout, for A/B runs).
+// RMA_DIAG frame_sides=all (the r1-r2 layout, for A/B runs).
 std::array<std::array<bool, 2>, 2> frame_sides(const Neighbors& nbr);
 
 struct PassGeom {
@@ -66,7 +66,7 @@ struct PassGeom {
 // first / last strip column and chunk row (a few % of the tile) instead of
 // ol-wide strips, which a trapezoid kernel computes at several times the
 // interior's cost per cell.
-// bands: height of the aligned y-bands, -1 = the default / RMA_FRAME_BANDS,
+// bands: height of the aligned y-bands, -1 = the default / RMA_DIAG frame_bands,
 // 0 = the ol-K rows the exchange needs, 1 = whole task rows.
 PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool hide,
                        int64_t bwx, int64_t bwy, int64_t olx, int64_t oly, int64_t task_w = 0,
@@ -81,7 +81,7 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
 // is exposed; half-height frame tasks finish at ~60 % of the pass (4096^2:
 // x 10.5 -> 1.1 %, y 7.6 -> 3.1 %, x+y 17.6 -> 2.2 % with ol-K bands; 8192^2
 // y 8.2 -> 3.1 % with ol-K bands).
-// RMA_FRAME_CHUNK_DIV / RMA_FRAME_BANDS override.
+// RMA_DIAG frame_chunk_div / frame_bands override.
 struct FrameLayout {
   int chunk_div = 1;
   int bands = -1;
@@ -97,7 +97,8 @@ FrameLayout frame_layout(int64_t ny, const Neighbors& nbr);
 // cells = nx*ny of the tile (0: the 288 GB tile): the nearest measured tile
 // class (4096^2, 8192^2, 16384^2, 101376^2) in log scale.
 std::vector<double> default_pass_costs(int kmax, bool fast5, double cells = 0);
-// RMA_PASS_COSTS="K:cost,K:cost,..." overrides entries (sweeps, tests).
+// RMA_DIAG pass_costs=K:cost/K:cost/... overrides entries (sweeps, tests;
+// this function takes the entries comma-separated).
 void apply_cost_overrides(std::vector<double>& cost, const char* spec);
 
 // Rows per (strip, chunk) task of the pipelined K-step kernels (stencil_pipe.h)

@@ -1,5 +1,6 @@
 // Registry of the kernels that live outside the core library: librma_lab.so
-// (csrc/lab) holds the superseded and experimental K-step kernels that stay
+// (csrc/lab) holds the superseded and experimental kernels (the LDS-tiled
+// one-step kernel, K-step kernels) that stay
 // useful as test oracles and for sweeps (kernels 0-2, 4-8 of the overlapped-
 // strip family, the pipelined kernel's alternative stage splits, its
 // ds_bpermute variant and the two-column blocks). The core dispatches to them
@@ -20,6 +21,10 @@ struct LabHooks {
                 stream_t stream) = nullptr;
   // pipelined (K, S, V, C, arithmetic) outside the default stage split
   bool (*pipe)(int K, int S, int V, int C, int arith, const pipe::PipeLaunch& a) = nullptr;
+  // one-step kernels other than the march (tune.kernel 1: LDS-tiled)
+  bool (*onestep)(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+                  const Rect* rects, int nrects, const StencilCoef& c, const StencilTuning& tune,
+                  stream_t stream) = nullptr;
 };
 
 void set_lab_hooks(const LabHooks& h);
@@ -31,6 +36,9 @@ bool kstep(int K, double* T2, const double* T, const double* iCp, int64_t nx, in
            const Rect* rects, int nrects, const StencilCoef& c, const StencilTuning& tune,
            stream_t stream);
 bool pipe(int K, int S, int V, int C, int arith, const pipe::PipeLaunch& a);
+bool onestep(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
+             const Rect* rects, int nrects, const StencilCoef& c, const StencilTuning& tune,
+             stream_t stream);
 }  // namespace lab
 
 }  // namespace rma

@@ -32,6 +32,7 @@
 
 #include "rma/hip_check.h"
 #include "rma/kernels.h"
+#include "lab_hooks.h"
 #include "stencil_device.h"
 
 namespace rma {
@@ -131,67 +132,8 @@ __global__ __launch_bounds__(kBlock) void stencil_march_kernel(double* __restric
                                                                int64_t nx, RectList L,
                                                                StencilCoef k, int chunk_rows,
                                                                int remap) {
-  // a fused one-step pass (RectList::sig): the frame rects' blocks come first,
-  // never XCD-remapped, and every one of their waves counts its completion
-  // (waves leave the body independently: column mode, padding waves)
-  const int64_t sig_first = L.sig ? L.sig_blocks : 0;
-  const int64_t b = remap ? xcd_remap_after(blockIdx.x, gridDim.x, sig_first) : (int64_t)blockIdx.x;
+  const int64_t b = remap ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   march_body<V, NT, kUnroll, NTL, NTT>(T2, T, iCp, nx, L, k, chunk_rows, b);
-  if (b < sig_first) signal_wave_done(L.sig, (int64_t)kWavesPerBlock * L.sig_blocks);
-}
-
-// ---------------------------------------------------------------------------
-// LDS-tiled variant (kernel=1), kept as the measured alternative to the march:
-// a 256-thread block stages a (TY+2) x (TX+2) tile of T in LDS (one row per
-// wave-instruction, 16-B loads), then every thread updates TY/4 cells of its
-// column from LDS. T is re-read (TY+2)/TY times through L2/MALL instead of
-// once; see profiles/ for the A/B against the march.
-// ---------------------------------------------------------------------------
-constexpr int kTileX = 256;  // cells per tile row (one double per thread)
-constexpr int kTileY = 16;
-
-template <bool NT>
-__global__ __launch_bounds__(kBlock) void stencil_lds_kernel(double* __restrict__ T2,
-                                                             const double* __restrict__ T,
-                                                             const double* __restrict__ iCp,
-                                                             int64_t nx, RectList L,
-                                                             StencilCoef k) {
-  __shared__ double tile[kTileY + 2][kTileX + 2];
-  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
-  int ri = 0;
-  while (ri < L.n - 1 && b >= L.block_end[ri]) ++ri;
-  const int64_t bstart = ri ? L.block_end[ri - 1] : 0;
-  const int64_t ntx = L.strips[ri];
-  const int64_t t = b - bstart;
-  const Rect r = L.r[ri];
-  const int64_t tx = t % ntx, ty = t / ntx;
-  const int64_t x0 = r.x0 + tx * kTileX;
-  const int64_t y0 = r.y0 + ty * kTileY;
-  const int tid = threadIdx.x;
-  // Stage rows y0-1 .. y0+TY (clamped to the rect's +-1 neighbourhood).
-  for (int j = tid >> 6; j < kTileY + 2; j += kWavesPerBlock) {
-    const int64_t gy = min(y0 - 1 + j, r.y1);
-    const double* src = T + gy * nx;
-    for (int i = tid & 63; i < kTileX + 2; i += kWave) {
-      const int64_t gx = min(x0 - 1 + i, r.x1);
-      tile[j][i] = src[gx];
-    }
-  }
-  __syncthreads();
-  const int64_t gx = x0 + tid;
-  if (gx >= r.x1) return;
-  for (int j = 1; j <= kTileY; ++j) {
-    const int64_t gy = y0 - 1 + j;
-    if (gy >= r.y1) break;
-    const double c = tile[j][tid + 1];
-    const double v = cell(tile[j][tid], c, tile[j][tid + 2], tile[j - 1][tid + 1],
-                          tile[j + 1][tid + 1], iCp[gy * nx + gx], k);
-    if constexpr (NT) {
-      __builtin_nontemporal_store(v, T2 + gy * nx + gx);
-    } else {
-      T2[gy * nx + gx] = v;
-    }
-  }
 }
 
 void validate_rects(int64_t nx, int64_t ny, const Rect* rects, int nrects) {
@@ -223,44 +165,22 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
   // 8-padded block rows win up to 64K-wide tiles (16384^2: 6.44 vs 6.26 TB/s);
   // per-XCD contiguous ranges win on the 288 GB tiles (101376^2: 6.25 vs 5.93).
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
-  const bool lds = tune.kernel == 1;
-  RectList L{};
-  int64_t total = 0;
-  if (lds) {
-    for (int i = 0; i < nrects; ++i) {
-      const Rect& r = rects[i];
-      if (r.empty()) continue;
-      const int n = L.n++;
-      L.r[n] = r;
-      L.xa[n] = r.x0;
-      L.strips[n] = (r.x1 - r.x0 + kTileX - 1) / kTileX;
-      L.chunks[n] = (r.y1 - r.y0 + kTileY - 1) / kTileY;
-      total += L.strips[n] * L.chunks[n];
-      L.block_end[n] = total;
-    }
-  } else {
-    total = plan_rects(L, rects, nrects, V, tune.chunk_rows, remap, true);
+  // the LDS-tiled one-step kernel (kernel 1, the measured loser against the
+  // march, 3.90 vs 6.20 TB/s at 16384^2: profiles/SUMMARY_r1.md) lives in the lab library
+  if (tune.kernel == 1) {
+    if (!lab_hooks().onestep) lab_missing("the LDS-tiled one-step kernel (kernel 1)");
+    RMA_CHECK_ARG(lab_hooks().onestep(T2, T, iCp, nx, ny, rects, nrects, c, tune, stream),
+                  "one-step kernel " << tune.kernel);
+    return;
   }
+  RMA_CHECK_ARG(!tune.signal, "a signalling launch needs a pipelined K-step kernel");
+  RectList L{};
+  const int64_t total = plan_rects(L, rects, nrects, V, tune.chunk_rows, remap, true);
   if (L.n == 0) return;
   RMA_CHECK_ARG(total < (int64_t(1) << 31), "grid too large: " << total << " blocks");
-  if (tune.signal) {  // fused one-step pass: the first signal_rects rects' waves signal
-    RMA_CHECK_ARG(!lds, "a signalling launch needs the march kernel");
-    RMA_CHECK_ARG(tune.signal_rects >= 1 && tune.signal_rects < nrects,
-                  "signal rects " << tune.signal_rects << " of " << nrects);
-    int ns = 0;
-    for (int i = 0; i < tune.signal_rects; ++i) ns += rects[i].empty() ? 0 : 1;
-    RMA_CHECK_ARG(ns > 0, "signalling launch without a non-empty signal rect");
-    L.sig = tune.signal;
-    L.sig_blocks = L.block_end[ns - 1];
-  }
   const dim3 grid((unsigned)total), block(kBlock);
   hipStream_t s = as_stream(stream);
-  if (lds) {
-    if (tune.nontemporal)
-      stencil_lds_kernel<true><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c);
-    else
-      stencil_lds_kernel<false><<<grid, block, 0, s>>>(T2, T, iCp, nx, L, c);
-  } else {
+  {
     const int u = tune.unroll;
     RMA_CHECK_ARG(u == 2 || u == 4 || u == 8, "unroll must be 2, 4 or 8");
     const bool nts = tune.nontemporal & 1, ntl = (tune.nontemporal >> 1) & 1;

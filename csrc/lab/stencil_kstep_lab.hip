@@ -535,6 +535,7 @@ struct Register {
     LabHooks h;
     h.kstep = &lab::kstep;
     h.pipe = &lab::pipe;
+    h.onestep = &lab::onestep;
     set_lab_hooks(h);
   }
 } g_register;

@@ -1,7 +1,7 @@
 // librma_lab.so, 5-cells-per-lane unit: the any-K pipelined kernel
 // (stencil_pipe.h) with fast5 arithmetic at 5 cells per lane (320-column
 // strips, v-major LDS rows, delayed factor ring), default stage split. An
-// experiment kept for sweeps (bench/pass_sweep.py --pipe5, RMA_PIPE_FAST=pipe5):
+// experiment kept for sweeps (bench/pass_sweep.py --pipe5, RMA_DIAG=pipe_fast=pipe5):
 // 3.5 % less fp64 work and 23 % fewer lane moves per cell update at K = 20,
 // but only 0.8-1.6 % faster per pass at 101120^2 (profiles/SUMMARY_r3.md),
 // about what the register-factor kernel (piper) gains at K = 20 without the

@@ -1,3 +1,4 @@
+#include "rma/config.h"
 #include "rma/comm.h"
 
 #include <hip/hip_runtime.h>
@@ -165,8 +166,7 @@ RcclComm::RcclComm(int nranks, int rank, const std::string& uid, int device,
     // with RCCL send/recv to self at 16384^2 one-step: 0.831 vs 0.832 ms of
     // host time per step (two groups) with polled group ends, i.e. the cost
     // is RCCL's own enqueue, not the polling (profiles/rccl_self_16k_k1_r2*.json)
-    const char* db = std::getenv("RMA_RCCL_DATA_BLOCKING");
-    if (db && db[0] == '1') split_blocking(rank);
+    if (diag_flag("rccl_data_blocking")) split_blocking(rank);  // RMA_DIAG rccl_data_blocking
   } else {
     RMA_NCCL_CHECK(rccl().CommInitRank(&c, nranks, id, rank));
     comm_ = c;
@@ -271,10 +271,7 @@ int RcclComm::count() const {
   return n;
 }
 
-bool RcclComm::capturable() const {
-  const char* v = std::getenv("RMA_RCCL_GRAPH");
-  return v && v[0] == '1';
-}
+bool RcclComm::capturable() const { return diag_flag("rccl_graph"); }  // RMA_DIAG rccl_graph
 
 void RcclComm::group_start() {
   RMA_NCCL_CHECK(rccl().GroupStart());

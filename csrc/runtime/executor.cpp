@@ -11,6 +11,7 @@
 #include <string>
 #include <utility>
 
+#include "rma/config.h"
 #include "rma/hip_check.h"
 #include "rma/trace.h"
 
@@ -24,7 +25,7 @@ hipEvent_t E(void* p) { return reinterpret_cast<hipEvent_t>(p); }
 // free pair (or creates one, low priority first) and returns it when it is
 // destroyed, so rebuilding executors (set_temporal, loopback ranks, tests)
 // reuses the same HIP streams instead of creating new ones
-// (RMA_EXEC_STREAMS=pool; profiles/stream_order_r2.json).
+// (RMA_DIAG exec_streams=pool, the default; profiles/stream_order_r2.json).
 std::mutex g_pool_mu;
 std::vector<std::pair<hipStream_t, hipStream_t>> g_pool;
 }  // namespace
@@ -65,10 +66,11 @@ StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c) {
   // (profiles/SUMMARY_r3.md), so K = 10..13 only on the large tile classes
   if ((K >= 14 || (K >= 10 && ny >= 65536)) && pipe_has(K, pipe_default_stages(K), 3))
     t.kernel = 12;
-  // RMA_PIPE_FAST=pipe | pipe5 forces the ring kernel at every depth (A/B runs;
-  // pipe5 = 5 cells per lane, lab library, K = 16..20 and nx % 5 == 0)
-  static const char* e = std::getenv("RMA_PIPE_FAST");
-  const std::string force = e ? e : "";
+  // RMA_DIAG pipe_fast=pipe | pipe5 forces the ring kernel at every depth (A/B
+  // runs; pipe5 = 5 cells per lane, lab library, K = 16..20 and nx % 5 == 0)
+  static const std::string force = diag_value("pipe_fast");
+  RMA_CHECK_ARG(force.empty() || force == "pipe" || force == "pipe5",
+                "RMA_DIAG pipe_fast=" << force << " (pipe | pipe5)");
   if (force == "pipe" || force == "pipe5") t.kernel = 9;
   if (force == "pipe5") t.vec = 5;
   return t;
@@ -132,11 +134,20 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   }
   if (p.temporal > 1 || fast5()) {
     cost_ = default_pass_costs(p.temporal, fast5(), (double)nx * (double)ny);
-    apply_cost_overrides(cost_, std::getenv("RMA_PASS_COSTS"));
+    {  // RMA_DIAG pass_costs=K:cost/K:cost/...
+      std::string pc = diag_value("pass_costs");
+      for (char& ch : pc)
+        if (ch == '/') ch = ',';
+      apply_cost_overrides(cost_, pc.empty() ? nullptr : pc.c_str());
+    }
     geom_.resize(p.temporal + 1);
     geom_ok_.assign(p.temporal + 1, 0);
     (void)geometry(p.temporal);  // throws now if the tile is too small
   }
+  // the destructor does not run for a constructor that throws: from here on
+  // what was acquired (streams, events, signal words) is released before the
+  // exception leaves
+  try {
   int least = 0, greatest = 0;
   RMA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   hipStream_t hi, lo;
@@ -151,9 +162,10 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
   // executor 25 % slower"); low-priority first puts only its tiny frame
   // kernels there. The pool additionally reuses the streams of destroyed
   // executors (rebuilds, set_temporal), so no new queues accumulate.
-  // RMA_EXEC_STREAMS=lofirst|hifirst|plain create per executor (diagnostics).
-  const char* sm = std::getenv("RMA_EXEC_STREAMS");
-  const std::string mode = sm ? sm : "pool";
+  // RMA_DIAG exec_streams=lofirst|hifirst|plain create per executor (diagnostics).
+  const std::string mode = diag_value("exec_streams", "pool");
+  RMA_CHECK_ARG(mode == "pool" || mode == "lofirst" || mode == "hifirst" || mode == "plain",
+                "RMA_DIAG exec_streams=" << mode << " (pool | lofirst | hifirst | plain)");
   if (mode == "pool") {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     if (!g_pool.empty()) {
@@ -175,82 +187,84 @@ DiffusionExecutor::DiffusionExecutor(double* T, double* T2, const double* iCp, i
     RMA_HIP_CHECK(hipStreamCreateWithPriority(&lo, hipStreamNonBlocking, least));
     RMA_HIP_CHECK(hipStreamCreateWithPriority(&hi, hipStreamNonBlocking, greatest));
   }
-  if (std::getenv("RMA_EXEC_VERBOSE"))
+  if (diag_flag("exec_verbose"))
     fprintf(stderr, "[executor] priority range least=%d greatest=%d mode=%s hi=%p lo=%p\n", least,
             greatest, mode.c_str(), (void*)hi, (void*)lo);
   s_hi_ = hi;
   s_lo_ = lo;
-  hipEvent_t a, b, c, d;
-  RMA_HIP_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
-  RMA_HIP_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
-  RMA_HIP_CHECK(hipEventCreateWithFlags(&c, hipEventDisableTiming));
-  RMA_HIP_CHECK(hipEventCreateWithFlags(&d, hipEventDisableTiming));
-  e_hi_ = a;
-  e_lo_ = b;
-  e_in_ = c;
-  e_fr_ = d;
+  for (void** e : {&e_hi_, &e_lo_, &e_in_, &e_fr_})  // straight into the members (release)
+    RMA_HIP_CHECK(hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(e), hipEventDisableTiming));
   // The interior of pass n+1 reads cells >= K away from the halo (its rect is
   // inset by the frame, >= ol - K = K cells) and writes the other buffer, so
   // it depends on pass n's frame and interior, not on pass n's exchange: with
   // the lag the exchange of pass n overlaps the interior of pass n+1 and only
   // pass n+1's frame (same stream as the exchange) waits for it.
-  // RMA_EXEC_LAG=0: every pass waits for the previous exchange.
-  const char* lg = std::getenv("RMA_EXEC_LAG");
-  lag_ = !(lg && lg[0] == '0');
+  // RMA_DIAG no_lag: every pass waits for the previous exchange.
+  lag_ = !diag_flag("no_lag");
   // Frame-first fused passes (see enqueue_pass). RMA_EXEC_FUSED=1 always (where
-  // the frame is aligned), 0 never, unset: by task waves (fused_pass_ok).
-  const char* fu = std::getenv("RMA_EXEC_FUSED");
-  fused_ = fu && fu[0] ? std::atoi(fu) : 2;  // 2: auto (fused_pass_ok)
+  // the frame is aligned), 0 never, auto (default): by task waves (fused_pass_ok).
+  const std::string fu = env_choice("RMA_EXEC_FUSED", "auto|0|1", "auto");
+  fused_ = fu == "auto" ? 2 : fu == "1" ? 1 : 0;
+  // bounded wait of the exchange stream for the frame tasks' flag (seconds)
+  fused_timeout_s_ = env_double("RMA_EXEC_FUSED_TIMEOUT", 60.0, 1e-9, 1e6);
   {
     int dev = 0, cus = 0;
     RMA_HIP_CHECK(hipGetDevice(&dev));
     RMA_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     cus_ = cus > 0 ? cus : 256;
   }
-  if (const char* ft = std::getenv("RMA_EXEC_FUSED_TIMEOUT")) fused_timeout_s_ = std::atof(ft);
-  if (const char* fs = std::getenv("RMA_EXEC_FUSED_STEP")) fused_step_ = fs[0] == '1';
-  if (const char* fd = std::getenv("RMA_FUSED_FRAME_DIV"))
-    fused_fdiv_ = fd[0] ? std::max(1, std::atoi(fd)) : 1;
-  if (fused_ && p_.mode == Mode::kHide) {
-    RMA_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&sig_), 2 * sizeof(uint64_t)));
-    // zeroed ON the executor's stream and waited for: a null-stream hipMemset
-    // is not ordered before work on these non-blocking streams, and a counter
-    // zeroed after (or never before) the first signalling launch never reaches
-    // its target, so the frame wait times out (seen with 4 processes sharing
-    // a GPU: the bench's shared-GPU rehearsal, profiles/SUMMARY_r5.md §6)
-    RMA_HIP_CHECK(hipMemsetAsync(sig_, 0, 2 * sizeof(uint64_t), S(s_lo_)));
-    RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
-    RMA_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ferr_host_), sizeof(uint32_t),
-                                hipHostMallocMapped));
-    *ferr_host_ = 0;
-    RMA_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ferr_dev_), ferr_host_, 0));
+    if (fused_ && p_.mode == Mode::kHide) {
+      RMA_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&sig_), 2 * sizeof(uint64_t)));
+      // zeroed ON the executor's stream and waited for: a null-stream hipMemset
+      // is not ordered before work on these non-blocking streams, and a counter
+      // zeroed after (or never before) the first signalling launch never reaches
+      // its target, so the frame wait times out (seen with 4 processes sharing
+      // a GPU: the bench's shared-GPU rehearsal, profiles/SUMMARY_r5.md §6)
+      RMA_HIP_CHECK(hipMemsetAsync(sig_, 0, 2 * sizeof(uint64_t), S(s_lo_)));
+      RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
+      RMA_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ferr_host_), sizeof(uint32_t),
+                                  hipHostMallocMapped));
+      *ferr_host_ = 0;
+      RMA_HIP_CHECK(
+          hipHostGetDevicePointer(reinterpret_cast<void**>(&ferr_dev_), ferr_host_, 0));
+    }
+    if (!diag_flag("no_prime")) prime();
+  } catch (...) {
+    release_resources();
+    throw;
   }
-  const char* pr = std::getenv("RMA_EXEC_PRIME");
-  if (!(pr && pr[0] == '0')) prime();
 }
 
-DiffusionExecutor::~DiffusionExecutor() {
+DiffusionExecutor::~DiffusionExecutor() { release_resources(); }
+
+void DiffusionExecutor::release_resources() {
   release_timing();
   if (graph_exec_) (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec_));
-  if (e_hi_) (void)hipEventDestroy(E(e_hi_));
-  if (e_lo_) (void)hipEventDestroy(E(e_lo_));
-  if (e_in_) (void)hipEventDestroy(E(e_in_));
-  if (e_fr_) (void)hipEventDestroy(E(e_fr_));
+  graph_exec_ = nullptr;
+  for (void** e : {&e_hi_, &e_lo_, &e_in_, &e_fr_}) {
+    if (*e) (void)hipEventDestroy(E(*e));
+    *e = nullptr;
+  }
   if (sig_ || ferr_host_) {  // the streams' flag kernels may still use them
-    (void)hipStreamSynchronize(S(s_hi_));
-    (void)hipStreamSynchronize(S(s_lo_));
+    if (s_hi_) (void)hipStreamSynchronize(S(s_hi_));
+    if (s_lo_) (void)hipStreamSynchronize(S(s_lo_));
     if (sig_) (void)hipFree(sig_);
     if (ferr_host_) (void)hipHostFree(ferr_host_);
+    sig_ = nullptr;
+    ferr_host_ = nullptr;
+    ferr_dev_ = nullptr;
   }
+  if (!s_hi_ && !s_lo_) return;
   if (pooled_) {  // back to the pool, drained
     (void)hipStreamSynchronize(S(s_hi_));
     (void)hipStreamSynchronize(S(s_lo_));
     std::lock_guard<std::mutex> lk(g_pool_mu);
     g_pool.emplace_back(S(s_lo_), S(s_hi_));
-    return;
+  } else {
+    if (s_hi_) (void)hipStreamDestroy(S(s_hi_));
+    if (s_lo_) (void)hipStreamDestroy(S(s_lo_));
   }
-  if (s_hi_) (void)hipStreamDestroy(S(s_hi_));
-  if (s_lo_) (void)hipStreamDestroy(S(s_lo_));
+  s_hi_ = s_lo_ = nullptr;
 }
 
 bool DiffusionExecutor::fast5() const {
@@ -320,10 +334,9 @@ void DiffusionExecutor::exchange(double* A, stream_t s) {
   // geometry of a rank with neighbours but skip its exchange (wrong results;
   // bench.py records it and refuses it with the halo check on)
   static const bool skip = [] {
-    const char* e = std::getenv("RMA_DIAG_SKIP_EXCHANGE");
-    const bool on = e && e[0] == '1';
+    const bool on = diag_flag("skip_exchange");
     if (on)
-      fprintf(stderr, "[rocm_mpi_amd] WARNING: RMA_DIAG_SKIP_EXCHANGE=1: every halo exchange is "
+      fprintf(stderr, "[rocm_mpi_amd] WARNING: RMA_DIAG skip_exchange: every halo exchange is "
                       "skipped, multi-rank results are WRONG (diagnosis only)\n");
     return on;
   }();
@@ -336,22 +349,16 @@ void DiffusionExecutor::exchange(double* A, stream_t s) {
   f.hw = {hwx_, hwy_, 1};
   // one-step passes only (temporal = 1): the 5-point update never reads a
   // corner halo cell, so all dimensions go in ONE RCCL group (one enqueue and
-  // one RCCL kernel per exchange instead of two; RMA_HALO_CROSS=0: per dimension).
+  // one RCCL kernel per exchange instead of two; RMA_DIAG no_halo_cross: per dimension).
   // K-step passes read the corners (diagonal dependencies) and keep the
   // dimension-ordered exchange.
-  static const bool cross_ok = [] {
-    const char* e = std::getenv("RMA_HALO_CROSS");
-    return !(e && e[0] == '0');
-  }();
+  static const bool cross_ok = !diag_flag("no_halo_cross");
   // The last pass of a run() exchanges with exact corners, so the arrays a
   // run leaves behind have consistent corner halos (IGG update_halo! semantics).
   // With x AND y neighbours the exact exchange is ONE group with the corner
   // blocks sent to the diagonal neighbours (halo_plan.h plan_exchange_merged)
-  // instead of one group per dimension (RMA_HALO_MERGED=0: per dimension).
-  static const bool merged_ok = [] {
-    const char* e = std::getenv("RMA_HALO_MERGED");
-    return !(e && e[0] == '0');
-  }();
+  // instead of one group per dimension (RMA_DIAG no_halo_merged: per dimension).
+  static const bool merged_ok = !diag_flag("no_halo_merged");
   const bool xy = (nbr_[0][0] >= 0 || nbr_[0][1] >= 0) && (nbr_[1][0] >= 0 || nbr_[1][1] >= 0);
   if (cross_ok && cross_pass_ && p_.temporal == 1 && p_.mode != Mode::kKp)
     halo_->exchange_cross({f}, s, 3);
@@ -395,17 +402,6 @@ void DiffusionExecutor::enqueue_step(double* Tin, double* Tout) {
     // the high stream stays idle (no per-step round trip between the queues);
     // a later overlapped step makes it wait for e_lo first
     if (p_.mode == Mode::kHide) RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
-    return;
-  }
-  if (fused_step_ok()) {
-    // frame-first fused one-step pass (enqueue_fused): one march launch over
-    // the frame rects (first, never XCD-remapped) and the interior, whose
-    // frame waves raise sig_[1] for the exchange stream
-    TraceRange tr("rma.step.fused");
-    enqueue_fused(frame_, interior_, p_.tune, Tout, ev,
-                  [&](const Rect* rs, int n, const StencilTuning& t) {
-                    stencil_rects_gpu(Tout, Tin, iCp_, nx_, ny_, rs, n, c, t, s_lo_);
-                  });
     return;
   }
   TraceRange tr("rma.step.hide");
@@ -469,15 +465,6 @@ bool DiffusionExecutor::fused_pass_ok(const PassGeom& g, const StencilTuning& tn
   // (440) 1.2 vs 8.7 %; 5120^2 (675) 12.2 vs 2.7 %, 6144^2 (720) 11.3 vs 2.0 %,
   // 7168^2 (980) 11.1 vs 0.4 %, 8192^2 5.6 vs 1.3 %
   return fused_ == 1 || g.tasks() > 2 * (int64_t)cus_;
-}
-
-bool DiffusionExecutor::fused_step_ok() const {
-  // one-step passes: only on request (RMA_EXEC_FUSED_STEP=1; A/B, see
-  // profiles/SUMMARY_r5.md section 6), the march kernel, a frame and an interior
-  if (!sig_ || !fused_step_ || p_.tune.kernel == 1 || interior_.empty()) return false;
-  int nf = 0;
-  for (const Rect& r : frame_) nf += r.empty() ? 0 : 1;
-  return nf > 0 && (int)frame_.size() + 1 <= kMaxRects;
 }
 
 template <typename Launch>
@@ -581,10 +568,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     // grid. The next pass waits for this exchange (its frame tasks read the
     // halo) and, in stream order, for this launch.
     TraceRange tr("rma.pass.fused");
-    StencilTuning ft = tn;
-    // shorter frame tasks finish earlier in the launch (fused_fdiv_)
-    if (fused_fdiv_ > 1) ft.signal_chunk_rows = std::max(1, tn.chunk_rows / fused_fdiv_);
-    enqueue_fused(g.frame, g.interior, ft, Tout, ev,
+    enqueue_fused(g.frame, g.interior, tn, Tout, ev,
                   [&](const Rect* rs, int n, const StencilTuning& t) {
                     multi_step(K, Tin, Tout, iCp_, nx_, ny_, rs, n, t, s_lo_);
                   });
@@ -705,6 +689,10 @@ void DiffusionExecutor::set_solo(bool on) {
 
 void DiffusionExecutor::prime() {
   if (p_.mode == Mode::kKp || (p_.temporal == 1 && !fast5())) return;
+  // drain both streams first: the priming signal below raises and lowers the
+  // same flag words a fused pass's exchange stream may still be waiting on
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_hi_)));
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
   // a tiny field with the same cells-per-lane class as the real one (nx mod 4)
   const int64_t tnx = 256 + nx_ % 4, tny = 64;
   const size_t bytes = (size_t)(tnx * tny) * sizeof(double);

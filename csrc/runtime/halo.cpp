@@ -1,3 +1,4 @@
+#include "rma/config.h"
 #include "rma/halo.h"
 
 #include <hip/hip_runtime.h>
@@ -106,10 +107,9 @@ void HaloExchanger::prepare(const std::vector<HaloField>& fields, int dims_mask)
 }
 
 namespace {
-// RMA_HALO_BATCH=0: one launch per plane copy (A/B and diagnosis)
+// RMA_DIAG no_halo_batch: one launch per plane copy (A/B and diagnosis)
 void launch_batches(const std::vector<CopyBatch>& bs, stream_t stream) {
-  static const char* e = std::getenv("RMA_HALO_BATCH");
-  const bool single = e && e[0] == '0';
+  static const bool single = diag_flag("no_halo_batch");
   for (const CopyBatch& b : bs) {
     if (single) {
       for (const Copy2d& c : b.copies) copy2d_batch_gpu(&c, 1, b.elem_bytes, stream);

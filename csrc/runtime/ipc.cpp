@@ -1,4 +1,5 @@
 // HIP IPC transport between processes of one node (rma/ipc.h).
+#include "rma/config.h"
 #include "rma/ipc.h"
 
 #include <fcntl.h>
@@ -189,10 +190,7 @@ void IpcTransport::abort_waits() {
 
 bool IpcTransport::capturable() const {
   if (mode_ != Mode::kStream) return false;
-  static const bool allow = [] {
-    const char* e = std::getenv("RMA_IPC_GRAPH");
-    return !(e && e[0] == '0');
-  }();
+  static const bool allow = !diag_flag("no_ipc_graph");  // RMA_DIAG no_ipc_graph
   return allow;
 }
 

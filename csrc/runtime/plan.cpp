@@ -1,3 +1,4 @@
+#include "rma/config.h"
 #include "rma/plan.h"
 
 #include <algorithm>
@@ -36,11 +37,11 @@ void split_rect(const Rect& out, int64_t bwx, int64_t bwy, std::vector<Rect>& fr
 std::array<std::array<bool, 2>, 2> frame_sides(const Neighbors& nbr) {
   // Only a side that sends needs its cells before the exchange: a side
   // without a neighbour (open boundary) is computed by the interior launch.
-  // RMA_FRAME_SIDES=all: every side once any neighbour exists (the r1-r2
+  // RMA_DIAG frame_sides=all: every side once any neighbour exists (the r1-r2
   // layout, kept for A/B runs).
-  static const char* fs = std::getenv("RMA_FRAME_SIDES");
+  static const bool fs_all = diag_value("frame_sides") == "all";
   const bool any = nbr[0][0] >= 0 || nbr[0][1] >= 0 || nbr[1][0] >= 0 || nbr[1][1] >= 0;
-  const bool all = any && fs && std::string(fs) == "all";
+  const bool all = any && fs_all;
   std::array<std::array<bool, 2>, 2> on{};
   for (int d = 0; d < 2; ++d)
     for (int s = 0; s < 2; ++s) on[d][s] = all || nbr[d][s] >= 0;
@@ -74,8 +75,8 @@ FrameLayout frame_layout(int64_t ny, const Neighbors& nbr) {
     else
       f.bands = 0;
   }
-  static const char* cd = std::getenv("RMA_FRAME_CHUNK_DIV");
-  if (cd && cd[0]) f.chunk_div = std::max(1, std::atoi(cd));
+  static const std::string cd = diag_value("frame_chunk_div");  // RMA_DIAG frame_chunk_div=N
+  if (!cd.empty()) f.chunk_div = std::max(1, std::atoi(cd.c_str()));
   return f;
 }
 
@@ -100,12 +101,12 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
   // tasks) vs 1.7 % (128-column strips); y 0.4-0.7 % (ol-wide bands) vs
   // 1.6 % (task-row bands); smaller tiles (profiles/frame_aligned_r2.json):
   // 16384^2 5.7 -> 0.1 %, 32768^2 2.3-3.1 -> ~0 %, 65536^2 1.9-2.2 -> 0.1-0.4 %.
-  // RMA_FRAME_ALIGNED=0 / 1 forces the layout (0: ol-wide strips everywhere);
-  // RMA_FRAME_BANDS=task / ol forces the band height.
-  static const char* fa = std::getenv("RMA_FRAME_ALIGNED");
-  static const char* fb = std::getenv("RMA_FRAME_BANDS");
-  const bool want = fa && fa[0] ? fa[0] != '0' : true;
-  const bool task_bands = fb && fb[0] ? fb[0] == 't' : bands >= 0 ? bands == 1 : task_h <= 1024;
+  // RMA_DIAG frame_aligned=0 / 1 forces the layout (0: ol-wide strips
+  // everywhere); frame_bands=task / ol forces the band height.
+  static const std::string fa = diag_value("frame_aligned");
+  static const std::string fb = diag_value("frame_bands");
+  const bool want = fa.empty() ? true : fa[0] != '0';
+  const bool task_bands = !fb.empty() ? fb[0] == 't' : bands >= 0 ? bands == 1 : task_h <= 1024;
   const int64_t band = task_bands ? task_h : need_y;  // y-band height
   if (want && hide && any_nbr && task_w >= need_x && task_h >= 1 && band >= need_y &&
       o.x1 - o.x0 >= 3 * task_w && o.y1 - o.y0 >= (task_bands ? 3 * task_h : 2 * band + 1)) {
@@ -141,9 +142,9 @@ PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool
     // the tall x-frames of a pipelined pass (K >= 5) run in 128-column strips
     // (2 cells per lane) that output 128 - 2K columns whatever the frame
     // width: widen the frame to that capacity, so those columns leave the
-    // interior instead of being computed twice (RMA_FRAME_FILL=0: off)
-    static const char* ff = std::getenv("RMA_FRAME_FILL");
-    if (K >= 5 && !(ff && ff[0] == '0'))
+    // interior instead of being computed twice (RMA_DIAG no_frame_fill: off)
+    static const bool fill = !diag_flag("no_frame_fill");
+    if (K >= 5 && fill)
       fx = std::max<int64_t>(fx, std::min<int64_t>(128 - 2 * K, (g.out.x1 - g.out.x0) / 4));
     const int64_t fy = std::max(bwy, oly - g.out.y0);
     const auto side = frame_sides(nbr);
@@ -255,11 +256,11 @@ void apply_cost_overrides(std::vector<double>& cost, const char* spec) {
     if (end == std::string::npos) end = s.size();
     const std::string item = s.substr(pos, end - pos);
     const size_t colon = item.find(':');
-    RMA_CHECK_ARG(colon != std::string::npos, "RMA_PASS_COSTS item '" << item << "' is not K:cost");
+    RMA_CHECK_ARG(colon != std::string::npos, "pass_costs item '" << item << "' is not K:cost");
     const int K = std::atoi(item.substr(0, colon).c_str());
     const double v = std::atof(item.substr(colon + 1).c_str());
-    RMA_CHECK_ARG(K >= 1 && K < (int)cost.size(), "RMA_PASS_COSTS: K=" << K << " out of range");
-    RMA_CHECK_ARG(v > 0, "RMA_PASS_COSTS: cost must be > 0 (inf disables), got " << v);
+    RMA_CHECK_ARG(K >= 1 && K < (int)cost.size(), "pass_costs: K=" << K << " out of range");
+    RMA_CHECK_ARG(v > 0, "pass_costs: cost must be > 0 (inf disables), got " << v);
     cost[K] = v;
     pos = end + 1;
   }

@@ -7,7 +7,7 @@
 // same capture segfaults (bench/rccl_graph_probe.py); this separates the
 // framework's capture sequence from that runtime combination.
 //
-//   RMA_RCCL_GRAPH=1 RMA_RCCL_BLOCKING=1 ./build/examples/rccl_graph_capi [n] [steps] [K]
+//   RMA_DIAG=rccl_graph RMA_RCCL_BLOCKING=1 ./build/examples/rccl_graph_capi [n] [steps] [K]
 #include <hip/hip_runtime.h>
 
 #include <chrono>

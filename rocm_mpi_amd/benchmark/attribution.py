@@ -37,8 +37,10 @@ def summarize_timings(ts: list, exchange: bool = True) -> dict:
 def _n1_cache_path() -> str:
     import tempfile
 
-    return os.environ.get("RMA_BENCH_N1_CACHE",
-                          os.path.join(tempfile.gettempdir(), "rma_bench_n1_record.json"))
+    from rocm_mpi_amd.config import diag_value
+
+    return (diag_value("bench_n1_cache")
+            or os.path.join(tempfile.gettempdir(), "rma_bench_n1_record.json"))
 
 
 def _build_id() -> str:

@@ -10,6 +10,7 @@ import hashlib
 import os
 import time
 
+from ..config import diag_flag, diag_value
 from .common import CheckFailed, agree, bounded_gather_tiles, bounded_status
 
 # fast-math drift bound (max |fast - canonical| after the run's steps on a
@@ -97,7 +98,7 @@ def halo_check(n: int, dims, K: int, dev: str, world: int, rank: int, timeout_s:
     field = coords = None
     info = {"local_tile": [n, n], "steps": [n_fast, n_can], "self_rccl": self_rccl}
     try:
-        fault = os.environ.get("RMA_BENCH_CHECK_RAISE", "") if inject and rank == world - 1 else ""
+        fault = diag_value("bench_check_raise") if inject and rank == world - 1 else ""
         if fault == "before":  # peers then block in the exchange: the watchdog path
             raise RuntimeError("injected halo-check failure before the run")
         field, coords, nxyz_g, transport, plan = _run_grid(n, n, dims, K, n_fast, n_can,
@@ -105,7 +106,7 @@ def halo_check(n: int, dims, K: int, dev: str, world: int, rank: int, timeout_s:
         if fault == "after":
             raise RuntimeError("injected halo-check failure after the run")
         info.update(global_grid=list(nxyz_g[:2]), transport=transport, fast_math_plan=plan)
-        if inject and os.environ.get("RMA_BENCH_CHECK_CORRUPT") == "1" and rank == world - 1:
+        if inject and diag_flag("bench_check_corrupt") and rank == world - 1:
             field[n // 2, n // 2] += 1e-12  # negative test (tests/test_multiprocess_cpu.py)
     except Exception as e:  # noqa: BLE001 - reported to every rank below
         err = f"{type(e).__name__}: {e}"
@@ -184,7 +185,7 @@ def snapshot_windows(model, h: int = WINDOW_ROWS) -> dict:
     rows = sorted({0, max(0, ny // 2 - h // 2), ny - h})
     geo = model.geometry()
     tiles = [model.field[r:r + h].detach().cpu().clone() for r in rows]
-    if os.environ.get("RMA_BENCH_WINDOW_CORRUPT") == "1" and g.me == g.nprocs - 1:
+    if diag_flag("bench_window_corrupt") and g.me == g.nprocs - 1:
         tiles[-1][h // 2, nx // 2] += 1e-12  # negative test (tests/test_multiprocess_cpu.py)
     return {"rows": rows, "h": h, "tiles": tiles,
             "nx": nx, "ny": ny, "geom": geo, "coef": model.coef, "seed": cfg.seed,
@@ -286,11 +287,11 @@ def full_field_check(field, init: tuple, steps: int, comm, world: int, rank: int
     1 - 2(gx + gy) >= 0.02 and gx, gy, so no value leaves the initial range;
     Dirichlet boundary cells keep their initial values and halo copies move
     values). The fp64 rounding of an update is below 8 ulps of the range's
-    magnitude per step, hence the tolerance. RMA_BENCH_FIELD_CORRUPT = nan |
+    magnitude per step, hence the tolerance. RMA_DIAG bench_field_corrupt=nan |
     hot | cold injects one bad cell on the last rank first (negative test).
     Raises CheckFailed on every rank on a violation."""
     t0 = time.perf_counter()
-    corrupt = os.environ.get("RMA_BENCH_FIELD_CORRUPT", "")
+    corrupt = diag_value("bench_field_corrupt")
     if corrupt and rank == world - 1:
         ny, nx = field.shape
         v = {"nan": float("nan"), "hot": init[2] + 0.5 * (abs(init[2]) + 1.0),

@@ -163,8 +163,10 @@ def hard_exit(rank: int, rc: int) -> None:
 
 
 def record_rc(rank: int, rc: int) -> None:
-    """RMA_BENCH_RC_DIR: every rank writes its exit status (tests)."""
-    d = os.environ.get("RMA_BENCH_RC_DIR")
+    """RMA_DIAG bench_rc_dir=<dir>: every rank writes its exit status (tests)."""
+    from rocm_mpi_amd.config import diag_value
+
+    d = diag_value("bench_rc_dir")
     if d:  # atomically: torchrun may end this rank right after (a half-written file)
         # one temp file per thread: the check-phase watchdog thread and the main
         # thread can both be exiting the rank at once; with one shared temp

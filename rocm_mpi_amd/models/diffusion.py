@@ -198,7 +198,7 @@ class Diffusion2D:
                 import warnings
 
                 warnings.warn(f"hipGraph replay disabled: the {g.transport} halo transport cannot "
-                              "be stream-captured (set RMA_RCCL_GRAPH=1 to force for RCCL)",
+                              "be stream-captured (RMA_DIAG=rccl_graph forces it for RCCL)",
                               RuntimeWarning, stacklevel=2)
                 use_graph = False
             self.use_graph = use_graph
@@ -264,10 +264,14 @@ class Diffusion2D:
         cfg, g = self.cfg, self.g
         nx, ny = cfg.nx, cfg.ny
         bwx, bwy = cfg.b_width
+        if cfg.kernel != "march" and self.T.is_cuda:  # the LDS-tiled one-step kernel: librma_lab.so
+            from .._native import load_lab
+
+            load_lab()
         return native().Executor(
             self.T.data_ptr(), self.T2.data_ptr() if self.T2 is not None else 0,
             self.iCp.data_ptr(), nx, ny, _MODE[cfg.variant], tuple(self.coef),
-            cfg.chunk_rows, int(cfg.nontemporal), ops.KERNELS[cfg.kernel], int(bwx), int(bwy),
+            cfg.chunk_rows, int(cfg.nontemporal), ops.kernel_id(cfg.kernel), int(bwx), int(bwy),
             int(self.use_graph), int(cfg.graph_steps), g.halo,
             self.QX.data_ptr() if cfg.variant == "kp" else 0,
             self.QY.data_ptr() if cfg.variant == "kp" else 0,

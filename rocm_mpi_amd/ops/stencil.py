@@ -26,7 +26,8 @@ Rect = tuple  # (x0, x1, y0, y1), half-open, 0-based cell indices
 
 # Kernel ids (StencilTuning.kernel names). The core library (librma_core.so)
 # holds what the executor and the ops run by default:
-#   one-step:  "march" (0, the fused one-step kernel), "lds" (1, LDS-tiled baseline);
+#   one-step:  "march" (0, the fused one-step kernel; "lds", 1, the LDS-tiled
+#              baseline, is in the lab library: 3.90 vs 6.20 TB/s, SUMMARY_r1);
 #   K-step:    "lds_dpp" (3: canonical, K = 2, 3, 4, 6, 8; LDS 1/Cp ring + DPP),
 #              "pipe" (9: the stage-pipelined fast-math kernel, ANY K in 1..24,
 #              csrc/kernels/stencil_pipe.h), "pipec" (10: the same pipeline with the
@@ -67,8 +68,8 @@ PIPE = ("pipe", "pipec", "pipeb", "piper", "pipe_diag1", "piper6", "piper7", "pi
          "piper_rot", "piper_diag_hb", "piper_u6s",
          "piper_sp", "piper_sp2", "piper_prio", "piper_prio_nr")
 PIPE_MAX_K = 24
-KERNELS = {"march": 0, "lds": 1, "lds_dpp": 3, "pipe": 9, "pipec": 10, "piper": 12}
-LAB_KERNELS = {"dpp": 2, "fast": 4, "fast5": 5, "fast5p2": 6, "fast5p4": 7, "fast5p8": 8,
+KERNELS = {"march": 0, "lds_dpp": 3, "pipe": 9, "pipec": 10, "piper": 12}
+LAB_KERNELS = {"lds": 1, "dpp": 2, "fast": 4, "fast5": 5, "fast5p2": 6, "fast5p4": 7, "fast5p8": 8,
                "pipeb": 11, "pipe_diag1": 13, "piper6": 14, "piper7": 15,
                "piper_u3": 16, "piper_iso": 17, "piper_diag_s0": 18, "piper_w1": 19,
                "piper_mask": 20, "piper_mask_ctl": 21, "piper_nosb": 22, "piper_rot": 23,
@@ -226,6 +227,10 @@ def stencil_step(T2: torch.Tensor, T: torch.Tensor, iCp: torch.Tensor, coef: Ste
         return
     tn = tuning or StencilTuning()
     if T.is_cuda:
+        if tn.kernel != "march":  # the LDS-tiled one-step kernel lives in librma_lab.so
+            from .._native import load_lab
+
+            load_lab()
         native().stencil_rects(_ptr(T2), _ptr(T), _ptr(iCp), nx, ny, rects, tuple(coef),
                                tn.chunk_rows, int(tn.nontemporal), kernel_id(tn.kernel),
                                stream_handle(T), True, tn.unroll, tn.vec, tn.xcd_remap)

@@ -460,8 +460,7 @@ class IpcComm(TorchDistComm):
             # unsatisfiable: release them from the host before draining
             # long: a live peer may be late (rank 0 gathering, checkpointing),
             # and releasing the waits under it corrupts its receives
-            tmo = float(os.environ.get("RMA_IPC_TEARDOWN_TIMEOUT",
-                                       os.environ.get("RMA_TEARDOWN_TIMEOUT", "300")))
+            tmo = max(float(os.environ.get("RMA_TEARDOWN_TIMEOUT", "30")), DEFAULT_TIMEOUT_S)
             aborted = None
             try:
                 work = dist.barrier(group=self._pg, async_op=True)
@@ -647,7 +646,9 @@ def node_local_rank(comm_rank: int, comm_size: int) -> tuple[int, int]:
         return local, int(lsize)
     if comm_size == 1 or not dist.is_initialized():
         return (local or 0), 1
-    host = os.environ.get("RMA_HOSTNAME", socket.gethostname())
+    from ..config import diag_value
+
+    host = diag_value("hostname") or socket.gethostname()
     names: list = [None] * comm_size
     dist.all_gather_object(names, host, group=_gloo_group())
     same = [r for r, h in enumerate(names) if h == host]

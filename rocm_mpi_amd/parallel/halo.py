@@ -19,6 +19,7 @@ import os
 
 import torch
 
+from ..config import diag_flag
 from . import comm as C
 from .implicit_grid import GlobalGrid, global_grid
 
@@ -91,11 +92,11 @@ def update_halo_(*arrays: torch.Tensor, dims=(0, 1, 2)) -> None:
         stream = torch.cuda.current_stream(dev).cuda_stream
         # x AND y neighbours, 2D fields: one group with the corner blocks sent to
         # the diagonal ranks (bitwise the same halos as the per-dimension groups;
-        # csrc/runtime/halo_plan.cpp plan_exchange_merged, RMA_HALO_MERGED=0: off)
+        # csrc/runtime/halo_plan.cpp plan_exchange_merged, RMA_DIAG no_halo_merged: off)
         nb = g.neighbors
         if (mask & 3) == 3 and all(f[1][2] == 1 for f in fields) and g.halo.has_diagonals \
                 and max(nb[0]) >= 0 and max(nb[1]) >= 0 \
-                and os.environ.get("RMA_HALO_MERGED", "1") != "0":
+                and not diag_flag("no_halo_merged"):
             g.halo.exchange_merged(fields, stream)
         else:
             g.halo.exchange(fields, stream, mask)

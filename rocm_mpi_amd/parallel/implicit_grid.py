@@ -25,6 +25,7 @@ from typing import Sequence
 
 import torch
 
+from ..config import diag_flag
 from . import comm as C
 from . import geometry as geo
 from .topology import CartTopology, dims_create
@@ -207,16 +208,16 @@ def init_global_grid(nx: int, ny: int, nz: int = 1, *, dimx: int = 0, dimy: int 
         except RuntimeError as e:
             # RCCL is the perf path: a failed init is fatal unless the caller
             # opted into the host-staged validation transport
-            # (RMA_RCCL_FALLBACK=1; bench.py never does: a scaling point must
+            # (RMA_DIAG=rccl_fallback; bench.py never does: a scaling point must
             # not silently run staged)
-            if (os.environ.get("RMA_RCCL_FALLBACK", "0") != "1"
+            if (not diag_flag("rccl_fallback")
                     or os.environ.get("RMA_RCCL_STRICT", "0") == "1"
                     or not torch.distributed.is_initialized()):
                 raise
             import warnings
 
             warnings.warn(f"RCCL communicator init failed ({e}); falling back to the host-staged "
-                          "transport (RMA_RCCL_FALLBACK=1)", RuntimeWarning, stacklevel=2)
+                          "transport (RMA_DIAG=rccl_fallback)", RuntimeWarning, stacklevel=2)
             tname = "staged"
             comm = C.TorchDistComm(staged=True)
     elif tname == "ipc":

@@ -1,6 +1,6 @@
 """Diagnosis: repeat the one-step perf_hide loopback cases that mismatched
 intermittently (2x1 vs golden, 2x2 periodic perf_hide vs perf) in ONE process
-and count mismatches; run under RMA_FRAME_SIDES / RMA_HALO_BATCH variants."""
+and count mismatches; run under RMA_DIAG frame_sides / no_halo_batch variants."""
 import json
 import os
 import sys
@@ -35,5 +35,5 @@ for i in range(reps):
     Tv, (nxg, nyg, _) = run_loopback(8, spmd, "perf_hide", 100, 68, 11, (4, 2), timeout=60)[0]
     bad["4x2_golden"] += int(not np.array_equal(Tv, golden.run(nxg, nyg, 11)[1:-1, 1:-1]))
 print(json.dumps({"reps": reps, "mismatches": bad,
-                  "env": {k: os.environ.get(k) for k in ("RMA_FRAME_SIDES", "RMA_HALO_BATCH")}}),
+                  "env": {"RMA_DIAG": os.environ.get("RMA_DIAG")}}),
       flush=True)

@@ -88,7 +88,9 @@ def node_local(rank, world, outdir, ranks_per_node):
     SURVEY.md §4.5); the global grid's device choice follows the local rank."""
     for k in ("LOCAL_RANK", "LOCAL_WORLD_SIZE"):
         os.environ.pop(k, None)
-    os.environ["RMA_HOSTNAME"] = f"node{rank // ranks_per_node}"
+    from rocm_mpi_amd.config import diag_with
+
+    os.environ["RMA_DIAG"] = diag_with(hostname=f"node{rank // ranks_per_node}")
     from rocm_mpi_amd.parallel import comm as C
     from rocm_mpi_amd.parallel import implicit_grid as gg
 

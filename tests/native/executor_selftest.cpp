@@ -21,6 +21,7 @@
 #include <cstring>
 #include <memory>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -57,11 +58,9 @@ std::atomic<long> g_signals{0};
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
                        const Rect* rects, int nrects, const StencilCoef& c, const StencilTuning& t,
                        stream_t) {
+  if (t.signal) throw std::runtime_error("a signalling one-step launch (fused one-step passes "
+                                         "were removed)");
   stencil_rects_cpu(T2, T, iCp, nx, ny, rects, nrects, c);
-  if (t.signal) {  // a fused one-step pass: the frame waves are done
-    reinterpret_cast<std::atomic<uint64_t>*>(t.signal + 1)->store(1, std::memory_order_release);
-    ++g_signals;
-  }
 }
 void stencil2_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
                         const Rect* rects, int nrects, const StencilCoef& c, const StencilTuning&,
@@ -144,7 +143,6 @@ struct Case {
   int nt;
   const char* fused;  // RMA_EXEC_FUSED for the multi-rank run ("" = auto)
   int chunk = 0;      // K-step rows per task (ExecParams::chunk_rows2; 0: the table)
-  bool fused_step = false;  // RMA_EXEC_FUSED_STEP=1 (one-step passes fused too)
 };
 
 struct TileResult {
@@ -215,16 +213,11 @@ int run_case(const Case& c) {
     setenv("RMA_EXEC_FUSED", c.fused, 1);
   else
     unsetenv("RMA_EXEC_FUSED");
-  if (c.fused_step)
-    setenv("RMA_EXEC_FUSED_STEP", "1", 1);
-  else
-    unsetenv("RMA_EXEC_FUSED_STEP");
   const auto multi = run_ranks(c, c.dims, c.nx, c.ny);
   // the same global grid on one rank: its tile is the global grid plus the
   // overlap cells (periodic: wrapped by the self exchange)
   const int64_t nx1 = c.dims[0] * (c.nx - ol) + ol, ny1 = c.dims[1] * (c.ny - ol) + ol;
   setenv("RMA_EXEC_FUSED", "0", 1);
-  unsetenv("RMA_EXEC_FUSED_STEP");
   const auto one = run_ranks(c, {1, 1, 1}, nx1, ny1);
   unsetenv("RMA_EXEC_FUSED");
   if (g_fail.load() != fails0) return 1;
@@ -243,7 +236,7 @@ int run_case(const Case& c) {
         }
       }
   }
-  const bool want_fused = std::string(c.fused) == "1" || c.fused_step;
+  const bool want_fused = std::string(c.fused) == "1";
   CHECK(!want_fused || fused > 0, "%s: no fused pass ran", c.name);
   CHECK(std::string(c.fused) != "0" || fused == 0, "%s: fused passes with RMA_EXEC_FUSED=0",
         c.name);
@@ -258,8 +251,7 @@ int main() {
   const Case cases[] = {
       {"perf_hide K=1 2x2 open", {2, 2, 1}, {0, 0, 0}, 40, 36, 1, Mode::kHide, 13, ""},
       {"perf K=1 3x1 periodic-x", {3, 1, 1}, {1, 0, 0}, 30, 28, 1, Mode::kPerf, 11, ""},
-      {"perf_hide K=1 2x2 periodic fused step", {2, 2, 1}, {1, 1, 0}, 40, 36, 1, Mode::kHide, 13,
-       "", 0, true},
+      {"perf_hide K=1 2x2 periodic", {2, 2, 1}, {1, 1, 0}, 40, 36, 1, Mode::kHide, 13, ""},
       {"perf_hide K=4 2x2 periodic", {2, 2, 1}, {1, 1, 0}, 48, 44, 4, Mode::kHide, 19, ""},
       {"perf_hide K=8 2x1 split", {2, 1, 1}, {0, 0, 0}, 800, 120, 8, Mode::kHide, 21, "0"},
       {"perf_hide K=8 2x1 fused", {2, 1, 1}, {0, 0, 0}, 800, 120, 8, Mode::kHide, 21, "1"},

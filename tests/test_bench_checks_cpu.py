@@ -55,7 +55,7 @@ def test_full_field_check_fails_on_injected_cell(monkeypatch, kind):
     f = torch.full((20, 30), 0.5, dtype=torch.float64)
     f[3, 4], f[9, 9] = 0.0, 1.0
     init = checks.field_stats_global(f, _Self())
-    monkeypatch.setenv("RMA_BENCH_FIELD_CORRUPT", kind)
+    monkeypatch.setenv("RMA_DIAG", f"bench_field_corrupt={kind}")
     with pytest.raises(CheckFailed) as ei:
         checks.full_field_check(f, init, 10, _Self(), 1, 0, 10.0)
     info = ei.value.args[1]
@@ -76,9 +76,9 @@ def test_full_field_check_tolerance_is_rounding_sized():
 @pytest.mark.parametrize("corrupt", ["", "nan"])
 def test_bench_cpu_records_full_field_check(tmp_path, corrupt):
     env = dict(os.environ, OMP_NUM_THREADS="2")
-    env.pop("RMA_BENCH_FIELD_CORRUPT", None)
+    env.pop("RMA_DIAG", None)
     if corrupt:
-        env["RMA_BENCH_FIELD_CORRUPT"] = corrupt
+        env["RMA_DIAG"] = f"bench_field_corrupt={corrupt}"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu",
                         "--nx", "130", "--steps", "12", "--warmup", "2",
                         "--single-step-steps", "2"], capture_output=True, text=True,

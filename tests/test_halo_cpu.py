@@ -226,7 +226,7 @@ def test_bench_record_rc_is_atomic_across_threads(tmp_path, monkeypatch):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
 
-    monkeypatch.setenv("RMA_BENCH_RC_DIR", str(tmp_path))
+    monkeypatch.setenv("RMA_DIAG", f"bench_rc_dir={tmp_path}")
     for it in range(50):
         ts = [threading.Thread(target=bench.record_rc, args=(1, 4 + (j % 3))) for j in range(4)]
         for t in ts:

@@ -3,7 +3,7 @@ ranks on cuda:0): the CPU suite's global-truth cases (tests/test_halo_cpu.py)
 -- 1-D/2-D/3-D, several fields per call, staggered sizes, halowidth 2,
 periodic dims. 2-D fields with x AND y neighbours take the merged group
 (corner blocks to the diagonal ranks); 3-D fields the per-dimension groups;
-RMA_HALO_MERGED=0 the per-dimension groups everywhere.
+RMA_DIAG=no_halo_merged the per-dimension groups everywhere.
 """
 import pytest
 import torch
@@ -62,7 +62,7 @@ PERIODIC = [((9, 7), (2, 2, 1), (1, 1, 0), (2, 2, 2), [(0, 0, 0)], 1),
 @pytest.mark.parametrize("case", CASES + PERIODIC,
                          ids=lambda c: f"n{c[0]}-d{c[1]}-p{c[2]}-ol{c[3][0]}-f{c[5]}")
 def test_update_halo_on_device_matches_global(case, merged, monkeypatch):
-    monkeypatch.setenv("RMA_HALO_MERGED", merged)
+    monkeypatch.setenv("RMA_DIAG", "no_halo_merged" if merged == "0" else "")
     nxyz, dims, periods, overlaps, staggers, nf = case
     nxyz3 = tuple(nxyz) + (1,) * (3 - len(nxyz))
     P = dims[0] * dims[1] * dims[2]

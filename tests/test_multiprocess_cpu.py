@@ -108,7 +108,7 @@ def test_bench_driver_contract_multirank(tmp_path, world, extra):
     if n1_ms:
         cache.write_text(json.dumps({"key": bench._n1_key(nx, nx, 20, 3, K, True, "perf_hide"),
                                      "ms_per_step": n1_ms, "pci_bus_id": "cpu"}))
-    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_N1_CACHE=str(cache))
+    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_DIAG=f"bench_n1_cache={cache}")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
                        env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -217,8 +217,8 @@ def test_bench_window_check_detects_a_wrong_cell(tmp_path):
            os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "12", "--warmup", "2",
            "--device", "cpu", "--nx", "64", "--temporal", "4", "--dims", "2,1",
            "--single-step-steps", "0", "--check", "0", "--drift-steps", "0"]
-    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_WINDOW_CORRUPT="1",
-               RMA_BENCH_N1_CACHE=str(tmp_path / "none.json"))
+    env = dict(os.environ, OMP_NUM_THREADS="1",
+               RMA_DIAG=f"bench_window_corrupt,bench_n1_cache={tmp_path / 'none.json'}")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
                        env=env)
     assert r.returncode != 0
@@ -247,7 +247,7 @@ def test_bench_halo_check_detects_a_wrong_tile(tmp_path):
            os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "2",
            "--device", "cpu", "--nx", "64", "--single-step-steps", "0", "--temporal", "4",
            "--solo-steps", "0"]
-    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_CHECK_CORRUPT="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_DIAG="bench_check_corrupt")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
                        env=env)
     assert r.returncode != 0
@@ -279,8 +279,8 @@ def test_bench_check_exception_fails_every_rank(tmp_path, where, tmo):
            os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "2",
            "--device", "cpu", "--nx", "64", "--single-step-steps", "0", "--temporal", "4",
            "--solo-steps", "0", "--drift-steps", "0", "--check-timeout", str(tmo)]
-    env = dict(os.environ, OMP_NUM_THREADS="1", RMA_BENCH_CHECK_RAISE=where,
-               RMA_BENCH_RC_DIR=str(rcdir))
+    env = dict(os.environ, OMP_NUM_THREADS="1",
+               RMA_DIAG=f"bench_check_raise={where},bench_rc_dir={rcdir}")
     t0 = time.time()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
                        env=env)

@@ -521,13 +521,12 @@ def spmd_fused(rank, hub, nx, ny, nt, dims, K, graph=False):
     return out
 
 
-@pytest.mark.parametrize("fdiv", ["1", "3"])
 @pytest.mark.parametrize("dims,K,nx,ny,nt,some", [((2, 2), 24, 1100, 3500, 53, True),
                                                   ((2, 1), 20, 1100, 1500, 47, True),
                                                   ((1, 2), 8, 800, 2600, 19, True),
                                                   ((2, 2), 16, 700, 900, 37, False),
                                                   ((2, 2), 12, 1000, 3000, 31, True)])
-def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, some, fdiv, monkeypatch):
+def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, some, monkeypatch):
     """RMA_EXEC_FUSED=1: every K-step pass with a neighbour is ONE pipelined
     launch, frame tasks first, whose last frame block raises the flag the
     exchange stream waits on (flags.hip); every tile == its window of the
@@ -535,7 +534,6 @@ def test_fused_frame_first_passes_bitwise(dims, K, nx, ny, nt, some, fdiv, monke
     the pass's grid) really ran fused -- the others (all of them in the
     700x900 case: tiles too small for aligned frames) keep the split launches."""
     monkeypatch.setenv("RMA_EXEC_FUSED", "1")
-    monkeypatch.setenv("RMA_FUSED_FRAME_DIV", fdiv)  # 3: frame tasks of 1/3 the rows
     P = dims[0] * dims[1]
     res = run_loopback(P, spmd_fused, nx, ny, nt, dims, K, timeout=240)
     nxg, nyg, _ = res[0][2]
@@ -576,58 +574,6 @@ def test_fused_passes_over_rccl_self_equal_the_split_passes(graph, monkeypatch):
     a, nfa = run(True)
     b, nfb = run(False)
     assert nfb == 0 and nfa >= 2, nfa  # (graph: counted once per captured pass)
-    assert np.array_equal(a, b)
-
-
-def spmd_step(rank, hub, nx, ny, nt, dims):
-    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], quiet=True, loopback=(hub, rank))
-    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=nt, init="random",
-                                    quiet=True, dims=dims))
-    m.step(nt)
-    out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g, m.executor.fused_passes)
-    m.close()
-    gg.finalize_global_grid()
-    return out
-
-
-@pytest.mark.parametrize("dims,nx,ny", [((2, 2), 300, 260), ((3, 1), 514, 200), ((1, 2), 130, 700)])
-def test_fused_one_step_passes_bitwise(dims, nx, ny, monkeypatch):
-    """RMA_EXEC_FUSED_STEP=1: the canonical one-step perf_hide passes run as
-    ONE march launch with the frame rects first (their waves raise the flag
-    the exchange stream waits on); every tile == the 1-rank run, bitwise."""
-    nt = 29
-    monkeypatch.setenv("RMA_EXEC_FUSED_STEP", "1")
-    res = run_loopback(dims[0] * dims[1], spmd_step, nx, ny, nt, dims, timeout=240)
-    nxg, nyg, _ = res[0][2]
-    monkeypatch.setenv("RMA_EXEC_FUSED_STEP", "0")
-    one = run_loopback(1, spmd_step, nxg, nyg, nt, (1, 1), timeout=240)[0][1]
-    for coords, T, _, fused in res:
-        assert fused == nt, (coords, fused)
-        gx0, gy0 = coords[0] * (nx - 2), coords[1] * (ny - 2)
-        assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
-
-
-def test_fused_one_step_passes_over_rccl_self_equal_split(monkeypatch):
-    """One periodic rank, halos through RCCL send/recv to itself: fused
-    one-step passes == split one-step passes, bitwise."""
-    n, nt = 1030, 57
-
-    def run(fused):
-        monkeypatch.setenv("RMA_EXEC_FUSED_STEP", "1" if fused else "0")
-        gg.init_global_grid(n, n, 1, periodx=1, periody=1, quiet=True, transport="rccl",
-                            self_via_transport=True)
-        m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=n, ny=n, nt=nt, init="random",
-                                        quiet=True, periods=(1, 1, 0)))
-        m.step(nt)
-        f = m.field.cpu().numpy().copy()
-        nf = m.executor.fused_passes
-        m.close()
-        gg.finalize_global_grid()
-        return f, nf
-
-    a, nfa = run(True)
-    b, nfb = run(False)
-    assert nfa == nt and nfb == 0
     assert np.array_equal(a, b)
 
 

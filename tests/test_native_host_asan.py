@@ -21,6 +21,7 @@ def test_host_selftest_asan_ubsan(tmp_path):
             os.path.join(ROOT, "csrc", "runtime", "topology.cpp"),
             os.path.join(ROOT, "csrc", "runtime", "errors.cpp"),
             os.path.join(ROOT, "csrc", "runtime", "plan.cpp"),
+            os.path.join(ROOT, "csrc", "runtime", "config.cpp"),
             os.path.join(ROOT, "csrc", "runtime", "halo_plan.cpp"),
             os.path.join(ROOT, "csrc", "kernels", "cpu_kernels.cpp")]
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-ffp-contract=off", "-fno-omit-frame-pointer",

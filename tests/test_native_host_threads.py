@@ -31,12 +31,12 @@ CLANG = "/opt/rocm/lib/llvm/bin/clang++"
 PRE_FIX = "5704426"
 SRCS = ["tests/native/threaded_selftest.cpp", "csrc/runtime/loopback.cpp", "csrc/runtime/halo.cpp",
         "csrc/runtime/halo_plan.cpp", "csrc/runtime/topology.cpp", "csrc/runtime/errors.cpp",
-        "csrc/runtime/ipc.cpp", "csrc/kernels/cpu_kernels.cpp"]
+        "csrc/runtime/ipc.cpp", "csrc/runtime/config.cpp", "csrc/kernels/cpu_kernels.cpp"]
 # the executor's time loop (csrc/runtime/executor.cpp) with the kernels' CPU twins
 EXEC_SRCS = ["tests/native/executor_selftest.cpp", "csrc/runtime/executor.cpp",
              "csrc/runtime/plan.cpp", "csrc/runtime/loopback.cpp", "csrc/runtime/halo.cpp",
              "csrc/runtime/halo_plan.cpp", "csrc/runtime/topology.cpp", "csrc/runtime/errors.cpp",
-             "csrc/runtime/trace.cpp", "csrc/kernels/cpu_kernels.cpp",
+             "csrc/runtime/trace.cpp", "csrc/runtime/config.cpp", "csrc/kernels/cpu_kernels.cpp",
              "csrc/kernels/kernel_select.cpp"]
 SAN = {"tsan": ["-fsanitize=thread"],
        "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]}
