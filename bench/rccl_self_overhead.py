@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
         chunk2: int = 0, dims: str = "xy", via_rccl: bool = True, init: str = "random",
-        spacing=None) -> dict:
+        spacing=None, direct: bool = False) -> dict:
     import torch
 
     from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
@@ -43,10 +43,11 @@ def run(n: int, K: int, steps: int, periodic: bool, variant: str = "perf_hide",
     py = 1 if periodic and "y" in dims else 0
     gg.init_global_grid(n, n, 1, periodx=px, periody=py, quiet=True, transport="rccl",
                         overlaps=(max(2, 2 * K), max(2, 2 * K), 2), halowidths=(K, K, 1),
-                        self_via_transport=periodic and via_rccl)
+                        self_via_transport=periodic and via_rccl and not direct)
     m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=n, nt=steps, quiet=True,
                                     init=init, periods=(px, py, 0), temporal=K,
-                                    fast_math=K > 1, chunk2=chunk2, spacing=spacing))
+                                    fast_math=K > 1, chunk2=chunk2, spacing=spacing,
+                                    halo_direct=periodic and direct))
     m.step(2 * K)
     m.synchronize()
     t0 = time.perf_counter()
@@ -85,7 +86,8 @@ def main(argv=None) -> int:
     ap.add_argument("--init", default="random", choices=["random", "gaussian"])
     ap.add_argument("--pattern", default="opop",
                     help="run order: o = open boundaries, p = periodic (each run allocates "
-                         "its own tile)")
+                         "its own tile), d = periodic with direct-store halos (the pass's "
+                         "kernel stores the periodic images itself, no exchange)")
     ap.add_argument("--spacing", default="grid", choices=["grid", "equal", "anisotropic"],
                     help="grid: dx = 10/nx_g, dy = 10/ny_g of each run (a periodic dim has "
                          "nx_g = n - 2K, so dx != dy and the coefficients differ from the open "
@@ -109,17 +111,20 @@ def main(argv=None) -> int:
            "frame_sides": os.environ.get("RMA_DIAG", "") or "neighbours", "variants": {}}
     for variant in a.variants.split(","):
         rows = []
-        for periodic in (c == "p" for c in a.pattern):
+        for c in a.pattern:
+            periodic, direct = c in "pd", c == "d"
             r = run(n, a.K, a.steps, periodic, variant, a.chunk2, a.periodic, not a.self_copies,
-                    a.init, spacing)
-            r.update({"periodic_rccl_self": periodic,
+                    a.init, spacing, direct)
+            r.update({"periodic_rccl_self": periodic and not direct, "periodic_direct": direct,
                       "teff_GBps": 3 * n * n * 8 / 1e9 / (r["ms_per_step"] / 1e3)})
             rows.append(r)
             print(json.dumps({"variant": variant, **r}), flush=True)
-        op = [r["ms_per_step"] for r in rows if not r["periodic_rccl_self"]]
+        op = [r["ms_per_step"] for r in rows if not r["periodic_rccl_self"] and not r["periodic_direct"]]
         pe = [r["ms_per_step"] for r in rows if r["periodic_rccl_self"]]
-        out["variants"][variant] = {"runs": rows,
-                                    "overhead": min(pe) / min(op) - 1.0 if pe and op else None}
+        pd = [r["ms_per_step"] for r in rows if r["periodic_direct"]]
+        out["variants"][variant] = {
+            "runs": rows, "overhead": min(pe) / min(op) - 1.0 if pe and op else None,
+            "overhead_direct": min(pd) / min(op) - 1.0 if pd and op else None}
     print(json.dumps(out), flush=True)
     if a.out:
         with open(a.out, "w") as f:

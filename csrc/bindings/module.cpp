@@ -560,6 +560,31 @@ PYBIND11_MODULE(_C, m) {
              }
              return out;
            })
+      .def(
+          "set_direct",
+          // peers: 8 tuples (rank, T ptr, T2 ptr, flag ptr) in DiffusionExecutor::kDirI/J
+          // order; in_flags: this rank's 8 device words (0: none)
+          [](DiffusionExecutor& e, const std::vector<std::tuple<int, uintptr_t, uintptr_t, uintptr_t>>& peers,
+             uintptr_t in_flags) {
+            RMA_CHECK_ARG(peers.size() == 8, "set_direct: 8 directions, got " << peers.size());
+            std::array<DiffusionExecutor::DirectPeer, 8> a{};
+            for (int d = 0; d < 8; ++d) {
+              a[d].rank = std::get<0>(peers[d]);
+              a[d].T = P<double>(std::get<1>(peers[d]));
+              a[d].T2 = P<double>(std::get<2>(peers[d]));
+              a[d].flag = P<uint64_t>(std::get<3>(peers[d]));
+            }
+            e.set_direct(a, P<uint64_t>(in_flags));
+          },
+          py::arg("peers"), py::arg("in_flags"), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("direct", &DiffusionExecutor::direct)
+      .def_property_readonly("direct_passes", &DiffusionExecutor::direct_passes)
+      .def_property_readonly_static("direct_dirs", [](py::object) {
+        std::vector<std::pair<int, int>> v;
+        for (int d = 0; d < 8; ++d)
+          v.emplace_back(DiffusionExecutor::kDirI[d], DiffusionExecutor::kDirJ[d]);
+        return v;
+      })
       .def("set_solo", &DiffusionExecutor::set_solo, py::arg("on"),
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("solo", &DiffusionExecutor::solo)

@@ -121,6 +121,33 @@ class DiffusionExecutor {
   // throws if a fused pass's bounded wait for its frame flag timed out (the
   // halos of that pass are wrong); also checked at every run() and timings()
   void check_error() const { check_fused_error(); }
+  // Direct-store halos (kernels.h DirectStores), replacing the exchange: every
+  // pass's pipelined kernel also stores the cells that are a neighbour's halo
+  // straight into that neighbour's output field. peers[d] for the 8
+  // directions d = (i, j) in kDirI / kDirJ order ((-1,-1), (0,-1), (1,-1),
+  // (-1,0), (1,0), (-1,1), (0,1), (1,1); opposite(d) = 7 - d): the peer's
+  // rank (-1: none, this rank: its own periodic images), its T / T2 (the same
+  // roles as ours: every rank runs the same pass plan) and, for another rank,
+  // the word of ITS in_flags that counts our passes. in_flags: this rank's 8
+  // device words (zeroed, quiescent peers), in_flags[d] counted by the peer in
+  // direction d. Pass n waits until every neighbour's count is >= n - 1 (its
+  // frame of pass n - 1 is done: our halo of that pass is complete and it no
+  // longer reads the field we are about to store into), then stores, and
+  // raises its count to n at the neighbours once its frame tasks are done.
+  // Needs fast-math K-step passes (pipelined kernels at every depth); no
+  // hipGraph replay with another rank (the counts are pass numbers). An
+  // all-(-1) peers array switches direct stores off (the halo exchange again).
+  struct DirectPeer {
+    int rank = -1;
+    double* T = nullptr;
+    double* T2 = nullptr;
+    uint64_t* flag = nullptr;
+  };
+  static constexpr int kDirI[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+  static constexpr int kDirJ[8] = {-1, -1, -1, 0, 0, 1, 1, 1};
+  void set_direct(const std::array<DirectPeer, 8>& peers, uint64_t* in_flags);
+  bool direct() const { return direct_on_; }
+  int64_t direct_passes() const { return direct_pass_; }
   std::vector<Rect> frame_rects() const { return frame_; }
   Rect interior_rect() const { return interior_; }
   Rect full_rect() const { return full_; }
@@ -188,6 +215,17 @@ class DiffusionExecutor {
   void enqueue_fused(const std::vector<Rect>& frame, const Rect& interior, StencilTuning tn,
                      double* Tout, void* const* ev, Launch&& launch);
   void check_fused_error() const;
+  // direct-store halos (set_direct)
+  bool direct_on_ = false;
+  std::array<DirectPeer, 8> dpeer_{};
+  uint64_t* din_flags_ = nullptr;
+  uint32_t din_mask_ = 0;      // directions with another rank (flags to wait on)
+  FlagTargets dout_{};         // the neighbours' words counting our passes
+  uint64_t direct_pass_ = 0;   // passes done in direct mode
+  bool direct_active() const { return direct_on_ && !solo_; }
+  bool direct_remote() const { return direct_active() && din_mask_ != 0; }
+  DirectStores direct_stores(const PassGeom& g, bool out_is_T2) const;
+  void ensure_error_word();
   void* graph_exec_ = nullptr;  // hipGraphExec_t
   int64_t graph_len_ = 0;
   int parity_ = 0;

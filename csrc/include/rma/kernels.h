@@ -25,6 +25,23 @@ using stream_t = void*;  // hipStream_t
 // ---------------------------------------------------------------------------
 constexpr int kMaxRects = 8;
 
+// Direct-store halos (pipelined K-step kernels only): cells of the output rect
+// that are a neighbour's halo are ALSO stored straight into the neighbour's
+// output field, at element index (my index + shift) -- its own tile in the
+// same process (loopback ranks), a mapped peer tile (IPC) or this tile's own
+// periodic images. Replaces the pack / send / receive / unpack of an exchange
+// (DiffusionExecutor::set_direct).
+constexpr int kMaxDirect = 8;
+struct DirectStore {
+  Rect r;              // cells of THIS tile whose images go to the peer
+  double* dst;         // the peer's output field
+  int64_t shift;       // peer element index = my element index + shift
+};
+struct DirectStores {
+  int n = 0;
+  DirectStore d[kMaxDirect];
+};
+
 struct StencilTuning {
   int chunk_rows = 4;      // rows marched by one wave-task
   int nontemporal = 3;     // bit 0: NT T2 stores; bit 1: NT 1/Cp loads; bit 2: NT T loads
@@ -44,6 +61,8 @@ struct StencilTuning {
   uint64_t* signal = nullptr;
   int signal_rects = 0;
   int signal_chunk_rows = 0;  // rows per task of the signal rects (0: chunk_rows)
+  // direct-store halos of this launch (pipelined kernels; nullptr: none)
+  const DirectStores* direct = nullptr;
 };
 
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
@@ -210,6 +229,15 @@ void stream_triad_gpu(double* c, const double* a, const double* b, double s, int
 void flag_wait_gpu(const uint64_t* flag, uint64_t want, double timeout_s, uint32_t* err,
                    uint32_t code, stream_t stream);
 void flag_write_gpu(uint64_t* flag, uint64_t value, stream_t stream);
+// Direct-store halo passes: wait until every flags[i] with bit i of mask set
+// is >= want (bounded, as flag_wait_gpu); store value into every non-null
+// dst[i] (system-scope release), i < 8. One 64-lane workgroup each.
+void flags_wait_ge_gpu(const uint64_t* flags, uint32_t mask, uint64_t want, double timeout_s,
+                       uint32_t* err, uint32_t code, stream_t stream);
+struct FlagTargets {
+  uint64_t* dst[8] = {};
+};
+void flags_write_gpu(const FlagTargets& t, uint64_t value, stream_t stream);
 
 // ---------------------------------------------------------------------------
 // Reductions for verification / NaN guards. Result is written

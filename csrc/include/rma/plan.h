@@ -68,9 +68,11 @@ struct PassGeom {
 // interior's cost per cell.
 // bands: height of the aligned y-bands, -1 = the default / RMA_DIAG frame_bands,
 // 0 = the ol-K rows the exchange needs, 1 = whole task rows.
+// out_k > 0: the output rect is owned_rect(out_k) whatever K (direct-store
+// halos: a pass never writes the halo planes [K, hw) its neighbours store).
 PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool hide,
                        int64_t bwx, int64_t bwy, int64_t olx, int64_t oly, int64_t task_w = 0,
-                       int64_t task_h = 0, int vec = 1, int bands = -1);
+                       int64_t task_h = 0, int vec = 1, int bands = -1, int out_k = 0);
 
 // Aligned frame layout per tile class and neighbour set (perf_hide K-step
 // passes, measured: RCCL-self overhead at K = 24, equal coefficients,

@@ -47,6 +47,30 @@ __global__ __launch_bounds__(64) void flag_write_kernel(uint64_t* flag, uint64_t
   if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// direct-store halos: lane i < 8 waits for its flag (monotonic pass counters,
+// so >=: a neighbour may already be one pass ahead); every lane exits
+__global__ __launch_bounds__(64) void flags_wait_ge_kernel(const uint64_t* flags, uint32_t mask,
+                                                           uint64_t want, uint64_t max_ticks,
+                                                           uint32_t* err, uint32_t code) {
+  const int i = threadIdx.x;
+  if (i >= 8 || !((mask >> i) & 1u)) return;
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    const uint64_t v = __hip_atomic_load(flags + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (v >= want) return;
+    if (wall_clock64() - t0 > max_ticks) {
+      __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+__global__ __launch_bounds__(64) void flags_write_kernel(FlagTargets t, uint64_t value) {
+  const int i = threadIdx.x;
+  if (i < 8 && t.dst[i]) __hip_atomic_store(t.dst[i], value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 uint64_t wall_ticks_per_s() {
   static const uint64_t rate = [] {
     int dev = 0, khz = 0;
@@ -67,6 +91,22 @@ void flag_wait_gpu(const uint64_t* flag, uint64_t want, double timeout_s, uint32
   const uint64_t ticks = (uint64_t)(timeout_s * (double)wall_ticks_per_s());
   hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, as_stream(stream), flag, want,
                      ticks, err, code);
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+void flags_wait_ge_gpu(const uint64_t* flags, uint32_t mask, uint64_t want, double timeout_s,
+                       uint32_t* err, uint32_t code, stream_t stream) {
+  RMA_CHECK_ARG(flags != nullptr && err != nullptr, "null flags or error word");
+  RMA_CHECK_ARG(timeout_s > 0 && timeout_s < 1e6, "flag wait timeout " << timeout_s << " s");
+  if (mask == 0) return;
+  const uint64_t ticks = (uint64_t)(timeout_s * (double)wall_ticks_per_s());
+  hipLaunchKernelGGL(flags_wait_ge_kernel, dim3(1), dim3(64), 0, as_stream(stream), flags, mask,
+                     want, ticks, err, code);
+  RMA_HIP_LAUNCH_CHECK();
+}
+
+void flags_write_gpu(const FlagTargets& t, uint64_t value, stream_t stream) {
+  hipLaunchKernelGGL(flags_write_kernel, dim3(1), dim3(64), 0, as_stream(stream), t, value);
   RMA_HIP_LAUNCH_CHECK();
 }
 

@@ -225,7 +225,7 @@ template <int K, int S, int V, int Ar, int C>
 __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double* __restrict__ T,
                                           const double* __restrict__ iCp, int64_t nx, int64_t ny,
                                           const RectList& L, const StencilCoef& k, int chunk_rows,
-                                          int remap) {
+                                          int remap, const DirectStores& DS) {
   using P = Plan<K, S>;
   constexpr bool Canon = Ar == kArCanon, kDpp = Ar != kArFast5Perm, kRegG = ar_reg(Ar);
   static_assert(!kRegG || (V != 5 && (C == 1 || V == 4)),
@@ -722,6 +722,16 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         wr2(&hand[par][S0 ? 0 : stage][0], res);
       } else if (row >= ya32 && row < yb32) {
         store_row<V, true>(const_cast<double*>(at(T2 + (int64_t)row * nx, xsob)), res, m);
+        // direct-store halos: the same values into the neighbours' halos (the
+        // descriptors are kernel arguments: uniform loop, uniform row test)
+        for (int q = 0; q < DS.n; ++q) {
+          const DirectStore& ds = DS.d[q];
+          if (row < ds.r.y0 || row >= ds.r.y1) continue;
+          bool md[V];
+#pragma unroll
+          for (int v = 0; v < V; ++v) md[v] = m[v] && x + v >= ds.r.x0 && x + v < ds.r.x1;
+          store_row<V, true>(ds.dst + ((int64_t)row * nx + x + ds.shift), res, md);
+        }
       }
     }
     };
@@ -802,8 +812,8 @@ __global__ __launch_bounds__(kWave * S * C) __attribute__((amdgpu_waves_per_eu(
                                                       const double* __restrict__ iCp,
                                                       int64_t nx, int64_t ny, RectList L,
                                                       StencilCoef k, int chunk_rows,
-                                                      int remap) {
-  pipe_body<K, S, V, Ar, C>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap);
+                                                      int remap, DirectStores D) {
+  pipe_body<K, S, V, Ar, C>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap, D);
 }
 
 struct PipeLaunch {
@@ -819,6 +829,7 @@ struct PipeLaunch {
   uint64_t* sig = nullptr;  // fused pass: the first sig_rects rects signal (RectList::sig)
   int sig_rects = 0;
   int sig_chunk_rows = 0;   // ...with this many rows per task (0: chunk_rows)
+  const DirectStores* direct = nullptr;  // direct-store halos (nullptr: none)
 };
 
 // Plans the (strip, chunk) tasks with this instantiation's block width
@@ -844,8 +855,10 @@ void launch(const PipeLaunch& a) {
     L.sig = a.sig;
     L.sig_blocks = L.block_end[ns - 1];
   }
+  DirectStores D{};
+  if (a.direct) D = *a.direct;
   pipe_kernel<K, S, V, Ar, C><<<dim3((unsigned)blocks), dim3(kWave * S * C), 0, a.stream>>>(
-      a.T2, a.T, a.iCp, a.nx, a.ny, L, a.k, a.chunk_rows, a.remap);
+      a.T2, a.T, a.iCp, a.nx, a.ny, L, a.k, a.chunk_rows, a.remap, D);
 }
 
 // Each stencil_pipe_{a,b,c}.hip unit instantiates a range of (K, S) of the

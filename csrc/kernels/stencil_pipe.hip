@@ -57,6 +57,24 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, rects, nrects, c, tune.chunk_rows, remap,
                      as_stream(stream)};
+  if (tune.direct) {
+    const DirectStores& D = *tune.direct;
+    RMA_CHECK_ARG(D.n >= 0 && D.n <= kMaxDirect, "direct stores n=" << D.n);
+    for (int i = 0; i < D.n; ++i) {
+      const DirectStore& d = D.d[i];
+      RMA_CHECK_ARG(d.dst != nullptr, "direct store " << i << ": null destination");
+      RMA_CHECK_ARG(V < 2 || (d.shift % 2 == 0 && (reinterpret_cast<uintptr_t>(d.dst) & 15) == 0),
+                    "direct store " << i << ": 16-byte stores need an even shift and an aligned "
+                                    "destination");
+      // every image lies inside the destination tile (same nx x ny as this one)
+      if (!d.r.empty()) {
+        const int64_t lo = d.r.y0 * nx + d.r.x0 + d.shift;
+        const int64_t hi = (d.r.y1 - 1) * nx + d.r.x1 - 1 + d.shift;
+        RMA_CHECK_ARG(lo >= 0 && hi < nx * ny, "direct store " << i << " maps outside the tile");
+      }
+    }
+    a.direct = &D;
+  }
   if (tune.signal) {
     RMA_CHECK_ARG(tune.signal_rects >= 1 && tune.signal_rects < nrects,
                   "signal rects " << tune.signal_rects << " of " << nrects);

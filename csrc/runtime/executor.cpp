@@ -284,8 +284,12 @@ const PassGeom& DiffusionExecutor::geometry(int K) {
       tw = (64 * vec - 2 * K) / vec * vec;
       th = t.chunk_rows;
     }
+    // direct-store halos: every pass writes the owned rect of the full halo
+    // width, never the halo planes its neighbours store into (a pass of depth
+    // K < hw would otherwise also write [K, hw))
     geom_[K] = pass_geometry(nx_, ny_, K, nbr_, p_.mode == Mode::kHide, p_.bwx, p_.bwy, p_.olx,
-                             p_.oly, tw, th, vec, frame_layout(ny_, nbr_).bands);
+                             p_.oly, tw, th, vec, frame_layout(ny_, nbr_).bands,
+                             direct_active() ? (int)std::max(hwx_, hwy_) : 0);
     geom_[K].task_w = tw;
     geom_[K].task_h = th;
     geom_ok_[K] = 1;
@@ -478,6 +482,11 @@ void DiffusionExecutor::enqueue_fused(const std::vector<Rect>& frame, const Rect
   // the whole launch waits for the previous exchange (its frame tasks read the
   // halo) and, in stream order, for the previous launch
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+  // direct-store halos: every neighbour's frame of the previous pass is done
+  // (our halo complete, its field free for our stores)
+  const bool dr = direct_remote();
+  if (dr)
+    flags_wait_ge_gpu(din_flags_, din_mask_, direct_pass_, fused_timeout_s_, ferr_dev_, 2, s_lo_);
   Rect rs[kMaxRects];
   int n = 0;
   for (const Rect& r : frame) rs[n++] = r;
@@ -499,7 +508,10 @@ void DiffusionExecutor::enqueue_fused(const std::vector<Rect>& frame, const Rect
   rec(1, s_hi_);
   {
     TraceRange th("rma.halo");
-    exchange(Tout, s_hi_);
+    if (dr)  // the halos are stored: raise our pass count at the neighbours
+      flags_write_gpu(dout_, direct_pass_ + 1, s_hi_);
+    else
+      exchange(Tout, s_hi_);
   }
   rec(2, s_hi_);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
@@ -509,15 +521,129 @@ void DiffusionExecutor::enqueue_fused(const std::vector<Rect>& frame, const Rect
 void DiffusionExecutor::check_fused_error() const {
   if (!ferr_host_) return;
   const uint32_t e = __atomic_load_n(ferr_host_, __ATOMIC_ACQUIRE);
-  RMA_CHECK_ARG(e == 0, "frame-first fused pass: the exchange stream's wait for the frame tasks "
+  RMA_CHECK_ARG(e != 1, "frame-first fused pass: the exchange stream's wait for the frame tasks "
                         "timed out after "
                             << fused_timeout_s_
                             << " s (RMA_EXEC_FUSED_TIMEOUT); the halos of that pass are wrong");
+  RMA_CHECK_ARG(e == 0, "direct-store halos: the wait for a neighbour's pass count timed out "
+                        "after "
+                            << fused_timeout_s_
+                            << " s (RMA_EXEC_FUSED_TIMEOUT; a neighbour died or runs another "
+                               "plan); the halos of that pass are wrong");
+}
+
+void DiffusionExecutor::ensure_error_word() {
+  if (ferr_host_) return;
+  RMA_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ferr_host_), sizeof(uint32_t),
+                              hipHostMallocMapped));
+  *ferr_host_ = 0;
+  RMA_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ferr_dev_), ferr_host_, 0));
+}
+
+void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint64_t* in_flags) {
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_hi_)));
+  RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
+  bool any = false;
+  uint32_t mask = 0;
+  FlagTargets out{};
+  const auto& nb = real_nbr_;
+  const bool diag = halo_ && halo_->has_diagonals();
+  for (int d = 0; d < 8; ++d) {
+    const int i = kDirI[d], j = kDirJ[d];
+    int want = -1;
+    if (j == 0)
+      want = nb[0][i > 0];
+    else if (i == 0)
+      want = nb[1][j > 0];
+    else if (nb[0][i > 0] >= 0 && nb[1][j > 0] >= 0) {
+      RMA_CHECK_ARG(diag, "direct-store halos with x and y neighbours need the diagonal ranks");
+      want = halo_->diagonals()[(j > 0) * 2 + (i > 0)];
+    }
+    const DirectPeer& p = peers[d];
+    RMA_CHECK_ARG(p.rank == want, "direct-store peer of direction (" << i << "," << j << "): rank "
+                                      << p.rank << ", the grid's neighbour is " << want);
+    if (p.rank < 0) continue;
+    any = true;
+    RMA_CHECK_ARG(p.T && p.T2, "direct-store peer (" << i << "," << j << "): null fields");
+    if (p.T == T_) {  // this rank: its own periodic images, ordered by the stream
+      RMA_CHECK_ARG(p.T2 == T2_, "direct-store self peer with another T2");
+      continue;
+    }
+    RMA_CHECK_ARG(p.flag, "direct-store peer (" << i << "," << j << "): null pass-count word");
+    mask |= 1u << d;
+    out.dst[d] = p.flag;
+  }
+  if (any) {
+    RMA_CHECK_ARG(p_.mode != Mode::kKp && fast5(),
+                  "direct-store halos need fast-math K-step passes (pipelined kernels at every "
+                  "depth)");
+    RMA_CHECK_ARG(mask == 0 || in_flags, "direct-store halos with another rank need in_flags");
+    ensure_error_word();
+  }
+  dpeer_ = peers;
+  din_flags_ = in_flags;
+  din_mask_ = any ? mask : 0;
+  dout_ = any ? out : FlagTargets{};
+  direct_on_ = any;
+  direct_pass_ = 0;
+  std::fill(geom_ok_.begin(), geom_ok_.end(), 0);  // pass rects follow direct_active()
+  if (graph_exec_) {  // captured with the exchange
+    (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec_));
+    graph_exec_ = nullptr;
+  }
+}
+
+DirectStores DiffusionExecutor::direct_stores(const PassGeom& g, bool out_is_T2) const {
+  DirectStores D;
+  // my cells whose images are the neighbour's halo: x columns [ol-hw, ol)
+  // (i = -1), [n-ol, n-ol+hw) (i = +1), the owned columns (i = 0); same in y
+  auto range = [](int s, int64_t n, int64_t ol, int64_t hw, int64_t lo, int64_t hi) {
+    int64_t a = lo, b = hi;
+    if (s < 0) a = std::max(lo, ol - hw), b = std::min(hi, ol);
+    if (s > 0) a = std::max(lo, n - ol), b = std::min(hi, n - ol + hw);
+    return std::make_pair(a, b);
+  };
+  for (int d = 0; d < 8; ++d) {
+    const DirectPeer& p = dpeer_[d];
+    if (p.rank < 0) continue;
+    const int i = kDirI[d], j = kDirJ[d];
+    const auto xr = range(i, nx_, p_.olx, hwx_, g.out.x0, g.out.x1);
+    const auto yr = range(j, ny_, p_.oly, hwy_, g.out.y0, g.out.y1);
+    const Rect r{xr.first, xr.second, yr.first, yr.second};
+    if (r.empty()) continue;
+    DirectStore& s = D.d[D.n++];
+    s.r = r;
+    s.dst = out_is_T2 ? p.T2 : p.T;
+    // the neighbour at (i, j) starts (n - ol) cells further: my (x, y) is its
+    // (x - i (nx - olx), y - j (ny - oly))
+    s.shift = -((int64_t)i * (nx_ - p_.olx) + (int64_t)j * (ny_ - p_.oly) * nx_);
+  }
+  return D;
 }
 
 void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   const PassGeom& g = geometry(K);
-  const StencilTuning tn = pass_tuning(K, 0);
+  // direct-store halos: every launch of the pass carries the stores (only the
+  // frame tasks' rows and columns hold any) instead of an exchange after it
+  const bool da = direct_active(), dr = direct_remote();
+  DirectStores ds;
+  if (da) ds = direct_stores(g, Tout == T2_);
+  struct DirectCount {  // counted however the pass is enqueued
+    uint64_t& n;
+    bool on;
+    ~DirectCount() {
+      if (on) ++n;
+    }
+  } dcount{direct_pass_, da};
+  StencilTuning tn = pass_tuning(K, 0);
+  if (da) tn.direct = &ds;
+  auto dwait = [&](void* stream) {
+    if (dr) flags_wait_ge_gpu(din_flags_, din_mask_, direct_pass_, fused_timeout_s_, ferr_dev_, 2,
+                              stream);
+  };
+  auto dpost = [&](void* stream) {
+    if (dr) flags_write_gpu(dout_, direct_pass_ + 1, stream);
+  };
   // timing events of this pass (nullptr when off)
   void* ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   if (timing_) {
@@ -531,11 +657,30 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     TraceRange tr("rma.pass.perf");
     rec(0, s_lo_);
     rec(3, s_lo_);
+    dwait(s_lo_);
     multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, tn, s_lo_);
     rec(4, s_lo_);
     rec(1, s_lo_);
-    exchange(Tout, s_lo_);
+    if (da)
+      dpost(s_lo_);
+    else
+      exchange(Tout, s_lo_);
     rec(2, s_lo_);
+    if (ev[4]) tseq_.push_back(1);
+    return;
+  }
+  if (da && !dr) {
+    // direct stores to this rank's own periodic images only: ONE launch over
+    // the owned rect, stream-ordered before the next pass (nothing to signal)
+    TraceRange tr("rma.pass.direct_self");
+    RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+    rec(0, s_lo_);
+    rec(3, s_lo_);
+    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, tn, s_lo_);
+    rec(4, s_lo_);
+    rec(1, s_lo_);
+    rec(2, s_lo_);
+    RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
     if (ev[4]) tseq_.push_back(1);
     return;
   }
@@ -578,7 +723,8 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_hi_), E(e_lo_), 0));
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(lag_ ? e_fr_ : e_hi_), 0));
   // host-synchronising transport (loopback, IPC): interior first, see enqueue_step
-  const bool interior_first = halo_ && !halo_->capturable();
+  // (direct stores never block the host)
+  const bool interior_first = !da && halo_ && !halo_->capturable();
   auto interior = [&]() {
     rec(3, s_lo_);
     if (!g.interior.empty()) {
@@ -590,6 +736,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   };
   if (interior_first) interior();
   rec(0, s_hi_);
+  dwait(s_hi_);
   if (!g.frame.empty()) {
     TraceRange tb("rma.boundary");
     if (g.aligned) {  // whole tasks of the interior grid: one launch, its tuning
@@ -604,19 +751,24 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
       ft.chunk_rows = frame_chunk_rows(K, tn.chunk_rows);
       multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame.data(), (int)g.frame.size(), ft, s_hi_);
     } else {
+      StencilTuning tw = pass_tuning(K, 1), tt = pass_tuning(K, 2);
+      if (da) tw.direct = tt.direct = &ds;
       if (!g.frame_wide.empty())
         multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_wide.data(), (int)g.frame_wide.size(),
-                   pass_tuning(K, 1), s_hi_);
+                   tw, s_hi_);
       if (!g.frame_tall.empty())
         multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_tall.data(), (int)g.frame_tall.size(),
-                   pass_tuning(K, 2), s_hi_);
+                   tt, s_hi_);
     }
   }
   RMA_HIP_CHECK(hipEventRecord(E(e_fr_), S(s_hi_)));
   rec(1, s_hi_);
   {
     TraceRange th("rma.halo");
-    exchange(Tout, s_hi_);
+    if (da)
+      dpost(s_hi_);
+    else
+      exchange(Tout, s_hi_);
   }
   rec(2, s_hi_);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
@@ -837,7 +989,7 @@ void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
   RMA_HIP_CHECK(hipEventRecord(E(e_fr_), hi));
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
   int64_t left = nsteps;
-  if (p_.use_graph) {
+  if (p_.use_graph && !direct_remote()) {
     // a replay must leave the buffer parity unchanged: capture the plan of gl
     // steps twice when it has an odd number of passes
     const int64_t gl = p_.graph_steps > 0 ? p_.graph_steps : 20;
@@ -859,6 +1011,12 @@ void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
     }
   }
   run_eager(left);
+  // direct-store halos: the field this run leaves is complete only once every
+  // neighbour's frame of the last pass has stored into our halo (the caller
+  // reads it: gather, checks, the next update_halo_; and a neighbour must not
+  // store into a field its owner already released)
+  if (direct_remote())
+    flags_wait_ge_gpu(din_flags_, din_mask_, direct_pass_, fused_timeout_s_, ferr_dev_, 2, hi);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
   RMA_HIP_CHECK(hipStreamWaitEvent(caller, E(e_hi_), 0));

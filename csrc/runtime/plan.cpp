@@ -82,9 +82,11 @@ FrameLayout frame_layout(int64_t ny, const Neighbors& nbr) {
 
 PassGeom pass_geometry(int64_t nx, int64_t ny, int K, const Neighbors& nbr, bool hide,
                        int64_t bwx, int64_t bwy, int64_t olx, int64_t oly, int64_t task_w,
-                       int64_t task_h, int vec, int bands) {
+                       int64_t task_h, int vec, int bands, int out_k) {
   PassGeom g;
-  g.out = K == 1 ? Rect{1, nx - 1, 1, ny - 1} : owned_rect(nx, ny, K, nbr);
+  g.out = out_k > 0 ? owned_rect(nx, ny, out_k, nbr)
+          : K == 1  ? Rect{1, nx - 1, 1, ny - 1}
+                    : owned_rect(nx, ny, K, nbr);
   const bool any_nbr = nbr[0][0] >= 0 || nbr[0][1] >= 0 || nbr[1][0] >= 0 || nbr[1][1] >= 0;
   const Rect& o = g.out;
   const int64_t need_x = std::max(bwx, olx - o.x0), need_y = std::max(bwy, oly - o.y0);

@@ -109,6 +109,11 @@ class DiffusionConfig:
     # equal to the canonical expression, bitwise equal to its C++ CPU twin
     # (which the CPU path then runs)
     fast_math: bool = False
+    # direct-store halos (native executor, fast-math K-step passes): the frame
+    # tasks store the neighbours' halo cells straight into their fields --
+    # periodic images of this rank, other ranks' tiles in this process
+    # (loopback); the halo exchange is not run (DiffusionExecutor::set_direct)
+    halo_direct: bool = False
     # (dx, dy) instead of (lx/nx_g, ly/ny_g): probes that compare decompositions
     # at equal coefficients (the pass energy, hence the power-capped clock,
     # depends on them: ry = (dx/dy)^2 = 1 makes two of the three fast-math
@@ -203,6 +208,7 @@ class Diffusion2D:
                 use_graph = False
             self.use_graph = use_graph
             self.executor = self._build_executor()
+            self._setup_direct()
         self._ap_graph = None
         if cfg.variant == "ap" and cfg.use_graph:
             # ap on a GPU is ~11 small torch launches per step: replay them from
@@ -279,6 +285,60 @@ class Diffusion2D:
             int(cfg.vec), int(cfg.temporal), int(g.overlaps[0]), int(g.overlaps[1]),
             int(cfg.chunk2), int(cfg.unroll2), int(bool(cfg.fast_math)))
 
+    def _direct_ranks(self) -> list:
+        """Rank of each of the 8 directions (native executor order
+        ``Executor.direct_dirs``): the Cartesian neighbours, the diagonals
+        where both axis neighbours exist, -1 elsewhere."""
+        g = self.g
+        nb = g.neighbors
+        diag = list(g.topo.diagonals(g.me))
+        out = []
+        for i, j in native().Executor.direct_dirs:
+            if j == 0:
+                out.append(nb[0][i > 0])
+            elif i == 0:
+                out.append(nb[1][j > 0])
+            elif nb[0][i > 0] >= 0 and nb[1][j > 0] >= 0:
+                out.append(diag[(j > 0) * 2 + (i > 0)])
+            else:
+                out.append(-1)
+        return out
+
+    def _setup_direct(self) -> None:
+        """Collective: hand the executor its direct-store peers (cfg.halo_direct).
+        Every rank's fields and pass-count words are exchanged (in-process:
+        the loopback hub), the counts zeroed while every rank is quiescent."""
+        if not self.cfg.halo_direct or self.executor is None:
+            return
+        g, cfg = self.g, self.cfg
+        if not (cfg.fast_math and cfg.variant in ("perf", "perf_hide")):
+            raise ValueError("halo_direct needs fast-math perf / perf_hide passes")
+        ranks = self._direct_ranks()
+        remote = any(r >= 0 and r != g.me for r in ranks)
+        if remote and g.transport != "loopback":
+            raise ValueError(f"halo_direct with other ranks needs their fields mapped in this "
+                             f"process (loopback transport), not {g.transport!r}")
+        if not hasattr(self, "_dflags"):
+            self._dflags = torch.zeros(8, dtype=torch.int64, device=self.T.device)
+        mine = (self.T.data_ptr(), self.T2.data_ptr(), self._dflags.data_ptr())
+        torch.cuda.synchronize(self.T.device)
+        if remote:
+            g.comm.barrier()  # every rank's previous executor drained
+        self._dflags.zero_()
+        torch.cuda.synchronize(self.T.device)
+        table = g.comm.hub.collect(g.me, mine) if remote else {g.me: mine}
+        peers = []
+        for d, r in enumerate(ranks):
+            if r < 0:
+                peers.append((-1, 0, 0, 0))
+                continue
+            T, T2, fl = table[r]
+            # the peer's count of OUR passes: from its side we are direction 7 - d
+            peers.append((r, T, T2, 0 if r == g.me else fl + 8 * (7 - d)))
+        self.executor.set_direct(peers, self._dflags.data_ptr() if remote else 0)
+        if remote:
+            g.comm.barrier()  # nobody stores before every rank has zeroed its counts
+
     def set_temporal(self, K: int, fast_math: bool | None = None) -> None:
         """Switch the steps per kernel pass (e.g. to time the one-step kernel on
         the same tile) and optionally the fast-math arithmetic. The grid
@@ -328,6 +388,7 @@ class Diffusion2D:
             self.T, self.T2 = self.T2, self.T
             self.parity = 0
         self.executor = self._build_executor()
+        self._setup_direct()
         if self._solo:
             self.executor.set_solo(True)
 

@@ -14,6 +14,7 @@
 // watching the threads meet in the loopback hub. Reference:
 // /root/reference/scripts/diffusion_2D_perf_hide.jl:63-101 (the overlapped
 // time loop this executor implements), diffusion_2D_perf.jl:22-58.
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -55,6 +56,26 @@ void flag_write_gpu(uint64_t* flag, uint64_t value, stream_t) {
   reinterpret_cast<std::atomic<uint64_t>*>(flag)->store(value, std::memory_order_release);
 }
 std::atomic<long> g_signals{0};
+std::atomic<long> g_direct_launches{0};
+void flags_wait_ge_gpu(const uint64_t* flags, uint32_t mask, uint64_t want, double timeout_s,
+                       uint32_t* err, uint32_t code, stream_t) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < 8; ++i) {
+    if (!((mask >> i) & 1u)) continue;
+    auto* f = reinterpret_cast<const std::atomic<uint64_t>*>(flags + i);
+    while (f->load(std::memory_order_acquire) < want) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+        __atomic_store_n(err, code, __ATOMIC_RELEASE);
+        return;
+      }
+      std::this_thread::yield();
+    }
+  }
+}
+void flags_write_gpu(const FlagTargets& t, uint64_t value, stream_t) {
+  for (uint64_t* p : t.dst)
+    if (p) reinterpret_cast<std::atomic<uint64_t>*>(p)->store(value, std::memory_order_release);
+}
 void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t nx, int64_t ny,
                        const Rect* rects, int nrects, const StencilCoef& c, const StencilTuning& t,
                        stream_t) {
@@ -72,10 +93,44 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
                         const StencilTuning& t, stream_t) {
   // fast5 family: kernel 5 and the pipelined kernels except 10 (canonical)
   const bool fast = t.kernel == 5 || (t.kernel >= 9 && t.kernel != 10);
-  if (fast)
-    stencilk5_rects_cpu(K, T2, T, iCp, nx, ny, rects, nrects, c);
-  else
-    stencilk_rects_cpu(K, T2, T, iCp, nx, ny, rects, nrects, c);
+  // like the GPU kernel, read only the cells the rects depend on (each rect
+  // grown by K, clamped to the tile): the CPU twin on that box, whose own
+  // edge cells stay fixed over the K levels, gives the rect cells bitwise (the
+  // dependency cone of K levels ends K cells out). Reading the whole tile
+  // would race with a neighbour's direct stores into halos no launch reads.
+  for (int i = 0; i < nrects; ++i) {
+    const Rect& r = rects[i];
+    if (r.empty()) continue;
+    const int64_t bx0 = std::max<int64_t>(0, r.x0 - K), bx1 = std::min<int64_t>(nx, r.x1 + K);
+    const int64_t by0 = std::max<int64_t>(0, r.y0 - K), by1 = std::min<int64_t>(ny, r.y1 + K);
+    const int64_t bw = bx1 - bx0, bh = by1 - by0;
+    std::vector<double> a((size_t)(bw * bh)), ic((size_t)(bw * bh)), o((size_t)(bw * bh));
+    for (int64_t y = 0; y < bh; ++y)
+      for (int64_t x = 0; x < bw; ++x) {
+        a[(size_t)(y * bw + x)] = T[(by0 + y) * nx + bx0 + x];
+        ic[(size_t)(y * bw + x)] = iCp[(by0 + y) * nx + bx0 + x];
+      }
+    const Rect lr{r.x0 - bx0, r.x1 - bx0, r.y0 - by0, r.y1 - by0};
+    if (fast)
+      stencilk5_rects_cpu(K, o.data(), a.data(), ic.data(), bw, bh, &lr, 1, c);
+    else
+      stencilk_rects_cpu(K, o.data(), a.data(), ic.data(), bw, bh, &lr, 1, c);
+    for (int64_t y = r.y0; y < r.y1; ++y)
+      for (int64_t x = r.x0; x < r.x1; ++x) T2[y * nx + x] = o[(size_t)((y - by0) * bw + x - bx0)];
+  }
+  if (t.direct) {  // direct-store halos: the launched cells' images into the peers' fields
+    if (t.kernel < 9) throw std::runtime_error("direct stores on a non-pipelined kernel");
+    for (int q = 0; q < t.direct->n; ++q) {
+      const DirectStore& d = t.direct->d[q];
+      for (int i = 0; i < nrects; ++i) {
+        const Rect& r = rects[i];
+        for (int64_t y = std::max(r.y0, d.r.y0); y < std::min(r.y1, d.r.y1); ++y)
+          for (int64_t x = std::max(r.x0, d.r.x0); x < std::min(r.x1, d.r.x1); ++x)
+            d.dst[y * nx + x + d.shift] = T2[y * nx + x];
+      }
+    }
+    ++g_direct_launches;
+  }
   if (t.signal) {  // the launch's frame blocks are done: raise the flag (stencil_device.h)
     if (t.kernel < 9) throw std::runtime_error("signal on a non-pipelined kernel");
     reinterpret_cast<std::atomic<uint64_t>*>(t.signal + 1)->store(1, std::memory_order_release);
@@ -143,6 +198,7 @@ struct Case {
   int nt;
   const char* fused;  // RMA_EXEC_FUSED for the multi-rank run ("" = auto)
   int chunk = 0;      // K-step rows per task (ExecParams::chunk_rows2; 0: the table)
+  bool direct = false;  // direct-store halos between the rank threads (set_direct)
 };
 
 struct TileResult {
@@ -152,8 +208,15 @@ struct TileResult {
 };
 
 // runs the case's grid on dims[0] x dims[1] rank threads; returns every tile
-std::vector<TileResult> run_ranks(const Case& c, std::array<int, 3> dims, int64_t nx, int64_t ny) {
+std::vector<TileResult> run_ranks(const Case& c, std::array<int, 3> dims, int64_t nx, int64_t ny,
+                                  bool direct = false) {
   const int P = dims[0] * dims[1] * dims[2];
+  // direct-store halos: every rank's fields and pass-count words, published
+  // before any rank runs (a one-shot barrier)
+  std::vector<std::array<double*, 2>> fields((size_t)P);
+  std::vector<std::array<uint64_t, 8>> counts((size_t)P);
+  for (auto& a : counts) a.fill(0);
+  std::atomic<int> published{0};
   const int64_t ol = std::max(2, 2 * c.K);
   const int64_t nxg = c.periods[0] ? dims[0] * (nx - ol) : dims[0] * (nx - ol) + ol;
   const int64_t nyg = c.periods[1] ? dims[1] * (ny - ol) : dims[1] * (ny - ol) + ol;
@@ -176,6 +239,9 @@ std::vector<TileResult> run_ranks(const Case& c, std::array<int, 3> dims, int64_
             iCp[(size_t)(y * nx + x)] = cell_value(gx0 + x, gy0 + y, nxg, nyg, 29, 0.5, 1.5);
           }
         T2 = T;
+        fields[(size_t)r] = {T.data(), T2.data()};
+        published.fetch_add(1, std::memory_order_acq_rel);
+        while (published.load(std::memory_order_acquire) < P) std::this_thread::yield();
         ExecParams p;
         p.mode = c.mode;
         const double dx = 10.0 / (double)nxg, dy = 10.0 / (double)nyg;
@@ -187,6 +253,25 @@ std::vector<TileResult> run_ranks(const Case& c, std::array<int, 3> dims, int64_
         TileResult& res = out[(size_t)r];
         {
           DiffusionExecutor ex(T.data(), T2.data(), iCp.data(), nx, ny, p, hx.get());
+          if (direct) {
+            std::array<DiffusionExecutor::DirectPeer, 8> peers{};
+            const auto nb = topo.neighbors(r);
+            const auto dg = topo.diagonals(r);
+            for (int d = 0; d < 8; ++d) {
+              const int i = DiffusionExecutor::kDirI[d], j = DiffusionExecutor::kDirJ[d];
+              int q = -1;
+              if (j == 0) q = nb[0][i > 0];
+              else if (i == 0) q = nb[1][j > 0];
+              else if (nb[0][i > 0] >= 0 && nb[1][j > 0] >= 0) q = dg[(j > 0) * 2 + (i > 0)];
+              if (q < 0) continue;
+              peers[d].rank = q;
+              peers[d].T = fields[(size_t)q][0];
+              peers[d].T2 = fields[(size_t)q][1];
+              // the peer counts our passes in its word of direction 7 - d
+              peers[d].flag = q == r ? nullptr : &counts[(size_t)q][(size_t)(7 - d)];
+            }
+            ex.set_direct(peers, counts[(size_t)r].data());
+          }
           ex.run(c.nt, nullptr);
           (void)hipDeviceSynchronize();
           res.fused_passes = ex.fused_passes();
@@ -213,7 +298,7 @@ int run_case(const Case& c) {
     setenv("RMA_EXEC_FUSED", c.fused, 1);
   else
     unsetenv("RMA_EXEC_FUSED");
-  const auto multi = run_ranks(c, c.dims, c.nx, c.ny);
+  const auto multi = run_ranks(c, c.dims, c.nx, c.ny, c.direct);
   // the same global grid on one rank: its tile is the global grid plus the
   // overlap cells (periodic: wrapped by the self exchange)
   const int64_t nx1 = c.dims[0] * (c.nx - ol) + ol, ny1 = c.dims[1] * (c.ny - ol) + ol;
@@ -236,7 +321,7 @@ int run_case(const Case& c) {
         }
       }
   }
-  const bool want_fused = std::string(c.fused) == "1";
+  const bool want_fused = std::string(c.fused) == "1" && !c.direct;
   CHECK(!want_fused || fused > 0, "%s: no fused pass ran", c.name);
   CHECK(std::string(c.fused) != "0" || fused == 0, "%s: fused passes with RMA_EXEC_FUSED=0",
         c.name);
@@ -261,6 +346,18 @@ int main() {
       {"perf_hide K=24 2x1 fused", {2, 1, 1}, {0, 0, 0}, 700, 400, 24, Mode::kHide, 50, "1", 64},
       {"perf_hide K=24 2x2 auto", {2, 2, 1}, {1, 1, 0}, 700, 400, 24, Mode::kHide, 48, "", 64},
       {"perf K=8 1x2 periodic-y", {1, 2, 1}, {0, 1, 0}, 64, 60, 8, Mode::kPerf, 17, ""},
+      // direct-store halos (set_direct): the neighbours' halos stored by the
+      // frame tasks, pass counts instead of the exchange; split and fused passes
+      {"direct perf_hide K=8 2x2 open split", {2, 2, 1}, {0, 0, 0}, 760, 400, 8, Mode::kHide, 17,
+       "0", 0, true},
+      {"direct perf_hide K=8 2x2 periodic fused", {2, 2, 1}, {1, 1, 0}, 760, 400, 8, Mode::kHide,
+       19, "1", 0, true},
+      {"direct perf_hide K=24 3x1 periodic-x", {3, 1, 1}, {1, 0, 0}, 700, 400, 24, Mode::kHide, 50,
+       "", 64, true},
+      {"direct perf K=4 2x2 periodic-y", {2, 2, 1}, {0, 1, 0}, 64, 60, 4, Mode::kPerf, 13, "",
+       0, true},
+      {"direct perf_hide K=6 1x1 periodic self", {1, 1, 1}, {1, 1, 0}, 90, 70, 6, Mode::kHide, 25,
+       "", 0, true},
   };
   for (const Case& c : cases)
     if (run_case(c)) return 1;
@@ -289,7 +386,8 @@ int main() {
     c.name = names.back().c_str();
     if (run_case(c)) return 1;
   }
-  std::printf("frame flags raised %ld\n", g_signals.load());
+  std::printf("frame flags raised %ld, direct-store launches %ld\n", g_signals.load(),
+              g_direct_launches.load());
   CHECK(rma_stub::live_events() == 0, "events leaked: %ld", rma_stub::live_events().load());
   if (g_fail.load()) return 1;
   std::printf("executor selftest OK\n");

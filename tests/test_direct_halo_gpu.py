@@ -1,0 +1,114 @@
+"""Direct-store halos: the pipelined K-step kernels store
+the cells that are a neighbour's halo straight into the neighbour's output
+field (csrc/kernels/stencil_pipe.h, DirectStores; executor set_direct), so a
+pass has no pack / send / receive / unpack. Pass counts in device words order
+the ranks: pass n waits until every neighbour's frame of pass n - 1 is done.
+
+Every case is bitwise equal to the exchange path / the 1-rank run of the same
+global grid (reference semantics: update_halo! in the time loop,
+scripts/diffusion_2D_perf_hide.jl:94-101, scripts/diffusion_2D_perf.jl:51)."""
+import numpy as np
+import pytest
+
+from helpers import run_loopback
+from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+from rocm_mpi_amd.parallel import implicit_grid as gg
+
+pytestmark = pytest.mark.gpu
+
+
+def run_self(n, K, nt, periods, direct, variant="perf_hide", ny=None):
+    ny = ny or n
+    gg.init_global_grid(n, ny, 1, periodx=periods[0], periody=periods[1], quiet=True,
+                        overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1))
+    m = Diffusion2D(DiffusionConfig(variant=variant, nx=n, ny=ny, nt=nt, init="random",
+                                    quiet=True, periods=(*periods, 0), temporal=K, fast_math=True,
+                                    halo_direct=direct))
+    try:
+        m.step(nt)
+        f = m.field.cpu().numpy().copy()
+        info = (m.executor.direct, m.executor.direct_passes, m.executor.passes_done)
+    finally:
+        m.close()
+        gg.finalize_global_grid()
+    return f, info
+
+
+@pytest.mark.parametrize("periods", [(1, 1), (1, 0), (0, 1)])
+@pytest.mark.parametrize("K,n,nt", [(24, 1028, 61), (8, 516, 37), (20, 2052, 45)])
+def test_direct_self_periodic_equals_exchange(periods, K, n, nt):
+    """One rank, periodic: the kernel stores its own periodic images (one
+    launch per pass, no exchange) == local self copies after each pass."""
+    a, (da, dp, npass) = run_self(n, K, nt, periods, True)
+    b, (db, _, _) = run_self(n, K, nt, periods, False)
+    assert da and not db and dp == npass >= 2
+    assert np.array_equal(a, b)
+
+
+def test_direct_self_perf_variant():
+    a, (da, _, _) = run_self(1028, 16, 40, (1, 1), True, variant="perf")
+    b, _ = run_self(1028, 16, 40, (1, 1), False, variant="perf")
+    assert da and np.array_equal(a, b)
+
+
+def spmd(rank, hub, nx, ny, nt, dims, periods, K, direct):
+    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], periodx=periods[0],
+                        periody=periods[1], overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
+                        quiet=True, loopback=(hub, rank))
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=nt, init="random",
+                                    quiet=True, dims=dims, periods=(*periods, 0), temporal=K,
+                                    fast_math=True, halo_direct=direct))
+    try:
+        m.step(nt)
+        m.synchronize()
+        out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g,
+               (m.executor.direct, m.executor.direct_passes, m.executor.fused_passes))
+    finally:
+        m.close()
+        gg.finalize_global_grid()
+    return out
+
+
+@pytest.mark.parametrize("dims,periods,K,nx,ny,nt,fused", [
+    ((2, 2), (0, 0), 24, 1028, 900, 53, "auto"),
+    ((2, 2), (1, 1), 24, 1028, 900, 49, "1"),
+    ((2, 2), (1, 0), 8, 516, 400, 29, "0"),
+    ((2, 1), (0, 1), 16, 1028, 600, 41, "auto"),
+    ((1, 2), (0, 0), 20, 776, 1000, 47, "1"),
+    ((3, 1), (1, 0), 12, 516, 300, 33, "0"),
+])
+def test_direct_loopback_ranks_equal_one_rank(dims, periods, K, nx, ny, nt, fused, monkeypatch):
+    """Rank threads of one process (loopback) storing into each other's
+    fields: every tile == its window of the 1-rank run, bitwise, with fused
+    and split passes; every pass ran in direct mode."""
+    P = dims[0] * dims[1]
+    monkeypatch.setenv("RMA_EXEC_FUSED", fused)
+    res = run_loopback(P, spmd, nx, ny, nt, dims, periods, K, True, timeout=240)
+    nxg, nyg, _ = res[0][2]
+    ol = 2 * K
+    # the 1-rank run of the same global grid (periodic: the tile of the
+    # global interior plus its overlap)
+    n1x = nxg + ol if periods[0] else nxg
+    n1y = nyg + ol if periods[1] else nyg
+    monkeypatch.setenv("RMA_EXEC_FUSED", "0")
+    one = run_loopback(1, spmd, n1x, n1y, nt, (1, 1), periods, K, False, timeout=240)[0][1]
+    for coords, T, _, (direct, dpasses, _) in res:
+        assert direct and dpasses >= 2, (coords, dpasses)
+        gx0, gy0 = coords[0] * (nx - ol), coords[1] * (ny - ol)
+        assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
+    if fused == "1":
+        assert all(r[3][2] > 0 for r in res)
+
+
+def test_direct_refuses_cross_process_transports_and_canonical():
+    """halo_direct needs the neighbours' fields in this process (or this
+    rank's own images) and the fast-math pipelined passes."""
+    gg.init_global_grid(516, 516, 1, periodx=1, periody=1, quiet=True, overlaps=(16, 16, 2),
+                        halowidths=(8, 8, 1))
+    try:
+        with pytest.raises(ValueError, match="fast-math"):
+            Diffusion2D(DiffusionConfig(variant="perf_hide", nx=516, ny=516, nt=8, quiet=True,
+                                        periods=(1, 1, 0), temporal=8, fast_math=False,
+                                        halo_direct=True))
+    finally:
+        gg.finalize_global_grid()

@@ -136,4 +136,9 @@ def test_executor_time_loop_on_rank_threads_clean_and_bitwise(kind, tmp_path):
     assert r.returncode == 0, (r.stdout + r.stderr)[-6000:]
     assert "executor selftest OK" in r.stdout
     assert "fused)" in r.stdout and "perf_hide K=24 2x2 auto OK" in r.stdout
+    # direct-store halos between the rank threads (DiffusionExecutor::set_direct)
+    for name in ("direct perf_hide K=8 2x2 open split OK", "direct perf_hide K=8 2x2 periodic fused OK",
+                 "direct perf_hide K=24 3x1 periodic-x OK", "direct perf K=4 2x2 periodic-y OK",
+                 "direct perf_hide K=6 1x1 periodic self OK"):
+        assert name in r.stdout, name
     assert "WARNING: ThreadSanitizer" not in r.stderr
