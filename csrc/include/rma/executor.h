@@ -224,7 +224,7 @@ class DiffusionExecutor {
   uint64_t direct_pass_ = 0;   // passes done in direct mode
   bool direct_active() const { return direct_on_ && !solo_; }
   bool direct_remote() const { return direct_active() && din_mask_ != 0; }
-  DirectStores direct_stores(const PassGeom& g, bool out_is_T2) const;
+  DirectStores direct_stores(bool out_is_T2) const;
   void ensure_error_word();
   void* graph_exec_ = nullptr;  // hipGraphExec_t
   int64_t graph_len_ = 0;

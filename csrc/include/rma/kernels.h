@@ -27,19 +27,24 @@ constexpr int kMaxRects = 8;
 
 // Direct-store halos (pipelined K-step kernels only): cells of the output rect
 // that are a neighbour's halo are ALSO stored straight into the neighbour's
-// output field, at element index (my index + shift) -- its own tile in the
-// same process (loopback ranks), a mapped peer tile (IPC) or this tile's own
-// periodic images. Replaces the pack / send / receive / unpack of an exchange
-// (DiffusionExecutor::set_direct).
-constexpr int kMaxDirect = 8;
-struct DirectStore {
-  Rect r;              // cells of THIS tile whose images go to the peer
-  double* dst;         // the peer's output field
-  int64_t shift;       // peer element index = my element index + shift
-};
+// output field -- its own tile in the same process (loopback ranks), a mapped
+// peer tile (IPC) or this tile's own periodic images. Replaces the pack /
+// send / receive / unpack of an exchange (DiffusionExecutor::set_direct).
+// Direction d = 0..7 is (i, j) = (kDirI[d], kDirJ[d]) of executor.h. A stored
+// cell (x, y) also goes to dst[d] when dst[d] is set, x lies in the i-range
+// (i = -1: [xm0, xm1), +1: [xp0, xp1), 0: any) and y in the j-range (same with
+// ym / yp), at element index (y * nx + x) - i * sx - j * syr * nx: every rank
+// has the same nx x ny tile, the neighbour's origin sx = nx - olx columns /
+// syr = ny - oly rows away. Eight fixed ranges rather than a list of rects:
+// the kernel decides per task (which ranges its window and rows touch) and per
+// row with a few scalar compares; a list walked per row costs a scalar load
+// chain per entry and doubled the K = 24 pass at 8192^2.
 struct DirectStores {
-  int n = 0;
-  DirectStore d[kMaxDirect];
+  int on = 0;  // any dst set
+  int32_t xm0 = 0, xm1 = 0, xp0 = 0, xp1 = 0;
+  int32_t ym0 = 0, ym1 = 0, yp0 = 0, yp1 = 0;
+  int64_t sx = 0, syr = 0;
+  double* dst[8] = {};
 };
 
 struct StencilTuning {

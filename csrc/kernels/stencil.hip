@@ -174,7 +174,7 @@ void stencil_rects_gpu(double* T2, const double* T, const double* iCp, int64_t n
     return;
   }
   RMA_CHECK_ARG(!tune.signal, "a signalling launch needs a pipelined K-step kernel");
-  RMA_CHECK_ARG(!tune.direct || tune.direct->n == 0,
+  RMA_CHECK_ARG(!tune.direct || !tune.direct->on,
                 "direct-store halos need a pipelined K-step kernel");
   RectList L{};
   const int64_t total = plan_rects(L, rects, nrects, V, tune.chunk_rows, remap, true);

@@ -34,7 +34,7 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
   RMA_CHECK_ARG(tune.kernel >= 0 && tune.kernel <= 29, "unknown K-step kernel " << tune.kernel);
   RMA_CHECK_ARG(!tune.signal || tune.kernel >= 9,
                 "a signalling (frame-first fused) launch needs a pipelined kernel, got " << tune.kernel);
-  RMA_CHECK_ARG(!tune.direct || tune.direct->n == 0 || tune.kernel >= 9,
+  RMA_CHECK_ARG(!tune.direct || !tune.direct->on || tune.kernel >= 9,
                 "direct-store halos need a pipelined kernel, got " << tune.kernel);
   if (tune.kernel >= 9) {  // any-K stage-pipelined kernels (stencil_pipe.h)
     stencil_pipe_rects_gpu(K, tune.stages, tune.kernel - 9, T2, T, iCp, nx, ny, rects, nrects,

@@ -221,6 +221,39 @@ __device__ __forceinline__ double from_prev_lane(double v) {
   }
 }
 
+// Direct-store halos of one stored row (DirectStores, kernels.h): the row's
+// images in the neighbours in directions d = (i, j) (executor.h kDirI /
+// kDirJ order) whose ranges hold it. dxm / dxp: the wave stores columns in the
+// i = -1 / +1 ranges (uniform, per task).
+template <int V>
+__device__ __forceinline__ void direct_row(const DirectStores& D, int row, int64_t nx, int64_t x,
+                                           const double (&res)[V], const bool (&m)[V], bool dxm,
+                                           bool dxp) {
+  const bool ym = row >= D.ym0 && row < D.ym1, yp = row >= D.yp0 && row < D.yp1;
+  const int64_t e = (int64_t)row * nx + x, sx = D.sx, sy = D.syr * nx;
+  auto put = [&](int d, int64_t off, const bool (&mk)[V]) {
+    if (D.dst[d]) store_row<V, true>(D.dst[d] + (e + off), res, mk);
+  };
+  if (ym) put(1, sy, m);   // (0, -1)
+  if (yp) put(6, -sy, m);  // (0, +1)
+  if (dxm) {
+    bool mk[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) mk[v] = m[v] && x + v >= D.xm0 && x + v < D.xm1;
+    put(3, sx, mk);                  // (-1, 0)
+    if (ym) put(0, sx + sy, mk);     // (-1, -1)
+    if (yp) put(5, sx - sy, mk);     // (-1, +1)
+  }
+  if (dxp) {
+    bool mk[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) mk[v] = m[v] && x + v >= D.xp0 && x + v < D.xp1;
+    put(4, -sx, mk);                 // (+1, 0)
+    if (ym) put(2, -sx + sy, mk);    // (+1, -1)
+    if (yp) put(7, -sx - sy, mk);    // (+1, +1)
+  }
+}
+
 template <int K, int S, int V, int Ar, int C>
 __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double* __restrict__ T,
                                           const double* __restrict__ iCp, int64_t nx, int64_t ny,
@@ -298,6 +331,21 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
     return reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + boff);
   };
   const bool xin = xw >= 1 && xw + W - 1 <= nx - 2;  // no x-boundary cell in the window
+  // direct-store halos (DirectStores): does this wave store into the x-image
+  // ranges (a lane with a stored column there), do its rows meet the y ones
+  bool dxm = false, dxp = false, dtask = false;
+  if (DS.on) {
+    bool pm = false, pp = false;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      pm = pm || (m[v] && x + v >= DS.xm0 && x + v < DS.xm1);
+      pp = pp || (m[v] && x + v >= DS.xp0 && x + v < DS.xp1);
+    }
+    dxm = __builtin_amdgcn_ballot_w64(pm) != 0;
+    dxp = __builtin_amdgcn_ballot_w64(pp) != 0;
+    const bool tym = ya < DS.ym1 && yb > DS.ym0, typ = ya < DS.yp1 && yb > DS.yp0;
+    dtask = dxm || dxp || tym || typ;
+  }
 
   // fast5 constants (the host guarantees fast5_ok); canonical uses k directly
   const double ax = (-k.mlam) * k.rdx * k.rdx;
@@ -722,16 +770,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         wr2(&hand[par][S0 ? 0 : stage][0], res);
       } else if (row >= ya32 && row < yb32) {
         store_row<V, true>(const_cast<double*>(at(T2 + (int64_t)row * nx, xsob)), res, m);
-        // direct-store halos: the same values into the neighbours' halos (the
-        // descriptors are kernel arguments: uniform loop, uniform row test)
-        for (int q = 0; q < DS.n; ++q) {
-          const DirectStore& ds = DS.d[q];
-          if (row < ds.r.y0 || row >= ds.r.y1) continue;
-          bool md[V];
-#pragma unroll
-          for (int v = 0; v < V; ++v) md[v] = m[v] && x + v >= ds.r.x0 && x + v < ds.r.x1;
-          store_row<V, true>(ds.dst + ((int64_t)row * nx + x + ds.shift), res, md);
-        }
+        // direct-store halos: the same values into the neighbours' halos;
+        // only tasks whose window or rows touch a halo image range (dtask,
+        // uniform) test the row
+        if (dtask) direct_row<V>(DS, row, nx, x, res, m, dxm, dxp);
       }
     }
     };

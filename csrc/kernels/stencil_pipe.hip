@@ -57,21 +57,22 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   const int remap = tune.xcd_remap >= 0 ? tune.xcd_remap : (nx > 65536 ? 1 : 0);
   pipe::PipeLaunch a{T2, T, iCp, nx, ny, rects, nrects, c, tune.chunk_rows, remap,
                      as_stream(stream)};
-  if (tune.direct) {
+  if (tune.direct && tune.direct->on) {
     const DirectStores& D = *tune.direct;
-    RMA_CHECK_ARG(D.n >= 0 && D.n <= kMaxDirect, "direct stores n=" << D.n);
-    for (int i = 0; i < D.n; ++i) {
-      const DirectStore& d = D.d[i];
-      RMA_CHECK_ARG(d.dst != nullptr, "direct store " << i << ": null destination");
-      RMA_CHECK_ARG(V < 2 || (d.shift % 2 == 0 && (reinterpret_cast<uintptr_t>(d.dst) & 15) == 0),
-                    "direct store " << i << ": 16-byte stores need an even shift and an aligned "
-                                    "destination");
-      // every image lies inside the destination tile (same nx x ny as this one)
-      if (!d.r.empty()) {
-        const int64_t lo = d.r.y0 * nx + d.r.x0 + d.shift;
-        const int64_t hi = (d.r.y1 - 1) * nx + d.r.x1 - 1 + d.shift;
-        RMA_CHECK_ARG(lo >= 0 && hi < nx * ny, "direct store " << i << " maps outside the tile");
-      }
+    // every image lies inside the destination tile (same nx x ny as this one):
+    // the x-ranges shifted by -i * sx, the y-ranges by -j * syr
+    auto inside = [](int64_t a0, int64_t a1, int64_t shift, int64_t n) {
+      return a0 >= a1 || (a0 + shift >= 0 && a1 + shift <= n);
+    };
+    RMA_CHECK_ARG(inside(D.xm0, D.xm1, D.sx, nx) && inside(D.xp0, D.xp1, -D.sx, nx) &&
+                      inside(D.ym0, D.ym1, D.syr, ny) && inside(D.yp0, D.yp1, -D.syr, ny),
+                  "direct-store ranges map outside the " << nx << "x" << ny << " tile");
+    for (int d = 0; d < 8; ++d) {
+      if (!D.dst[d]) continue;
+      RMA_CHECK_ARG(V < 2 || (D.sx % 2 == 0 && (D.syr * nx) % 2 == 0 &&
+                              (reinterpret_cast<uintptr_t>(D.dst[d]) & 15) == 0),
+                    "direct store " << d << ": 16-byte stores need even shifts and an aligned "
+                                       "destination");
     }
     a.direct = &D;
   }

@@ -574,6 +574,8 @@ void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint6
     out.dst[d] = p.flag;
   }
   if (any) {
+    RMA_CHECK_ARG(nx_ < (int64_t(1) << 30) && ny_ < (int64_t(1) << 30),
+                  "direct-store halos: 32-bit image ranges");
     RMA_CHECK_ARG(p_.mode != Mode::kKp && fast5(),
                   "direct-store halos need fast-math K-step passes (pipelined kernels at every "
                   "depth)");
@@ -593,30 +595,27 @@ void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint6
   }
 }
 
-DirectStores DiffusionExecutor::direct_stores(const PassGeom& g, bool out_is_T2) const {
+DirectStores DiffusionExecutor::direct_stores(bool out_is_T2) const {
   DirectStores D;
-  // my cells whose images are the neighbour's halo: x columns [ol-hw, ol)
-  // (i = -1), [n-ol, n-ol+hw) (i = +1), the owned columns (i = 0); same in y
-  auto range = [](int s, int64_t n, int64_t ol, int64_t hw, int64_t lo, int64_t hi) {
-    int64_t a = lo, b = hi;
-    if (s < 0) a = std::max(lo, ol - hw), b = std::min(hi, ol);
-    if (s > 0) a = std::max(lo, n - ol), b = std::min(hi, n - ol + hw);
-    return std::make_pair(a, b);
-  };
+  // my cells whose images are the neighbours' halos: x columns [ol-hw, ol)
+  // (i = -1), [n-ol, n-ol+hw) (i = +1), any stored column (i = 0); same in y.
+  // The neighbour at (i, j) starts (n - ol) cells further: my (x, y) is its
+  // (x - i (nx - olx), y - j (ny - oly))
+  D.xm0 = (int32_t)(p_.olx - hwx_);
+  D.xm1 = (int32_t)p_.olx;
+  D.xp0 = (int32_t)(nx_ - p_.olx);
+  D.xp1 = (int32_t)(nx_ - p_.olx + hwx_);
+  D.ym0 = (int32_t)(p_.oly - hwy_);
+  D.ym1 = (int32_t)p_.oly;
+  D.yp0 = (int32_t)(ny_ - p_.oly);
+  D.yp1 = (int32_t)(ny_ - p_.oly + hwy_);
+  D.sx = nx_ - p_.olx;
+  D.syr = ny_ - p_.oly;
   for (int d = 0; d < 8; ++d) {
     const DirectPeer& p = dpeer_[d];
     if (p.rank < 0) continue;
-    const int i = kDirI[d], j = kDirJ[d];
-    const auto xr = range(i, nx_, p_.olx, hwx_, g.out.x0, g.out.x1);
-    const auto yr = range(j, ny_, p_.oly, hwy_, g.out.y0, g.out.y1);
-    const Rect r{xr.first, xr.second, yr.first, yr.second};
-    if (r.empty()) continue;
-    DirectStore& s = D.d[D.n++];
-    s.r = r;
-    s.dst = out_is_T2 ? p.T2 : p.T;
-    // the neighbour at (i, j) starts (n - ol) cells further: my (x, y) is its
-    // (x - i (nx - olx), y - j (ny - oly))
-    s.shift = -((int64_t)i * (nx_ - p_.olx) + (int64_t)j * (ny_ - p_.oly) * nx_);
+    D.dst[d] = out_is_T2 ? p.T2 : p.T;
+    D.on = 1;
   }
   return D;
 }
@@ -627,7 +626,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   // frame tasks' rows and columns hold any) instead of an exchange after it
   const bool da = direct_active(), dr = direct_remote();
   DirectStores ds;
-  if (da) ds = direct_stores(g, Tout == T2_);
+  if (da) ds = direct_stores(Tout == T2_);
   struct DirectCount {  // counted however the pass is enqueued
     uint64_t& n;
     bool on;

@@ -120,13 +120,21 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
   }
   if (t.direct) {  // direct-store halos: the launched cells' images into the peers' fields
     if (t.kernel < 9) throw std::runtime_error("direct stores on a non-pipelined kernel");
-    for (int q = 0; q < t.direct->n; ++q) {
-      const DirectStore& d = t.direct->d[q];
+    const DirectStores& D = *t.direct;
+    auto in = [](int64_t a, int s, int64_t m0, int64_t m1, int64_t p0, int64_t p1) {
+      return s == 0 || (s < 0 ? a >= m0 && a < m1 : a >= p0 && a < p1);
+    };
+    for (int d = 0; d < 8; ++d) {
+      if (!D.dst[d]) continue;
+      const int di = DiffusionExecutor::kDirI[d], dj = DiffusionExecutor::kDirJ[d];
+      const int64_t off = -di * D.sx - dj * D.syr * nx;
       for (int i = 0; i < nrects; ++i) {
         const Rect& r = rects[i];
-        for (int64_t y = std::max(r.y0, d.r.y0); y < std::min(r.y1, d.r.y1); ++y)
-          for (int64_t x = std::max(r.x0, d.r.x0); x < std::min(r.x1, d.r.x1); ++x)
-            d.dst[y * nx + x + d.shift] = T2[y * nx + x];
+        for (int64_t y = r.y0; y < r.y1; ++y) {
+          if (!in(y, dj, D.ym0, D.ym1, D.yp0, D.yp1)) continue;
+          for (int64_t x = r.x0; x < r.x1; ++x)
+            if (in(x, di, D.xm0, D.xm1, D.xp0, D.xp1)) D.dst[d][y * nx + x + off] = T2[y * nx + x];
+        }
       }
     }
     ++g_direct_launches;

@@ -59,10 +59,19 @@ def spmd(rank, hub, nx, ny, nt, dims, periods, K, direct):
                                     quiet=True, dims=dims, periods=(*periods, 0), temporal=K,
                                     fast_math=True, halo_direct=direct))
     try:
+        plan = list(m.executor.plan(nt))
+        geos = {k: m.executor.geometry(k) for k in set(plan)}
+
+        def fusable(g):  # aligned frames around a non-empty interior
+            x0, x1, y0, y1 = g["interior"]
+            return g["aligned"] and x1 > x0 and y1 > y0 and any(
+                r[1] > r[0] and r[3] > r[2] for r in g["frame"])
+
+        want = sum(1 for k in plan if fusable(geos[k]))
         m.step(nt)
         m.synchronize()
         out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g,
-               (m.executor.direct, m.executor.direct_passes, m.executor.fused_passes))
+               (m.executor.direct, m.executor.direct_passes, m.executor.fused_passes, want))
     finally:
         m.close()
         gg.finalize_global_grid()
@@ -71,16 +80,18 @@ def spmd(rank, hub, nx, ny, nt, dims, periods, K, direct):
 
 @pytest.mark.parametrize("dims,periods,K,nx,ny,nt,fused", [
     ((2, 2), (0, 0), 24, 1028, 900, 53, "auto"),
-    ((2, 2), (1, 1), 24, 1028, 900, 49, "1"),
+    ((2, 2), (1, 1), 24, 1100, 3500, 49, "1"),
     ((2, 2), (1, 0), 8, 516, 400, 29, "0"),
     ((2, 1), (0, 1), 16, 1028, 600, 41, "auto"),
-    ((1, 2), (0, 0), 20, 776, 1000, 47, "1"),
+    ((1, 2), (0, 0), 20, 1100, 3000, 47, "1"),
     ((3, 1), (1, 0), 12, 516, 300, 33, "0"),
 ])
 def test_direct_loopback_ranks_equal_one_rank(dims, periods, K, nx, ny, nt, fused, monkeypatch):
     """Rank threads of one process (loopback) storing into each other's
     fields: every tile == its window of the 1-rank run, bitwise, with fused
-    and split passes; every pass ran in direct mode."""
+    and split passes; every pass ran in direct mode (tiles too small for
+    aligned frames keep the split launches even with RMA_EXEC_FUSED=1, as in
+    test_multirank_gpu.py::test_fused_frame_first_passes_bitwise)."""
     P = dims[0] * dims[1]
     monkeypatch.setenv("RMA_EXEC_FUSED", fused)
     res = run_loopback(P, spmd, nx, ny, nt, dims, periods, K, True, timeout=240)
@@ -92,12 +103,12 @@ def test_direct_loopback_ranks_equal_one_rank(dims, periods, K, nx, ny, nt, fuse
     n1y = nyg + ol if periods[1] else nyg
     monkeypatch.setenv("RMA_EXEC_FUSED", "0")
     one = run_loopback(1, spmd, n1x, n1y, nt, (1, 1), periods, K, False, timeout=240)[0][1]
-    for coords, T, _, (direct, dpasses, _) in res:
+    for coords, T, _, (direct, dpasses, _, _) in res:
         assert direct and dpasses >= 2, (coords, dpasses)
         gx0, gy0 = coords[0] * (nx - ol), coords[1] * (ny - ol)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
-    if fused == "1":
-        assert all(r[3][2] > 0 for r in res)
+    if fused == "1":  # the passes with aligned frames ran fused (the geometries ask for some)
+        assert all(r[3][2] == r[3][3] > 0 for r in res), [r[3] for r in res]
 
 
 def test_direct_refuses_cross_process_transports_and_canonical():
