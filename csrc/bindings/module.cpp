@@ -367,6 +367,13 @@ PYBIND11_MODULE(_C, m) {
                              })
       .def_property_readonly("poisoned", &IpcTransport::poisoned)
       .def_property_readonly("host_waits", &IpcTransport::host_waits);
+  py::class_<IpcMap>(m, "IpcMap")
+      .def(py::init<>())
+      .def_static("export_ptr",
+                  [](uintptr_t p) { return py::bytes(IpcMap::export_ptr((const void*)p)); })
+      .def("open", [](IpcMap& m, py::bytes blob) { return (uintptr_t)m.open(blob); })
+      .def("close_all", &IpcMap::close_all)
+      .def_property_readonly("mappings", &IpcMap::mappings);
   py::class_<RcclComm, P2PTransport>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def(py::init([](int nranks, int rank, py::bytes uid, int device, double init_timeout_s) {
@@ -565,7 +572,7 @@ PYBIND11_MODULE(_C, m) {
           // peers: 8 tuples (rank, T ptr, T2 ptr, flag ptr) in DiffusionExecutor::kDirI/J
           // order; in_flags: this rank's 8 device words (0: none)
           [](DiffusionExecutor& e, const std::vector<std::tuple<int, uintptr_t, uintptr_t, uintptr_t>>& peers,
-             uintptr_t in_flags) {
+             uintptr_t in_flags, bool host_wait) {
             RMA_CHECK_ARG(peers.size() == 8, "set_direct: 8 directions, got " << peers.size());
             std::array<DiffusionExecutor::DirectPeer, 8> a{};
             for (int d = 0; d < 8; ++d) {
@@ -574,9 +581,10 @@ PYBIND11_MODULE(_C, m) {
               a[d].T2 = P<double>(std::get<2>(peers[d]));
               a[d].flag = P<uint64_t>(std::get<3>(peers[d]));
             }
-            e.set_direct(a, P<uint64_t>(in_flags));
+            e.set_direct(a, P<uint64_t>(in_flags), host_wait);
           },
-          py::arg("peers"), py::arg("in_flags"), py::call_guard<py::gil_scoped_release>())
+          py::arg("peers"), py::arg("in_flags"), py::arg("host_wait") = false,
+          py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("direct", &DiffusionExecutor::direct)
       .def_property_readonly("direct_passes", &DiffusionExecutor::direct_passes)
       .def_property_readonly_static("direct_dirs", [](py::object) {

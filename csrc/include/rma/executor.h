@@ -145,7 +145,11 @@ class DiffusionExecutor {
   };
   static constexpr int kDirI[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
   static constexpr int kDirJ[8] = {-1, -1, -1, 0, 0, 1, 1, 1};
-  void set_direct(const std::array<DirectPeer, 8>& peers, uint64_t* in_flags);
+  // host_wait: the ranks are threads of this process and in_flags / the
+  // peers' words are pinned host memory; the host waits for the counts before
+  // enqueueing a pass instead of a wait kernel on the stream (see direct_wait)
+  void set_direct(const std::array<DirectPeer, 8>& peers, uint64_t* in_flags,
+                  bool host_wait = false);
   bool direct() const { return direct_on_; }
   int64_t direct_passes() const { return direct_pass_; }
   std::vector<Rect> frame_rects() const { return frame_; }
@@ -185,6 +189,7 @@ class DiffusionExecutor {
   std::vector<PassGeom> geom_;   // index K (lazily filled)
   std::vector<char> geom_ok_;
   std::vector<double> cost_;     // index K: relative pass cost (plan_passes)
+  std::vector<double> cost_base_;  // ...without the direct-store pricing (set_direct)
   int64_t hwx_ = 1, hwy_ = 1;
   void* s_hi_ = nullptr;  // hipStream_t
   void* s_lo_ = nullptr;
@@ -222,9 +227,13 @@ class DiffusionExecutor {
   uint32_t din_mask_ = 0;      // directions with another rank (flags to wait on)
   FlagTargets dout_{};         // the neighbours' words counting our passes
   uint64_t direct_pass_ = 0;   // passes done in direct mode
+  bool dhost_ = false;         // host waits for the counts (set_direct host_wait)
+  void direct_wait(uint64_t want, void* stream);
   bool direct_active() const { return direct_on_ && !solo_; }
   bool direct_remote() const { return direct_active() && din_mask_ != 0; }
   DirectStores direct_stores(bool out_is_T2) const;
+  bool images_in_frame(const PassGeom& g) const;
+  DirectStores dstores_[2];  // [out is T2]
   void ensure_error_word();
   void* graph_exec_ = nullptr;  // hipGraphExec_t
   int64_t graph_len_ = 0;

@@ -139,4 +139,35 @@ class IpcTransport : public P2PTransport {
 
 std::string ipc_shm_name(const std::string& token, int rank);
 
+// Device memory of other processes of this node, mapped into this one
+// (direct-store halos, DiffusionExecutor::set_direct: a neighbour's T / T2
+// and its pass-count words, so this rank's kernels store straight into them
+// -- on-device when the ranks share a GPU, over xGMI between GPUs).
+// export_ptr(p): the IPC handle of p's allocation (hipMemGetAddressRange:
+// torch's caching allocator hands out pieces of larger hipMalloc segments)
+// plus p's offset in it and the creating process id; open(blob): p in this
+// process. A handle is opened once however many pointers into its
+// allocation are asked for (a peer that is two of my neighbours); the
+// destructor closes every mapping, so it must outlive every kernel that
+// stores through them.
+class IpcMap {
+ public:
+  IpcMap() = default;
+  ~IpcMap();
+  IpcMap(const IpcMap&) = delete;
+  IpcMap& operator=(const IpcMap&) = delete;
+  static std::string export_ptr(const void* p);
+  void* open(const std::string& blob);
+  size_t mappings() const { return maps_.size(); }
+  void close_all() noexcept;
+
+ private:
+  struct Mapping {
+    std::string key;  // exporter pid : allocation base
+    void* base;
+    size_t bytes;
+  };
+  std::vector<Mapping> maps_;
+};
+
 }  // namespace rma

@@ -38,7 +38,8 @@ constexpr int kMaxRects = 8;
 // syr = ny - oly rows away. Eight fixed ranges rather than a list of rects:
 // the kernel decides per task (which ranges its window and rows touch) and per
 // row with a few scalar compares; a list walked per row costs a scalar load
-// chain per entry and doubled the K = 24 pass at 8192^2.
+// chain per entry and doubled the K = 24 pass at 8192^2. Passed by value (a
+// kernel argument).
 struct DirectStores {
   int on = 0;  // any dst set
   int32_t xm0 = 0, xm1 = 0, xp0 = 0, xp1 = 0;
@@ -121,6 +122,10 @@ int pipe_default_cols(int K, int stages, int arith);
 // aligned accesses), else 4 / 2 with 16-B aligned arrays and nx % 4 / % 2,
 // else 1. The executor's frame geometry uses the same answer.
 int pipe_vec(int K, int stages, int arith, int64_t nx, int requested, bool aligned16);
+// Blocks per CU of the core pipelined kernel (occ[0]) and of its direct-store
+// variant (occ[1]; 0 when it has none) for (K, stages, arith, V): the
+// executor prices direct-store passes with it (DiffusionExecutor::set_direct).
+void stencil_pipe_occupancy(int K, int stages, int arith, int V, int occ[2]);
 // arith: 0 fast5, 1 canonical, 2 fast5 with ds_bpermute lane moves (kernel 11)
 void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const double* T,
                             const double* iCp, int64_t nx, int64_t ny, const Rect* rects,

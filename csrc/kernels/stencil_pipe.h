@@ -35,6 +35,7 @@
 
 #include "pipe_arith.h"
 #include "rma/common.h"
+#include "rma/hip_check.h"
 #include "rma/kernels.h"
 #include "stencil_device.h"
 
@@ -224,37 +225,34 @@ __device__ __forceinline__ double from_prev_lane(double v) {
 // Direct-store halos of one stored row (DirectStores, kernels.h): the row's
 // images in the neighbours in directions d = (i, j) (executor.h kDirI /
 // kDirJ order) whose ranges hold it. dxm / dxp: the wave stores columns in the
-// i = -1 / +1 ranges (uniform, per task).
+// i = -1 / +1 ranges (uniform, per task). The lane masks are recomputed per
+// row rather than held in registers across the row loop.
 template <int V>
-__device__ __forceinline__ void direct_row(const DirectStores& D, int row, int64_t nx, int64_t x,
-                                           const double (&res)[V], const bool (&m)[V], bool dxm,
-                                           bool dxp) {
+__device__ __forceinline__ void direct_row(const DirectStores& D, int row, int64_t nx, int x32,
+                                           int64_t e, const double (&res)[V],
+                                           const bool (&m)[V], bool dxm, bool dxp) {
+  // e: element index of the lane's first cell, x32 its column
   const bool ym = row >= D.ym0 && row < D.ym1, yp = row >= D.yp0 && row < D.yp1;
-  const int64_t e = (int64_t)row * nx + x, sx = D.sx, sy = D.syr * nx;
+  const int64_t sx = D.sx, sy = D.syr * nx;
   auto put = [&](int d, int64_t off, const bool (&mk)[V]) {
     if (D.dst[d]) store_row<V, true>(D.dst[d] + (e + off), res, mk);
   };
   if (ym) put(1, sy, m);   // (0, -1)
   if (yp) put(6, -sy, m);  // (0, +1)
-  if (dxm) {
+  // the x-image columns, with their diagonal images in the y-image rows
+  auto xside = [&](int dx, int dd0, int dd1, int64_t ox, int32_t a0, int32_t a1) {
     bool mk[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) mk[v] = m[v] && x + v >= D.xm0 && x + v < D.xm1;
-    put(3, sx, mk);                  // (-1, 0)
-    if (ym) put(0, sx + sy, mk);     // (-1, -1)
-    if (yp) put(5, sx - sy, mk);     // (-1, +1)
-  }
-  if (dxp) {
-    bool mk[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) mk[v] = m[v] && x + v >= D.xp0 && x + v < D.xp1;
-    put(4, -sx, mk);                 // (+1, 0)
-    if (ym) put(2, -sx + sy, mk);    // (+1, -1)
-    if (yp) put(7, -sx - sy, mk);    // (+1, +1)
-  }
+    for (int v = 0; v < V; ++v) mk[v] = m[v] && x32 + v >= a0 && x32 + v < a1;
+    put(dx, ox, mk);
+    if (ym) put(dd0, ox + sy, mk);
+    if (yp) put(dd1, ox - sy, mk);
+  };
+  if (dxm) xside(3, 0, 5, sx, D.xm0, D.xm1);    // (-1, 0), (-1, -1), (-1, +1)
+  if (dxp) xside(4, 2, 7, -sx, D.xp0, D.xp1);   // (+1, 0), (+1, -1), (+1, +1)
 }
 
-template <int K, int S, int V, int Ar, int C>
+template <int K, int S, int V, int Ar, int C, bool Dir>
 __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double* __restrict__ T,
                                           const double* __restrict__ iCp, int64_t nx, int64_t ny,
                                           const RectList& L, const StencilCoef& k, int chunk_rows,
@@ -334,7 +332,7 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   // direct-store halos (DirectStores): does this wave store into the x-image
   // ranges (a lane with a stored column there), do its rows meet the y ones
   bool dxm = false, dxp = false, dtask = false;
-  if (DS.on) {
+  if constexpr (Dir) {
     bool pm = false, pp = false;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
@@ -773,7 +771,10 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
         // direct-store halos: the same values into the neighbours' halos;
         // only tasks whose window or rows touch a halo image range (dtask,
         // uniform) test the row
-        if (dtask) direct_row<V>(DS, row, nx, x, res, m, dxm, dxp);
+        if constexpr (Dir) {
+          if (dtask)
+            direct_row<V>(DS, row, nx, (int)xso, (int64_t)row * nx + x, res, m, dxm, dxp);
+        }
       }
     }
     };
@@ -847,7 +848,12 @@ __device__ __forceinline__ void pipe_body(double* __restrict__ T2, const double*
   if (b < sig_first) signal_block_done(L.sig, L.sig_blocks);  // block-uniform
 }
 
-template <int K, int S, int V, int Ar, int C>
+// Dir: the direct-store halo variant (DirectStores). A separate instantiation:
+// the direct-store code costs the row loop registers and scheduling (~4 % per
+// task measured when every task of a pass ran it, K = 20 then at one wave
+// per SIMD), so the plain kernels carry none of it and the executor gives the
+// Dir variant the frame launches only, which hold every image cell.
+template <int K, int S, int V, int Ar, int C, bool Dir = false>
 __global__ __launch_bounds__(kWave * S * C) __attribute__((amdgpu_waves_per_eu(
     kernel_waves<K, S, V, Ar, C>()))) void pipe_kernel(double* __restrict__ T2,
                                                       const double* __restrict__ T,
@@ -855,7 +861,14 @@ __global__ __launch_bounds__(kWave * S * C) __attribute__((amdgpu_waves_per_eu(
                                                       int64_t nx, int64_t ny, RectList L,
                                                       StencilCoef k, int chunk_rows,
                                                       int remap, DirectStores D) {
-  pipe_body<K, S, V, Ar, C>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap, D);
+  pipe_body<K, S, V, Ar, C, Dir>(T2, T, iCp, nx, ny, L, k, chunk_rows, remap, D);
+}
+
+// direct-store variants exist for the production fast-math arithmetics
+// (kArFast5 at every K, the register-factor kArFast5Reg) at one column wave
+template <int V, int Ar, int C>
+constexpr bool has_direct() {
+  return C == 1 && V != 5 && (Ar == kArFast5 || Ar == kArFast5Reg);
 }
 
 struct PipeLaunch {
@@ -872,12 +885,24 @@ struct PipeLaunch {
   int sig_rects = 0;
   int sig_chunk_rows = 0;   // ...with this many rows per task (0: chunk_rows)
   const DirectStores* direct = nullptr;  // direct-store halos (nullptr: none)
+  int* occupancy = nullptr;  // non-null: launch nothing, store the blocks per CU of the
+                             // plain kernel [0] and of its direct-store variant [1] (0: none)
 };
 
 // Plans the (strip, chunk) tasks with this instantiation's block width
 // (Geo::WB, kStep), so host planning and kernel geometry cannot disagree.
 template <int K, int S, int V, int Ar, int C = 1>
 void launch(const PipeLaunch& a) {
+  if (a.occupancy) {
+    const int bs = kWave * S * C;
+    a.occupancy[0] = a.occupancy[1] = 0;
+    RMA_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &a.occupancy[0], pipe_kernel<K, S, V, Ar, C, false>, bs, 0));
+    if constexpr (has_direct<V, Ar, C>())
+      RMA_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &a.occupancy[1], pipe_kernel<K, S, V, Ar, C, true>, bs, 0));
+    return;
+  }
   int rows_buf[kMaxRects] = {};
   const int* rows = nullptr;
   if (a.sig && a.sig_chunk_rows > 0) {
@@ -897,10 +922,19 @@ void launch(const PipeLaunch& a) {
     L.sig = a.sig;
     L.sig_blocks = L.block_end[ns - 1];
   }
-  DirectStores D{};
-  if (a.direct) D = *a.direct;
-  pipe_kernel<K, S, V, Ar, C><<<dim3((unsigned)blocks), dim3(kWave * S * C), 0, a.stream>>>(
-      a.T2, a.T, a.iCp, a.nx, a.ny, L, a.k, a.chunk_rows, a.remap, D);
+  const dim3 grid((unsigned)blocks), block(kWave * S * C);
+  if (a.direct && a.direct->on) {
+    if constexpr (has_direct<V, Ar, C>()) {
+      pipe_kernel<K, S, V, Ar, C, true><<<grid, block, 0, a.stream>>>(
+          a.T2, a.T, a.iCp, a.nx, a.ny, L, a.k, a.chunk_rows, a.remap, *a.direct);
+    } else {
+      RMA_CHECK_ARG(false, "no direct-store variant of the pipelined kernel K=" << K << " S=" << S
+                                << " V=" << V << " arithmetic " << Ar << " columns " << C);
+    }
+    return;
+  }
+  pipe_kernel<K, S, V, Ar, C><<<grid, block, 0, a.stream>>>(a.T2, a.T, a.iCp, a.nx, a.ny, L, a.k,
+                                                           a.chunk_rows, a.remap, DirectStores{});
 }
 
 // Each stencil_pipe_{a,b,c}.hip unit instantiates a range of (K, S) of the

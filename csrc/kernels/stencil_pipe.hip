@@ -16,6 +16,19 @@ namespace rma {
 // pipe_default_stages, pipe_has, pipe_has_cols, pipe_default_cols, pipe_vec:
 // kernel_select.cpp (host code, shared with the sanitizer builds)
 
+void stencil_pipe_occupancy(int K, int stages, int arith, int V, int occ[2]) {
+  const int S = stages > 0 ? stages : pipe_default_stages(K);
+  RMA_CHECK_ARG(pipe_has(K, S, arith), "no pipelined kernel for K=" << K << " S=" << S
+                                                                   << " arithmetic " << arith);
+  pipe::PipeLaunch a{nullptr, nullptr, nullptr, 0, 0, nullptr, 0, StencilCoef{}, 1, 0, nullptr};
+  a.occupancy = occ;
+  const bool ok = V != 5 && (pipe::dispatch_r(K, S, V, arith, a) || pipe::dispatch_a(K, S, V, arith, a) ||
+                             pipe::dispatch_b(K, S, V, arith, a) || pipe::dispatch_c(K, S, V, arith, a));
+  RMA_CHECK_ARG(ok, "occupancy query: pipelined kernel K=" << K << " S=" << S << " V=" << V
+                                                           << " arithmetic " << arith
+                                                           << " not in the core library");
+}
+
 void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const double* T,
                             const double* iCp, int64_t nx, int64_t ny, const Rect* rects,
                             int nrects, const StencilCoef& c, const StencilTuning& tune,

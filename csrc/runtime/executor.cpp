@@ -4,11 +4,14 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <limits>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 
 #include "rma/config.h"
@@ -458,6 +461,9 @@ void DiffusionExecutor::multi_step(int K, double* Tin, double* Tout, const doubl
 
 bool DiffusionExecutor::fused_pass_ok(const PassGeom& g, const StencilTuning& tn) const {
   if (!sig_ || !g.aligned || tn.kernel < 9 || g.interior.empty()) return false;
+  // direct-store halos: split passes, the interior on the plain kernel (one
+  // fused launch would run every task in the direct-store variant, ~4 % slower)
+  if (direct_active()) return false;
   int nf = 0;
   for (const Rect& r : g.frame) nf += r.empty() ? 0 : 1;
   if (nf == 0 || (int)g.frame.size() + 1 > kMaxRects) return false;
@@ -482,11 +488,6 @@ void DiffusionExecutor::enqueue_fused(const std::vector<Rect>& frame, const Rect
   // the whole launch waits for the previous exchange (its frame tasks read the
   // halo) and, in stream order, for the previous launch
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
-  // direct-store halos: every neighbour's frame of the previous pass is done
-  // (our halo complete, its field free for our stores)
-  const bool dr = direct_remote();
-  if (dr)
-    flags_wait_ge_gpu(din_flags_, din_mask_, direct_pass_, fused_timeout_s_, ferr_dev_, 2, s_lo_);
   Rect rs[kMaxRects];
   int n = 0;
   for (const Rect& r : frame) rs[n++] = r;
@@ -508,10 +509,7 @@ void DiffusionExecutor::enqueue_fused(const std::vector<Rect>& frame, const Rect
   rec(1, s_hi_);
   {
     TraceRange th("rma.halo");
-    if (dr)  // the halos are stored: raise our pass count at the neighbours
-      flags_write_gpu(dout_, direct_pass_ + 1, s_hi_);
-    else
-      exchange(Tout, s_hi_);
+    exchange(Tout, s_hi_);
   }
   rec(2, s_hi_);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
@@ -540,7 +538,32 @@ void DiffusionExecutor::ensure_error_word() {
   RMA_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ferr_dev_), ferr_host_, 0));
 }
 
-void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint64_t* in_flags) {
+void DiffusionExecutor::direct_wait(uint64_t want, void* stream) {
+  if (!dhost_) {
+    flags_wait_ge_gpu(din_flags_, din_mask_, want, fused_timeout_s_, ferr_dev_, 2, stream);
+    return;
+  }
+  // ranks of one process (host_wait): the host waits before enqueueing. A
+  // spinning wait kernel per rank would share the process's few hardware
+  // queues with the neighbours' passes it waits for (8 rank streams over
+  // GPU_MAX_HW_QUEUES = 4) and could block them behind itself.
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int d = 0; d < 8; ++d) {
+    if (!((din_mask_ >> d) & 1u)) continue;
+    while (__atomic_load_n(din_flags_ + d, __ATOMIC_ACQUIRE) < want) {
+      const double dt =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      RMA_CHECK_ARG(dt < fused_timeout_s_,
+                    "direct-store halos: the host wait for the pass count of direction "
+                        << d << " timed out after " << fused_timeout_s_
+                        << " s (RMA_EXEC_FUSED_TIMEOUT; a neighbour died or runs another plan)");
+      std::this_thread::yield();
+    }
+  }
+}
+
+void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint64_t* in_flags,
+                                   bool host_wait) {
   RMA_HIP_CHECK(hipStreamSynchronize(S(s_hi_)));
   RMA_HIP_CHECK(hipStreamSynchronize(S(s_lo_)));
   bool any = false;
@@ -572,6 +595,8 @@ void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint6
     RMA_CHECK_ARG(p.flag, "direct-store peer (" << i << "," << j << "): null pass-count word");
     mask |= 1u << d;
     out.dst[d] = p.flag;
+    if (host_wait)  // the peer's words are pinned host memory: their device address
+      RMA_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&out.dst[d]), p.flag, 0));
   }
   if (any) {
     RMA_CHECK_ARG(nx_ < (int64_t(1) << 30) && ny_ < (int64_t(1) << 30),
@@ -583,7 +608,34 @@ void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint6
     ensure_error_word();
   }
   dpeer_ = peers;
+  // price the depths for the planner: a depth whose direct-store kernel holds
+  // fewer blocks per CU than the plain one (the register cap, stencil_pipe.h
+  // pipe_kernel_dir) costs that much more per pass
+  if (cost_base_.empty()) cost_base_ = cost_;
+  cost_ = cost_base_;
+  if (any) {
+    const bool al = ((reinterpret_cast<uintptr_t>(T_) | reinterpret_cast<uintptr_t>(T2_) |
+                      reinterpret_cast<uintptr_t>(iCp_)) & 15) == 0;
+    for (int K = 2; K < (int)cost_.size(); ++K) {
+      if (!std::isfinite(cost_[K])) continue;
+      const StencilTuning t = pass_tuning(K, 0);
+      if (t.kernel < 9) continue;
+      const int arith = t.kernel - 9;
+      const int S = t.stages > 0 ? t.stages : pipe_default_stages(K);
+      int occ[2] = {0, 0};
+      stencil_pipe_occupancy(K, S, arith, pipe_vec(K, S, arith, nx_, t.vec, al), occ);
+      if (occ[1] <= 0)
+        cost_[K] = std::numeric_limits<double>::infinity();
+      else if (occ[1] < occ[0])
+        cost_[K] *= (double)occ[0] / occ[1];
+    }
+  }
+  if (any) {  // the descriptors of both buffer parities
+    dstores_[0] = direct_stores(false);
+    dstores_[1] = direct_stores(true);
+  }
   din_flags_ = in_flags;
+  dhost_ = host_wait;
   din_mask_ = any ? mask : 0;
   dout_ = any ? out : FlagTargets{};
   direct_on_ = any;
@@ -593,6 +645,42 @@ void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint6
     (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec_));
     graph_exec_ = nullptr;
   }
+}
+
+bool DiffusionExecutor::images_in_frame(const PassGeom& g) const {
+  // the image strips (clamped to the pass's output) minus the frame rects
+  // (disjoint) must be empty: compare areas
+  const DirectStores& D = dstores_[0];
+  const Rect& o = g.out;
+  auto clip = [&](Rect r) {
+    r.x0 = std::max(r.x0, o.x0), r.x1 = std::min(r.x1, o.x1);
+    r.y0 = std::max(r.y0, o.y0), r.y1 = std::min(r.y1, o.y1);
+    return r;
+  };
+  auto area = [](const Rect& r) { return r.empty() ? 0 : (r.x1 - r.x0) * (r.y1 - r.y0); };
+  bool side[4] = {false, false, false, false};  // any peer at i = -1, +1, j = -1, +1
+  for (int d = 0; d < 8; ++d) {
+    if (!dstores_[0].dst[d]) continue;
+    if (kDirI[d] < 0) side[0] = true;
+    if (kDirI[d] > 0) side[1] = true;
+    if (kDirJ[d] < 0) side[2] = true;
+    if (kDirJ[d] > 0) side[3] = true;
+  }
+  const Rect strips[4] = {{D.xm0, D.xm1, o.y0, o.y1}, {D.xp0, D.xp1, o.y0, o.y1},
+                          {o.x0, o.x1, D.ym0, D.ym1}, {o.x0, o.x1, D.yp0, D.yp1}};
+  for (int k = 0; k < 4; ++k) {
+    if (!side[k]) continue;
+    const Rect st = clip(strips[k]);
+    int64_t in = 0;
+    for (const Rect& f : g.frame) {
+      Rect c = st;
+      c.x0 = std::max(c.x0, f.x0), c.x1 = std::min(c.x1, f.x1);
+      c.y0 = std::max(c.y0, f.y0), c.y1 = std::min(c.y1, f.y1);
+      in += area(c);
+    }
+    if (in != area(st)) return false;
+  }
+  return true;
 }
 
 DirectStores DiffusionExecutor::direct_stores(bool out_is_T2) const {
@@ -622,11 +710,11 @@ DirectStores DiffusionExecutor::direct_stores(bool out_is_T2) const {
 
 void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   const PassGeom& g = geometry(K);
-  // direct-store halos: every launch of the pass carries the stores (only the
-  // frame tasks' rows and columns hold any) instead of an exchange after it
+  // direct-store halos: the launches that hold image cells (the one launch of
+  // perf and of a one-wave tile, the frame launches of a split pass) run the
+  // kernels' direct-store variant instead of an exchange after the pass; a
+  // split pass's interior launch stays the plain kernel
   const bool da = direct_active(), dr = direct_remote();
-  DirectStores ds;
-  if (da) ds = direct_stores(Tout == T2_);
   struct DirectCount {  // counted however the pass is enqueued
     uint64_t& n;
     bool on;
@@ -635,10 +723,15 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     }
   } dcount{direct_pass_, da};
   StencilTuning tn = pass_tuning(K, 0);
-  if (da) tn.direct = &ds;
+  auto with_direct = [&](StencilTuning t) {
+    if (da) t.direct = &dstores_[Tout == T2_ ? 1 : 0];
+    return t;
+  };
+  // every image cell lies in the frame rects (else the interior carries the
+  // stores as well: correct, slower)
+  const StencilTuning tin = da && !images_in_frame(g) ? with_direct(tn) : tn;
   auto dwait = [&](void* stream) {
-    if (dr) flags_wait_ge_gpu(din_flags_, din_mask_, direct_pass_, fused_timeout_s_, ferr_dev_, 2,
-                              stream);
+    if (dr) direct_wait(direct_pass_, stream);
   };
   auto dpost = [&](void* stream) {
     if (dr) flags_write_gpu(dout_, direct_pass_ + 1, stream);
@@ -657,7 +750,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     rec(0, s_lo_);
     rec(3, s_lo_);
     dwait(s_lo_);
-    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, tn, s_lo_);
+    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, with_direct(tn), s_lo_);
     rec(4, s_lo_);
     rec(1, s_lo_);
     if (da)
@@ -668,16 +761,21 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     if (ev[4]) tseq_.push_back(1);
     return;
   }
-  if (da && !dr) {
-    // direct stores to this rank's own periodic images only: ONE launch over
-    // the owned rect, stream-ordered before the next pass (nothing to signal)
-    TraceRange tr("rma.pass.direct_self");
+  if (da && (g.frame.empty() || g.tasks() <= 2 * (int64_t)cus_)) {
+    // direct stores, tiles of one wave of tasks: ONE launch of the direct-store
+    // kernel over the owned rect (every task starts at once, so a frame launch
+    // beside the interior's would end with the pass anyway and only add its
+    // latency: 2048^2 periodic x+y at K=24 +3-5 % vs +39-61 % split), after the
+    // neighbours' counts of the previous pass, our count raised after it
+    TraceRange tr("rma.pass.direct");
     RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
     rec(0, s_lo_);
     rec(3, s_lo_);
-    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, tn, s_lo_);
+    dwait(s_lo_);
+    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, with_direct(tn), s_lo_);
     rec(4, s_lo_);
     rec(1, s_lo_);
+    dpost(s_lo_);
     rec(2, s_lo_);
     RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
     if (ev[4]) tseq_.push_back(1);
@@ -728,7 +826,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     rec(3, s_lo_);
     if (!g.interior.empty()) {
       TraceRange ti("rma.interior");
-      multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.interior, 1, tn, s_lo_);
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.interior, 1, tin, s_lo_);
     }
     rec(4, s_lo_);
     RMA_HIP_CHECK(hipEventRecord(E(e_lo_), S(s_lo_)));
@@ -745,13 +843,12 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
       // all long ones on the last XCD, which then finishes its share of the
       // interior one task-wave late (+3 ms per K=24 pass at the 288 GB tile
       // with x and y neighbours; profiles/SUMMARY_r3.md)
-      StencilTuning ft = tn;
+      StencilTuning ft = with_direct(tn);
       ft.xcd_remap = 0;
       ft.chunk_rows = frame_chunk_rows(K, tn.chunk_rows);
       multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame.data(), (int)g.frame.size(), ft, s_hi_);
     } else {
-      StencilTuning tw = pass_tuning(K, 1), tt = pass_tuning(K, 2);
-      if (da) tw.direct = tt.direct = &ds;
+      const StencilTuning tw = with_direct(pass_tuning(K, 1)), tt = with_direct(pass_tuning(K, 2));
       if (!g.frame_wide.empty())
         multi_step(K, Tin, Tout, iCp_, nx_, ny_, g.frame_wide.data(), (int)g.frame_wide.size(),
                    tw, s_hi_);
@@ -1014,8 +1111,7 @@ void DiffusionExecutor::run(int64_t nsteps, stream_t caller_stream) {
   // neighbour's frame of the last pass has stored into our halo (the caller
   // reads it: gather, checks, the next update_halo_; and a neighbour must not
   // store into a field its owner already released)
-  if (direct_remote())
-    flags_wait_ge_gpu(din_flags_, din_mask_, direct_pass_, fused_timeout_s_, ferr_dev_, 2, hi);
+  if (direct_remote()) direct_wait(direct_pass_, hi);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), hi));
   RMA_HIP_CHECK(hipEventRecord(E(e_lo_), lo));
   RMA_HIP_CHECK(hipStreamWaitEvent(caller, E(e_hi_), 0));

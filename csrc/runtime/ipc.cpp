@@ -399,4 +399,52 @@ void IpcTransport::enqueue_group() {
   }
 }
 
+namespace {
+struct IpcExport {
+  hipIpcMemHandle_t h;
+  uint64_t offset, bytes, pid, base, magic;  // base: the allocation in the exporter
+};
+constexpr uint64_t kIpcExportMagic = 0x524d41495043ULL;  // "RMAIPC"
+}  // namespace
+
+std::string IpcMap::export_ptr(const void* p) {
+  RMA_CHECK_ARG(p != nullptr, "IPC export of a null pointer");
+  void* base = nullptr;
+  size_t bytes = 0;
+  RMA_HIP_CHECK(hipMemGetAddressRange(&base, &bytes, const_cast<void*>(p)));
+  IpcExport e{};
+  RMA_HIP_CHECK(hipIpcGetMemHandle(&e.h, base));
+  e.offset = (uint64_t)((const char*)p - (const char*)base);
+  e.bytes = bytes;
+  e.pid = (uint64_t)getpid();
+  e.base = (uint64_t)(uintptr_t)base;
+  e.magic = kIpcExportMagic;
+  return std::string(reinterpret_cast<const char*>(&e), sizeof e);
+}
+
+void* IpcMap::open(const std::string& blob) {
+  IpcExport e{};
+  RMA_CHECK_ARG(blob.size() == sizeof e, "IPC pointer export of " << blob.size() << " bytes");
+  std::memcpy(&e, blob.data(), sizeof e);
+  RMA_CHECK_ARG(e.magic == kIpcExportMagic && e.offset < e.bytes, "not an IpcMap export");
+  RMA_CHECK_ARG(e.pid != (uint64_t)getpid(),
+                "IPC pointer export of this process: use the pointer itself");
+  // one mapping per exporter allocation (two exports of one allocation need
+  // not carry identical handle bytes)
+  const std::string key = std::to_string(e.pid) + ":" + std::to_string(e.base);
+  for (const Mapping& m : maps_)
+    if (m.key == key) return static_cast<char*>(m.base) + e.offset;
+  void* base = nullptr;
+  RMA_HIP_CHECK(hipIpcOpenMemHandle(&base, e.h, hipIpcMemLazyEnablePeerAccess));
+  maps_.push_back({key, base, (size_t)e.bytes});
+  return static_cast<char*>(base) + e.offset;
+}
+
+void IpcMap::close_all() noexcept {
+  for (const Mapping& m : maps_) (void)hipIpcCloseMemHandle(m.base);
+  maps_.clear();
+}
+
+IpcMap::~IpcMap() { close_all(); }
+
 }  // namespace rma

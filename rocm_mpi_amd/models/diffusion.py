@@ -25,10 +25,12 @@ loopback transports) the same steps are issued from Python.
 """
 from __future__ import annotations
 
+import socket
 from dataclasses import dataclass
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from .. import ops
 from .._native import native
@@ -306,8 +308,11 @@ class Diffusion2D:
 
     def _setup_direct(self) -> None:
         """Collective: hand the executor its direct-store peers (cfg.halo_direct).
-        Every rank's fields and pass-count words are exchanged (in-process:
-        the loopback hub), the counts zeroed while every rank is quiescent."""
+        Every rank's fields and pass-count words are exchanged -- in-process
+        through the loopback hub; between processes of one node as IPC
+        exports (``IpcMap``: the peers' T / T2 / count words mapped into this
+        process) gathered over the gloo group -- and the counts zeroed while
+        every rank is quiescent."""
         if not self.cfg.halo_direct or self.executor is None:
             return
         g, cfg = self.g, self.cfg
@@ -315,18 +320,27 @@ class Diffusion2D:
             raise ValueError("halo_direct needs fast-math perf / perf_hide passes")
         ranks = self._direct_ranks()
         remote = any(r >= 0 and r != g.me for r in ranks)
-        if remote and g.transport != "loopback":
+        procs = remote and g.transport != "loopback"
+        if procs and not (dist.is_available() and dist.is_initialized()):
             raise ValueError(f"halo_direct with other ranks needs their fields mapped in this "
-                             f"process (loopback transport), not {g.transport!r}")
-        if not hasattr(self, "_dflags"):
-            self._dflags = torch.zeros(8, dtype=torch.int64, device=self.T.device)
+                             f"process (loopback) or IPC between processes, not {g.transport!r}")
+        # the words the neighbours count our passes in: device memory between
+        # processes (wait kernels); pinned host memory for ranks of this
+        # process, whose host threads wait (DiffusionExecutor::direct_wait)
+        host_wait = remote and not procs
+        if getattr(self, "_dflags", None) is None or self._dflags.is_cuda == host_wait:
+            self._dflags = (torch.zeros(8, dtype=torch.int64, pin_memory=True) if host_wait
+                            else torch.zeros(8, dtype=torch.int64, device=self.T.device))
         mine = (self.T.data_ptr(), self.T2.data_ptr(), self._dflags.data_ptr())
         torch.cuda.synchronize(self.T.device)
         if remote:
             g.comm.barrier()  # every rank's previous executor drained
         self._dflags.zero_()
         torch.cuda.synchronize(self.T.device)
-        table = g.comm.hub.collect(g.me, mine) if remote else {g.me: mine}
+        if procs:
+            table = self._direct_ipc_table(ranks, mine)
+        else:
+            table = g.comm.hub.collect(g.me, mine) if remote else {g.me: mine}
         peers = []
         for d, r in enumerate(ranks):
             if r < 0:
@@ -335,9 +349,33 @@ class Diffusion2D:
             T, T2, fl = table[r]
             # the peer's count of OUR passes: from its side we are direction 7 - d
             peers.append((r, T, T2, 0 if r == g.me else fl + 8 * (7 - d)))
-        self.executor.set_direct(peers, self._dflags.data_ptr() if remote else 0)
+        self.executor.set_direct(peers, self._dflags.data_ptr() if remote else 0, host_wait)
         if remote:
             g.comm.barrier()  # nobody stores before every rank has zeroed its counts
+
+    def _direct_ipc_table(self, ranks: list, mine: tuple) -> dict:
+        """IPC exports of every rank's (T, T2, count words), gathered over the
+        gloo group; the direct-store peers' opened in this process. Every peer
+        must be a process of this node (its handle opens here)."""
+        from ..parallel.comm import _gloo_group
+
+        n = native()
+        host = socket.gethostname()
+        exp = (host, tuple(n.IpcMap.export_ptr(p) for p in mine))
+        allx: list = [None] * dist.get_world_size()
+        dist.all_gather_object(allx, exp, group=_gloo_group())
+        me = self.g.me
+        others = sorted({r for r in ranks if r >= 0 and r != me})
+        far = [r for r in others if allx[r][0] != host]
+        if far:
+            raise ValueError(f"halo_direct: ranks {far} run on other nodes ({allx[far[0]][0]}); "
+                             f"IPC maps device memory of this node only")
+        if getattr(self, "_ipc_map", None) is None:
+            self._ipc_map = n.IpcMap()
+        table = {me: mine}
+        for r in others:
+            table[r] = tuple(self._ipc_map.open(b) for b in allx[r][1])
+        return table
 
     def set_temporal(self, K: int, fast_math: bool | None = None) -> None:
         """Switch the steps per kernel pass (e.g. to time the one-step kernel on
@@ -703,6 +741,14 @@ class Diffusion2D:
             self.synchronize()  # raises a pending executor error; resources go either way
         finally:
             self.executor = None
+            if getattr(self, "_ipc_map", None) is not None:
+                # every rank's kernels are done storing into the mapped peers
+                # (its synchronize above) before any rank unmaps or frees
+                try:
+                    self.g.comm.barrier()
+                finally:
+                    self._ipc_map.close_all()
+                    self._ipc_map = None
             self._ap_graph = None
             if self._owns_grid:
                 gg.finalize_global_grid()

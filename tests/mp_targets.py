@@ -268,3 +268,32 @@ def fuzz_tile(rank, world, outdir, seed):
         f.write(f"{g.coords[0]} {g.coords[1]} {g.nxyz_g[0]} {g.nxyz_g[1]} {g.transport}")
     m.close()
     gg.finalize_global_grid()
+
+
+def direct_tiles(rank, world, outdir, nx, ny, nt, dims, periods, K, direct):
+    """Processes sharing cuda:0 (RMA_TRANSPORT decides the exchange when
+    direct is off): perf_hide fast-math K-step passes; with direct on the
+    kernels store the neighbours' halos into their IPC-mapped fields
+    (DiffusionExecutor::set_direct). Saves the tile, coords and the direct
+    counters."""
+    from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
+    from rocm_mpi_amd.parallel import implicit_grid as gg
+
+    gg.init_global_grid(nx, ny, 1, dimx=dims[0], dimy=dims[1], periodx=periods[0],
+                        periody=periods[1], overlaps=(2 * K, 2 * K, 2), halowidths=(K, K, 1),
+                        quiet=True, device="cuda:0")
+    g = gg.global_grid()
+    m = Diffusion2D(DiffusionConfig(variant="perf_hide", nx=nx, ny=ny, nt=nt, init="random",
+                                    quiet=True, dims=(*dims, 0), periods=(*periods, 0),
+                                    temporal=K, fast_math=True, device="cuda:0",
+                                    halo_direct=bool(direct)))
+    m.step(nt)
+    m.synchronize()
+    ex = m.executor
+    maps = m._ipc_map.mappings if getattr(m, "_ipc_map", None) is not None else 0
+    info = f"{int(ex.direct)} {ex.direct_passes} {ex.passes_done} {maps}"
+    np.save(os.path.join(outdir, f"tile{g.me}.npy"), m.field.cpu().numpy())
+    with open(os.path.join(outdir, f"meta{g.me}.txt"), "w") as f:
+        f.write(f"{g.coords[0]} {g.coords[1]} {g.transport} {info}")
+    m.close()
+    gg.finalize_global_grid()

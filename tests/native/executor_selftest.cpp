@@ -145,6 +145,12 @@ void stencilk_rects_gpu(int K, double* T2, const double* T, const double* iCp, i
     ++g_signals;
   }
 }
+// the direct-store kernel variants' occupancy (set_direct's planner pricing):
+// depth 20 at half the plain kernel's, as the register-capped GPU build
+void stencil_pipe_occupancy(int K, int, int, int, int occ[2]) {
+  occ[0] = 2;
+  occ[1] = K == 20 ? 1 : 2;
+}
 void flux_gpu(double* QX, double* QY, const double* T, int64_t nx, int64_t ny, double mlam,
               double rdx, double rdy, stream_t) {
   flux_cpu(QX, QY, T, nx, ny, mlam, rdx, rdy);
@@ -207,6 +213,7 @@ struct Case {
   const char* fused;  // RMA_EXEC_FUSED for the multi-rank run ("" = auto)
   int chunk = 0;      // K-step rows per task (ExecParams::chunk_rows2; 0: the table)
   bool direct = false;  // direct-store halos between the rank threads (set_direct)
+  bool host_wait = false;  // ...with host-side count waits (the loopback mode)
 };
 
 struct TileResult {
@@ -278,7 +285,7 @@ std::vector<TileResult> run_ranks(const Case& c, std::array<int, 3> dims, int64_
               // the peer counts our passes in its word of direction 7 - d
               peers[d].flag = q == r ? nullptr : &counts[(size_t)q][(size_t)(7 - d)];
             }
-            ex.set_direct(peers, counts[(size_t)r].data());
+            ex.set_direct(peers, counts[(size_t)r].data(), c.host_wait);
           }
           ex.run(c.nt, nullptr);
           (void)hipDeviceSynchronize();
@@ -366,6 +373,13 @@ int main() {
        0, true},
       {"direct perf_hide K=6 1x1 periodic self", {1, 1, 1}, {1, 1, 0}, 90, 70, 6, Mode::kHide, 25,
        "", 0, true},
+      // the same with the host waiting for the counts (ranks of one process)
+      {"direct host-wait perf_hide K=8 2x2 open split", {2, 2, 1}, {0, 0, 0}, 760, 400, 8,
+       Mode::kHide, 17, "0", 0, true, true},
+      {"direct host-wait perf_hide K=8 2x2 periodic fused", {2, 2, 1}, {1, 1, 0}, 760, 400, 8,
+       Mode::kHide, 19, "1", 0, true, true},
+      {"direct host-wait perf K=4 2x2 periodic-y", {2, 2, 1}, {0, 1, 0}, 64, 60, 4, Mode::kPerf,
+       13, "", 0, true, true},
   };
   for (const Case& c : cases)
     if (run_case(c)) return 1;

@@ -288,3 +288,8 @@ inline hipError_t hipIpcOpenMemHandle(void** p, hipIpcMemHandle_t h, unsigned) {
   return hipSuccess;
 }
 inline hipError_t hipIpcCloseMemHandle(void*) { return hipSuccess; }
+inline hipError_t hipMemGetAddressRange(void** base, size_t* bytes, void* p) {
+  *base = p;  // the stub does not track allocation extents: p is its own base
+  *bytes = size_t(1) << 40;
+  return hipSuccess;
+}

@@ -88,10 +88,8 @@ def spmd(rank, hub, nx, ny, nt, dims, periods, K, direct):
 ])
 def test_direct_loopback_ranks_equal_one_rank(dims, periods, K, nx, ny, nt, fused, monkeypatch):
     """Rank threads of one process (loopback) storing into each other's
-    fields: every tile == its window of the 1-rank run, bitwise, with fused
-    and split passes; every pass ran in direct mode (tiles too small for
-    aligned frames keep the split launches even with RMA_EXEC_FUSED=1, as in
-    test_multirank_gpu.py::test_fused_frame_first_passes_bitwise)."""
+    fields: every tile == its window of the 1-rank run, bitwise, with
+    one-launch and split passes; every pass ran in direct mode."""
     P = dims[0] * dims[1]
     monkeypatch.setenv("RMA_EXEC_FUSED", fused)
     res = run_loopback(P, spmd, nx, ny, nt, dims, periods, K, True, timeout=240)
@@ -107,13 +105,18 @@ def test_direct_loopback_ranks_equal_one_rank(dims, periods, K, nx, ny, nt, fuse
         assert direct and dpasses >= 2, (coords, dpasses)
         gx0, gy0 = coords[0] * (nx - ol), coords[1] * (ny - ol)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
-    if fused == "1":  # the passes with aligned frames ran fused (the geometries ask for some)
-        assert all(r[3][2] == r[3][3] > 0 for r in res), [r[3] for r in res]
+    # direct mode never fuses (one launch would run every task in the kernels'
+    # direct-store variant): one launch per pass for one-wave tiles, split
+    # passes beyond, even where RMA_EXEC_FUSED=1 and the frames align (the
+    # geometries of the "1" cases do)
+    assert all(r[3][2] == 0 for r in res), [r[3] for r in res]
+    if fused == "1":
+        assert all(r[3][3] > 0 for r in res), [r[3] for r in res]
 
 
-def test_direct_refuses_cross_process_transports_and_canonical():
-    """halo_direct needs the neighbours' fields in this process (or this
-    rank's own images) and the fast-math pipelined passes."""
+def test_direct_refuses_canonical_passes():
+    """halo_direct needs the fast-math pipelined passes (the only kernels
+    with direct-store variants)."""
     gg.init_global_grid(516, 516, 1, periodx=1, periody=1, quiet=True, overlaps=(16, 16, 2),
                         halowidths=(8, 8, 1))
     try:
@@ -123,3 +126,34 @@ def test_direct_refuses_cross_process_transports_and_canonical():
                                         halo_direct=True))
     finally:
         gg.finalize_global_grid()
+
+
+@pytest.mark.parametrize("dims,periods,K,nx,ny,nt", [
+    ((2, 2), (0, 0), 8, 260, 200, 29),
+    ((2, 2), (1, 1), 24, 1100, 1200, 53),
+    ((2, 1), (1, 0), 16, 516, 300, 35),
+])
+def test_direct_ipc_processes_equal_the_exchange(tmp_path, dims, periods, K, nx, ny, nt):
+    """Separate processes sharing cuda:0: every rank's kernels store its
+    neighbours' halos straight into their fields, mapped once through HIP IPC
+    (IpcMap: T, T2 and the pass-count words of each peer). Every tile ==
+    the same processes' run with the IPC halo exchange, bitwise; every pass ran
+    direct and each peer's allocations were opened once."""
+    from helpers import run_procs
+
+    P = dims[0] * dims[1]
+    env = {"RMA_TRANSPORT": "ipc", "RMA_IPC_MAILBOX_MB": "2"}
+    out = {}
+    for direct in (1, 0):
+        d = tmp_path / f"d{direct}"
+        d.mkdir()
+        run_procs(P, "mp_targets:direct_tiles", str(d), nx, ny, nt, dims, periods, K, direct,
+                  env=env, timeout=240)
+        out[direct] = [(open(d / f"meta{r}.txt").read().split(), np.load(d / f"tile{r}.npy"))
+                       for r in range(P)]
+    for (ma, a), (mb, b) in zip(out[1], out[0]):
+        assert ma[:3] == mb[:3] and ma[2] == "ipc"
+        on, dpasses, npass, maps = map(int, ma[3:])
+        assert on == 1 and dpasses == npass >= 2 and maps >= 1, ma
+        assert int(mb[3]) == 0
+        assert np.array_equal(a, b), ma[:2]
