@@ -64,6 +64,8 @@ struct StencilTuning {
   // one resets it and stores 1 into signal[1] with system-scope release. A
   // flag_wait_gpu(signal + 1, 1, ...) on another stream then orders work after
   // those rects without waiting for the rest of the launch.
+  // Without signal, signal_rects > 0 only gives the first rects their own
+  // rows per task (the direct-store one-launch pass: shorter edge tasks).
   uint64_t* signal = nullptr;
   int signal_rects = 0;
   int signal_chunk_rows = 0;  // rows per task of the signal rects (0: chunk_rows)

@@ -905,7 +905,7 @@ void launch(const PipeLaunch& a) {
   }
   int rows_buf[kMaxRects] = {};
   const int* rows = nullptr;
-  if (a.sig && a.sig_chunk_rows > 0) {
+  if (a.sig_rects > 0 && a.sig_chunk_rows > 0) {  // lead rects with their own task rows
     for (int i = 0; i < a.sig_rects && i < kMaxRects; ++i) rows_buf[i] = a.sig_chunk_rows;
     rows = rows_buf;
   }

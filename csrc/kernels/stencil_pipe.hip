@@ -89,7 +89,7 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
     }
     a.direct = &D;
   }
-  if (tune.signal) {
+  if (tune.signal || tune.signal_rects > 0) {  // lead rects (with or without the signal)
     RMA_CHECK_ARG(tune.signal_rects >= 1 && tune.signal_rects < nrects,
                   "signal rects " << tune.signal_rects << " of " << nrects);
     a.sig = tune.signal;

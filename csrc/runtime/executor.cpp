@@ -772,7 +772,21 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     rec(0, s_lo_);
     rec(3, s_lo_);
     dwait(s_lo_);
-    multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, with_direct(tn), s_lo_);
+    if (g.aligned && !g.interior.empty() && g.frame.size() + 1 <= (size_t)kMaxRects) {
+      // the aligned frame rects first with shorter tasks: the tasks that
+      // store images are the launch's slowest, and in one wave of tasks the
+      // slowest sets the pass (idle block slots take the extra tasks)
+      Rect rs[kMaxRects];
+      int n = 0;
+      for (const Rect& r : g.frame) rs[n++] = r;
+      rs[n++] = g.interior;
+      StencilTuning t = with_direct(tn);
+      t.signal_rects = n - 1;
+      t.signal_chunk_rows = frame_chunk_rows(K, tn.chunk_rows);
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, rs, n, t, s_lo_);
+    } else {
+      multi_step(K, Tin, Tout, iCp_, nx_, ny_, &g.out, 1, with_direct(tn), s_lo_);
+    }
     rec(4, s_lo_);
     rec(1, s_lo_);
     dpost(s_lo_);
