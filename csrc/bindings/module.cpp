@@ -620,6 +620,7 @@ PYBIND11_MODULE(_C, m) {
             d["frame_wide"] = rl(g.frame_wide);
             d["frame_tall"] = rl(g.frame_tall);
             d["interior"] = from_rect(g.interior);
+            d["tasks"] = g.tasks();  // the interior grid's tasks (fused / one-launch policy)
             return d;
           },
           py::arg("K"));

@@ -461,9 +461,8 @@ void DiffusionExecutor::multi_step(int K, double* Tin, double* Tout, const doubl
 
 bool DiffusionExecutor::fused_pass_ok(const PassGeom& g, const StencilTuning& tn) const {
   if (!sig_ || !g.aligned || tn.kernel < 9 || g.interior.empty()) return false;
-  // direct-store halos: split passes, the interior on the plain kernel (one
-  // fused launch would run every task in the direct-store variant, ~4 % slower)
-  if (direct_active()) return false;
+  // direct-store halos of this rank's own images: the one-launch pass
+  if (direct_active() && !direct_remote()) return false;
   int nf = 0;
   for (const Rect& r : g.frame) nf += r.empty() ? 0 : 1;
   if (nf == 0 || (int)g.frame.size() + 1 > kMaxRects) return false;
@@ -488,6 +487,10 @@ void DiffusionExecutor::enqueue_fused(const std::vector<Rect>& frame, const Rect
   // the whole launch waits for the previous exchange (its frame tasks read the
   // halo) and, in stream order, for the previous launch
   RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
+  // direct-store halos: every neighbour's frame of the previous pass is done
+  // (our halo complete, its field free for our stores)
+  const bool dr = direct_remote();
+  if (dr) direct_wait(direct_pass_, s_lo_);
   Rect rs[kMaxRects];
   int n = 0;
   for (const Rect& r : frame) rs[n++] = r;
@@ -509,7 +512,10 @@ void DiffusionExecutor::enqueue_fused(const std::vector<Rect>& frame, const Rect
   rec(1, s_hi_);
   {
     TraceRange th("rma.halo");
-    exchange(Tout, s_hi_);
+    if (dr)  // the images are stored: raise our pass count at the neighbours
+      flags_write_gpu(dout_, direct_pass_ + 1, s_hi_);
+    else
+      exchange(Tout, s_hi_);
   }
   rec(2, s_hi_);
   RMA_HIP_CHECK(hipEventRecord(E(e_hi_), S(s_hi_)));
@@ -761,12 +767,15 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     if (ev[4]) tseq_.push_back(1);
     return;
   }
-  if (da && (g.frame.empty() || g.tasks() <= 2 * (int64_t)cus_)) {
-    // direct stores, tiles of one wave of tasks: ONE launch of the direct-store
-    // kernel over the owned rect (every task starts at once, so a frame launch
-    // beside the interior's would end with the pass anyway and only add its
-    // latency: 2048^2 periodic x+y at K=24 +3-5 % vs +39-61 % split), after the
-    // neighbours' counts of the previous pass, our count raised after it
+  if (da && (!dr || g.frame.empty() || g.tasks() <= 2 * (int64_t)cus_)) {
+    // direct stores to this rank's own periodic images, or tiles of one wave
+    // of tasks: ONE launch of the direct-store kernel over the owned rect
+    // (one wave: every task starts at once, so a frame launch beside the
+    // interior's would end with the pass anyway and only add its latency:
+    // 2048^2 periodic x+y at K=24 +3-5 % vs +39-61 % split), after the
+    // neighbours' counts of the previous pass, our count raised after it.
+    // Several waves with other ranks: the fused pass below (counts raised
+    // when the frame tasks are done)
     TraceRange tr("rma.pass.direct");
     RMA_HIP_CHECK(hipStreamWaitEvent(S(s_lo_), E(e_hi_), 0));
     rec(0, s_lo_);
@@ -824,7 +833,7 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
     // grid. The next pass waits for this exchange (its frame tasks read the
     // halo) and, in stream order, for this launch.
     TraceRange tr("rma.pass.fused");
-    enqueue_fused(g.frame, g.interior, tn, Tout, ev,
+    enqueue_fused(g.frame, g.interior, with_direct(tn), Tout, ev,
                   [&](const Rect* rs, int n, const StencilTuning& t) {
                     multi_step(K, Tin, Tout, iCp_, nx_, ny_, rs, n, t, s_lo_);
                   });

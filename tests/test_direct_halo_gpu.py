@@ -9,6 +9,7 @@ global grid (reference semantics: update_halo! in the time loop,
 scripts/diffusion_2D_perf_hide.jl:94-101, scripts/diffusion_2D_perf.jl:51)."""
 import numpy as np
 import pytest
+import torch
 
 from helpers import run_loopback
 from rocm_mpi_amd.models import Diffusion2D, DiffusionConfig
@@ -67,7 +68,10 @@ def spmd(rank, hub, nx, ny, nt, dims, periods, K, direct):
             return g["aligned"] and x1 > x0 and y1 > y0 and any(
                 r[1] > r[0] and r[3] > r[2] for r in g["frame"])
 
-        want = sum(1 for k in plan if fusable(geos[k]))
+        # direct mode fuses only with other ranks and more than one wave of
+        # tasks (one-wave tiles: one launch per pass)
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        want = sum(1 for k in plan if fusable(geos[k]) and geos[k]["tasks"] > 2 * cus)
         m.step(nt)
         m.synchronize()
         out = (m.g.coords, m.field.cpu().numpy().copy(), m.g.nxyz_g,
@@ -81,6 +85,7 @@ def spmd(rank, hub, nx, ny, nt, dims, periods, K, direct):
 @pytest.mark.parametrize("dims,periods,K,nx,ny,nt,fused", [
     ((2, 2), (0, 0), 24, 1028, 900, 53, "auto"),
     ((2, 2), (1, 1), 24, 1100, 3500, 49, "1"),
+    ((2, 1), (1, 0), 24, 3000, 5000, 49, "1"),
     ((2, 2), (1, 0), 8, 516, 400, 29, "0"),
     ((2, 1), (0, 1), 16, 1028, 600, 41, "auto"),
     ((1, 2), (0, 0), 20, 1100, 3000, 47, "1"),
@@ -89,7 +94,7 @@ def spmd(rank, hub, nx, ny, nt, dims, periods, K, direct):
 def test_direct_loopback_ranks_equal_one_rank(dims, periods, K, nx, ny, nt, fused, monkeypatch):
     """Rank threads of one process (loopback) storing into each other's
     fields: every tile == its window of the 1-rank run, bitwise, with
-    one-launch and split passes; every pass ran in direct mode."""
+    one-launch, fused and split passes; every pass ran in direct mode."""
     P = dims[0] * dims[1]
     monkeypatch.setenv("RMA_EXEC_FUSED", fused)
     res = run_loopback(P, spmd, nx, ny, nt, dims, periods, K, True, timeout=240)
@@ -105,13 +110,14 @@ def test_direct_loopback_ranks_equal_one_rank(dims, periods, K, nx, ny, nt, fuse
         assert direct and dpasses >= 2, (coords, dpasses)
         gx0, gy0 = coords[0] * (nx - ol), coords[1] * (ny - ol)
         assert np.array_equal(T, one[gy0:gy0 + ny, gx0:gx0 + nx]), coords
-    # direct mode never fuses (one launch would run every task in the kernels'
-    # direct-store variant): one launch per pass for one-wave tiles, split
-    # passes beyond, even where RMA_EXEC_FUSED=1 and the frames align (the
-    # geometries of the "1" cases do)
-    assert all(r[3][2] == 0 for r in res), [r[3] for r in res]
+    # RMA_EXEC_FUSED=1: every pass with aligned frames and more than one wave
+    # of tasks ran fused (frame tasks first, counts raised at their flag);
+    # one-wave tiles ran one launch per pass; 0: never fused
     if fused == "1":
-        assert all(r[3][3] > 0 for r in res), [r[3] for r in res]
+        assert all(r[3][2] == r[3][3] for r in res), [r[3] for r in res]
+        assert nx * ny < 10**7 or all(r[3][2] > 0 for r in res)  # the big case fuses
+    if fused == "0":
+        assert all(r[3][2] == 0 for r in res), [r[3] for r in res]
 
 
 def test_direct_refuses_canonical_passes():
