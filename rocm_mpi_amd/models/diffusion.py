@@ -211,6 +211,9 @@ class Diffusion2D:
             self.use_graph = use_graph
             self.executor = self._build_executor()
             self._setup_direct()
+        elif cfg.halo_direct:
+            raise ValueError("halo_direct needs the native GPU executor (fast-math perf / "
+                             "perf_hide on a GPU); the CPU and torch paths exchange halos")
         self._ap_graph = None
         if cfg.variant == "ap" and cfg.use_graph:
             # ap on a GPU is ~11 small torch launches per step: replay them from
