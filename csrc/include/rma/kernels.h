@@ -125,7 +125,8 @@ int pipe_default_cols(int K, int stages, int arith);
 // else 1. The executor's frame geometry uses the same answer.
 int pipe_vec(int K, int stages, int arith, int64_t nx, int requested, bool aligned16);
 // Blocks per CU of the core pipelined kernel (occ[0]) and of its direct-store
-// variant (occ[1]; 0 when it has none) for (K, stages, arith, V): the
+// variant (occ[1]; 0 when it has none; both 0 outside the core library) for
+// (K, stages, arith, V): the
 // executor prices direct-store passes with it (DiffusionExecutor::set_direct).
 void stencil_pipe_occupancy(int K, int stages, int arith, int V, int occ[2]);
 // arith: 0 fast5, 1 canonical, 2 fast5 with ds_bpermute lane moves (kernel 11)

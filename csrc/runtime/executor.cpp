@@ -622,10 +622,13 @@ void DiffusionExecutor::set_direct(const std::array<DirectPeer, 8>& peers, uint6
   if (any) {
     const bool al = ((reinterpret_cast<uintptr_t>(T_) | reinterpret_cast<uintptr_t>(T2_) |
                       reinterpret_cast<uintptr_t>(iCp_)) & 15) == 0;
-    for (int K = 2; K < (int)cost_.size(); ++K) {
+    for (int K = 1; K < (int)cost_.size(); ++K) {
       if (!std::isfinite(cost_[K])) continue;
       const StencilTuning t = pass_tuning(K, 0);
-      if (t.kernel < 9) continue;
+      if (t.kernel < 9) {  // no pipelined kernel at this depth: no direct-store variant
+        cost_[K] = std::numeric_limits<double>::infinity();
+        continue;
+      }
       const int arith = t.kernel - 9;
       const int S = t.stages > 0 ? t.stages : pipe_default_stages(K);
       int occ[2] = {0, 0};
