@@ -168,6 +168,11 @@ def build_parser(variant: str) -> argparse.ArgumentParser:
     ap.add_argument("--canonical", dest="fast_math", action="store_false",
                     help="the bitwise-canonical arithmetic in every pass (the reference's "
                          "flux form; K-step passes stay bitwise equal to K one-step updates)")
+    ap.add_argument("--halo-direct", dest="halo_direct", action="store_true",
+                    help="direct-store halos: the K-step kernels store the neighbours' halo "
+                         "cells into their fields (own periodic images, loopback ranks, IPC "
+                         "processes of one node) instead of an exchange; fast-math perf / "
+                         "perf_hide passes on a GPU (e.g. with --bench-plan)")
     ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf guard period")
     ap.add_argument("--checkpoint", default="", help="save the final state to this directory")
     ap.add_argument("--resume", default="", help="start from a checkpoint directory")
@@ -207,13 +212,15 @@ def resolve(variant: str, argv=None):
         parser.error("--temporal > 1 applies to the perf and perf_hide variants")
     if a.fast_math and base not in ("perf", "perf_hide"):
         parser.error("--fast-math applies to the perf and perf_hide variants")
+    if a.halo_direct and base not in ("perf", "perf_hide"):
+        parser.error("--halo-direct applies to the perf and perf_hide variants")
     opts = dict(variant=base, nx=a.nx, ny=a.ny, nt=a.nt, warmup=a.warmup, b_width=a.b_width,
                 init=a.init, init_on=a.init_on, seed=a.seed, dims=tuple(a.dims) + (0,),
                 periods=tuple(a.periods) + (0,), transport=a.transport, device=a.device,
                 chunk_rows=a.chunk_rows, unroll=a.unroll, vec=a.vec, kernel=a.kernel,
                 nontemporal=a.nontemporal, use_graph=a.graph, do_vis=a.do_vis, outdir=a.outdir,
                 profile=a.profile, check_every=a.check_every, quiet=a.quiet,
-                chunk2=a.chunk2, unroll2=a.unroll2)
+                chunk2=a.chunk2, unroll2=a.unroll2, halo_direct=a.halo_direct)
     if a.auto_size:
         rank, size, _ = C.env_world()
         if size > 1:

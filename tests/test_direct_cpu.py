@@ -65,3 +65,17 @@ def test_ipc_map_rejects_malformed_exports_before_any_hip_call():
     with pytest.raises(RuntimeError, match="IPC pointer export"):
         m.open(b"too short")
     assert m.mappings == 0
+
+
+def test_entry_points_take_halo_direct():
+    """--halo-direct reaches the model config of the perf / perf_hide entry
+    points (the reference-named scripts) and is refused for the others."""
+    from rocm_mpi_amd.apps.cli import resolve
+
+    cfg, _ = resolve("perf_hide", ["--nx", "260", "--ny", "260", "--nt", "40", "--temporal", "8",
+                                   "--halo-direct", "--device", "cpu"])
+    assert cfg.halo_direct and cfg.fast_math and cfg.temporal > 1
+    cfg, _ = resolve("perf", ["--nx", "130", "--ny", "130", "--nt", "20", "--device", "cpu"])
+    assert not cfg.halo_direct
+    with pytest.raises(SystemExit):
+        resolve("kp", ["--nx", "130", "--ny", "130", "--halo-direct"])
