@@ -946,6 +946,8 @@ bool dispatch_b(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
 // register-resident factors (stencil_pipe_r.hip): fast5, S = 4, K = 10..24
 bool dispatch_r(int K, int S, int V, int ar, const PipeLaunch& a);
+// ... K = 20 of it, compiled with another machine scheduler (stencil_pipe_r20.hip)
+bool dispatch_r20(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe
 }  // namespace rma

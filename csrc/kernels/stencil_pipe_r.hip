@@ -25,7 +25,7 @@ bool dispatch_r(int K, int S, int V, int ar, const PipeLaunch& a) {
   RMA_PIPE_CASE(17, 4, kArFast5Reg)
   RMA_PIPE_CASE(18, 4, kArFast5Reg)
   RMA_PIPE_CASE(19, 4, kArFast5Reg)
-  RMA_PIPE_CASE(20, 4, kArFast5Reg)
+  // K = 20: stencil_pipe_r20.hip
   RMA_PIPE_CASE(21, 4, kArFast5Reg)
   RMA_PIPE_CASE(22, 4, kArFast5Reg)
   RMA_PIPE_CASE(23, 4, kArFast5Reg)

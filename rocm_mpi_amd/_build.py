@@ -98,9 +98,13 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"-I{INC}", "-Wall"
 OFFLOAD = [f"--offload-arch={ARCH}", "--offload-compress"]
 
 
+# per-unit compiler flags (measured; the unit's header comment says why)
+UNIT_FLAGS = {"stencil_pipe_r20.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
+
+
 def _hip_cmd(src: Path, obj: Path) -> list[str]:
-    return [_hipcc(), "-x", "hip", *OFFLOAD, *COMMON, "-munsafe-fp-atomics",
-            "-c", str(src), "-o", str(obj)]
+    return [_hipcc(), "-x", "hip", *OFFLOAD, *COMMON, *UNIT_FLAGS.get(src.name, []),
+            "-munsafe-fp-atomics", "-c", str(src), "-o", str(obj)]
 
 
 def _host_cmd(src: Path, obj: Path) -> list[str]:
@@ -121,7 +125,8 @@ def source_stamp() -> str:
     h = hashlib.sha1()
     # flags with the checkout's absolute path taken out: a snapshot of the same
     # tree under another directory (a GPU box) has the same stamp
-    flags = " ".join(COMMON + OFFLOAD + [sysconfig.get_config_var("EXT_SUFFIX") or ""])
+    flags = " ".join(COMMON + OFFLOAD + [sysconfig.get_config_var("EXT_SUFFIX") or ""] +
+                     [f"{k}:{' '.join(v)}" for k, v in sorted(UNIT_FLAGS.items())])
     h.update(flags.replace(str(ROOT), "<root>").encode())
     for p in sorted(set(HIP_SOURCES + LAB_SOURCES + HOST_SOURCES + EXAMPLES + TOOLS + _headers())):
         h.update(str(p.relative_to(ROOT)).encode())
