@@ -746,9 +746,23 @@ class Diffusion2D:
             self.executor = None
             if getattr(self, "_ipc_map", None) is not None:
                 # every rank's kernels are done storing into the mapped peers
-                # (its synchronize above) before any rank unmaps or frees
+                # (its synchronize above) before any rank unmaps or frees. Our
+                # own run already waited for every neighbour's last stores into
+                # us, so a dead peer only costs this bounded wait
+                import datetime
+                import os
+                import warnings
+
+                from ..parallel.comm import _gloo_group
+
+                tmo = float(os.environ.get("RMA_TEARDOWN_TIMEOUT", "30"))
                 try:
-                    self.g.comm.barrier()
+                    dist.barrier(group=_gloo_group(), async_op=True).wait(
+                        timeout=datetime.timedelta(seconds=tmo))
+                except Exception as e:  # noqa: BLE001 - a dead peer must not hang close()
+                    warnings.warn(f"halo_direct teardown: the peers' barrier did not complete "
+                                  f"within {tmo:.0f} s ({e}); unmapping anyway",
+                                  RuntimeWarning, stacklevel=2)
                 finally:
                     self._ipc_map.close_all()
                     self._ipc_map = None

@@ -163,3 +163,32 @@ def test_direct_ipc_processes_equal_the_exchange(tmp_path, dims, periods, K, nx,
         assert on == 1 and dpasses == npass >= 2 and maps >= 1, ma
         assert int(mb[3]) == 0
         assert np.array_equal(a, b), ma[:2]
+
+
+def test_entry_point_runs_direct_halos():
+    """The reference-named perf_hide entry point with --halo-direct on a
+    periodic single-rank grid: runs, reports, and its field equals the same
+    run without direct stores (checkpointed tiles compared bitwise)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import tempfile
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for direct in (True, False):
+            ck = os.path.join(td, f"ck{int(direct)}")
+            cmd = [sys.executable, "-m", "rocm_mpi_amd.apps.diffusion_2D_perf_hide", "--nx", "1028",
+                   "--ny", "1028", "--nt", "60", "--temporal", "24", "--periods", "1,1",
+                   "--no-vis", "--json", "--quiet", "--checkpoint", ck]
+            if direct:
+                cmd.append("--halo-direct")
+            r = subprocess.run(cmd, capture_output=True, text=True, cwd=root, timeout=240,
+                               env=dict(os.environ, RMA_AUTOBUILD="0"))
+            assert r.returncode == 0, r.stderr[-3000:]
+            rec = json.loads(r.stdout.strip().splitlines()[-1])
+            assert rec["nt"] == 60
+            out[direct] = np.load(os.path.join(ck, "rank0.npy"), allow_pickle=False)
+    assert np.array_equal(out[True], out[False])
