@@ -39,6 +39,16 @@ if which == "fast":  # fast-math K-step kernels at the executor's tuning (bench 
     torch.cuda.synchronize()
     print(f"probe done n={n} reps={reps} set={which} K={K} chunk={ch}")
     sys.exit(0)
+if which == "piper":  # the executor's register-factor kernel alone (scheduler A/B counters)
+    K = int(os.environ.get("RMA_PROBE_K", "20"))
+    ch = nat.pipe_chunk_rows(K, n, False) or nat.default_chunk_k(K, n)
+    rect = [ops.interior_rect(n, n)]
+    for _ in range(reps):
+        ops.stencilk_step(K, T2, T, iCp, c, rect,
+                          ops.StencilTuning(chunk_rows=ch, xcd_remap=1, kernel="piper", vec=4))
+    torch.cuda.synchronize()
+    print(f"probe done n={n} reps={reps} set={which} K={K} chunk={ch}")
+    sys.exit(0)
 if which == "cols":  # piper with 1 vs 2 column waves per stage
     from rocm_mpi_amd._native import load_lab
 
