@@ -868,7 +868,7 @@ __global__ __launch_bounds__(kWave * S * C) __attribute__((amdgpu_waves_per_eu(
 // (kArFast5 at every K, the register-factor kArFast5Reg) at one column wave
 template <int V, int Ar, int C>
 constexpr bool has_direct() {
-  return C == 1 && V != 5 && (Ar == kArFast5 || Ar == kArFast5Reg);
+  return C == 1 && V != 5 && (Ar == kArFast5 || Ar == kArFast5Reg || Ar == kArFast5RegNoSB);
 }
 
 struct PipeLaunch {
@@ -948,6 +948,9 @@ bool dispatch_c(int K, int S, int V, int ar, const PipeLaunch& a);
 bool dispatch_r(int K, int S, int V, int ar, const PipeLaunch& a);
 // ... K = 20 of it, compiled with another machine scheduler (stencil_pipe_r20.hip)
 bool dispatch_r20(int K, int S, int V, int ar, const PipeLaunch& a);
+// the executor's K = 24 kernel: piper without in-level sched_barriers, the
+// same scheduler (stencil_pipe_r24.hip)
+bool dispatch_r24(int K, int S, int V, int ar, const PipeLaunch& a);
 
 }  // namespace pipe
 }  // namespace rma

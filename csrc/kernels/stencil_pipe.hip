@@ -26,7 +26,8 @@ void stencil_pipe_occupancy(int K, int stages, int arith, int V, int occ[2]) {
   // lab variants (other splits, 5 cells per lane, ...) have no direct-store
   // instantiation: {0, 0}, which the executor prices as unavailable
   if (V != 5)
-    (void)(pipe::dispatch_r20(K, S, V, arith, a) || pipe::dispatch_r(K, S, V, arith, a) ||
+    (void)(pipe::dispatch_r20(K, S, V, arith, a) || pipe::dispatch_r24(K, S, V, arith, a) ||
+           pipe::dispatch_r(K, S, V, arith, a) ||
            pipe::dispatch_a(K, S, V, arith, a) ||
            pipe::dispatch_b(K, S, V, arith, a) || pipe::dispatch_c(K, S, V, arith, a));
 }
@@ -101,7 +102,8 @@ void stencil_pipe_rects_gpu(int K, int stages, int arith, double* T2, const doub
   }
   // V = 5 only in the lab (the core units' cases take any V other than 4 and 2 as 1)
   bool ok = C == 1 && V != 5 &&
-            (pipe::dispatch_r20(K, S, V, arith, a) || pipe::dispatch_r(K, S, V, arith, a) ||
+            (pipe::dispatch_r20(K, S, V, arith, a) || pipe::dispatch_r24(K, S, V, arith, a) ||
+           pipe::dispatch_r(K, S, V, arith, a) ||
              pipe::dispatch_a(K, S, V, arith, a) ||
              pipe::dispatch_b(K, S, V, arith, a) || pipe::dispatch_c(K, S, V, arith, a));
   if (!ok) {  // alternative stage splits, pipeb, two-column blocks, 5 cells: librma_lab.so

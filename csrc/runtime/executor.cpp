@@ -69,6 +69,9 @@ StencilTuning fast_tune_k(int K, int64_t ny, const StencilCoef& c) {
   // (profiles/SUMMARY_r3.md), so K = 10..13 only on the large tile classes
   if ((K >= 14 || (K >= 10 && ny >= 65536)) && pipe_has(K, pipe_default_stages(K), 3))
     t.kernel = 12;
+  // K = 24: piper without the in-level sched_barriers under the iterative-ILP
+  // scheduler (kernel 22, stencil_pipe_r24.hip): -1.3 % per pass at 101376^2
+  if (K == 24 && t.kernel == 12) t.kernel = 22;  // 9 + kArFast5RegNoSB
   // RMA_DIAG pipe_fast=pipe | pipe5 forces the ring kernel at every depth (A/B
   // runs; pipe5 = 5 cells per lane, lab library, K = 16..20 and nx % 5 == 0)
   static const std::string force = diag_value("pipe_fast");

@@ -99,7 +99,8 @@ OFFLOAD = [f"--offload-arch={ARCH}", "--offload-compress"]
 
 
 # per-unit compiler flags (measured; the unit's header comment says why)
-UNIT_FLAGS = {"stencil_pipe_r20.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
+UNIT_FLAGS = {"stencil_pipe_r20.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+              "stencil_pipe_r24.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 
 
 def _hip_cmd(src: Path, obj: Path) -> list[str]:
