@@ -506,10 +506,10 @@ def run(a, world: int, rank: int) -> int:
                     kern, kvec, kch = native().fast_kernel_k(depth, ny, tuple(model.coef))
                 else:
                     kern, kvec, kch = native().canonical_kernel_k(depth, ny)
-                names = {v: k for k, v in ops.KERNELS.items()}
+
                 if kern >= 9:  # the cells per lane the kernel runs (vec 5 needs nx % 5 == 0)
                     kvec = native().pipe_vec(depth, 0, kern - 9, nx, kvec, True)
-                kinfo = {"kernel": names[kern], "vec": kvec, "chunk_rows": a.chunk2 or kch,
+                kinfo = {"kernel": ops.kernel_name(kern), "vec": kvec, "chunk_rows": a.chunk2 or kch,
                          "stages": native().pipe_default_stages(depth) if kern >= 9 else None}
         model.close()
         del model

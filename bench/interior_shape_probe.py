@@ -64,8 +64,7 @@ def main() -> int:
         dx = 10.0 / n
         coef = ops.StencilCoef.from_physics(1.0, dx, dx, dx * dx / 4.1)
     kern, vec, ch = native().fast_kernel_k(K, n, tuple(coef))
-    names = {v: k for k, v in ops.KERNELS.items()}
-    tn = ops.StencilTuning(chunk_rows=ch, kernel=names[kern], vec=vec, xcd_remap=1)
+    tn = ops.StencilTuning(chunk_rows=ch, kernel=ops.kernel_name(kern), vec=vec, xcd_remap=1)
     f = 128 - 2 * K + K  # interior start next to an ol-wide frame strip (frame fill)
     rects = {
         "open": (1, n - 1, 1, n - 1),

@@ -183,7 +183,8 @@ constexpr double kInf = std::numeric_limits<double>::infinity();
 // K >= 21 canonical passes drop to one wave per SIMD (188 ms at 101376^2). Round 6: the
 // fast5 K = 20 entry of the 288 GB row and the K = 24 entries of the 8192^2 / 16384^2 /
 // 288 GB rows scaled by the measured scheduler / no-sched-barrier ratios
-// (profiles/r6/sched_strategy_ab.md: K = 20 x0.989; K = 24 x0.932 / x0.997 / x0.989).
+// (profiles/r6/sched_strategy_ab.md; scripts/fit_pass_costs.py r6_ratios: K = 20 x0.9886;
+// K = 24 x0.9320 / x0.9975 / x0.9893).
 constexpr int kTables = 4;
 constexpr double kTileCells[kTables] = {4096.0 * 4096, 8192.0 * 8192, 16384.0 * 16384,
                                         101376.0 * 101376};
@@ -195,7 +196,7 @@ constexpr double kFast5[kTables][25] = {
     {0, 1.373, 1.375, 1.412, 1.298, 1.282, 1.275, 1.273, 1.217, 1.414, 1.326, 1.328, 1.294,
      1.410, 1.440, 1.605, 1.575, 1.896, 1.922, 1.885, 1.943, 2.101, 2.119, 2.168, 2.197},
     {0, 1.235, 1.230, 1.215, 1.163, 1.232, 1.210, 1.199, 1.126, 1.149, 1.138, 1.144, 1.119,
-     1.244, 1.306, 1.371, 1.399, 1.595, 1.640, 1.676, 1.659, 1.886, 1.903, 1.971, 1.961}
+     1.244, 1.306, 1.371, 1.399, 1.595, 1.640, 1.676, 1.658, 1.886, 1.903, 1.971, 1.962}
 };
 constexpr double kCanon[kTables][25] = {
     {0, 1.000, 1.058, 1.095, 1.246, 1.335, 1.326, 1.757, 1.897, 2.226, 2.214, 2.295, 2.384,

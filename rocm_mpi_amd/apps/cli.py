@@ -261,7 +261,7 @@ def plan_line(model, steps: int) -> str:
                 kid = native().fast_kernel_k(K, cfg.ny, tuple(model.coef))[0]
             else:
                 kid = native().canonical_kernel_k(K, cfg.ny)[0]
-            kern = ", kernel " + {v: k for k, v in ops.KERNELS.items()}.get(kid, str(kid))
+            kern = ", kernel " + ops.kernel_name(kid)
         except Exception:  # noqa: BLE001 - informational only
             pass
     arith = ("fast-math (5-point sum, folded factor; rounding-level vs canonical)"

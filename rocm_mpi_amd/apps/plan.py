@@ -31,7 +31,6 @@ def describe(nx: int, ny: int, steps: int, temporal: int = 24, fast_math: bool =
     plan = list(N.plan_passes(int(steps), costs))
     unit_ms = _MS_PER_CELL * cells
     kernels = {}
-    names = {v: k for k, v in ops.KERNELS.items()}
     for K in sorted(set(plan)):
         if fast_math:
             kern, vec, ch = N.fast_kernel_k(K, ny, (-1.0, 1.0, 1.0, 0.1))
@@ -39,7 +38,7 @@ def describe(nx: int, ny: int, steps: int, temporal: int = 24, fast_math: bool =
             kern, vec, ch = 0, 2, N.default_chunk_k(1, ny)
         else:
             kern, vec, ch = N.canonical_kernel_k(K, ny)
-        kernels[K] = {"kernel": names.get(kern, kern), "vec": vec, "chunk_rows": ch,
+        kernels[K] = {"kernel": ops.kernel_name(kern), "vec": vec, "chunk_rows": ch,
                       "stages": N.pipe_default_stages(K) if kern >= 9 else None,
                       "rel_cost": round(costs[K], 3), "pred_ms_per_pass": round(costs[K] * unit_ms, 3)}
     pred = sum(costs[K] for K in plan) * unit_ms

@@ -538,7 +538,7 @@ class Diffusion2D:
                 fn = native().fast_kernel_k if fast else None
                 kern, vec, ch = (fn(K, cfg.ny, tuple(self.coef)) if fn
                                  else native().canonical_kernel_k(K, cfg.ny))
-                name = {v: k for k, v in ops.KERNELS.items()}[kern]
+                name = ops.kernel_name(kern)
                 tn = ops.StencilTuning(chunk_rows=cfg.chunk2 or ch, xcd_remap=1, kernel=name,
                                        vec=vec)
             else:  # the C++ twin of the pass arithmetic

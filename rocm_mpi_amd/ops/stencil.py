@@ -87,8 +87,21 @@ def kernel_id(name: str) -> int:
     raise ValueError(f"unknown kernel {name!r}: one of {sorted(KERNELS) + sorted(LAB_KERNELS)}")
 
 
+def kernel_name(kid: int) -> str:
+    """Name of a numeric kernel id (core or lab table). The executor's own
+    choices include lab-named ids: its K = 24 kernel is "piper_nosb" (22),
+    instantiated in the core as well (csrc/kernels/stencil_pipe_r24.hip)."""
+    for table in (KERNELS, LAB_KERNELS):
+        for k, v in table.items():
+            if v == kid:
+                return k
+    raise ValueError(f"unknown kernel id {kid}")
+
+
 def _kstep_needs_lab(K: int, tn: "StencilTuning") -> bool:
     """Does this K-step launch run a librma_lab.so kernel?"""
+    if tn.kernel == "piper_nosb" and K == 24 and tn.cols != 2 and not tn.stages:
+        return False  # the executor's K = 24 kernel, in the core (stencil_pipe_r24.hip)
     if tn.kernel not in KSTEP_CORE or tn.cols == 2 or (tn.kernel == "pipe" and tn.vec == 5):
         return True
     if tn.kernel in PIPE and tn.stages and has_native():

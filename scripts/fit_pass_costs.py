@@ -8,6 +8,7 @@ canonical pipelined kernel from K=5), missing depths interpolated linearly.
     python scripts/fit_pass_costs.py profiles/pass_sweep_r2.json profiles/pass_sweep_{16384,8192,4096}_r2.json
 """
 import json
+import os
 import sys
 
 KMAX = 24
@@ -110,6 +111,43 @@ def u6_ratios(path: str) -> dict:
 def apply_u6(fast: list, ratios: dict) -> list:
     """Scale the measured depths (K = 17..20) by the unroll-by-6 ratios
     (rounded to the table's 3 decimals after the round-3 scaling, as committed)."""
+    out = list(fast)
+    for K, f in ratios.items():
+        out[K - 1] = round(round(fast[K - 1], 3) * f, 3)
+    return out
+
+
+# round 6 (profiles/r6/sched_strategy_ab.md): the K = 20 unit under the iterative-ILP
+# scheduler (288 GB class, previous vs adopted library, 3 alternations) and the K = 24
+# kernel without in-level sched_barriers under it (same process as the previous piper,
+# per tile class)
+R6_K20 = {101376: ("r6/sched_ab/r20_sweep_base_{}.json", "r6/sched_ab/r20_sweep_r20_{}.json")}
+R6_K24 = {101376: "r6/sched_ab/r24/sweep_0.json", 16384: "r6/sched_ab/r24/sweep_16384.json",
+          8192: "r6/sched_ab/r24/sweep_8192.json"}
+
+
+def _exec_ms(path: str, K: int, kernel: str = "exec") -> float:
+    with open(path) as f:
+        d = json.load(f)
+    return next(r["ms_per_pass"] for r in d["rows"] if r["kernel"] == kernel and r["K"] == K)
+
+
+def r6_ratios(tile: int, root: str) -> dict:
+    """{K: new / old pass time} of the round-6 kernel changes measured at this tile class."""
+    out = {}
+    if tile in R6_K20:
+        old, new = R6_K20[tile]
+        o = [_exec_ms(os.path.join(root, old.format(i)), 20) for i in (1, 2, 3)]
+        n = [_exec_ms(os.path.join(root, new.format(i)), 20) for i in (1, 2, 3)]
+        out[20] = sum(n) / sum(o)
+    if tile in R6_K24:
+        p = os.path.join(root, R6_K24[tile])
+        out[24] = _exec_ms(p, 24) / _exec_ms(p, 24, "piper")
+    return out
+
+
+def apply_r6(fast: list, ratios: dict) -> list:
+    """Scale the committed table entries (3 decimals) by the round-6 ratios."""
     out = list(fast)
     for K, f in ratios.items():
         out[K - 1] = round(round(fast[K - 1], 3) * f, 3)

@@ -33,6 +33,8 @@ def test_planner_tables_come_from_the_committed_sweeps(tile):
             [os.path.join(P, q) for q in fpc.PIPER_SWEEPS_101376]), 10)
     # round 4: K = 17..20 scaled by the unroll-by-6 / unroll-by-3 ratios
     fast = fpc.apply_u6(fast, fpc.u6_ratios(os.path.join(P, fpc.U6_SWEEPS[tile])))
+    # round 6: the K = 20 / K = 24 kernels under the iterative-ILP scheduler
+    fast = fpc.apply_r6(fast, fpc.r6_ratios(tile, P))
     cells = float(tile) * tile
     got_f = list(N.default_pass_costs(24, True, cells))[1:]
     got_c = list(N.default_pass_costs(24, False, cells))[1:]
@@ -92,7 +94,8 @@ def test_pipe_chunk_rows_by_tile_class():
 def test_fast_kernel_choice_by_depth():
     """The executor's fast-math kernel per pass depth: the register-factor
     pipelined kernel ("piper", 12) from K = 14 (from K = 10 on tiles of >= 65536
-    rows), the ring kernel ("pipe", 9) below; cells per lane as the kernel will run them (pipe_vec: 5 only for the
+    rows), at K = 24 its variant without in-level sched_barriers ("piper_nosb",
+    22, round 6), the ring kernel ("pipe", 9) below; cells per lane as the kernel will run them (pipe_vec: 5 only for the
     lab's fast5 K = 16..20 on nx % 5 == 0, else 4 / 2 / 1 by alignment)."""
     nat = pytest.importorskip("rocm_mpi_amd._native")
     try:
@@ -101,10 +104,10 @@ def test_fast_kernel_choice_by_depth():
         pytest.skip(f"native core not built: {e}")
     coef = (-1.0, 10.0, 10.0, 1e-3)
     kern = {K: N.fast_kernel_k(K, 101376, coef)[0] for K in range(3, 25)}
-    assert all(kern[K] == 12 for K in range(10, 25)), kern
+    assert all(kern[K] == 12 for K in range(10, 24)) and kern[24] == 22, kern
     assert all(kern[K] == 9 for K in range(3, 10)), kern
     small = {K: N.fast_kernel_k(K, 16384, coef)[0] for K in range(3, 25)}
-    assert all(small[K] == 12 for K in range(14, 25)), small
+    assert all(small[K] == 12 for K in range(14, 24)) and small[24] == 22, small
     assert all(small[K] == 9 for K in range(3, 14)), small
     assert N.pipe_vec(20, 0, 0, 101120, 5, True) == 5
     assert N.pipe_vec(20, 0, 0, 101376, 5, True) == 4      # nx % 5 != 0
