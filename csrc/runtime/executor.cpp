@@ -464,8 +464,6 @@ void DiffusionExecutor::multi_step(int K, double* Tin, double* Tout, const doubl
 
 bool DiffusionExecutor::fused_pass_ok(const PassGeom& g, const StencilTuning& tn) const {
   if (!sig_ || !g.aligned || tn.kernel < 9 || g.interior.empty()) return false;
-  // direct-store halos of this rank's own images: the one-launch pass
-  if (direct_active() && !direct_remote()) return false;
   int nf = 0;
   for (const Rect& r : g.frame) nf += r.empty() ? 0 : 1;
   if (nf == 0 || (int)g.frame.size() + 1 > kMaxRects) return false;
@@ -726,7 +724,13 @@ void DiffusionExecutor::enqueue_pass(int K, double* Tin, double* Tout) {
   // perf and of a one-wave tile, the frame launches of a split pass) run the
   // kernels' direct-store variant instead of an exchange after the pass; a
   // split pass's interior launch stays the plain kernel
-  const bool da = direct_active(), dr = direct_remote();
+  // A rank whose only direct peer is itself, on a tile of several task waves,
+  // keeps the exchange (local copies): there the direct-store variant's slower
+  // row loop costs more than the exchange it saves (periodic x+y K=24 8192^2:
+  // +9 % vs +0 %); the stores win where the exchange latency is the pass (one
+  // wave of tasks: 2048^2 +4 % vs +53 %). Other ranks always store.
+  const bool dr = direct_remote();
+  const bool da = direct_active() && (dr || g.tasks() <= 2 * (int64_t)cus_);
   struct DirectCount {  // counted however the pass is enqueued
     uint64_t& n;
     bool on;

@@ -39,10 +39,15 @@ def run_self(n, K, nt, periods, direct, variant="perf_hide", ny=None):
 @pytest.mark.parametrize("K,n,nt", [(24, 1028, 61), (8, 516, 37), (20, 2052, 45)])
 def test_direct_self_periodic_equals_exchange(periods, K, n, nt):
     """One rank, periodic: the kernel stores its own periodic images (one
-    launch per pass, no exchange) == local self copies after each pass."""
+    launch per pass, no exchange) == local self copies after each pass. A
+    single rank stores only on passes of one wave of tasks (beyond, its local
+    copies cost less than the direct-store kernel's row loop): every pass of
+    the small tiles, some of the 2052^2 K=20 plan's."""
     a, (da, dp, npass) = run_self(n, K, nt, periods, True)
     b, (db, _, _) = run_self(n, K, nt, periods, False)
-    assert da and not db and dp == npass >= 2
+    assert da and not db and npass >= 2 and 1 <= dp <= npass
+    if n <= 1028:
+        assert dp == npass
     assert np.array_equal(a, b)
 
 
