@@ -14,7 +14,7 @@ trap 'cp "$OUT/librma_core.orig" $PKG/librma_core.so' EXIT
 for r in $(seq 1 "${ROUNDS:-2}"); do
   for v in ${VARIANTS:-base ilp iter}; do
     cp "$PKG/librma_core_$v.so.alt" $PKG/librma_core.so
-    timeout -k 10 240 python3 bench/pass_sweep.py --pipe "" --exec "${EXEC:-20,24}" --pipec "" --ldsdpp "" \
+    timeout -k 10 240 python3 bench/pass_sweep.py --pipe "" --exec "${EXEC:-20,24}" --pipec "${PIPEC:-}" --ldsdpp "" \
         --old "" --alt "" --rounds 3 --out "$OUT/sweep_${v}_$r.json" > "$OUT/sweep_${v}_$r.log" 2>&1
     echo "round $r variant $v done"
   done
