@@ -42,8 +42,14 @@ VALU_CATS = ("fp64 arithmetic", "DPP lane moves", "row-register moves",
 
 
 def compile_asm(unit: str, out: str) -> str:
+    """The unit's gfx950 assembly, with the unit's own flags of the build
+    (rocm_mpi_amd/_build.py UNIT_FLAGS: the K = 20 / 24 scheduler units)."""
+    sys.path.insert(0, ROOT)
+    from rocm_mpi_amd._build import UNIT_FLAGS
+
     cmd = ["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O3", "-std=c++17",
            "-fPIC", "-ffp-contract=off", f"-I{ROOT}/csrc/include", "-munsafe-fp-atomics",
+           *UNIT_FLAGS.get(os.path.basename(unit), []),
            "--cuda-device-only", "-S", "-o", out, os.path.join(ROOT, unit)]
     subprocess.run(cmd, check=True, capture_output=True)
     return out
@@ -116,20 +122,34 @@ def main(argv=None) -> int:
     ap.add_argument("--K", type=int, nargs="+", default=[20, 24])
     ap.add_argument("--S", type=int, default=4)
     ap.add_argument("--V", type=int, default=4)
-    ap.add_argument("--ar", type=int, default=3, help="arithmetic template (3 = piper)")
-    ap.add_argument("--unit", default="csrc/kernels/stencil_pipe_r.hip")
+    ap.add_argument("--ar", type=int, default=-1,
+                    help="arithmetic template (-1: the executor's: 13 = piper without in-level "
+                         "barriers at K = 24, 3 = piper elsewhere)")
+    ap.add_argument("--unit", default="auto",
+                    help="translation unit (auto: the one holding the executor's kernel per K: "
+                         "stencil_pipe_r20.hip / _r24.hip / _r.hip)")
     ap.add_argument("--asm", default="", help="an existing .s instead of compiling")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
-    asm = a.asm or compile_asm(a.unit, "/tmp/isa_budget_unit.s")
-    lines = open(asm).read().splitlines()
+    def unit_of(K):
+        if a.unit != "auto":
+            return a.unit
+        return {20: "csrc/kernels/stencil_pipe_r20.hip",
+                24: "csrc/kernels/stencil_pipe_r24.hip"}.get(K, "csrc/kernels/stencil_pipe_r.hip")
+
+    asms = {}
     rows = []
     md = ["| K | loop (stage) | trip insts | lane-updates / trip | " +
           " | ".join(n for n, _ in CATS) + " | VALU total | VALU per update x recompute |",
           "|" + "---|" * (len(CATS) + 5)]
     for K in a.K:
         # the instantiation is named pipe_kernel<K, S, V, C, Ar>? find by prefix K,S,V
-        pref = f"_ZN3rma4pipe11pipe_kernelILi{K}ELi{a.S}ELi{a.V}ELi{a.ar}ELi1EE"
+        ar = a.ar if a.ar >= 0 else (13 if K == 24 else 3)
+        asm = a.asm or asms.setdefault(unit_of(K), compile_asm(
+            unit_of(K), f"/tmp/isa_budget_{os.path.basename(unit_of(K))}.s"))
+        lines = open(asm).read().splitlines()
+        # the plain instantiation (Dir = false; the direct-store variant is Lb1)
+        pref = f"_ZN3rma4pipe11pipe_kernelILi{K}ELi{a.S}ELi{a.V}ELi{ar}ELi1ELb0EE"
         body = [ln for ln in lines]
         try:
             kb = kernel_body(body, pref)
